@@ -1,0 +1,167 @@
+/*
+ * vdmi.h — C-ABI of libvdmi.so, the MI355X-native detect-and-blur hot path.
+ *
+ * This is the drop-in boundary for the per-frame path of the reference
+ * (xdu-Liu-learn/Video-desensitization). Each entry point names the reference
+ * interface it replaces (paths relative to the reference repository root):
+ *
+ *   vd_create / vd_load_weights  <- Retinaface.__init__/generate   detect_face/face.py:29-60
+ *                                   YOLO(plate_model_path).cuda()   combine_detect.py:872
+ *   vd_detect                    <- Retinaface.detect_images        detect_face/face.py:120-150
+ *                                   (preprocess :65-88, net :133, postprocess :93-115,
+ *                                    scaling :139-146) + int() at combine_detect.py:243
+ *   vd_detect_plates             <- plate_detector(batch, verbose=False, conf=0.5)
+ *                                                                    combine_detect.py:217
+ *   vd_mosaic                    <- mosaic_rectangle_region_single  combine_detect.py:138-161,
+ *                                   applied per box in order at     combine_detect.py:246-249
+ *   vd_process                   <- the per-batch body of batch_process_images
+ *                                                                    combine_detect.py:214-251
+ *   vd_sync / vd_last_error / vd_destroy: runtime plumbing (no reference equivalent;
+ *                                   errors map to the reference's drop-the-batch
+ *                                   behaviour at combine_detect.py:226-228 in the
+ *                                   Python wrapper).
+ *
+ * Conventions: plain pointers and sizes only. Frames are uint8 RGB, HxWx3,
+ * row pitch in bytes, frame i at base + i*h*pitch. `where` says whether a
+ * pointer is host (VD_HOST) or device (VD_DEVICE) memory of the context's GPU.
+ * The caller owns frames and box arrays; the library owns weights, device
+ * workspace and its stream. No pointer is retained past a call. Calls are
+ * asynchronous on the context stream only when every pointer is VD_DEVICE;
+ * otherwise they return after results are in the caller's host memory.
+ * Return value: VD_OK (0) or a negative VD_ERR_*; vd_last_error() gives a
+ * thread-local message. Calls on one context are serialised by a mutex;
+ * different contexts are independent (one per device/stream).
+ */
+#ifndef VDMI_H
+#define VDMI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VDMI_ABI_VERSION 1
+
+#define VD_OK            0
+#define VD_ERR_ARG      -1   /* bad argument / shape */
+#define VD_ERR_HIP      -2   /* HIP runtime error */
+#define VD_ERR_CAPACITY -3   /* a per-frame box/candidate capacity was exceeded */
+#define VD_ERR_WEIGHTS  -4   /* weight blob missing a tensor / wrong shape */
+#define VD_ERR_STATE    -5   /* call out of order (e.g. detect before weights) */
+#define VD_ERR_NOMEM    -6   /* device allocation failed */
+
+#define VD_HOST   0
+#define VD_DEVICE 1
+
+#define VD_PREC_BF16 0       /* bf16 operands, f32 accumulate (performance mode) */
+#define VD_PREC_FP32 1       /* f32 operands, exact-f32 MFMA (parity mode)       */
+
+#define VD_NET_RETINAFACE 0  /* detect_face/retinaface.py, cfg_re50 */
+#define VD_NET_YOLOV8N    1  /* ultralytics YOLOv8n plate detector [ext] */
+
+#define VD_WEIGHTS_VDW1   1  /* "VDW1" named-tensor container, see DESIGN.md */
+
+/* vd_mosaic modes */
+#define VD_MOSAIC_OUT_OF_PLACE 0   /* out = in with boxes applied (reference new-array semantics) */
+
+/* vd_process flags */
+#define VD_PROC_FACES        1     /* run the RetinaFace branch */
+#define VD_PROC_PLATES       2     /* run the YOLOv8n branch (forward + NMS) */
+#define VD_PROC_MOSAIC       4     /* write mosaicked frames to `out` */
+#define VD_PROC_MOSAIC_PLATES 8    /* "intended mode": mosaic plate boxes too. Without it
+                                      plate boxes are discarded like the reference
+                                      (combine_detect.py:239 always yields []). */
+
+typedef struct vd_ctx vd_ctx;
+
+typedef struct vd_cfg {
+    int32_t input_h, input_w;      /* RetinaFace net input; combine_detect.py:860 uses 640x640 */
+    int32_t max_batch;             /* frames per call (config.ini:35 batch_size = 64) */
+    int32_t max_frame_h, max_frame_w;
+    int32_t precision;             /* VD_PREC_* */
+    int32_t max_boxes;             /* per-frame capacity of the NMS output list */
+    float   confidence;            /* face score threshold, inclusive (utils_bbox.py:116) */
+    double  nms_iou;               /* face NMS IoU (combine_detect.py:862 -> 0.4) */
+    int32_t mosaic_level;          /* combine_detect.py:249 -> 8 */
+    int32_t plate_imgsz;           /* ultralytics imgsz (640) */
+    int32_t plate_nc;              /* plate model classes */
+    float   plate_conf;            /* combine_detect.py:217 conf=0.5 */
+    double  plate_iou;             /* ultralytics default 0.7 [ext] */
+    int32_t plate_max_det;         /* ultralytics default 300 [ext] */
+    int32_t reserved[8];
+} vd_cfg;
+
+/* Per-frame box lists, caller-allocated. Frame f's boxes live at
+ * [f*cap, f*cap + min(count[f], cap)). count[f] may exceed cap; the call then
+ * returns VD_ERR_CAPACITY after filling the first cap boxes. */
+typedef struct vd_boxes {
+    int32_t  cap;
+    int32_t  where;     /* VD_HOST or VD_DEVICE for every array below */
+    int32_t* count;     /* [n]            */
+    int32_t* xyxy;      /* [n][cap][4]    int() of the source-pixel box (combine_detect.py:243) */
+    float*   xyxy_f;    /* [n][cap][4]    float32 source-pixel box before int(); may be NULL */
+    float*   score;     /* [n][cap]       may be NULL */
+    int32_t* label;     /* [n][cap]       anchor index (faces) / class id (plates); may be NULL */
+} vd_boxes;
+
+int         vd_default_cfg(vd_cfg* cfg);
+int         vd_abi_version(void);
+const char* vd_last_error(void);
+
+int   vd_create(const vd_cfg* cfg, int device, vd_ctx** out);
+int   vd_destroy(vd_ctx* ctx);
+int   vd_load_weights(vd_ctx* ctx, int net, const void* blob, size_t bytes, int fmt);
+int   vd_set_stream(vd_ctx* ctx, void* hip_stream);   /* NULL -> library-owned stream */
+void* vd_get_stream(vd_ctx* ctx);
+int   vd_sync(vd_ctx* ctx);
+
+int vd_detect(vd_ctx* ctx, const uint8_t* frames, int n, int h, int w, size_t pitch,
+              int where, vd_boxes* faces);
+int vd_detect_plates(vd_ctx* ctx, const uint8_t* frames, int n, int h, int w, size_t pitch,
+                     int where, vd_boxes* plates);
+int vd_mosaic(vd_ctx* ctx, const uint8_t* in, uint8_t* out, int n, int h, int w, size_t pitch,
+              int where, const vd_boxes* boxes, int level, int mode);
+int vd_process(vd_ctx* ctx, const uint8_t* in, uint8_t* out, int n, int h, int w, size_t pitch,
+               int where, int flags, vd_boxes* faces, vd_boxes* plates);
+
+/* ---- instrumentation (bench / profiling) ---------------------------------- */
+/* When enabled, every launch of kernel family `fam` is bracketed by HIP events
+ * on the context stream; vd_timing_read returns the summed duration (ms), the
+ * launch count and the summed algorithmic work (FLOP or bytes) since the last
+ * reset. Families: 0 = conv (MFMA implicit GEMM), 1 = mosaic, 2 = letterbox,
+ * 3 = post (decode/NMS), 4 = other. */
+int vd_timing_enable(vd_ctx* ctx, int on);
+int vd_timing_reset(vd_ctx* ctx);
+int vd_timing_read(vd_ctx* ctx, int fam, double* ms, int64_t* launches, double* work);
+
+/* ---- test hooks (parity tests call these; same kernels as the product path) -- */
+/* Letterboxed RetinaFace input, NHWC with cpad channels (f32 regardless of precision). */
+int vdt_letterbox(vd_ctx* ctx, const uint8_t* frames, int n, int h, int w, size_t pitch,
+                  int where, float* out_nhwc, int cpad);
+/* Raw head outputs after the forward, host f32: loc [n][A][4], conf logits [n][A][2],
+ * landm [n][A][10], A = number of anchors. */
+int vdt_forward_heads(vd_ctx* ctx, const uint8_t* frames, int n, int h, int w, size_t pitch,
+                      int where, float* loc, float* conf, float* landm);
+/* Post-processing only (decode, score, threshold, NMS, correction, int()) on
+ * caller-provided host head outputs; img_hw = [n][2] source sizes. */
+int vdt_postprocess(vd_ctx* ctx, const float* loc, const float* conf, int n,
+                    const int32_t* img_hw, vd_boxes* faces);
+/* One convolution through the product conv kernel (host f32 NHWC in/out,
+ * weights [cout][kh][kw][cin] f32, BN as per-channel scale/shift, act 0=none
+ * 1=relu 2=leaky(slope) 3=silu; res (optional, NHWC [n][oh][ow][cout]) added
+ * before the activation when res_mode=1, after it when res_mode=2). */
+int vdt_conv2d(vd_ctx* ctx, const float* x, int n, int h, int w, int cin,
+               const float* wgt, int cout, int kh, int kw, int stride, int pad,
+               const float* scale, const float* shift, int act, float slope,
+               const float* res, int res_mode, float* y, int* oh, int* ow);
+/* Raw YOLO outputs [n][4+nc][A] (decoded boxes xywh in letterbox pixels + class
+ * sigmoid scores), host f32, A = anchors at the letterboxed size. */
+int vdt_plate_raw(vd_ctx* ctx, const uint8_t* frames, int n, int h, int w, size_t pitch,
+                  int where, float* out, int* anchors);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VDMI_H */

@@ -1,0 +1,157 @@
+"""End-to-end parity: letterbox -> RetinaFace forward -> decode/NMS -> correction ->
+int() -> mosaic, GPU (C-ABI) vs the CPU oracle on identical synthetic frames.
+
+* fp32 (exact-f32 MFMA) mode: head outputs within 1e-4 of the torch-CPU oracle
+  (relative to each tensor's max |value|); kept anchor indices identical except
+  for candidates whose decision is within 1e-4 of a threshold (score vs 0.5,
+  IoU vs 0.4), which the test excludes and counts; mosaic pixels bit-exact given
+  the boxes.
+* bf16 mode: heads within 6e-2 relative; >= 90 % of oracle boxes matched by a
+  GPU box at IoU >= 0.9 (bf16 rounding moves near-threshold decisions, so box
+  parity is claimed for fp32 mode only).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import anchors as oanchors
+from oracle import bbox as obbox
+from oracle import letterbox as olb
+from oracle import mosaic as omosaic
+from oracle.retinaface import build_oracle_model
+
+from conftest import face_weights
+
+pytestmark = pytest.mark.gpu
+F32 = np.float32
+
+_ORACLE = {}
+
+
+def _oracle_heads(frames, wkind="default"):
+    key = (wkind, frames.shape, int(frames[:, ::97, ::89].sum()))
+    if key not in _ORACLE:
+        torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+        m = build_oracle_model(face_weights(wkind))
+        x, _ = olb.preprocess(list(frames))
+        with torch.no_grad():
+            loc, cls, ldm = m.forward_raw(torch.from_numpy(x))
+        _ORACLE[key] = (loc.numpy(), cls.numpy(), ldm.numpy())
+    return _ORACLE[key]
+
+
+def _frames(n, h, w, seed=0):
+    from vdmi import synth
+    return synth.frames(n, h, w, seed=seed)
+
+
+def _rel(a, b):
+    return np.abs(a - b).max() / (np.abs(b).max() + 1e-12)
+
+
+@pytest.mark.parametrize("h,w", [(1080, 1920), (720, 1280)])
+def test_heads_fp32_match_oracle(gpu, face_ctx_factory, h, w):
+    ctx = face_ctx_factory("fp32", 8)
+    fr = _frames(2, h, w)
+    loc, conf, ldm = ctx.forward_heads(fr)
+    eloc, econf, eldm = _oracle_heads(fr)
+    assert _rel(loc, eloc) < 1e-4 and _rel(conf, econf) < 1e-4 and _rel(ldm, eldm) < 1e-4
+
+
+def test_heads_bf16_close(gpu, face_ctx_factory):
+    ctx = face_ctx_factory("bf16", 8)
+    fr = _frames(2, 1080, 1920)
+    loc, conf, _ = ctx.forward_heads(fr)
+    eloc, econf, _ = _oracle_heads(fr)
+    assert _rel(loc, eloc) < 6e-2 and _rel(conf, econf) < 6e-2
+
+
+def _near_decision(conf_b, boxes_norm, thr=0.5, iou=0.4, eps=1e-4):
+    """Anchors whose score is within eps of thr, or whose IoU with another candidate
+    is within eps of the NMS threshold: decisions there are ulp-sensitive."""
+    score = obbox.softmax2(conf_b)[:, 1]
+    near = np.abs(score - thr) < eps
+    cand = np.nonzero(score >= thr)[0]
+    b = boxes_norm[cand]
+    if len(cand) > 1:
+        x1 = np.maximum(b[:, None, 0], b[None, :, 0]); y1 = np.maximum(b[:, None, 1], b[None, :, 1])
+        x2 = np.minimum(b[:, None, 2], b[None, :, 2]); y2 = np.minimum(b[:, None, 3], b[None, :, 3])
+        inter = np.clip(x2 - x1, 0, None) * np.clip(y2 - y1, 0, None)
+        ar = (b[:, 2] - b[:, 0]) * (b[:, 3] - b[:, 1])
+        iou_m = inter / (ar[:, None] + ar[None, :] - inter + 1e-30)
+        np.fill_diagonal(iou_m, 0)
+        near[cand[(np.abs(iou_m - iou) < eps).any(1)]] = True
+    return near
+
+
+def test_detect_fp32_matches_oracle(gpu, face_ctx_factory):
+    ctx = face_ctx_factory("fp32", 8)
+    fr = _frames(3, 1080, 1920, seed=2)
+    got = ctx.detect(fr)
+    eloc, econf, _ = _oracle_heads(fr)
+    pri = oanchors.get_anchors((640, 640))
+    exact = 0
+    for b in range(3):
+        idx, boxes, _ = obbox.postprocess_frame(eloc[b], econf[b], pri, 0.5, 0.4)
+        xi, xf, sc, lab = got.frame(b)
+        near = _near_decision(econf[b], obbox.decode(eloc[b], pri))
+        if near[idx].any() or near[lab].any():
+            continue                      # ulp-sensitive frame: excluded (counted below)
+        exact += 1
+        np.testing.assert_array_equal(lab, idx)
+        fb = obbox.correct_and_scale(boxes, 1080, 1920)
+        np.testing.assert_allclose(xf, fb, rtol=0, atol=0.05)     # pixels; forward differs in ulps
+    assert exact >= 2, "too many near-threshold frames to judge parity"
+
+
+def test_process_mosaic_exact_given_boxes(gpu, face_ctx_factory):
+    """vd_process output == oracle sequential mosaic applied to the GPU's own int boxes."""
+    for prec in ("fp32", "bf16"):
+        ctx = face_ctx_factory(prec, 8)
+        fr = _frames(2, 1080, 1920, seed=4)
+        out, faces, _ = ctx.process(fr)
+        for b in range(2):
+            xi = faces.frame(b)[0]
+            exp = omosaic.mosaic_frame(fr[b], [tuple(int(v) for v in r) for r in xi], 8)
+            np.testing.assert_array_equal(out[b], exp)
+        assert int(faces.count.sum()) > 0
+
+
+def test_detect_bf16_agrees(gpu, face_ctx_factory):
+    ctx = face_ctx_factory("bf16", 8)
+    fr = _frames(2, 1080, 1920)
+    got = ctx.detect(fr)
+    eloc, econf, _ = _oracle_heads(fr)
+    pri = oanchors.get_anchors((640, 640))
+    matched = total = 0
+    for b in range(2):
+        _, boxes, _ = obbox.postprocess_frame(eloc[b], econf[b], pri, 0.5, 0.4)
+        e = obbox.correct_and_scale(boxes, 1080, 1920)
+        g = got.frame(b)[1]
+        total += len(e)
+        for r in e:
+            if len(g) == 0:
+                break
+            x1 = np.maximum(r[0], g[:, 0]); y1 = np.maximum(r[1], g[:, 1])
+            x2 = np.minimum(r[2], g[:, 2]); y2 = np.minimum(r[3], g[:, 3])
+            inter = np.clip(x2 - x1, 0, None) * np.clip(y2 - y1, 0, None)
+            iou = inter / ((r[2] - r[0]) * (r[3] - r[1]) + (g[:, 2] - g[:, 0]) * (g[:, 3] - g[:, 1]) - inter)
+            matched += iou.max() >= 0.9
+    assert total > 0 and matched / total >= 0.9, (matched, total)
+
+
+def test_retinaface_drop_in(gpu):
+    from vdmi import Retinaface
+    det = Retinaface(model_path="/nonexistent.pth", backbone="resnet50", input_shape=[640, 640, 3],
+                     confidence=0.5, nms_iou=0.4, letterbox_image=True, cuda=True, precision="fp32",
+                     max_batch=4, weights=face_weights())
+    imgs = list(_frames(3, 720, 1280, seed=9)) + [_frames(1, 1080, 1920, seed=9)[0]]
+    res = det.detect_images(imgs)
+    assert len(res) == 4
+    for (img, boxes), src in zip(res, imgs):
+        assert img is src
+        assert isinstance(boxes, list) and all(len(b) == 4 and isinstance(b[0], float) for b in boxes)
+    # int() of the returned floats == the library's int boxes
+    raw = det.detect_boxes(imgs)
+    for (_, boxes), (xf, xi, _) in zip(res, raw):
+        assert [[int(v) for v in b] for b in boxes] == xi.tolist()

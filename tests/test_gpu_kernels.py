@@ -1,0 +1,192 @@
+"""GPU parity of the individual HIP kernels against the CPU oracle (through the C-ABI).
+
+Bar: bit-exact for integer/byte/index work (mosaic, letterbox, NMS keep lists,
+int boxes); the conv kernel against a torch-CPU fp32 conv with the tolerances
+written in each test (exact-f32 MFMA mode: 1e-5 relative to the layer's scale;
+bf16 mode: 2e-2 relative)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import anchors as oanchors
+from oracle import bbox as obbox
+from oracle import letterbox as olb
+from oracle import mosaic as omosaic
+
+pytestmark = pytest.mark.gpu
+F32 = np.float32
+
+
+# ------------------------------------------------------------------ mosaic
+def _rand_boxes(rng, n, h, w, k):
+    out = []
+    for _ in range(n):
+        bl = []
+        for _ in range(k):
+            bw, bh = rng.integers(1, max(2, w // 3)), rng.integers(1, max(2, h // 3))
+            x1, y1 = rng.integers(-bw, w), rng.integers(-bh, h)
+            bl.append((int(x1), int(y1), int(x1 + bw), int(y1 + bh)))
+        # degenerate / inverted / fully outside
+        bl += [(5, 5, 5, 9), (9, 9, 3, 3), (w + 3, 0, w + 9, 4)]
+        rng.shuffle(bl)
+        out.append(bl)
+    return out
+
+
+@pytest.mark.parametrize("h,w,k", [(64, 80, 12), (37, 51, 30), (1080, 1920, 16), (720, 1280, 8)])
+def test_mosaic_matches_oracle(gpu, face_ctx_factory, h, w, k):
+    from vdmi import mosaic_frames, synth
+    ctx = face_ctx_factory("bf16", 8)
+    rng = np.random.default_rng(h * 1000 + w)
+    n = 3
+    frames = synth.frames(n, h, w, seed=7)
+    boxes = _rand_boxes(rng, n, h, w, k)
+    got = mosaic_frames(frames, boxes, 8, ctx=ctx)
+    for i in range(n):
+        exp = omosaic.mosaic_frame(frames[i], boxes[i], 8)
+        np.testing.assert_array_equal(got[i], exp)
+
+
+def test_mosaic_nested_chain_and_levels(gpu, face_ctx_factory):
+    """Deeply nested boxes force walks that leave a row band (global fallback)."""
+    from vdmi import mosaic_frames, synth
+    ctx = face_ctx_factory("bf16", 8)
+    frames = synth.frames(2, 300, 200, seed=3)
+    boxes = [[(10 + 3 * i, 5 + 9 * i, 190 - 2 * i, 295 - i) for i in range(25)],
+             [(0, 0, 200, 300), (50, 50, 60, 61), (0, 150, 100, 300), (20, 0, 23, 300)]]
+    for level in (2, 8, 16):
+        got = mosaic_frames(frames, boxes, level, ctx=ctx)
+        for i in range(2):
+            np.testing.assert_array_equal(got[i], omosaic.mosaic_frame(frames[i], boxes[i], level))
+
+
+def test_mosaic_many_boxes_band_overflow(gpu, face_ctx_factory):
+    from vdmi import mosaic_frames, synth
+    ctx = face_ctx_factory("bf16", 8)
+    rng = np.random.default_rng(5)
+    frames = synth.frames(1, 96, 128, seed=4)
+    boxes = [[tuple(int(v) for v in (x, y, x + rng.integers(1, 30), y + rng.integers(1, 30)))
+              for x, y in zip(rng.integers(-10, 128, 600), rng.integers(-10, 96, 600))]]
+    got = mosaic_frames(frames, boxes, 8, ctx=ctx)
+    np.testing.assert_array_equal(got[0], omosaic.mosaic_frame(frames[0], boxes[0], 8))
+
+
+def test_mosaic_single_drop_in(gpu):
+    from vdmi import mosaic_rectangle_region_single, synth
+    img = synth.frame(120, 160, 0)
+    for box in [(10, 20, 90, 100), (-5, -5, 7, 9), (150, 100, 400, 400), (30, 30, 30, 40)]:
+        got = mosaic_rectangle_region_single(img, *box, mosaic_level=8)
+        np.testing.assert_array_equal(got, omosaic.mosaic_rectangle_region_single(img, *box, 8))
+        assert got is not img
+
+
+# ------------------------------------------------------------------ letterbox
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("h,w", [(1080, 1920), (720, 1280), (2160, 3840), (640, 640), (480, 640), (333, 517)])
+def test_letterbox_matches_oracle(gpu, face_ctx_factory, prec, h, w):
+    from vdmi import synth
+    ctx = face_ctx_factory(prec, 8)
+    frames = synth.frames(2, h, w, seed=11)
+    got = ctx.letterbox(frames, cpad=3)                 # NHWC, 3 real channels
+    exp, _ = olb.preprocess(list(frames))               # NCHW
+    np.testing.assert_array_equal(got, exp.transpose(0, 2, 3, 1))   # integers: exact in bf16 too
+
+
+# ------------------------------------------------------------------ conv
+CONV_CASES = [
+    # (n, h, w, cin, cout, k, stride, pad, act, res_mode)
+    (2, 17, 19, 64, 64, 1, 1, 0, 1, 0),
+    (2, 17, 19, 64, 128, 3, 1, 1, 1, 0),
+    (1, 33, 31, 128, 256, 3, 2, 1, 1, 0),
+    (2, 20, 20, 256, 64, 1, 1, 0, 0, 1),
+    (1, 40, 36, 3, 64, 7, 2, 3, 1, 0),        # stem, generic tap loader
+    (2, 24, 20, 16, 32, 3, 2, 1, 3, 0),       # YOLO-style small C, SiLU
+    (1, 16, 16, 48, 24, 1, 1, 0, 3, 2),       # cin 48 generic, res after act
+    (1, 12, 10, 256, 32, 1, 1, 0, 0, 0),      # heads (BN=32 tile)
+    (1, 9, 11, 512, 200, 3, 1, 1, 2, 1),      # cout not a tile multiple, leaky
+]
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_matches_torch(gpu, face_ctx_factory, prec, case):
+    n, h, w, cin, cout, k, s, p, act, res_mode = case
+    ctx = face_ctx_factory(prec, 8)
+    rng = np.random.default_rng(cin * 7 + cout)
+    x = rng.standard_normal((n, h, w, cin)).astype(F32)
+    wt = (rng.standard_normal((cout, cin, k, k)) * np.sqrt(2.0 / (cin * k * k))).astype(F32)
+    scale = rng.uniform(0.5, 1.5, cout).astype(F32)
+    shift = rng.standard_normal(cout).astype(F32) * F32(0.1)
+    oh, ow = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
+    res = rng.standard_normal((n, oh, ow, cout)).astype(F32) if res_mode else None
+    if prec == "bf16":   # the kernel sees bf16 operands: compare against the same rounded inputs
+        bf = lambda a: torch.from_numpy(a).bfloat16().float().numpy()
+        x, wt = bf(x), bf(wt)
+        res = bf(res) if res is not None else None
+    got = ctx.conv2d(x, wt, s, p, scale, shift, act, 0.1, res, res_mode)
+    y = torch.nn.functional.conv2d(torch.from_numpy(x).permute(0, 3, 1, 2), torch.from_numpy(wt), stride=s,
+                                   padding=p).permute(0, 2, 3, 1).double().numpy()
+    y = y * scale + shift
+    if res_mode == 1:
+        y = y + res
+    y = {0: lambda v: v, 1: lambda v: np.maximum(v, 0), 2: lambda v: np.where(v > 0, v, 0.1 * v),
+         3: lambda v: v / (1 + np.exp(-v))}[act](y)
+    if res_mode == 2:
+        y = y + res
+    tol = 2e-5 if prec == "fp32" else 2e-2
+    err = np.abs(got - y).max() / (np.abs(y).max() + 1e-6)
+    assert got.shape == y.shape
+    assert err < tol, f"rel err {err}"
+
+
+# ------------------------------------------------------------------ post-processing
+def _heads(rng, n, A, bias):
+    loc = (rng.standard_normal((n, A, 4)) * 1.5).astype(F32)
+    conf = rng.standard_normal((n, A, 2)).astype(F32)
+    conf[..., 1] += F32(bias)
+    return loc, conf
+
+
+def _oracle_post(loc, conf, img_h, img_w, thr=0.5, iou=0.4):
+    pri = oanchors.get_anchors((640, 640))
+    res = []
+    for b in range(loc.shape[0]):
+        idx, boxes, sc = obbox.postprocess_frame(loc[b], conf[b], pri, thr, iou)
+        fb = obbox.correct_and_scale(boxes, img_h, img_w)
+        res.append((idx, fb, obbox.truncate_boxes(fb), sc))
+    return res
+
+
+@pytest.mark.parametrize("bias,hw", [(-4.0, (1080, 1920)), (-2.0, (720, 1280)), (-1.0, (640, 640)),
+                                     (0.3, (2160, 3840)), (-9.0, (1080, 1920))])
+def test_postprocess_bit_exact(gpu, face_ctx_factory, bias, hw):
+    """Same loc/conf into both sides -> identical keep lists, float boxes, int boxes, scores.
+    bias -4 ~ 2 % candidates (LDS path); -1 / 0.3 put > 2048 candidates through the global path."""
+    ctx = face_ctx_factory("fp32", 8)
+    rng = np.random.default_rng(int(abs(bias) * 100))
+    loc, conf = _heads(rng, 3, 16800, bias)
+    got = ctx.postprocess(loc, conf, hw, cap=16800)
+    exp = _oracle_post(loc, conf, *hw)
+    for b in range(3):
+        xi, xf, sc, lab = got.frame(b)
+        e_idx, e_f, e_i, e_sc = exp[b]
+        assert int(got.count[b]) == len(e_idx)
+        np.testing.assert_array_equal(lab, e_idx)
+        np.testing.assert_array_equal(xf, e_f)
+        np.testing.assert_array_equal(xi, e_i)
+        np.testing.assert_array_equal(sc, e_sc)
+
+
+def test_postprocess_ties_and_capacity(gpu, face_ctx_factory):
+    from vdmi import VdCapacityError
+    ctx = face_ctx_factory("fp32", 8)
+    A = 16800
+    loc = np.zeros((1, A, 4), F32)
+    conf = np.zeros((1, A, 2), F32)
+    conf[0, ::7, 1] = 2.0           # many exactly-equal scores: stable order decides
+    conf[0, ::11, 1] = 3.0
+    got = ctx.postprocess(loc, conf, (1080, 1920), cap=8192)
+    e = _oracle_post(loc, conf, 1080, 1920)[0]
+    np.testing.assert_array_equal(got.frame(0)[3], e[0])
+    with pytest.raises(VdCapacityError):
+        ctx.postprocess(loc, conf, (1080, 1920), cap=4)

@@ -1,0 +1,54 @@
+"""Weight plumbing: reference key sets, VDW1 round trip, synthetic inputs."""
+import numpy as np
+import torch
+
+from oracle.retinaface import RetinaFaceR50, build_oracle_model
+
+
+def test_retinaface_keys_match_reference_module_tree():
+    from vdmi import weights
+    sd = weights.retinaface_state_dict(0)
+    ref = {k: tuple(v.shape) for k, v in RetinaFaceR50().state_dict().items()
+           if not k.endswith("num_batches_tracked")}
+    assert set(sd) == set(ref)
+    for k, v in sd.items():
+        assert v.shape == ref[k], k
+    # spot-check reference names (retinaface.py:73-92, layers.py:44-52,72-77)
+    for k in ("body.conv1.weight", "body.layer1.0.conv1.weight", "body.layer2.0.downsample.0.weight",
+              "fpn.output1.0.weight", "fpn.merge2.1.running_var", "ssh1.conv3X3.0.weight",
+              "ssh3.conv7x7_3.1.bias", "ClassHead.0.conv1x1.weight", "LandmarkHead.2.conv1x1.bias"):
+        assert k in sd
+    assert sum(v.size for k, v in sd.items() if k.endswith("weight") and v.ndim == 4) > 27e6
+
+
+def test_weights_deterministic_and_vdw_roundtrip():
+    from vdmi import weights
+    a = weights.retinaface_state_dict(0)
+    b = weights.retinaface_state_dict(0)
+    assert all(np.array_equal(a[k], b[k]) for k in a)
+    blob = weights.pack_vdw(a)
+    assert blob[:4] == b"VDW1"
+    back = weights.unpack_vdw(blob)
+    assert set(back) == set(a) and all(np.array_equal(back[k], a[k]) for k in a)
+    # integer buffers are skipped
+    assert "x" not in weights.unpack_vdw(weights.pack_vdw({"x": np.arange(3), "y": np.ones(2, np.float32)}))
+
+
+def test_oracle_model_runs_small():
+    from vdmi import weights
+    m = build_oracle_model(weights.retinaface_state_dict(0))
+    with torch.no_grad():
+        loc, conf, ldm = m(torch.zeros(1, 3, 64, 64))
+    assert loc.shape == (1, 2 * (64 + 16 + 4), 4) and conf.shape[-1] == 2 and ldm.shape[-1] == 10
+    assert torch.allclose(conf.sum(-1), torch.ones(1, 168))
+
+
+def test_synthetic_frames_deterministic():
+    from vdmi import synth
+    f1 = synth.frames(2, 16, 24, seed=0)
+    f2 = synth.frames(2, 16, 24, seed=0)
+    assert f1.dtype == np.uint8 and np.array_equal(f1, f2)
+    assert not np.array_equal(f1[0], f1[1])
+    assert not np.array_equal(synth.frame(16, 24, 0, seed=1), f1[0])
+    b = synth.box_lists(4, 1080, 1920)
+    assert b.shape == (4, 8, 4) and (b[..., 2] > b[..., 0]).all()

@@ -1,0 +1,41 @@
+"""Calibrate the RetinaFace random-weight class head (vdmi.weights.CLS_*).
+
+Runs the CPU oracle on a synthetic 1920x1080 frame with uncalibrated heads,
+measures the per-level distribution of the (class1 - class0) logit difference,
+and prints the bias that gives the target pass rate at score >= 0.5.
+Uses the oracle as a measuring tool only (test infrastructure).
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "video-desensitization_amd"))
+
+from oracle.letterbox import preprocess          # noqa: E402
+from oracle.retinaface import build_oracle_model  # noqa: E402
+from vdmi import synth, weights                   # noqa: E402
+
+
+def main(target=0.03, seed=0):
+    torch.set_num_threads(os.cpu_count())
+    sd = weights.retinaface_state_dict(seed, cls_bias=0.0)
+    m = build_oracle_model(sd)
+    img = synth.frame(1080, 1920, 0)
+    x, _ = preprocess([img])
+    with torch.no_grad():
+        loc, cls, _ = m.forward_raw(torch.from_numpy(x))
+    d = (cls[0, :, 1] - cls[0, :, 0]).numpy()
+    offs = [0, 12800, 16000, 16800]
+    for lvl in range(3):
+        dl = d[offs[lvl]:offs[lvl + 1]]
+        q = np.quantile(dl, 1 - target)
+        print(f"level {lvl}: d mean {dl.mean():.3f} std {dl.std():.3f} -> bias {-q:.3f}")
+    print("loc std", loc.std().item())
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,250 @@
+// conv.hip — NHWC implicit-GEMM convolution on CDNA4 MFMA.
+//
+// Replaces every nn.Conv2d + BatchNorm2d(eval) + activation of the RetinaFace
+// forward (detect_face/retinaface.py:71-92 via torchvision resnet50 [ext],
+// detect_face/nets/layers.py:10-66,79-114) and of the YOLOv8n plate forward.
+//
+//   GEMM view: D[m][n] = sum_k A[m][k] * B[n][k]
+//     m = output pixel (b, oy, ox)                 M = B*OH*OW
+//     n = output channel                           N = Cout
+//     k = (kh, kw, c) with c fastest               K = KH*KW*Cin_pad
+//   A is gathered from the NHWC input on the fly (zero outside the image =
+//   conv padding); B is the weight packed [Npad][Kpad] at load time.
+//
+//   Block tile BM x BN x (128 bytes of K), 256 threads = 4 wave64s, each wave
+//   a (BM/WAVES_M) x (BN/WAVES_N) sub-tile of 16x16 MFMA tiles. K tiles are
+//   register-staged into a double-buffered LDS image with 128-byte rows and a
+//   (row>>1)&7 XOR swizzle on 16-byte chunks, which makes the ds_read_b128
+//   fragment reads of a 16x16x32 operand conflict-free.
+//   bf16 mode : v_mfma_f32_16x16x32_bf16, one 16-B fragment per lane per step.
+//   f32  mode : v_mfma_f32_16x16x4_f32 (exact f32), four MFMAs per 16-B fragment.
+//   Epilogue (fused): y = acc*scale + shift (BN eval, same form as torch's
+//   CPU inference kernel), optional residual add before/after the activation
+//   (ResNet bottleneck; FPN lateral + nearest-2x upsample, layers.py:102-110),
+//   activation (ReLU / LeakyReLU / SiLU), store at a channel offset.
+//   Block -> tile mapping is XCD-aware: blocks that share an A (pixel) panel
+//   are placed on one XCD so the panel is fetched into that XCD's L2 once.
+#include "vd_common.h"
+#include <type_traits>
+
+namespace {
+
+template <typename T> struct Elem;
+template <> struct Elem<__bf16> { static constexpr int VEC = 8; };
+template <> struct Elem<float>  { static constexpr int VEC = 4; };
+
+__device__ __forceinline__ int lds_off(int row, int chunk) {
+    return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
+}
+
+__device__ __forceinline__ float act_apply(float v, int act, float slope) {
+    if (act == VD_ACT_RELU) return v > 0.f ? v : 0.f;
+    if (act == VD_ACT_LEAKY) return v > 0.f ? v : v * slope;
+    if (act == VD_ACT_SILU) return v / (1.0f + __expf(-v));
+    return v;
+}
+
+template <typename T>
+__device__ __forceinline__ float load_elem(const void* p, size_t off) {
+    if constexpr (std::is_same<T, float>::value) return ((const float*)p)[off];
+    else return (float)((const __bf16*)p)[off];
+}
+
+template <typename T, int BM, int BN, bool DENSE>
+__global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
+    constexpr int VEC = Elem<T>::VEC;
+    constexpr int BKE = 8 * VEC;                 // K elements per 128-byte tile row
+    constexpr int WAVES_N = (BN >= 64) ? 2 : 1;
+    constexpr int WAVES_M = 4 / WAVES_N;
+    constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
+    constexpr int TM = WTM / 16, TN = WTN / 16;
+    constexpr int A_IT = BM / 32, B_IT = BN / 32;
+    constexpr int KSTEP = std::is_same<T, float>::value ? 16 : 32;  // K per fragment step
+    constexpr int NKS = BKE / KSTEP;                                 // = 2
+    constexpr int BUF = (BM + BN) * 128;
+
+    __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid / WAVES_N, wn = wid % WAVES_N;
+
+    // XCD-aware bijective remap (blocks b, b+8, ... share an XCD).
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int q = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
+    const int wg = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (bid >> 3);
+    const int tn = wg % a.ntiles_n, tm = wg / a.ntiles_n;
+    const int m0 = tm * BM, n0 = tn * BN;
+
+    // ---- per-thread A-row decomposition (fixed across K) ----
+    const int chunk = tid & 7, rbase = tid >> 3;
+    const T* xrow[A_IT];
+    int iy0[A_IT], ix0[A_IT];
+    const int ohw = a.yh * a.yw;
+#pragma unroll
+    for (int i = 0; i < A_IT; ++i) {
+        int m = m0 + rbase + 32 * i;
+        if (m < a.M) {
+            int b = m / ohw, rem = m - b * ohw;
+            int oy = rem / a.yw, ox = rem - oy * a.yw;
+            iy0[i] = oy * a.stride - a.pad;
+            ix0[i] = ox * a.stride - a.pad;
+            xrow[i] = (const T*)a.x + (size_t)b * a.xh * a.xw * a.ldx + a.xcoff;
+        } else {
+            iy0[i] = -(1 << 28); ix0[i] = 0; xrow[i] = (const T*)a.x;
+        }
+    }
+    const T* wbase = (const T*)a.w + (size_t)(n0 + rbase) * a.kpad + chunk * VEC;
+
+    uint4 ra[A_IT], rb[B_IT];
+    const int nk = a.kpad / BKE;
+    const int cvec = a.cin_pad / VEC, ntap = a.kh * a.kw;
+
+    // DENSE: whole tile inside one tap; track (kh, kw, c) incrementally.
+    int t_kh = 0, t_kw = 0, t_c = 0;
+
+    auto load_tile = [&](int kt) {
+        int dy, dx, c;
+        bool kval = true;
+        if constexpr (DENSE) {
+            dy = t_kh; dx = t_kw; c = t_c + chunk * VEC;
+        } else {
+            int kv = kt * 8 + chunk;
+            int tap = kv / cvec;
+            c = (kv - tap * cvec) * VEC;
+            kval = tap < ntap;
+            dy = tap / a.kw; dx = tap - dy * a.kw;
+        }
+#pragma unroll
+        for (int i = 0; i < A_IT; ++i) {
+            int iy = iy0[i] + dy, ix = ix0[i] + dx;
+            bool ok = kval && (unsigned)iy < (unsigned)a.xh && (unsigned)ix < (unsigned)a.xw;
+            if (ok) ra[i] = *(const uint4*)(xrow[i] + ((size_t)iy * a.xw + ix) * a.ldx + c);
+            else ra[i] = make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < B_IT; ++i)
+            rb[i] = *(const uint4*)(wbase + (size_t)(32 * i) * a.kpad + (size_t)kt * BKE);
+        if constexpr (DENSE) {
+            t_c += BKE;
+            if (t_c >= a.cin_pad) { t_c = 0; if (++t_kw == a.kw) { t_kw = 0; ++t_kh; } }
+        }
+    };
+    auto store_tile = [&](int buf) {
+        char* As = smem + buf * BUF;
+        char* Bs = As + BM * 128;
+#pragma unroll
+        for (int i = 0; i < A_IT; ++i) *(uint4*)(As + lds_off(rbase + 32 * i, chunk)) = ra[i];
+#pragma unroll
+        for (int i = 0; i < B_IT; ++i) *(uint4*)(Bs + lds_off(rbase + 32 * i, chunk)) = rb[i];
+    };
+
+    f32x4_t acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    load_tile(0);
+    store_tile(0);
+    __syncthreads();
+
+    for (int kt = 0; kt < nk; ++kt) {
+        const int cur = kt & 1;
+        if (kt + 1 < nk) load_tile(kt + 1);
+        const char* As = smem + cur * BUF;
+        const char* Bs = As + BM * 128;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+            const int ch = ks * 4 + (lane >> 4);
+            uint4 af[TM], bfr[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+                af[i] = *(const uint4*)(As + lds_off(wm * WTM + i * 16 + (lane & 15), ch));
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                bfr[j] = *(const uint4*)(Bs + lds_off(wn * WTN + j * 16 + (lane & 15), ch));
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    if constexpr (std::is_same<T, float>::value) {
+                        const float* fa = (const float*)&af[i];
+                        const float* fb = (const float*)&bfr[j];
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[e], fb[e], acc[i][j], 0, 0, 0);
+                    } else {
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                            __builtin_bit_cast(bf16x8_t, af[i]), __builtin_bit_cast(bf16x8_t, bfr[j]),
+                            acc[i][j], 0, 0, 0);
+                    }
+                }
+        }
+        if (kt + 1 < nk) store_tile(cur ^ 1);
+        __syncthreads();
+    }
+
+    // ---- fused epilogue ----
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn * WTN + j * 16 + (lane & 15);
+        if (n >= a.cout) continue;
+        const float sc = a.scale[n], sh = a.shift[n];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int m = m0 + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
+                if (m >= a.M) continue;
+                float v = acc[i][j][r] * sc + sh;
+                float rv = 0.f;
+                if (a.res_mode != VD_RES_NONE) {
+                    size_t roff;
+                    if (a.res_up) {
+                        int b = m / ohw, rem = m - b * ohw;
+                        int oy = rem / a.yw, ox = rem - oy * a.yw;
+                        roff = ((size_t)(b * a.rh + (oy >> 1)) * a.rw + (ox >> 1)) * a.res_ld;
+                    } else {
+                        roff = (size_t)m * a.res_ld;
+                    }
+                    rv = load_elem<T>(a.res, roff + a.res_coff + n);
+                }
+                if (a.res_mode == VD_RES_PRE_ACT) v += rv;
+                v = act_apply(v, a.act, a.slope);
+                if (a.res_mode == VD_RES_POST_ACT) v += rv;
+                const size_t yo = (size_t)m * a.ldy + a.ycoff + n;
+                if (a.out_f32 || std::is_same<T, float>::value) ((float*)a.y)[yo] = v;
+                else ((__bf16*)a.y)[yo] = (__bf16)v;
+            }
+        }
+    }
+}
+
+template <typename T, int BM, int BN>
+hipError_t launch_bn(const ConvArgs& a0, bool dense, hipStream_t s) {
+    ConvArgs a = a0;
+    a.ntiles_n = (a.cout + BN - 1) / BN;
+    const int mt = (a.M + BM - 1) / BM;
+    dim3 grid(mt * a.ntiles_n), block(256);
+    if (dense) hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, true>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, false>), grid, block, 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+// Tile selection: BN follows Cout (32 heads / 64 / 128), BM = 128.
+// Weights must be packed with Npad a multiple of the chosen BN (runtime pads to 128).
+hipError_t vd_launch_conv(const ConvArgs& a, bool f32, hipStream_t s) {
+    const int vec = f32 ? 4 : 8;
+    const int bke = 8 * vec;
+    const bool dense = (a.cin_pad % bke) == 0;
+    if (f32) {
+        if (a.cout <= 32) return launch_bn<float, 128, 32>(a, dense, s);
+        if (a.cout <= 64) return launch_bn<float, 128, 64>(a, dense, s);
+        return launch_bn<float, 128, 128>(a, dense, s);
+    }
+    if (a.cout <= 32) return launch_bn<__bf16, 128, 32>(a, dense, s);
+    if (a.cout <= 64) return launch_bn<__bf16, 128, 64>(a, dense, s);
+    return launch_bn<__bf16, 128, 128>(a, dense, s);
+}

@@ -1,0 +1,183 @@
+// face_net.cpp — RetinaFace-ResNet50 plan (cfg_re50) on the conv/pool kernels.
+//
+// Module tree = reference state_dict keys (detect_face/retinaface.py:53-92):
+//   body.*            torchvision resnet50 up to layer4 [ext] (v1.5, stride on the 3x3)
+//   fpn.output{1,2,3} 1x1 conv+BN+ReLU (layers.py:72-74; leaky=0 as out=256>64, :71)
+//   fpn.merge{1,2}    3x3 conv+BN+ReLU, input = lateral + nearest-2x(upper) (:100-110)
+//   ssh{1,2,3}        SSH (layers.py:37-66): concat of three branches, then ReLU
+//   {Bbox,Class,Landmark}Head.{l}.conv1x1   1x1 heads (retinaface.py:13-51)
+// Fusions: BN (eval) + activation + residual in every conv epilogue; the FPN
+// upsample-add is the lateral conv's epilogue (nearest-2x residual); the SSH
+// concat is three convs writing channel slices [0,128), [128,192), [192,256)
+// of one buffer with the post-concat ReLU applied per slice; the three heads
+// of a level are one 256->32 conv (channels 0-7 bbox, 8-11 class, 12-31 landm).
+#include "nets.h"
+#include "vd_math.h"
+
+#include <cmath>
+#include <string>
+#include <vector>
+
+namespace {
+constexpr float BN_EPS = 1e-5f;   // nn.BatchNorm2d default (torchvision + layers.py)
+
+int conv_bn(Ctx& c, const WMap& W, const std::string& conv, const std::string& bn, int stride, int pad, int act,
+            int* idx) {
+    return c.make_conv_bn(W, conv, bn, BN_EPS, stride, pad, act, 0.f, idx);
+}
+}  // namespace
+
+int vd_build_face(Ctx& c, const WMap& W) {
+    FaceNet& F = c.face;
+    F.in_h = c.cfg.input_h;
+    F.in_w = c.cfg.input_w;
+    const int H = F.in_h, Wd = F.in_w;
+    const int cpad = c.f32 ? 4 : 8;
+    int rc;
+    if ((rc = c.act(F.input, H, Wd, cpad))) return rc;
+
+    // ---- stem: conv1 7x7/2 + bn1 + relu, maxpool 3x3/2 pad 1 ----
+    int ci;
+    if ((rc = conv_bn(c, W, "body.conv1.weight", "body.bn1", 2, 3, VD_ACT_RELU, &ci))) return rc;
+    Act stem, pool;
+    if ((rc = c.act(stem, H / 2, Wd / 2, 64))) return rc;
+    if ((rc = c.add_conv(F.net, ci, F.input, 0, stem, 0))) return rc;
+    if ((rc = c.act(pool, H / 4, Wd / 4, 64))) return rc;
+    {
+        Op op;
+        op.kind = OP_MAXPOOL;
+        op.x = stem; op.y = pool; op.ch = 64; op.k = 3; op.s = 2; op.p = 1;
+        F.net.ops.push_back(op);
+    }
+
+    // ---- layer1..4 (Bottleneck x [3,4,6,3]) ----
+    Act x = pool;
+    Act feats[3];
+    const int planes_l[4] = {64, 128, 256, 512}, blocks_l[4] = {3, 4, 6, 3}, stride_l[4] = {1, 2, 2, 2};
+    for (int li = 0; li < 4; ++li) {
+        const int planes = planes_l[li];
+        for (int bi = 0; bi < blocks_l[li]; ++bi) {
+            const std::string pre = "body.layer" + std::to_string(li + 1) + "." + std::to_string(bi);
+            const int s = bi == 0 ? stride_l[li] : 1;
+            int c1, c2, c3, cd = -1;
+            if ((rc = conv_bn(c, W, pre + ".conv1.weight", pre + ".bn1", 1, 0, VD_ACT_RELU, &c1))) return rc;
+            if ((rc = conv_bn(c, W, pre + ".conv2.weight", pre + ".bn2", s, 1, VD_ACT_RELU, &c2))) return rc;
+            if ((rc = conv_bn(c, W, pre + ".conv3.weight", pre + ".bn3", 1, 0, VD_ACT_RELU, &c3))) return rc;
+            const bool has_ds = find_t(W, pre + ".downsample.0.weight") != nullptr;
+            if (has_ds && (rc = conv_bn(c, W, pre + ".downsample.0.weight", pre + ".downsample.1", s, 0, VD_ACT_NONE, &cd)))
+                return rc;
+            if (!has_ds && (s != 1 || x.c != planes * 4))
+                return vd_set_error(VD_ERR_WEIGHTS, "%s: missing downsample", pre.c_str());
+            const int oh = x.h / s, ow = x.w / s;
+            Act t1, t2, out, ds;
+            if ((rc = c.act(t1, x.h, x.w, planes))) return rc;
+            if ((rc = c.act(t2, oh, ow, planes))) return rc;
+            if ((rc = c.act(out, oh, ow, planes * 4))) return rc;
+            if ((rc = c.add_conv(F.net, c1, x, 0, t1, 0))) return rc;
+            if ((rc = c.add_conv(F.net, c2, t1, 0, t2, 0))) return rc;
+            const Act* idt = &x;
+            if (has_ds) {
+                if ((rc = c.act(ds, oh, ow, planes * 4))) return rc;
+                if ((rc = c.add_conv(F.net, cd, x, 0, ds, 0))) return rc;
+                idt = &ds;
+            }
+            // relu(bn3(conv3(t2)) + identity)
+            if ((rc = c.add_conv(F.net, c3, t2, 0, out, 0, idt, 0, VD_RES_PRE_ACT, 0))) return rc;
+            x = out;
+        }
+        if (li >= 1) feats[li - 1] = x;   // layer2/3/4 -> C3/C4/C5 (config.py:26)
+    }
+
+    // ---- FPN ----
+    int o1c, o2c, o3c, m1c, m2c;
+    if ((rc = conv_bn(c, W, "fpn.output1.0.weight", "fpn.output1.1", 1, 0, VD_ACT_RELU, &o1c))) return rc;
+    if ((rc = conv_bn(c, W, "fpn.output2.0.weight", "fpn.output2.1", 1, 0, VD_ACT_RELU, &o2c))) return rc;
+    if ((rc = conv_bn(c, W, "fpn.output3.0.weight", "fpn.output3.1", 1, 0, VD_ACT_RELU, &o3c))) return rc;
+    if ((rc = conv_bn(c, W, "fpn.merge1.0.weight", "fpn.merge1.1", 1, 1, VD_ACT_RELU, &m1c))) return rc;
+    if ((rc = conv_bn(c, W, "fpn.merge2.0.weight", "fpn.merge2.1", 1, 1, VD_ACT_RELU, &m2c))) return rc;
+    const int oc = c.convs[o1c].cout;
+    Act o1, o2, o3, m1, m2;
+    if ((rc = c.act(o3, feats[2].h, feats[2].w, oc))) return rc;
+    if ((rc = c.act(o2, feats[1].h, feats[1].w, oc))) return rc;
+    if ((rc = c.act(m2, feats[1].h, feats[1].w, oc))) return rc;
+    if ((rc = c.act(o1, feats[0].h, feats[0].w, oc))) return rc;
+    if ((rc = c.act(m1, feats[0].h, feats[0].w, oc))) return rc;
+    if ((rc = c.add_conv(F.net, o3c, feats[2], 0, o3, 0))) return rc;
+    // output2 = relu(bn(conv(C4))) + nearest_up(output3)   (layers.py:102-103)
+    if ((rc = c.add_conv(F.net, o2c, feats[1], 0, o2, 0, &o3, 0, VD_RES_POST_ACT, 1))) return rc;
+    if ((rc = c.add_conv(F.net, m2c, o2, 0, m2, 0))) return rc;
+    if ((rc = c.add_conv(F.net, o1c, feats[0], 0, o1, 0, &m2, 0, VD_RES_POST_ACT, 1))) return rc;
+    if ((rc = c.add_conv(F.net, m1c, o1, 0, m1, 0))) return rc;
+    const Act fpn_out[3] = {m1, m2, o3};
+
+    // ---- SSH x3 + fused heads ----
+    for (int l = 0; l < 3; ++l) {
+        const std::string pre = "ssh" + std::to_string(l + 1);
+        int s3, s51, s52, s72, s73;
+        if ((rc = conv_bn(c, W, pre + ".conv3X3.0.weight", pre + ".conv3X3.1", 1, 1, VD_ACT_RELU, &s3))) return rc;
+        if ((rc = conv_bn(c, W, pre + ".conv5X5_1.0.weight", pre + ".conv5X5_1.1", 1, 1, VD_ACT_RELU, &s51))) return rc;
+        if ((rc = conv_bn(c, W, pre + ".conv5X5_2.0.weight", pre + ".conv5X5_2.1", 1, 1, VD_ACT_RELU, &s52))) return rc;
+        if ((rc = conv_bn(c, W, pre + ".conv7X7_2.0.weight", pre + ".conv7X7_2.1", 1, 1, VD_ACT_RELU, &s72))) return rc;
+        if ((rc = conv_bn(c, W, pre + ".conv7x7_3.0.weight", pre + ".conv7x7_3.1", 1, 1, VD_ACT_RELU, &s73))) return rc;
+        const Act& f = fpn_out[l];
+        const int c3o = c.convs[s3].cout, c5o = c.convs[s52].cout, c7o = c.convs[s73].cout;
+        Act cat, t5, t7;
+        if ((rc = c.act(cat, f.h, f.w, c3o + c5o + c7o))) return rc;
+        if ((rc = c.act(t5, f.h, f.w, c.convs[s51].cout))) return rc;
+        if ((rc = c.act(t7, f.h, f.w, c.convs[s72].cout))) return rc;
+        if ((rc = c.add_conv(F.net, s3, f, 0, cat, 0))) return rc;
+        if ((rc = c.add_conv(F.net, s51, f, 0, t5, 0))) return rc;
+        if ((rc = c.add_conv(F.net, s52, t5, 0, cat, c3o))) return rc;
+        if ((rc = c.add_conv(F.net, s72, t5, 0, t7, 0))) return rc;
+        if ((rc = c.add_conv(F.net, s73, t7, 0, cat, c3o + c5o))) return rc;
+        int hc;
+        const std::string L = std::to_string(l);
+        if ((rc = c.make_conv_cat(W,
+                                  {"BboxHead." + L + ".conv1x1.weight", "ClassHead." + L + ".conv1x1.weight",
+                                   "LandmarkHead." + L + ".conv1x1.weight"},
+                                  {"BboxHead." + L + ".conv1x1.bias", "ClassHead." + L + ".conv1x1.bias",
+                                   "LandmarkHead." + L + ".conv1x1.bias"},
+                                  VD_ACT_NONE, &hc)))
+            return rc;
+        if (c.convs[hc].cout != 32) return vd_set_error(VD_ERR_WEIGHTS, "heads of level %d: %d channels != 32", l, c.convs[hc].cout);
+        if ((rc = c.act(F.heads[l], f.h, f.w, 32, true))) return rc;
+        if ((rc = c.add_conv(F.net, hc, cat, 0, F.heads[l], 0))) return rc;
+    }
+
+    // ---- anchors (anchors.py:22-41, Python doubles -> float32) ----
+    static const int steps[3] = {8, 16, 32};
+    static const int min_sizes[3][2] = {{16, 32}, {64, 128}, {256, 512}};
+    std::vector<float> anc;
+    int A = 0;
+    for (int l = 0; l < 3; ++l) {
+        const int fh = (H + steps[l] - 1) / steps[l], fw = (Wd + steps[l] - 1) / steps[l];
+        if (fh != F.heads[l].h || fw != F.heads[l].w)
+            return vd_set_error(VD_ERR_ARG, "anchor grid %dx%d != head %dx%d", fh, fw, F.heads[l].h, F.heads[l].w);
+        F.loff[l] = A;
+        for (int i = 0; i < fh; ++i)
+            for (int j = 0; j < fw; ++j)
+                for (int k = 0; k < 2; ++k) {
+                    const double ms = min_sizes[l][k];
+                    anc.push_back((float)((j + 0.5) * steps[l] / Wd));
+                    anc.push_back((float)((i + 0.5) * steps[l] / H));
+                    anc.push_back((float)(ms / Wd));
+                    anc.push_back((float)(ms / H));
+                    ++A;
+                }
+    }
+    F.A = A;
+    if ((rc = c.dalloc((void**)&F.anchors, anc.size() * 4))) return rc;
+    VD_CHECK_HIP(hipMemcpy(F.anchors, anc.data(), anc.size() * 4, hipMemcpyHostToDevice));
+    const size_t B = c.cfg.max_batch;
+    int P = 1;
+    while (P < A) P <<= 1;
+    F.sort_cap = P;
+    if ((rc = c.dalloc((void**)&F.cand_keys, B * A * 8))) return rc;
+    if ((rc = c.dalloc((void**)&F.cand_count, B * 4))) return rc;
+    if ((rc = c.dalloc((void**)&F.scratch_box, B * A * 16))) return rc;
+    if ((rc = c.dalloc((void**)&F.scratch_area, B * A * 4))) return rc;
+    if ((rc = c.dalloc((void**)&F.scratch_keys, B * (size_t)P * 8))) return rc;
+    if ((rc = c.dalloc((void**)&F.scratch_supp, B * A))) return rc;
+    F.loaded = true;
+    return VD_OK;
+}

@@ -1,0 +1,145 @@
+// nets.h — host-side context, network plans and builders (internal).
+#pragma once
+#include "../../include/vdmi.h"
+#include "vd_common.h"
+
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+struct HT {   // host tensor from the VDW1 container
+    std::vector<int> shape;
+    std::vector<float> data;
+};
+using WMap = std::unordered_map<std::string, HT>;
+int vd_parse_vdw1(const void* blob, size_t bytes, WMap& out);
+const HT* find_t(const WMap& W, const std::string& k);
+void vd_resize_mode(int ih, int iw, int nh, int nw, int* mode, double* sx, double* sy);
+
+struct Act {          // NHWC activation buffer sized for cfg.max_batch frames
+    void* p = nullptr;
+    int h = 0, w = 0, c = 0;   // c = channel stride
+    bool f32 = false;
+};
+
+struct Conv {
+    int cin = 0, cin_pad = 0, cout = 0, npad = 0, kh = 0, kw = 0, stride = 1, pad = 0, kpad = 0, act = 0;
+    float slope = 0.f;
+    void* w = nullptr;
+    float* scale = nullptr;
+    float* shift = nullptr;
+    double flops_per_px = 0;   // algorithmic FLOPs per output pixel (real Cin, no padding)
+};
+
+enum { OP_CONV = 0, OP_MAXPOOL = 1, OP_UPSAMPLE = 2 };
+
+struct Op {
+    int kind = OP_CONV;
+    int conv = -1;
+    Act x; int xcoff = 0;
+    Act y; int ycoff = 0;
+    Act r; int rcoff = 0; int rmode = 0; int rup = 0;
+    int ch = 0, k = 0, s = 0, p = 0;   // maxpool / upsample
+};
+
+struct Net {
+    std::vector<Op> ops;
+};
+
+struct FaceNet {
+    bool loaded = false;
+    int in_h = 640, in_w = 640;
+    Act input;
+    Net net;
+    Act heads[3];
+    int loff[3] = {0, 0, 0};
+    int A = 0;
+    float* anchors = nullptr;
+    uint64_t* cand_keys = nullptr;
+    int* cand_count = nullptr;
+    float4* scratch_box = nullptr;
+    float* scratch_area = nullptr;
+    uint64_t* scratch_keys = nullptr;
+    uint8_t* scratch_supp = nullptr;
+    int sort_cap = 0;
+};
+
+struct PlateNet {
+    bool loaded = false;
+    int nc = 1;
+    int in_h = 0, in_w = 0;         // letterboxed canvas planned for (max frame, auto stride padding)
+    int imgsz = 640;
+    Act input;
+    Net net;
+    Act head[3];                    // per level [H][W][64+nc] f32 (box DFL logits | class logits)
+    int lh[3] = {0, 0, 0}, lw[3] = {0, 0, 0};
+    float* dfl = nullptr;           // scratch
+    // post scratch
+    float* cand = nullptr;          // [B][A][6]
+    int* cand_count = nullptr;
+    uint64_t* keys = nullptr;
+    int A = 0;
+    int cur_h = 0, cur_w = 0;       // canvas of the current call
+};
+
+struct BoxTargets {
+    int cap = 0;
+    int* count = nullptr;
+    int* xyxy = nullptr;
+    float* xyxy_f = nullptr;
+    float* score = nullptr;
+    int* label = nullptr;
+};
+
+struct TimedEv {
+    hipEvent_t a, b;
+    int fam;
+    double work;
+};
+
+struct Ctx {
+    vd_cfg cfg{};
+    int device = 0;
+    bool f32 = false;
+    hipStream_t stream = nullptr, own_stream = nullptr;
+    std::mutex mu;
+    std::vector<void*> allocs;
+    std::vector<Conv> convs;
+    FaceNet face;
+    PlateNet plate;
+    void* stage_in = nullptr;  size_t stage_in_bytes = 0;
+    void* stage_out = nullptr; size_t stage_out_bytes = 0;
+    void* stage_box = nullptr; size_t stage_box_bytes = 0;
+    void* stage_box2 = nullptr; size_t stage_box2_bytes = 0;
+    bool timing = false;
+    std::vector<TimedEv> ev_pool;
+    size_t ev_used = 0;
+
+    int dalloc(void** p, size_t bytes);
+    int act(Act& a, int h, int w, int c, bool f32out = false);
+    int ensure_staging(void** p, size_t* have, size_t need);
+    int upload_conv(Conv& cv, const std::vector<float>& w_oihw, const std::vector<float>& scale,
+                    const std::vector<float>& shift);
+    int make_conv_bn(const WMap& W, const std::string& wkey, const std::string& bn, float eps, int stride, int pad,
+                     int act, float slope, int* out_idx);
+    int make_conv_cat(const WMap& W, const std::vector<std::string>& wkeys, const std::vector<std::string>& bkeys,
+                      int act, int* out_idx);
+    int add_conv(Net& net, int ci, const Act& x, int xcoff, Act& y, int ycoff, const Act* res = nullptr,
+                 int rcoff = 0, int rmode = 0, int rup = 0);
+    void t_begin(int fam, double work);
+    void t_end();
+    int run_conv_op(const Op& op, int n);
+    int run_net(const Net& net, int n);
+    const uint8_t* frames_to_device(const uint8_t* frames, int n, int h, size_t pitch, int where, int* rc);
+    int check_frames(int n, int h, int w, size_t pitch);
+    int box_targets(vd_boxes* out, int n, BoxTargets& t);
+    int box_finish(vd_boxes* out, int n, const BoxTargets& t);
+    int face_letterbox(const uint8_t* dframes, int n, int h, int w, size_t pitch);
+    int face_post(int n, int img_h, int img_w, const BoxTargets& t);
+};
+
+int vd_build_face(Ctx& ctx, const WMap& W);
+int vd_build_plate(Ctx& ctx, const WMap& W);
+int vd_plate_forward(Ctx& ctx, const uint8_t* dframes, int n, int h, int w, size_t pitch);
+int vd_plate_post(Ctx& ctx, int n, int img_h, int img_w, const BoxTargets& t);

@@ -1,0 +1,171 @@
+// pre.hip — letterbox/normalise/pack, max-pool and nearest-upsample kernels.
+//
+// letterbox_kernel replaces, in one HBM pass per frame batch:
+//   Retinaface.preprocess (detect_face/face.py:65-88) = letterbox_image
+//   (detect_face/utils/utils.py:8-18: cv2.resize INTER_LINEAR [ext] + paste in a
+//   128-filled canvas) + preprocess_input (:27-28, subtract (104,117,123) in
+//   RGB order) + HWC->CHW + float32 + H2D; and the ultralytics LetterBox
+//   (stride-32 auto padding, value 114, BGR<->RGB flip, /255) [ext] of the plate
+//   detector call (combine_detect.py:217). Output is NHWC with `cpad` channels
+//   (3 real + zeros) so the stem conv reads one 16-byte vector per tap.
+//   cv2.resize rounding is restated exactly (oracle/letterbox.py):
+//     COPY  (dsize == ssize), AREA2 (exact 2x: (a+b+c+d+2)>>2),
+//     LINEAR (11-bit fixed point, SIMD vertical form).
+#include "vd_common.h"
+#include "vd_math.h"
+
+namespace {
+
+struct Tap { int s0, s1, a0, a1; };
+
+__device__ __forceinline__ Tap linear_tap(int d, int ssize, double scale) {
+    // fx = (float)((dx + 0.5) * scale_x - 0.5); sx = floor(fx); fx -= sx; border clamps
+    float f = (float)VD_DSUB(VD_DMUL(VD_DADD((double)d, 0.5), scale), 0.5);
+    int s = (int)floorf(f);
+    f = VD_FSUB(f, (float)s);
+    if (s < 0) { f = 0.f; s = 0; }
+    if (s >= ssize - 1) { f = 0.f; s = ssize - 1; }
+    Tap t;
+    t.s0 = s;
+    t.s1 = min(s + 1, ssize - 1);
+    t.a0 = __float2int_rn(VD_FMUL(VD_FSUB(1.0f, f), 2048.0f));
+    t.a1 = __float2int_rn(VD_FMUL(f, 2048.0f));
+    return t;
+}
+
+__device__ __forceinline__ int resized_px(const LetterboxArgs& a, const uint8_t* img, int y, int x, int c) {
+    if (a.mode == LB_COPY) return img[(size_t)y * a.pitch + x * 3 + c];
+    if (a.mode == LB_AREA2) {
+        const uint8_t* p = img + (size_t)(2 * y) * a.pitch + (2 * x) * 3 + c;
+        return (p[0] + p[3] + p[a.pitch] + p[a.pitch + 3] + 2) >> 2;
+    }
+    Tap tx = linear_tap(x, a.iw, a.scale_x);
+    Tap ty = linear_tap(y, a.ih, a.scale_y);
+    const uint8_t* r0 = img + (size_t)ty.s0 * a.pitch;
+    const uint8_t* r1 = img + (size_t)ty.s1 * a.pitch;
+    int d0 = r0[tx.s0 * 3 + c] * tx.a0 + r0[tx.s1 * 3 + c] * tx.a1;
+    int d1 = r1[tx.s0 * 3 + c] * tx.a0 + r1[tx.s1 * 3 + c] * tx.a1;
+    int v = ((((d0 >> 4) * ty.a0) >> 16) + (((d1 >> 4) * ty.a1) >> 16) + 2) >> 2;
+    return v < 0 ? 0 : (v > 255 ? 255 : v);
+}
+
+__global__ __launch_bounds__(256) void letterbox_kernel(LetterboxArgs a) {
+    const int x = blockIdx.x * 256 + threadIdx.x;
+    const int y = blockIdx.y;
+    const int f = blockIdx.z;
+    if (x >= a.ow) return;
+    const uint8_t* img = a.src + (size_t)f * a.ih * a.pitch;
+    float v[3];
+    const int ry = y - a.top, rx = x - a.left;
+    const bool inside = (unsigned)ry < (unsigned)a.nh && (unsigned)rx < (unsigned)a.nw;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        int sc = a.flip ? 2 - c : c;
+        float px = inside ? (float)resized_px(a, img, ry, rx, sc) : a.pad_value;
+        v[c] = VD_FDIV(VD_FSUB(px, a.mean[c]), a.div);
+    }
+    const size_t o = (((size_t)f * a.oh + y) * a.ow + x) * a.cpad;
+    if (a.out_f32) {
+        float* out = (float*)a.out + o;
+        float4 w0 = make_float4(v[0], v[1], v[2], 0.f);
+        *(float4*)out = w0;
+        for (int c = 4; c < a.cpad; c += 4) *(float4*)(out + c) = make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+        __bf16* out = (__bf16*)a.out + o;
+        __bf16 tmp[8];
+        tmp[0] = (__bf16)v[0]; tmp[1] = (__bf16)v[1]; tmp[2] = (__bf16)v[2];
+        for (int c = 3; c < 8; ++c) tmp[c] = (__bf16)0.f;
+        *(uint4*)out = *(const uint4*)tmp;
+        for (int c = 8; c < a.cpad; c += 8) *(uint4*)(out + c) = make_uint4(0, 0, 0, 0);
+    }
+}
+
+// NHWC max-pool (torch semantics: padded taps ignored), vectorised 16 B per thread.
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool_kernel(const T* x, int xh, int xw, int ldx, int xcoff,
+                                                      T* y, int yh, int yw, int ldy, int ycoff,
+                                                      int c, int k, int s, int p, int total) {
+    constexpr int VEC = 16 / sizeof(T);
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= total) return;
+    const int cv = c / VEC;
+    const int ci = (idx % cv) * VEC;
+    int pix = idx / cv;
+    const int ox = pix % yw; pix /= yw;
+    const int oy = pix % yh;
+    const int b = pix / yh;
+    float m[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) m[e] = -__builtin_huge_valf();
+    for (int dy = 0; dy < k; ++dy) {
+        int iy = oy * s - p + dy;
+        if ((unsigned)iy >= (unsigned)xh) continue;
+        for (int dx = 0; dx < k; ++dx) {
+            int ix = ox * s - p + dx;
+            if ((unsigned)ix >= (unsigned)xw) continue;
+            uint4 u = *(const uint4*)(x + (((size_t)b * xh + iy) * xw + ix) * ldx + xcoff + ci);
+            const T* t = (const T*)&u;
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) m[e] = fmaxf(m[e], (float)t[e]);
+        }
+    }
+    T o[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) o[e] = (T)m[e];
+    *(uint4*)(y + (((size_t)b * yh + oy) * yw + ox) * ldy + ycoff + ci) = *(const uint4*)o;
+}
+
+// Nearest 2x upsample into a channel slice (ultralytics nn.Upsample + Concat).
+template <typename T>
+__global__ __launch_bounds__(256) void upsample2x_kernel(const T* x, int xh, int xw, int ldx, int xcoff,
+                                                         T* y, int ldy, int ycoff, int c, int total) {
+    constexpr int VEC = 16 / sizeof(T);
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= total) return;
+    const int cv = c / VEC;
+    const int ci = (idx % cv) * VEC;
+    int pix = idx / cv;
+    const int yw = 2 * xw, yh = 2 * xh;
+    const int ox = pix % yw; pix /= yw;
+    const int oy = pix % yh;
+    const int b = pix / yh;
+    uint4 u = *(const uint4*)(x + (((size_t)b * xh + (oy >> 1)) * xw + (ox >> 1)) * ldx + xcoff + ci);
+    *(uint4*)(y + (((size_t)b * yh + oy) * yw + ox) * ldy + ycoff + ci) = u;
+}
+
+}  // namespace
+
+hipError_t vd_launch_letterbox(const LetterboxArgs& a, hipStream_t s) {
+    dim3 grid((a.ow + 255) / 256, a.oh, a.n);
+    hipLaunchKernelGGL(letterbox_kernel, grid, dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t vd_launch_maxpool(bool f32, const void* x, int n, int xh, int xw, int ldx, int xcoff,
+                             void* y, int yh, int yw, int ldy, int ycoff, int c, int k, int st, int p,
+                             hipStream_t s) {
+    const int vec = f32 ? 4 : 8;
+    const int total = n * yh * yw * (c / vec);
+    dim3 grid((total + 255) / 256);
+    if (f32)
+        hipLaunchKernelGGL(maxpool_kernel<float>, grid, dim3(256), 0, s, (const float*)x, xh, xw, ldx, xcoff,
+                           (float*)y, yh, yw, ldy, ycoff, c, k, st, p, total);
+    else
+        hipLaunchKernelGGL(maxpool_kernel<__bf16>, grid, dim3(256), 0, s, (const __bf16*)x, xh, xw, ldx, xcoff,
+                           (__bf16*)y, yh, yw, ldy, ycoff, c, k, st, p, total);
+    return hipGetLastError();
+}
+
+hipError_t vd_launch_upsample2x(bool f32, const void* x, int n, int xh, int xw, int ldx, int xcoff,
+                                void* y, int ldy, int ycoff, int c, hipStream_t s) {
+    const int vec = f32 ? 4 : 8;
+    const int total = n * 4 * xh * xw * (c / vec);
+    dim3 grid((total + 255) / 256);
+    if (f32)
+        hipLaunchKernelGGL(upsample2x_kernel<float>, grid, dim3(256), 0, s, (const float*)x, xh, xw, ldx, xcoff,
+                           (float*)y, ldy, ycoff, c, total);
+    else
+        hipLaunchKernelGGL(upsample2x_kernel<__bf16>, grid, dim3(256), 0, s, (const __bf16*)x, xh, xw, ldx, xcoff,
+                           (__bf16*)y, ldy, ycoff, c, total);
+    return hipGetLastError();
+}

@@ -1,0 +1,868 @@
+// runtime.cpp — libvdmi.so: context, weights, network plans and the C-ABI.
+//
+// Host side of the MI355X detect-and-blur path. One vd_ctx = one GPU + one HIP
+// stream + device-resident weights and workspace sized for cfg.max_batch
+// frames (replaces the reference's nn.DataParallel replicate-per-forward,
+// detect_face/face.py:55-56: weights are uploaded once, workspace is
+// allocated once, nothing is allocated on the per-batch path).
+#include "../../include/vdmi.h"
+#include "vd_common.h"
+#include "vd_math.h"
+#include "nets.h"
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+static thread_local std::string g_err;
+
+int vd_set_error(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+// ----------------------------------------------------------------------------
+// weights container
+// ----------------------------------------------------------------------------
+int vd_parse_vdw1(const void* blob, size_t bytes, WMap& out) {
+    const uint8_t* p = (const uint8_t*)blob;
+    const uint8_t* end = p + bytes;
+    auto need = [&](size_t k) { return (size_t)(end - p) >= k; };
+    if (!need(8) || memcmp(p, "VDW1", 4) != 0) return vd_set_error(VD_ERR_WEIGHTS, "weights: bad magic");
+    uint32_t count;
+    memcpy(&count, p + 4, 4);
+    p += 8;
+    for (uint32_t i = 0; i < count; ++i) {
+        if (!need(2)) return vd_set_error(VD_ERR_WEIGHTS, "weights: truncated header %u", i);
+        uint16_t nl;
+        memcpy(&nl, p, 2);
+        p += 2;
+        if (!need(nl + 2)) return vd_set_error(VD_ERR_WEIGHTS, "weights: truncated name %u", i);
+        std::string name((const char*)p, nl);
+        p += nl;
+        uint8_t dtype = p[0], ndim = p[1];
+        p += 2;
+        if (dtype != 0 || ndim > 8 || !need(4u * ndim))
+            return vd_set_error(VD_ERR_WEIGHTS, "weights: bad tensor header for %s", name.c_str());
+        HT t;
+        size_t numel = 1;
+        for (int d = 0; d < ndim; ++d) {
+            uint32_t v;
+            memcpy(&v, p, 4);
+            p += 4;
+            t.shape.push_back((int)v);
+            numel *= v;
+        }
+        if (!need(numel * 4)) return vd_set_error(VD_ERR_WEIGHTS, "weights: truncated data for %s", name.c_str());
+        t.data.resize(numel);
+        memcpy(t.data.data(), p, numel * 4);
+        p += numel * 4;
+        out[name] = std::move(t);
+    }
+    return VD_OK;
+}
+
+// ----------------------------------------------------------------------------
+// device memory helpers
+// ----------------------------------------------------------------------------
+int Ctx::dalloc(void** p, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    hipError_t e = hipMalloc(p, bytes);
+    if (e != hipSuccess) return vd_set_error(VD_ERR_NOMEM, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+    allocs.push_back(*p);
+    return VD_OK;
+}
+
+int Ctx::act(Act& a, int h, int w, int c, bool f32out) {
+    a.h = h; a.w = w; a.c = c;
+    a.f32 = f32out || f32;
+    size_t bytes = (size_t)cfg.max_batch * h * w * c * (a.f32 ? 4 : 2);
+    int rc = dalloc(&a.p, bytes);
+    if (rc) return rc;
+    hipMemset(a.p, 0, bytes);
+    return VD_OK;
+}
+
+int Ctx::ensure_staging(void** p, size_t* have, size_t need) {
+    if (*have >= need) return VD_OK;
+    if (*p) hipFree(*p);
+    *p = nullptr;
+    *have = 0;
+    hipError_t e = hipMalloc(p, need);
+    if (e != hipSuccess) return vd_set_error(VD_ERR_NOMEM, "hipMalloc(%zu) failed", need);
+    *have = need;
+    return VD_OK;
+}
+
+// ----------------------------------------------------------------------------
+// conv construction: OIHW f32 -> packed [npad][kpad] in the compute type with
+// k = (kh*KW + kw)*cin_pad + c; BN(eval) -> per-channel scale/shift.
+// ----------------------------------------------------------------------------
+static uint16_t f32_to_bf16_rne(float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+
+int Ctx::upload_conv(Conv& cv, const std::vector<float>& w_oihw, const std::vector<float>& scale,
+                     const std::vector<float>& shift) {
+    const int vec = f32 ? 4 : 8;
+    const int bke = 8 * vec;
+    cv.cin_pad = (cv.cin + vec - 1) / vec * vec;
+    cv.npad = (cv.cout + 127) / 128 * 128;
+    const int K = cv.kh * cv.kw * cv.cin_pad;
+    cv.kpad = (K + bke - 1) / bke * bke;
+    std::vector<float> packed((size_t)cv.npad * cv.kpad, 0.f);
+    for (int n = 0; n < cv.cout; ++n)
+        for (int c = 0; c < cv.cin; ++c)
+            for (int y = 0; y < cv.kh; ++y)
+                for (int x = 0; x < cv.kw; ++x)
+                    packed[(size_t)n * cv.kpad + (y * cv.kw + x) * cv.cin_pad + c] =
+                        w_oihw[(((size_t)n * cv.cin + c) * cv.kh + y) * cv.kw + x];
+    int rc;
+    if (f32) {
+        rc = dalloc(&cv.w, packed.size() * 4);
+        if (rc) return rc;
+        VD_CHECK_HIP(hipMemcpy(cv.w, packed.data(), packed.size() * 4, hipMemcpyHostToDevice));
+    } else {
+        std::vector<uint16_t> h(packed.size());
+        for (size_t i = 0; i < packed.size(); ++i) h[i] = f32_to_bf16_rne(packed[i]);
+        rc = dalloc(&cv.w, h.size() * 2);
+        if (rc) return rc;
+        VD_CHECK_HIP(hipMemcpy(cv.w, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+    }
+    std::vector<float> sc(cv.npad, 0.f), sh(cv.npad, 0.f);
+    for (int n = 0; n < cv.cout; ++n) { sc[n] = scale[n]; sh[n] = shift[n]; }
+    rc = dalloc((void**)&cv.scale, cv.npad * 4);
+    if (rc) return rc;
+    rc = dalloc((void**)&cv.shift, cv.npad * 4);
+    if (rc) return rc;
+    VD_CHECK_HIP(hipMemcpy(cv.scale, sc.data(), cv.npad * 4, hipMemcpyHostToDevice));
+    VD_CHECK_HIP(hipMemcpy(cv.shift, sh.data(), cv.npad * 4, hipMemcpyHostToDevice));
+    cv.flops_per_px = 2.0 * cv.cout * cv.kh * cv.kw * cv.cin;
+    return VD_OK;
+}
+
+const HT* find_t(const WMap& W, const std::string& k) {
+    auto it = W.find(k);
+    return it == W.end() ? nullptr : &it->second;
+}
+
+// conv weight `wkey` [cout][cin][kh][kw] + BatchNorm at `bn` (eval: alpha =
+// gamma/sqrt(var+eps), beta = bias - mean*alpha, as torch's CPU inference kernel).
+int Ctx::make_conv_bn(const WMap& W, const std::string& wkey, const std::string& bn, float eps, int stride,
+                      int pad, int act, float slope, int* out_idx) {
+    const HT* w = find_t(W, wkey);
+    if (!w || w->shape.size() != 4) return vd_set_error(VD_ERR_WEIGHTS, "missing/bad conv weight %s", wkey.c_str());
+    Conv cv{};
+    cv.cout = w->shape[0]; cv.cin = w->shape[1]; cv.kh = w->shape[2]; cv.kw = w->shape[3];
+    cv.stride = stride; cv.pad = pad; cv.act = act; cv.slope = slope;
+    std::vector<float> sc(cv.cout, 1.f), sh(cv.cout, 0.f);
+    if (!bn.empty()) {
+        const HT* g = find_t(W, bn + ".weight");
+        const HT* b = find_t(W, bn + ".bias");
+        const HT* m = find_t(W, bn + ".running_mean");
+        const HT* v = find_t(W, bn + ".running_var");
+        if (!g || !b || !m || !v) return vd_set_error(VD_ERR_WEIGHTS, "missing BatchNorm tensors under %s", bn.c_str());
+        for (int n = 0; n < cv.cout; ++n) {
+            float alpha = g->data[n] / std::sqrt(v->data[n] + eps);
+            sc[n] = alpha;
+            sh[n] = b->data[n] - m->data[n] * alpha;
+        }
+    }
+    int rc = upload_conv(cv, w->data, sc, sh);
+    if (rc) return rc;
+    convs.push_back(cv);
+    *out_idx = (int)convs.size() - 1;
+    return VD_OK;
+}
+
+// Several 1x1 conv heads with bias fused along Cout (retinaface.py:90-92,140-142).
+int Ctx::make_conv_cat(const WMap& W, const std::vector<std::string>& wkeys, const std::vector<std::string>& bkeys,
+                       int act, int* out_idx) {
+    Conv cv{};
+    std::vector<float> wall, sc, sh;
+    for (size_t i = 0; i < wkeys.size(); ++i) {
+        const HT* w = find_t(W, wkeys[i]);
+        const HT* b = bkeys[i].empty() ? nullptr : find_t(W, bkeys[i]);
+        if (!w || w->shape.size() != 4 || (!bkeys[i].empty() && !b))
+            return vd_set_error(VD_ERR_WEIGHTS, "missing head tensor %s", wkeys[i].c_str());
+        if (i == 0) { cv.cin = w->shape[1]; cv.kh = w->shape[2]; cv.kw = w->shape[3]; }
+        if (w->shape[1] != cv.cin || w->shape[2] != cv.kh || w->shape[3] != cv.kw)
+            return vd_set_error(VD_ERR_WEIGHTS, "head shape mismatch at %s", wkeys[i].c_str());
+        wall.insert(wall.end(), w->data.begin(), w->data.end());
+        for (int n = 0; n < w->shape[0]; ++n) { sc.push_back(1.f); sh.push_back(b ? b->data[n] : 0.f); }
+        cv.cout += w->shape[0];
+    }
+    cv.stride = 1; cv.pad = cv.kh / 2; cv.act = act; cv.slope = 0.f;
+    int rc = upload_conv(cv, wall, sc, sh);
+    if (rc) return rc;
+    convs.push_back(cv);
+    *out_idx = (int)convs.size() - 1;
+    return VD_OK;
+}
+
+int Ctx::add_conv(Net& net, int ci, const Act& x, int xcoff, Act& y, int ycoff, const Act* res, int rcoff, int rmode,
+                  int rup) {
+    const Conv& cv = convs[ci];
+    Op op{};
+    op.kind = OP_CONV;
+    op.conv = ci;
+    op.x = x; op.xcoff = xcoff;
+    op.y = y; op.ycoff = ycoff;
+    if (res) { op.r = *res; op.rcoff = rcoff; op.rmode = rmode; op.rup = rup; }
+    const int oh = (x.h + 2 * cv.pad - cv.kh) / cv.stride + 1;
+    const int ow = (x.w + 2 * cv.pad - cv.kw) / cv.stride + 1;
+    if (oh != y.h || ow != y.w || ycoff + cv.cout > y.c || xcoff + cv.cin > x.c)
+        return vd_set_error(VD_ERR_ARG, "conv plan shape mismatch (%dx%d vs %dx%d)", oh, ow, y.h, y.w);
+    net.ops.push_back(op);
+    return VD_OK;
+}
+
+// ----------------------------------------------------------------------------
+// plan execution
+// ----------------------------------------------------------------------------
+void Ctx::t_begin(int fam, double work) {
+    if (!timing) return;
+    if (ev_used == ev_pool.size()) {
+        TimedEv t{};
+        hipEventCreate(&t.a);
+        hipEventCreate(&t.b);
+        ev_pool.push_back(t);
+    }
+    TimedEv& t = ev_pool[ev_used];
+    t.fam = fam;
+    t.work = work;
+    hipEventRecord(t.a, stream);
+}
+
+void Ctx::t_end() {
+    if (!timing) return;
+    hipEventRecord(ev_pool[ev_used].b, stream);
+    ++ev_used;
+}
+
+int Ctx::run_conv_op(const Op& op, int n) {
+    const Conv& cv = convs[op.conv];
+    ConvArgs a{};
+    a.x = op.x.p; a.xh = op.x.h; a.xw = op.x.w; a.ldx = op.x.c; a.xcoff = op.xcoff;
+    a.w = cv.w; a.scale = cv.scale; a.shift = cv.shift;
+    a.res = op.r.p; a.res_ld = op.r.c; a.res_coff = op.rcoff; a.res_up = op.rup; a.rh = op.r.h; a.rw = op.r.w;
+    a.res_mode = op.r.p ? op.rmode : VD_RES_NONE;
+    a.y = op.y.p; a.yh = op.y.h; a.yw = op.y.w; a.ldy = op.y.c; a.ycoff = op.ycoff;
+    a.B = n; a.cin_pad = cv.cin_pad; a.cout = cv.cout; a.kpad = cv.kpad;
+    a.kh = cv.kh; a.kw = cv.kw; a.stride = cv.stride; a.pad = cv.pad;
+    a.M = n * op.y.h * op.y.w;
+    a.act = cv.act; a.slope = cv.slope; a.out_f32 = op.y.f32 ? 1 : 0;
+    t_begin(0, cv.flops_per_px * a.M);
+    hipError_t e = vd_launch_conv(a, f32, stream);
+    t_end();
+    if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "conv launch: %s", hipGetErrorString(e));
+    return VD_OK;
+}
+
+int Ctx::run_net(const Net& net, int n) {
+    for (const Op& op : net.ops) {
+        int rc = VD_OK;
+        if (op.kind == OP_CONV) {
+            rc = run_conv_op(op, n);
+        } else if (op.kind == OP_MAXPOOL) {
+            t_begin(4, 0);
+            hipError_t e = vd_launch_maxpool(f32, op.x.p, n, op.x.h, op.x.w, op.x.c, op.xcoff, op.y.p, op.y.h,
+                                             op.y.w, op.y.c, op.ycoff, op.ch, op.k, op.s, op.p, stream);
+            t_end();
+            if (e != hipSuccess) rc = vd_set_error(VD_ERR_HIP, "maxpool: %s", hipGetErrorString(e));
+        } else if (op.kind == OP_UPSAMPLE) {
+            t_begin(4, 0);
+            hipError_t e = vd_launch_upsample2x(f32, op.x.p, n, op.x.h, op.x.w, op.x.c, op.xcoff, op.y.p, op.y.c,
+                                                op.ycoff, op.ch, stream);
+            t_end();
+            if (e != hipSuccess) rc = vd_set_error(VD_ERR_HIP, "upsample: %s", hipGetErrorString(e));
+        }
+        if (rc) return rc;
+    }
+    return VD_OK;
+}
+
+// cv2.resize mode selection (resize.cpp hal::resize [ext]; oracle/letterbox.py)
+void vd_resize_mode(int ih, int iw, int nh, int nw, int* mode, double* sx, double* sy) {
+    if (nh == ih && nw == iw) { *mode = LB_COPY; *sx = *sy = 1.0; return; }
+    double inv_x = (double)nw / iw, inv_y = (double)nh / ih;
+    double scx = 1.0 / inv_x, scy = 1.0 / inv_y;
+    int isx = (int)std::nearbyint(scx), isy = (int)std::nearbyint(scy);
+    bool area_fast = std::fabs(scx - isx) < 2.220446049250313e-16 && std::fabs(scy - isy) < 2.220446049250313e-16;
+    *mode = (area_fast && isx == 2 && isy == 2) ? LB_AREA2 : LB_LINEAR;
+    *sx = scx;
+    *sy = scy;
+}
+
+const uint8_t* Ctx::frames_to_device(const uint8_t* frames, int n, int h, size_t pitch, int where, int* rc) {
+    *rc = VD_OK;
+    if (where == VD_DEVICE) return frames;
+    size_t bytes = (size_t)n * h * pitch;
+    *rc = ensure_staging(&stage_in, &stage_in_bytes, bytes);
+    if (*rc) return nullptr;
+    hipError_t e = hipMemcpyAsync(stage_in, frames, bytes, hipMemcpyHostToDevice, stream);
+    if (e != hipSuccess) {
+        *rc = vd_set_error(VD_ERR_HIP, "H2D frames: %s", hipGetErrorString(e));
+        return nullptr;
+    }
+    return (const uint8_t*)stage_in;
+}
+
+int Ctx::check_frames(int n, int h, int w, size_t pitch) {
+    if (n <= 0 || n > cfg.max_batch) return vd_set_error(VD_ERR_ARG, "n=%d outside [1, max_batch=%d]", n, cfg.max_batch);
+    if (h <= 0 || w <= 0 || pitch < (size_t)w * 3) return vd_set_error(VD_ERR_ARG, "bad frame geometry %dx%d pitch %zu", w, h, pitch);
+    return VD_OK;
+}
+
+// Box outputs: kernels write straight into caller arrays when they are device
+// memory; host outputs go through ctx staging + one D2H at the end.
+int Ctx::box_targets(vd_boxes* out, int n, BoxTargets& t) {
+    if (!out || !out->count || !out->xyxy || out->cap <= 0) return vd_set_error(VD_ERR_ARG, "vd_boxes needs count, xyxy, cap>0");
+    t.cap = out->cap;
+    if (out->where == VD_DEVICE) {
+        t.count = out->count; t.xyxy = out->xyxy; t.xyxy_f = out->xyxy_f; t.score = out->score; t.label = out->label;
+        return VD_OK;
+    }
+    size_t nb = (size_t)n * out->cap;
+    size_t need = n * 4 + nb * (16 + 16 + 4 + 4);
+    int rc = ensure_staging(&stage_box, &stage_box_bytes, need + 64);
+    if (rc) return rc;
+    char* p = (char*)stage_box;
+    t.count = (int*)p; p += ((n * 4 + 15) / 16) * 16;
+    t.xyxy = (int*)p; p += nb * 16;
+    t.xyxy_f = (float*)p; p += nb * 16;
+    t.score = (float*)p; p += nb * 4;
+    t.label = (int*)p;
+    return VD_OK;
+}
+
+int Ctx::box_finish(vd_boxes* out, int n, const BoxTargets& t) {
+    if (out->where == VD_DEVICE) return VD_OK;
+    size_t nb = (size_t)n * out->cap;
+    VD_CHECK_HIP(hipMemcpyAsync(out->count, t.count, n * 4, hipMemcpyDeviceToHost, stream));
+    VD_CHECK_HIP(hipMemcpyAsync(out->xyxy, t.xyxy, nb * 16, hipMemcpyDeviceToHost, stream));
+    if (out->xyxy_f) VD_CHECK_HIP(hipMemcpyAsync(out->xyxy_f, t.xyxy_f, nb * 16, hipMemcpyDeviceToHost, stream));
+    if (out->score) VD_CHECK_HIP(hipMemcpyAsync(out->score, t.score, nb * 4, hipMemcpyDeviceToHost, stream));
+    if (out->label) VD_CHECK_HIP(hipMemcpyAsync(out->label, t.label, nb * 4, hipMemcpyDeviceToHost, stream));
+    VD_CHECK_HIP(hipStreamSynchronize(stream));
+    for (int i = 0; i < n; ++i)
+        if (out->count[i] > out->cap)
+            return vd_set_error(VD_ERR_CAPACITY, "frame %d kept %d boxes > cap %d", i, out->count[i], out->cap);
+    return VD_OK;
+}
+
+int Ctx::face_letterbox(const uint8_t* dframes, int n, int h, int w, size_t pitch) {
+    LetterboxArgs a{};
+    a.src = dframes; a.n = n; a.ih = h; a.iw = w; a.pitch = pitch;
+    a.oh = face.in_h; a.ow = face.in_w;
+    // utils/utils.py:9-13 (Python doubles)
+    double scale = std::min((double)a.ow / w, (double)a.oh / h);
+    a.nw = (int)(w * scale);
+    a.nh = (int)(h * scale);
+    a.top = (a.oh - a.nh) / 2;
+    a.left = (a.ow - a.nw) / 2;
+    vd_resize_mode(h, w, a.nh, a.nw, &a.mode, &a.scale_x, &a.scale_y);
+    a.pad_value = 128.f;
+    a.mean[0] = 104.f; a.mean[1] = 117.f; a.mean[2] = 123.f;
+    a.div = 1.f;
+    a.flip = 0;
+    a.out = face.input.p; a.cpad = face.input.c; a.out_f32 = f32 ? 1 : 0;
+    t_begin(2, (double)n * (a.nh * (double)w * 3 + (double)a.oh * a.ow * a.cpad * (f32 ? 4 : 2)));
+    hipError_t e = vd_launch_letterbox(a, stream);
+    t_end();
+    if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "letterbox: %s", hipGetErrorString(e));
+    return VD_OK;
+}
+
+int Ctx::face_post(int n, int img_h, int img_w, const BoxTargets& t) {
+    FacePostArgs p{};
+    for (int l = 0; l < 3; ++l) {
+        p.heads[l] = (const float*)face.heads[l].p;
+        p.lh[l] = face.heads[l].h;
+        p.lw[l] = face.heads[l].w;
+        p.loff[l] = face.loff[l];
+    }
+    p.anchors = face.anchors; p.A = face.A; p.B = n;
+    p.conf = cfg.confidence; p.iou = cfg.nms_iou;
+    p.cand_keys = face.cand_keys; p.cand_count = face.cand_count;
+    p.scratch_box = face.scratch_box; p.scratch_area = face.scratch_area;
+    p.scratch_keys = face.scratch_keys; p.scratch_supp = face.scratch_supp; p.sort_cap = face.sort_cap;
+    p.img_h = img_h; p.img_w = img_w; p.in_h = face.in_h; p.in_w = face.in_w;
+    p.cap = t.cap; p.out_count = t.count; p.out_xyxy = t.xyxy; p.out_xyxy_f = t.xyxy_f;
+    p.out_score = t.score; p.out_label = t.label;
+    t_begin(3, (double)n * face.A * 16 * 4);
+    hipError_t e = vd_launch_face_post(p, stream);
+    t_end();
+    if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "face post: %s", hipGetErrorString(e));
+    return VD_OK;
+}
+
+// ----------------------------------------------------------------------------
+// C-ABI
+// ----------------------------------------------------------------------------
+#define VD_ENTRY(ctx)                                                          \
+    if (!(ctx)) return vd_set_error(VD_ERR_ARG, "null context");              \
+    std::lock_guard<std::mutex> _lk((ctx)->mu);                                \
+    if (hipSetDevice((ctx)->device) != hipSuccess)                             \
+        return vd_set_error(VD_ERR_HIP, "hipSetDevice(%d) failed", (ctx)->device)
+
+extern "C" {
+
+int vd_abi_version(void) { return VDMI_ABI_VERSION; }
+const char* vd_last_error(void) { return g_err.c_str(); }
+
+int vd_default_cfg(vd_cfg* c) {
+    if (!c) return vd_set_error(VD_ERR_ARG, "null cfg");
+    memset(c, 0, sizeof *c);
+    c->input_h = 640; c->input_w = 640;     // combine_detect.py:860
+    c->max_batch = 64;                      // config.ini:35
+    c->max_frame_h = 2160; c->max_frame_w = 3840;
+    c->precision = VD_PREC_BF16;
+    c->max_boxes = 256;
+    c->confidence = 0.5f;                   // combine_detect.py:861
+    c->nms_iou = 0.4;                       // combine_detect.py:862
+    c->mosaic_level = 8;                    // combine_detect.py:249
+    c->plate_imgsz = 640;
+    c->plate_nc = 1;
+    c->plate_conf = 0.5f;                   // combine_detect.py:217
+    c->plate_iou = 0.7;                     // ultralytics default [ext]
+    c->plate_max_det = 300;                 // ultralytics default [ext]
+    return VD_OK;
+}
+
+int vd_create(const vd_cfg* cfg, int device, vd_ctx** out) {
+    if (!out) return vd_set_error(VD_ERR_ARG, "null out");
+    *out = nullptr;
+    vd_cfg c;
+    if (cfg) c = *cfg; else vd_default_cfg(&c);
+    if (c.max_batch <= 0 || c.input_h % 32 || c.input_w % 32 || c.input_h <= 0 || c.input_w <= 0)
+        return vd_set_error(VD_ERR_ARG, "cfg: max_batch>0 and input dims multiple of 32 required");
+    if (c.precision != VD_PREC_BF16 && c.precision != VD_PREC_FP32) return vd_set_error(VD_ERR_ARG, "cfg: bad precision");
+    if (c.mosaic_level <= 0) c.mosaic_level = 8;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+        return vd_set_error(VD_ERR_HIP, "no HIP device %d (count %d)", device, ndev);
+    if (hipSetDevice(device) != hipSuccess) return vd_set_error(VD_ERR_HIP, "hipSetDevice(%d)", device);
+    Ctx* ctx = new Ctx();
+    ctx->cfg = c;
+    ctx->device = device;
+    ctx->f32 = c.precision == VD_PREC_FP32;
+    if (hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return vd_set_error(VD_ERR_HIP, "hipStreamCreate failed");
+    }
+    ctx->stream = ctx->own_stream;
+    *out = (vd_ctx*)ctx;
+    return VD_OK;
+}
+
+int vd_destroy(vd_ctx* h) {
+    Ctx* ctx = (Ctx*)h;
+    if (!ctx) return VD_OK;
+    hipSetDevice(ctx->device);
+    hipStreamSynchronize(ctx->stream);
+    for (void* p : ctx->allocs) hipFree(p);
+    if (ctx->stage_in) hipFree(ctx->stage_in);
+    if (ctx->stage_out) hipFree(ctx->stage_out);
+    if (ctx->stage_box) hipFree(ctx->stage_box);
+    if (ctx->stage_box2) hipFree(ctx->stage_box2);
+    for (auto& t : ctx->ev_pool) { hipEventDestroy(t.a); hipEventDestroy(t.b); }
+    hipStreamDestroy(ctx->own_stream);
+    delete ctx;
+    return VD_OK;
+}
+
+int vd_load_weights(vd_ctx* h, int net, const void* blob, size_t bytes, int fmt) {
+    Ctx* ctx = (Ctx*)h;
+    VD_ENTRY(ctx);
+    if (fmt != VD_WEIGHTS_VDW1) return vd_set_error(VD_ERR_ARG, "unknown weight format %d", fmt);
+    if (!blob) return vd_set_error(VD_ERR_ARG, "null weight blob");
+    WMap W;
+    int rc = vd_parse_vdw1(blob, bytes, W);
+    if (rc) return rc;
+    if (net == VD_NET_RETINAFACE) {
+        if (ctx->face.loaded) return vd_set_error(VD_ERR_STATE, "RetinaFace weights already loaded");
+        return vd_build_face(*ctx, W);
+    }
+    if (net == VD_NET_YOLOV8N) {
+        if (ctx->plate.loaded) return vd_set_error(VD_ERR_STATE, "plate weights already loaded");
+        return vd_build_plate(*ctx, W);
+    }
+    return vd_set_error(VD_ERR_ARG, "unknown net %d", net);
+}
+
+int vd_set_stream(vd_ctx* h, void* s) {
+    Ctx* ctx = (Ctx*)h;
+    VD_ENTRY(ctx);
+    ctx->stream = s ? (hipStream_t)s : ctx->own_stream;
+    return VD_OK;
+}
+
+void* vd_get_stream(vd_ctx* h) { return h ? (void*)((Ctx*)h)->stream : nullptr; }
+
+int vd_sync(vd_ctx* h) {
+    Ctx* ctx = (Ctx*)h;
+    VD_ENTRY(ctx);
+    VD_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    return VD_OK;
+}
+
+int vd_detect(vd_ctx* h, const uint8_t* frames, int n, int fh, int fw, size_t pitch, int where, vd_boxes* faces) {
+    Ctx* ctx = (Ctx*)h;
+    VD_ENTRY(ctx);
+    if (!ctx->face.loaded) return vd_set_error(VD_ERR_STATE, "RetinaFace weights not loaded");
+    int rc = ctx->check_frames(n, fh, fw, pitch);
+    if (rc) return rc;
+    BoxTargets t;
+    rc = ctx->box_targets(faces, n, t);
+    if (rc) return rc;
+    const uint8_t* d = ctx->frames_to_device(frames, n, fh, pitch, where, &rc);
+    if (rc) return rc;
+    if ((rc = ctx->face_letterbox(d, n, fh, fw, pitch))) return rc;
+    if ((rc = ctx->run_net(ctx->face.net, n))) return rc;
+    if ((rc = ctx->face_post(n, fh, fw, t))) return rc;
+    return ctx->box_finish(faces, n, t);
+}
+
+int vd_detect_plates(vd_ctx* h, const uint8_t* frames, int n, int fh, int fw, size_t pitch, int where,
+                     vd_boxes* plates) {
+    Ctx* ctx = (Ctx*)h;
+    VD_ENTRY(ctx);
+    if (!ctx->plate.loaded) return vd_set_error(VD_ERR_STATE, "plate weights not loaded");
+    int rc = ctx->check_frames(n, fh, fw, pitch);
+    if (rc) return rc;
+    BoxTargets t;
+    rc = ctx->box_targets(plates, n, t);
+    if (rc) return rc;
+    const uint8_t* d = ctx->frames_to_device(frames, n, fh, pitch, where, &rc);
+    if (rc) return rc;
+    if ((rc = vd_plate_forward(*ctx, d, n, fh, fw, pitch))) return rc;
+    if ((rc = vd_plate_post(*ctx, n, fh, fw, t))) return rc;
+    return ctx->box_finish(plates, n, t);
+}
+
+int vd_mosaic(vd_ctx* h, const uint8_t* in, uint8_t* out, int n, int fh, int fw, size_t pitch, int where,
+              const vd_boxes* boxes, int level, int mode) {
+    Ctx* ctx = (Ctx*)h;
+    VD_ENTRY(ctx);
+    if (mode != VD_MOSAIC_OUT_OF_PLACE) return vd_set_error(VD_ERR_ARG, "unsupported mosaic mode %d", mode);
+    if (!in || !out || !boxes || !boxes->count || !boxes->xyxy || boxes->cap <= 0)
+        return vd_set_error(VD_ERR_ARG, "vd_mosaic: null argument");
+    if (n <= 0 || fh <= 0 || fw <= 0 || pitch < (size_t)fw * 3 || level <= 0)
+        return vd_set_error(VD_ERR_ARG, "vd_mosaic: bad geometry");
+    int rc = VD_OK;
+    const uint8_t* din = in;
+    uint8_t* dout = out;
+    size_t bytes = (size_t)n * fh * pitch;
+    if (where == VD_HOST) {
+        if ((rc = ctx->ensure_staging(&ctx->stage_in, &ctx->stage_in_bytes, bytes))) return rc;
+        if ((rc = ctx->ensure_staging(&ctx->stage_out, &ctx->stage_out_bytes, bytes))) return rc;
+        VD_CHECK_HIP(hipMemcpyAsync(ctx->stage_in, in, bytes, hipMemcpyHostToDevice, ctx->stream));
+        din = (const uint8_t*)ctx->stage_in;
+        dout = (uint8_t*)ctx->stage_out;
+    }
+    const int* cnt = boxes->count;
+    const int* xy = boxes->xyxy;
+    if (boxes->where == VD_HOST) {
+        size_t nb = (size_t)n * boxes->cap;
+        if ((rc = ctx->ensure_staging(&ctx->stage_box2, &ctx->stage_box2_bytes, n * 4 + nb * 16 + 16))) return rc;
+        int* dc = (int*)ctx->stage_box2;
+        int* dx = dc + ((n + 3) / 4) * 4;
+        VD_CHECK_HIP(hipMemcpyAsync(dc, boxes->count, n * 4, hipMemcpyHostToDevice, ctx->stream));
+        VD_CHECK_HIP(hipMemcpyAsync(dx, boxes->xyxy, nb * 16, hipMemcpyHostToDevice, ctx->stream));
+        cnt = dc;
+        xy = dx;
+    }
+    ctx->t_begin(1, 2.0 * n * (double)fh * fw * 3);
+    hipError_t e = vd_launch_mosaic(din, dout, n, fh, fw, pitch, cnt, xy, boxes->cap, nullptr, nullptr, 0, level,
+                                    ctx->stream);
+    ctx->t_end();
+    if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "mosaic: %s", hipGetErrorString(e));
+    if (where == VD_HOST) {
+        VD_CHECK_HIP(hipMemcpyAsync(out, dout, bytes, hipMemcpyDeviceToHost, ctx->stream));
+        VD_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    } else if (boxes->where == VD_HOST) {
+        VD_CHECK_HIP(hipStreamSynchronize(ctx->stream));   // staging reused by the next call
+    }
+    return VD_OK;
+}
+
+int vd_process(vd_ctx* h, const uint8_t* in, uint8_t* out, int n, int fh, int fw, size_t pitch, int where,
+               int flags, vd_boxes* faces, vd_boxes* plates) {
+    Ctx* ctx = (Ctx*)h;
+    VD_ENTRY(ctx);
+    const bool do_faces = flags & VD_PROC_FACES, do_plates = flags & VD_PROC_PLATES;
+    const bool do_mosaic = flags & VD_PROC_MOSAIC, mosaic_plates = flags & VD_PROC_MOSAIC_PLATES;
+    if (do_faces && !ctx->face.loaded) return vd_set_error(VD_ERR_STATE, "RetinaFace weights not loaded");
+    if (do_plates && !ctx->plate.loaded) return vd_set_error(VD_ERR_STATE, "plate weights not loaded");
+    if (mosaic_plates && !do_plates) return vd_set_error(VD_ERR_ARG, "MOSAIC_PLATES needs PLATES");
+    if (do_mosaic && !out) return vd_set_error(VD_ERR_ARG, "MOSAIC needs an output buffer");
+    int rc = ctx->check_frames(n, fh, fw, pitch);
+    if (rc) return rc;
+    BoxTargets tf{}, tp{};
+    if (do_faces && (rc = ctx->box_targets(faces, n, tf))) return rc;
+    if (do_plates) {
+        // plate box staging must not alias the face staging
+        if (plates->where == VD_DEVICE) {
+            tp.cap = plates->cap; tp.count = plates->count; tp.xyxy = plates->xyxy; tp.xyxy_f = plates->xyxy_f;
+            tp.score = plates->score; tp.label = plates->label;
+        } else {
+            size_t nb = (size_t)n * plates->cap;
+            if ((rc = ctx->ensure_staging(&ctx->stage_box2, &ctx->stage_box2_bytes, n * 4 + nb * 40 + 64))) return rc;
+            char* p = (char*)ctx->stage_box2;
+            tp.cap = plates->cap;
+            tp.count = (int*)p; p += ((n * 4 + 15) / 16) * 16;
+            tp.xyxy = (int*)p; p += nb * 16;
+            tp.xyxy_f = (float*)p; p += nb * 16;
+            tp.score = (float*)p; p += nb * 4;
+            tp.label = (int*)p;
+        }
+    }
+    const uint8_t* d = ctx->frames_to_device(in, n, fh, pitch, where, &rc);
+    if (rc) return rc;
+    if (do_faces) {
+        if ((rc = ctx->face_letterbox(d, n, fh, fw, pitch))) return rc;
+        if ((rc = ctx->run_net(ctx->face.net, n))) return rc;
+        if ((rc = ctx->face_post(n, fh, fw, tf))) return rc;
+    }
+    if (do_plates) {
+        if ((rc = vd_plate_forward(*ctx, d, n, fh, fw, pitch))) return rc;
+        if ((rc = vd_plate_post(*ctx, n, fh, fw, tp))) return rc;
+    }
+    if (do_mosaic) {
+        uint8_t* dout = out;
+        size_t bytes = (size_t)n * fh * pitch;
+        if (where == VD_HOST) {
+            if ((rc = ctx->ensure_staging(&ctx->stage_out, &ctx->stage_out_bytes, bytes))) return rc;
+            dout = (uint8_t*)ctx->stage_out;
+        }
+        ctx->t_begin(1, 2.0 * n * (double)fh * fw * 3);
+        hipError_t e = vd_launch_mosaic(d, dout, n, fh, fw, pitch, do_faces ? tf.count : nullptr,
+                                        do_faces ? tf.xyxy : nullptr, do_faces ? tf.cap : 0,
+                                        mosaic_plates ? tp.count : nullptr, mosaic_plates ? tp.xyxy : nullptr,
+                                        mosaic_plates ? tp.cap : 0, ctx->cfg.mosaic_level, ctx->stream);
+        ctx->t_end();
+        if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "mosaic: %s", hipGetErrorString(e));
+        if (where == VD_HOST) VD_CHECK_HIP(hipMemcpyAsync(out, dout, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    int rc2 = VD_OK;
+    if (do_faces) rc2 = ctx->box_finish(faces, n, tf);
+    if (do_plates) {
+        int rc3 = ctx->box_finish(plates, n, tp);
+        if (!rc2) rc2 = rc3;
+    }
+    if (where == VD_HOST) VD_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    return rc2;
+}
+
+int vd_timing_enable(vd_ctx* h, int on) {
+    Ctx* ctx = (Ctx*)h;
+    VD_ENTRY(ctx);
+    ctx->timing = on != 0;
+    return VD_OK;
+}
+
+int vd_timing_reset(vd_ctx* h) {
+    Ctx* ctx = (Ctx*)h;
+    VD_ENTRY(ctx);
+    VD_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    ctx->ev_used = 0;
+    return VD_OK;
+}
+
+int vd_timing_read(vd_ctx* h, int fam, double* ms, int64_t* launches, double* work) {
+    Ctx* ctx = (Ctx*)h;
+    VD_ENTRY(ctx);
+    VD_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    double tot = 0, wk = 0;
+    int64_t cnt = 0;
+    for (size_t i = 0; i < ctx->ev_used; ++i) {
+        const TimedEv& t = ctx->ev_pool[i];
+        if (t.fam != fam) continue;
+        float e = 0.f;
+        VD_CHECK_HIP(hipEventElapsedTime(&e, t.a, t.b));
+        tot += e;
+        wk += t.work;
+        ++cnt;
+    }
+    if (ms) *ms = tot;
+    if (launches) *launches = cnt;
+    if (work) *work = wk;
+    return VD_OK;
+}
+
+// ---- test hooks ----
+int vdt_letterbox(vd_ctx* h, const uint8_t* frames, int n, int fh, int fw, size_t pitch, int where, float* out,
+                  int cpad) {
+    Ctx* ctx = (Ctx*)h;
+    VD_ENTRY(ctx);
+    if (!ctx->face.loaded) return vd_set_error(VD_ERR_STATE, "RetinaFace weights not loaded");
+    int rc = ctx->check_frames(n, fh, fw, pitch);
+    if (rc) return rc;
+    const uint8_t* d = ctx->frames_to_device(frames, n, fh, pitch, where, &rc);
+    if (rc) return rc;
+    if ((rc = ctx->face_letterbox(d, n, fh, fw, pitch))) return rc;
+    const Act& in = ctx->face.input;
+    size_t px = (size_t)n * in.h * in.w;
+    std::vector<uint16_t> hb;
+    std::vector<float> hf;
+    VD_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    if (ctx->f32) {
+        hf.resize(px * in.c);
+        VD_CHECK_HIP(hipMemcpy(hf.data(), in.p, hf.size() * 4, hipMemcpyDeviceToHost));
+    } else {
+        hb.resize(px * in.c);
+        VD_CHECK_HIP(hipMemcpy(hb.data(), in.p, hb.size() * 2, hipMemcpyDeviceToHost));
+    }
+    for (size_t i = 0; i < px; ++i)
+        for (int c = 0; c < cpad; ++c) {
+            float v = 0.f;
+            if (c < in.c) {
+                if (ctx->f32) v = hf[i * in.c + c];
+                else { uint32_t u = (uint32_t)hb[i * in.c + c] << 16; memcpy(&v, &u, 4); }
+            }
+            out[i * cpad + c] = v;
+        }
+    return VD_OK;
+}
+
+int vdt_forward_heads(vd_ctx* h, const uint8_t* frames, int n, int fh, int fw, size_t pitch, int where, float* loc,
+                      float* conf, float* landm) {
+    Ctx* ctx = (Ctx*)h;
+    VD_ENTRY(ctx);
+    if (!ctx->face.loaded) return vd_set_error(VD_ERR_STATE, "RetinaFace weights not loaded");
+    int rc = ctx->check_frames(n, fh, fw, pitch);
+    if (rc) return rc;
+    const uint8_t* d = ctx->frames_to_device(frames, n, fh, pitch, where, &rc);
+    if (rc) return rc;
+    if ((rc = ctx->face_letterbox(d, n, fh, fw, pitch))) return rc;
+    if ((rc = ctx->run_net(ctx->face.net, n))) return rc;
+    VD_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    const int A = ctx->face.A;
+    for (int l = 0; l < 3; ++l) {
+        const Act& hd = ctx->face.heads[l];
+        std::vector<float> buf((size_t)n * hd.h * hd.w * 32);
+        VD_CHECK_HIP(hipMemcpy(buf.data(), hd.p, buf.size() * 4, hipMemcpyDeviceToHost));
+        for (int b = 0; b < n; ++b)
+            for (int px = 0; px < hd.h * hd.w; ++px)
+                for (int k = 0; k < 2; ++k) {
+                    const float* src = &buf[((size_t)b * hd.h * hd.w + px) * 32];
+                    size_t a = (size_t)b * A + ctx->face.loff[l] + px * 2 + k;
+                    if (loc) for (int j = 0; j < 4; ++j) loc[a * 4 + j] = src[4 * k + j];
+                    if (conf) for (int j = 0; j < 2; ++j) conf[a * 2 + j] = src[8 + 2 * k + j];
+                    if (landm) for (int j = 0; j < 10; ++j) landm[a * 10 + j] = src[12 + 10 * k + j];
+                }
+    }
+    return VD_OK;
+}
+
+int vdt_postprocess(vd_ctx* h, const float* loc, const float* conf, int n, const int32_t* img_hw, vd_boxes* faces) {
+    Ctx* ctx = (Ctx*)h;
+    VD_ENTRY(ctx);
+    if (!ctx->face.loaded) return vd_set_error(VD_ERR_STATE, "RetinaFace weights not loaded");
+    if (n <= 0 || n > ctx->cfg.max_batch || !loc || !conf || !img_hw) return vd_set_error(VD_ERR_ARG, "vdt_postprocess args");
+    for (int i = 1; i < n; ++i)
+        if (img_hw[2 * i] != img_hw[0] || img_hw[2 * i + 1] != img_hw[1])
+            return vd_set_error(VD_ERR_ARG, "vdt_postprocess: frames of one call share a size");
+    const int A = ctx->face.A;
+    for (int l = 0; l < 3; ++l) {
+        const Act& hd = ctx->face.heads[l];
+        std::vector<float> buf((size_t)n * hd.h * hd.w * 32, 0.f);
+        for (int b = 0; b < n; ++b)
+            for (int px = 0; px < hd.h * hd.w; ++px)
+                for (int k = 0; k < 2; ++k) {
+                    float* dst = &buf[((size_t)b * hd.h * hd.w + px) * 32];
+                    size_t a = (size_t)b * A + ctx->face.loff[l] + px * 2 + k;
+                    for (int j = 0; j < 4; ++j) dst[4 * k + j] = loc[a * 4 + j];
+                    for (int j = 0; j < 2; ++j) dst[8 + 2 * k + j] = conf[a * 2 + j];
+                }
+        VD_CHECK_HIP(hipMemcpy(hd.p, buf.data(), buf.size() * 4, hipMemcpyHostToDevice));
+    }
+    BoxTargets t;
+    int rc = ctx->box_targets(faces, n, t);
+    if (rc) return rc;
+    if ((rc = ctx->face_post(n, img_hw[0], img_hw[1], t))) return rc;
+    rc = ctx->box_finish(faces, n, t);
+    VD_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    return rc;
+}
+
+int vdt_conv2d(vd_ctx* h, const float* x, int n, int xh, int xw, int cin, const float* wgt, int cout, int kh, int kw,
+               int stride, int pad, const float* scale, const float* shift, int act, float slope, const float* res,
+               int res_mode, float* y, int* oh_out, int* ow_out) {
+    Ctx* ctx = (Ctx*)h;
+    VD_ENTRY(ctx);
+    if (n <= 0 || xh <= 0 || xw <= 0 || cin <= 0 || cout <= 0 || kh <= 0 || kw <= 0 || stride <= 0 || pad < 0)
+        return vd_set_error(VD_ERR_ARG, "vdt_conv2d: bad shape");
+    Conv cv{};
+    cv.cin = cin; cv.cout = cout; cv.kh = kh; cv.kw = kw; cv.stride = stride; cv.pad = pad; cv.act = act;
+    cv.slope = slope;
+    std::vector<float> w(wgt, wgt + (size_t)cout * cin * kh * kw);
+    std::vector<float> sc(scale, scale + cout), sh(shift, shift + cout);
+    const size_t nalloc = ctx->allocs.size();
+    int rc = ctx->upload_conv(cv, w, sc, sh);
+    if (rc) return rc;
+    const int oh = (xh + 2 * pad - kh) / stride + 1, ow = (xw + 2 * pad - kw) / stride + 1;
+    const int es = ctx->f32 ? 4 : 2;
+    const int ldx = cv.cin_pad;
+    const int ldy = (cout + 7) / 8 * 8;
+    std::vector<char> xb((size_t)n * xh * xw * ldx * es, 0), rb;
+    for (size_t p = 0; p < (size_t)n * xh * xw; ++p)
+        for (int c = 0; c < cin; ++c) {
+            float v = x[p * cin + c];
+            if (ctx->f32) memcpy(&xb[(p * ldx + c) * 4], &v, 4);
+            else { uint16_t b = f32_to_bf16_rne(v); memcpy(&xb[(p * ldx + c) * 2], &b, 2); }
+        }
+    void *dx = nullptr, *dy = nullptr, *dr = nullptr;
+    if ((rc = ctx->dalloc(&dx, xb.size()))) return rc;
+    if ((rc = ctx->dalloc(&dy, (size_t)n * oh * ow * ldy * 4))) return rc;   // f32 output
+    VD_CHECK_HIP(hipMemcpy(dx, xb.data(), xb.size(), hipMemcpyHostToDevice));
+    if (res && res_mode) {
+        rb.assign((size_t)n * oh * ow * ldy * es, 0);
+        for (size_t p = 0; p < (size_t)n * oh * ow; ++p)
+            for (int c = 0; c < cout; ++c) {
+                float v = res[p * cout + c];
+                if (ctx->f32) memcpy(&rb[(p * ldy + c) * 4], &v, 4);
+                else { uint16_t b = f32_to_bf16_rne(v); memcpy(&rb[(p * ldy + c) * 2], &b, 2); }
+            }
+        if ((rc = ctx->dalloc(&dr, rb.size()))) return rc;
+        VD_CHECK_HIP(hipMemcpy(dr, rb.data(), rb.size(), hipMemcpyHostToDevice));
+    }
+    ConvArgs a{};
+    a.x = dx; a.xh = xh; a.xw = xw; a.ldx = ldx; a.xcoff = 0;
+    a.w = cv.w; a.scale = cv.scale; a.shift = cv.shift;
+    a.res = dr; a.res_ld = ldy; a.res_coff = 0; a.res_up = 0; a.rh = oh; a.rw = ow;
+    a.res_mode = dr ? res_mode : VD_RES_NONE;
+    a.y = dy; a.yh = oh; a.yw = ow; a.ldy = ldy; a.ycoff = 0;
+    a.B = n; a.cin_pad = cv.cin_pad; a.cout = cout; a.kpad = cv.kpad;
+    a.kh = kh; a.kw = kw; a.stride = stride; a.pad = pad; a.M = n * oh * ow;
+    a.act = act; a.slope = slope; a.out_f32 = 1;
+    hipError_t e = vd_launch_conv(a, ctx->f32, ctx->stream);
+    if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "conv launch: %s", hipGetErrorString(e));
+    VD_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    std::vector<float> yb((size_t)n * oh * ow * ldy);
+    VD_CHECK_HIP(hipMemcpy(yb.data(), dy, yb.size() * 4, hipMemcpyDeviceToHost));
+    for (size_t p = 0; p < (size_t)n * oh * ow; ++p)
+        for (int c = 0; c < cout; ++c) y[p * cout + c] = yb[p * ldy + c];
+    if (oh_out) *oh_out = oh;
+    if (ow_out) *ow_out = ow;
+    // release this call's temporaries
+    for (size_t i = nalloc; i < ctx->allocs.size(); ++i) hipFree(ctx->allocs[i]);
+    ctx->allocs.resize(nalloc);
+    return VD_OK;
+}
+
+}  // extern "C"

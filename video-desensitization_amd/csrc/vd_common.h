@@ -1,0 +1,98 @@
+// vd_common.h — internal types shared by the HIP kernels and the runtime.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+#include <stddef.h>
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+enum VdAct { VD_ACT_NONE = 0, VD_ACT_RELU = 1, VD_ACT_LEAKY = 2, VD_ACT_SILU = 3 };
+enum VdResMode { VD_RES_NONE = 0, VD_RES_PRE_ACT = 1, VD_RES_POST_ACT = 2 };
+
+// Implicit-GEMM convolution parameters (device side). Activations are NHWC with
+// an explicit channel stride (ld) and channel offset (coff) so a conv can read
+// a channel slice of a concat buffer and write into one (SSH concat,
+// layers.py:64; YOLO C2f/Concat).
+struct ConvArgs {
+    const void* x;  int xh, xw, ldx, xcoff;     // input  [B][xh][xw][ldx]
+    const void* w;                               // packed weights [Npad][Kpad]
+    const float* scale; const float* shift;      // BN eval as y = acc*scale + shift (len Npad)
+    const void* res; int res_ld, res_coff, res_up;  // residual NHWC; res_up: 1 = nearest 2x source
+    int rh, rw;                                  // residual spatial dims
+    void* y;  int yh, yw, ldy, ycoff;            // output [B][yh][yw][ldy]
+    int B, cin_pad, cout, kpad;                  // cin_pad: channels per tap in the K order
+    int kh, kw, stride, pad;
+    int M;                                       // B*yh*yw
+    int act; float slope; int res_mode; int out_f32;
+    int ntiles_n;                                // ceil(cout / BN)
+};
+
+// Device buffers for one frame batch's face post-processing.
+struct FacePostArgs {
+    const float* heads[3];   // per level NHWC [B][H][W][32] f32: 0..7 bbox, 8..11 cls, 12..31 landm
+    int lh[3], lw[3];        // level dims
+    int loff[3];             // first anchor index per level
+    const float* anchors;    // [A][4]
+    int A;                   // anchors per frame
+    int B;
+    float conf;
+    double iou;
+    uint64_t* cand_keys;     // [B][A] candidate keys
+    int* cand_count;         // [B]
+    float4* scratch_box;     // [B][A] global scratch for large candidate sets
+    float* scratch_area;     // [B][A]
+    uint64_t* scratch_keys;  // [B][2^ceil(log2 A)] global sort scratch
+    uint8_t* scratch_supp;   // [B][A]
+    int sort_cap;            // power of two >= A
+    int img_h, img_w;        // source frame size (all frames of a call share it)
+    int in_h, in_w;          // net input size
+    int cap;                 // output capacity per frame
+    int* out_count;          // [B]
+    int* out_xyxy;           // [B][cap][4]
+    float* out_xyxy_f;       // [B][cap][4]
+    float* out_score;        // [B][cap]
+    int* out_label;          // [B][cap]
+};
+
+enum { LB_COPY = 0, LB_AREA2 = 1, LB_LINEAR = 2 };
+
+struct LetterboxArgs {
+    const uint8_t* src; int n, ih, iw; size_t pitch;
+    int oh, ow;            // canvas size
+    int nh, nw;            // resized size
+    int top, left;         // paste offset
+    int mode;
+    double scale_x, scale_y;   // 1 / inv_scale (resize.cpp)
+    float pad_value;       // canvas fill (128 RetinaFace / 114 YOLO)
+    float mean[3];         // subtracted per output channel
+    float div;             // divisor after mean (1, or 255 for ultralytics' im /= 255)
+    int flip;              // 1: output channel c takes source channel 2-c
+    void* out; int cpad; int out_f32;
+};
+
+// ---- kernel launchers (one translation unit each) ----
+hipError_t vd_launch_conv(const ConvArgs& a, bool f32, hipStream_t s);
+hipError_t vd_launch_letterbox(const LetterboxArgs& a, hipStream_t s);
+hipError_t vd_launch_maxpool(bool f32, const void* x, int n, int xh, int xw, int ldx, int xcoff,
+                             void* y, int yh, int yw, int ldy, int ycoff, int c, int k, int st, int p,
+                             hipStream_t s);
+hipError_t vd_launch_upsample2x(bool f32, const void* x, int n, int xh, int xw, int ldx, int xcoff,
+                                void* y, int ldy, int ycoff, int c, hipStream_t s);
+hipError_t vd_launch_face_post(const FacePostArgs& p, hipStream_t s);
+hipError_t vd_launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w, size_t pitch,
+                            const int* cnt0, const int* xy0, int cap0,
+                            const int* cnt1, const int* xy1, int cap1, int level, hipStream_t s);
+
+#define VD_CHECK_HIP(expr)                                                     \
+    do {                                                                       \
+        hipError_t _e = (expr);                                                \
+        if (_e != hipSuccess) {                                                \
+            vd_set_error(VD_ERR_HIP, "%s:%d %s -> %s", __FILE__, __LINE__,      \
+                         #expr, hipGetErrorString(_e));                        \
+            return VD_ERR_HIP;                                                 \
+        }                                                                      \
+    } while (0)
+
+int vd_set_error(int code, const char* fmt, ...);

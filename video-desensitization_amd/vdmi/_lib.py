@@ -1,0 +1,155 @@
+"""ctypes binding of libvdmi.so (include/vdmi.h). No torch types cross this boundary.
+
+The library is built in-tree by ``video-desensitization_amd/build.py``; loading
+fails loudly when it is missing (there is no CPU fallback on the product path).
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("VDMI_LIB", os.path.join(HERE, "libvdmi.so"))
+
+VD_OK = 0
+VD_ERR_ARG, VD_ERR_HIP, VD_ERR_CAPACITY, VD_ERR_WEIGHTS, VD_ERR_STATE, VD_ERR_NOMEM = -1, -2, -3, -4, -5, -6
+VD_HOST, VD_DEVICE = 0, 1
+VD_PREC_BF16, VD_PREC_FP32 = 0, 1
+VD_NET_RETINAFACE, VD_NET_YOLOV8N = 0, 1
+VD_WEIGHTS_VDW1 = 1
+VD_MOSAIC_OUT_OF_PLACE = 0
+VD_PROC_FACES, VD_PROC_PLATES, VD_PROC_MOSAIC, VD_PROC_MOSAIC_PLATES = 1, 2, 4, 8
+FAM_CONV, FAM_MOSAIC, FAM_LETTERBOX, FAM_POST, FAM_OTHER = 0, 1, 2, 3, 4
+
+_ERRNAMES = {VD_ERR_ARG: "VD_ERR_ARG", VD_ERR_HIP: "VD_ERR_HIP", VD_ERR_CAPACITY: "VD_ERR_CAPACITY",
+             VD_ERR_WEIGHTS: "VD_ERR_WEIGHTS", VD_ERR_STATE: "VD_ERR_STATE", VD_ERR_NOMEM: "VD_ERR_NOMEM"}
+
+
+class VdError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"{_ERRNAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+class VdCapacityError(VdError):
+    pass
+
+
+class vd_cfg(ctypes.Structure):
+    _fields_ = [("input_h", ctypes.c_int32), ("input_w", ctypes.c_int32),
+                ("max_batch", ctypes.c_int32),
+                ("max_frame_h", ctypes.c_int32), ("max_frame_w", ctypes.c_int32),
+                ("precision", ctypes.c_int32), ("max_boxes", ctypes.c_int32),
+                ("confidence", ctypes.c_float), ("nms_iou", ctypes.c_double),
+                ("mosaic_level", ctypes.c_int32),
+                ("plate_imgsz", ctypes.c_int32), ("plate_nc", ctypes.c_int32),
+                ("plate_conf", ctypes.c_float), ("plate_iou", ctypes.c_double),
+                ("plate_max_det", ctypes.c_int32),
+                ("reserved", ctypes.c_int32 * 8)]
+
+
+class vd_boxes(ctypes.Structure):
+    _fields_ = [("cap", ctypes.c_int32), ("where", ctypes.c_int32),
+                ("count", ctypes.c_void_p), ("xyxy", ctypes.c_void_p),
+                ("xyxy_f", ctypes.c_void_p), ("score", ctypes.c_void_p),
+                ("label", ctypes.c_void_p)]
+
+
+# (name, restype, argtypes) for every symbol of include/vdmi.h
+_P, _I, _SZ, _F, _D = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_float, ctypes.c_double
+SIGNATURES = [
+    ("vd_default_cfg", _I, [ctypes.POINTER(vd_cfg)]),
+    ("vd_abi_version", _I, []),
+    ("vd_last_error", ctypes.c_char_p, []),
+    ("vd_create", _I, [ctypes.POINTER(vd_cfg), _I, ctypes.POINTER(_P)]),
+    ("vd_destroy", _I, [_P]),
+    ("vd_load_weights", _I, [_P, _I, _P, _SZ, _I]),
+    ("vd_set_stream", _I, [_P, _P]),
+    ("vd_get_stream", _P, [_P]),
+    ("vd_sync", _I, [_P]),
+    ("vd_detect", _I, [_P, _P, _I, _I, _I, _SZ, _I, ctypes.POINTER(vd_boxes)]),
+    ("vd_detect_plates", _I, [_P, _P, _I, _I, _I, _SZ, _I, ctypes.POINTER(vd_boxes)]),
+    ("vd_mosaic", _I, [_P, _P, _P, _I, _I, _I, _SZ, _I, ctypes.POINTER(vd_boxes), _I, _I]),
+    ("vd_process", _I, [_P, _P, _P, _I, _I, _I, _SZ, _I, _I, ctypes.POINTER(vd_boxes),
+                        ctypes.POINTER(vd_boxes)]),
+    ("vd_timing_enable", _I, [_P, _I]),
+    ("vd_timing_reset", _I, [_P]),
+    ("vd_timing_read", _I, [_P, _I, ctypes.POINTER(_D), ctypes.POINTER(ctypes.c_int64),
+                            ctypes.POINTER(_D)]),
+    ("vdt_letterbox", _I, [_P, _P, _I, _I, _I, _SZ, _I, _P, _I]),
+    ("vdt_forward_heads", _I, [_P, _P, _I, _I, _I, _SZ, _I, _P, _P, _P]),
+    ("vdt_postprocess", _I, [_P, _P, _P, _I, _P, ctypes.POINTER(vd_boxes)]),
+    ("vdt_conv2d", _I, [_P, _P, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _P, _P, _I, _F, _P, _I, _P,
+                        ctypes.POINTER(_I), ctypes.POINTER(_I)]),
+    ("vdt_plate_raw", _I, [_P, _P, _I, _I, _I, _SZ, _I, _P, ctypes.POINTER(_I)]),
+]
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load(path=None):
+    """Load libvdmi.so and bind every exported entry point. Raises OSError if absent."""
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise OSError(f"libvdmi.so not found at {p}; run `python video-desensitization_amd/build.py` "
+                          "(the HIP extension is required; there is no CPU fallback)")
+        lib = ctypes.CDLL(p)
+        for name, res, args in SIGNATURES:
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def last_error():
+    return (load().vd_last_error() or b"").decode(errors="replace")
+
+
+def check(rc):
+    if rc != VD_OK:
+        msg = last_error()
+        if rc == VD_ERR_CAPACITY:
+            raise VdCapacityError(rc, msg)
+        raise VdError(rc, msg)
+    return rc
+
+
+def ptr(a):
+    """Host address of a C-contiguous numpy array (or None)."""
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"], "array must be C-contiguous"
+    return a.ctypes.data
+
+
+def default_cfg():
+    c = vd_cfg()
+    check(load().vd_default_cfg(ctypes.byref(c)))
+    return c
+
+
+class HostBoxes:
+    """Caller-owned host box arrays (vd_boxes with where=VD_HOST)."""
+
+    def __init__(self, n, cap):
+        self.n, self.cap = n, cap
+        self.count = np.zeros(n, np.int32)
+        self.xyxy = np.zeros((n, cap, 4), np.int32)
+        self.xyxy_f = np.zeros((n, cap, 4), np.float32)
+        self.score = np.zeros((n, cap), np.float32)
+        self.label = np.zeros((n, cap), np.int32)
+
+    def struct(self):
+        return vd_boxes(self.cap, VD_HOST, ptr(self.count), ptr(self.xyxy), ptr(self.xyxy_f),
+                        ptr(self.score), ptr(self.label))
+
+    def frame(self, i):
+        k = min(int(self.count[i]), self.cap)
+        return self.xyxy[i, :k], self.xyxy_f[i, :k], self.score[i, :k], self.label[i, :k]

@@ -1,0 +1,232 @@
+"""Python handle over one libvdmi context (one GPU, one stream).
+
+Frames may be numpy uint8 [n,h,w,3] (host) or torch uint8 tensors on the
+context's GPU (device); torch is used only to hand over device pointers and
+streams (plumbing), never for compute.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, ptr
+
+
+def _is_torch(x):
+    return type(x).__module__.startswith("torch")
+
+
+def _frames_arg(frames):
+    """-> (pointer, n, h, w, pitch, where, keepalive)."""
+    if _is_torch(frames):
+        if frames.dtype.__str__() != "torch.uint8" or frames.dim() != 4 or frames.shape[3] != 3:
+            raise ValueError("frames must be uint8 [n,h,w,3]")
+        if not frames.is_contiguous():
+            frames = frames.contiguous()
+        n, h, w, _ = frames.shape
+        where = _lib.VD_DEVICE if frames.is_cuda else _lib.VD_HOST
+        return frames.data_ptr(), n, h, w, w * 3, where, frames
+    a = np.ascontiguousarray(frames, dtype=np.uint8)
+    if a.ndim == 3:
+        a = a[None]
+    if a.ndim != 4 or a.shape[3] != 3:
+        raise ValueError("frames must be uint8 [n,h,w,3]")
+    n, h, w, _ = a.shape
+    return a.ctypes.data, n, h, w, w * 3, _lib.VD_HOST, a
+
+
+class DeviceBoxes:
+    """vd_boxes backed by torch device tensors (kernels write them directly)."""
+
+    def __init__(self, n, cap, device):
+        import torch
+        self.n, self.cap = n, cap
+        self.count = torch.zeros(n, dtype=torch.int32, device=device)
+        self.xyxy = torch.zeros((n, cap, 4), dtype=torch.int32, device=device)
+        self.xyxy_f = torch.zeros((n, cap, 4), dtype=torch.float32, device=device)
+        self.score = torch.zeros((n, cap), dtype=torch.float32, device=device)
+        self.label = torch.zeros((n, cap), dtype=torch.int32, device=device)
+
+    def struct(self):
+        return _lib.vd_boxes(self.cap, _lib.VD_DEVICE, self.count.data_ptr(), self.xyxy.data_ptr(),
+                             self.xyxy_f.data_ptr(), self.score.data_ptr(), self.label.data_ptr())
+
+
+class Context:
+    """vd_create/vd_destroy with the reference-facing knobs as keyword args."""
+
+    def __init__(self, device=0, precision="bf16", max_batch=64, input_shape=(640, 640), confidence=0.5,
+                 nms_iou=0.4, max_boxes=256, mosaic_level=8, plate_nc=1, plate_conf=0.5, plate_iou=0.7,
+                 plate_max_det=300, plate_imgsz=640):
+        lib = _lib.load()
+        cfg = _lib.default_cfg()
+        cfg.input_h, cfg.input_w = int(input_shape[0]), int(input_shape[1])
+        cfg.max_batch = int(max_batch)
+        cfg.precision = _lib.VD_PREC_FP32 if precision in ("fp32", "f32", "float32") else _lib.VD_PREC_BF16
+        cfg.confidence = float(confidence)
+        cfg.nms_iou = float(nms_iou)
+        cfg.max_boxes = int(max_boxes)
+        cfg.mosaic_level = int(mosaic_level)
+        cfg.plate_nc, cfg.plate_conf, cfg.plate_iou = int(plate_nc), float(plate_conf), float(plate_iou)
+        cfg.plate_max_det, cfg.plate_imgsz = int(plate_max_det), int(plate_imgsz)
+        self.cfg = cfg
+        self.device = int(device)
+        self.precision = "fp32" if cfg.precision == _lib.VD_PREC_FP32 else "bf16"
+        h = ctypes.c_void_p()
+        check(lib.vd_create(ctypes.byref(cfg), self.device, ctypes.byref(h)))
+        self._h = h
+        self._lib = lib
+
+    # -- lifecycle -------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            self._lib.vd_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def load_weights(self, net, state_dict_or_blob):
+        from .weights import pack_vdw
+        blob = state_dict_or_blob if isinstance(state_dict_or_blob, (bytes, bytearray)) else pack_vdw(state_dict_or_blob)
+        buf = ctypes.create_string_buffer(bytes(blob), len(blob))
+        check(self._lib.vd_load_weights(self._h, net, buf, len(blob), _lib.VD_WEIGHTS_VDW1))
+
+    def set_stream(self, stream_ptr):
+        check(self._lib.vd_set_stream(self._h, stream_ptr))
+
+    def stream(self):
+        return self._lib.vd_get_stream(self._h)
+
+    def sync(self):
+        check(self._lib.vd_sync(self._h))
+
+    # -- hot path ----------------------------------------------------------
+    def _boxes(self, boxes, n):
+        if boxes is None:
+            boxes = _lib.HostBoxes(n, self.cfg.max_boxes)
+        return boxes
+
+    def detect(self, frames, boxes=None):
+        p, n, h, w, pitch, where, keep = _frames_arg(frames)
+        boxes = self._boxes(boxes, n)
+        s = boxes.struct()
+        check(self._lib.vd_detect(self._h, p, n, h, w, pitch, where, ctypes.byref(s)))
+        return boxes
+
+    def detect_plates(self, frames, boxes=None):
+        p, n, h, w, pitch, where, keep = _frames_arg(frames)
+        boxes = self._boxes(boxes, n)
+        s = boxes.struct()
+        check(self._lib.vd_detect_plates(self._h, p, n, h, w, pitch, where, ctypes.byref(s)))
+        return boxes
+
+    def mosaic(self, frames, boxes_xyxy, counts=None, level=None, out=None):
+        """Out-of-place mosaic. boxes_xyxy: int32 [n][cap][4] (host numpy) or a
+        HostBoxes/DeviceBoxes; counts: int32 [n] (host) when boxes_xyxy is an array."""
+        p, n, h, w, pitch, where, keep = _frames_arg(frames)
+        if isinstance(boxes_xyxy, (_lib.HostBoxes, DeviceBoxes)):
+            s = boxes_xyxy.struct()
+        else:
+            xy = np.ascontiguousarray(boxes_xyxy, np.int32).reshape(n, -1, 4)
+            cnt = np.ascontiguousarray(counts if counts is not None else np.full(n, xy.shape[1]), np.int32)
+            cap = max(1, xy.shape[1])
+            if xy.shape[1] == 0:
+                xy = np.zeros((n, 1, 4), np.int32)
+            keep = (keep, xy, cnt)
+            s = _lib.vd_boxes(cap, _lib.VD_HOST, ptr(cnt), ptr(xy), None, None, None)
+        if out is None:
+            if where == _lib.VD_HOST:
+                out = np.empty((n, h, w, 3), np.uint8)
+            else:
+                import torch
+                out = torch.empty_like(frames)
+        optr = out.data_ptr() if _is_torch(out) else ptr(out)
+        check(self._lib.vd_mosaic(self._h, p, optr, n, h, w, pitch, where, ctypes.byref(s),
+                                  int(level or self.cfg.mosaic_level), _lib.VD_MOSAIC_OUT_OF_PLACE))
+        return out
+
+    def process(self, frames, out=None, faces=None, plates=None, flags=None):
+        p, n, h, w, pitch, where, keep = _frames_arg(frames)
+        if flags is None:
+            flags = _lib.VD_PROC_FACES | _lib.VD_PROC_MOSAIC
+        if out is None and flags & _lib.VD_PROC_MOSAIC:
+            if where == _lib.VD_HOST:
+                out = np.empty((n, h, w, 3), np.uint8)
+            else:
+                import torch
+                out = torch.empty_like(frames)
+        fs = ps = None
+        if flags & _lib.VD_PROC_FACES:
+            faces = self._boxes(faces, n)
+            fs = faces.struct()
+        if flags & _lib.VD_PROC_PLATES:
+            plates = self._boxes(plates, n)
+            ps = plates.struct()
+        optr = None if out is None else (out.data_ptr() if _is_torch(out) else ptr(out))
+        check(self._lib.vd_process(self._h, p, optr, n, h, w, pitch, where, flags,
+                                   ctypes.byref(fs) if fs is not None else None,
+                                   ctypes.byref(ps) if ps is not None else None))
+        return out, faces, plates
+
+    # -- instrumentation ------------------------------------------------------
+    def timing(self, on=True):
+        check(self._lib.vd_timing_enable(self._h, 1 if on else 0))
+
+    def timing_reset(self):
+        check(self._lib.vd_timing_reset(self._h))
+
+    def timing_read(self, fam):
+        ms, n, work = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
+        check(self._lib.vd_timing_read(self._h, fam, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(work)))
+        return ms.value, n.value, work.value
+
+    # -- test hooks --------------------------------------------------------------
+    def letterbox(self, frames, cpad=4):
+        p, n, h, w, pitch, where, keep = _frames_arg(frames)
+        out = np.zeros((n, self.cfg.input_h, self.cfg.input_w, cpad), np.float32)
+        check(self._lib.vdt_letterbox(self._h, p, n, h, w, pitch, where, ptr(out), cpad))
+        return out
+
+    def forward_heads(self, frames):
+        p, n, h, w, pitch, where, keep = _frames_arg(frames)
+        A = sum((self.cfg.input_h // s) * (self.cfg.input_w // s) * 2 for s in (8, 16, 32))
+        loc = np.zeros((n, A, 4), np.float32)
+        conf = np.zeros((n, A, 2), np.float32)
+        landm = np.zeros((n, A, 10), np.float32)
+        check(self._lib.vdt_forward_heads(self._h, p, n, h, w, pitch, where, ptr(loc), ptr(conf), ptr(landm)))
+        return loc, conf, landm
+
+    def postprocess(self, loc, conf, img_hw, cap=None):
+        loc = np.ascontiguousarray(loc, np.float32)
+        conf = np.ascontiguousarray(conf, np.float32)
+        n = loc.shape[0]
+        hw = np.ascontiguousarray(np.broadcast_to(np.asarray(img_hw, np.int32), (n, 2)))
+        boxes = _lib.HostBoxes(n, cap or self.cfg.max_boxes)
+        s = boxes.struct()
+        check(self._lib.vdt_postprocess(self._h, ptr(loc), ptr(conf), n, ptr(hw), ctypes.byref(s)))
+        return boxes
+
+    def conv2d(self, x, w, stride=1, pad=0, scale=None, shift=None, act=0, slope=0.0, res=None, res_mode=0):
+        """x: f32 NHWC [n,h,w,cin]; w: f32 [cout,cin,kh,kw] -> f32 NHWC."""
+        x = np.ascontiguousarray(x, np.float32)
+        w = np.ascontiguousarray(w, np.float32)
+        n, h, wd, cin = x.shape
+        cout, _, kh, kw = w.shape
+        scale = np.ascontiguousarray(np.ones(cout, np.float32) if scale is None else scale, np.float32)
+        shift = np.ascontiguousarray(np.zeros(cout, np.float32) if shift is None else shift, np.float32)
+        oh, ow = (h + 2 * pad - kh) // stride + 1, (wd + 2 * pad - kw) // stride + 1
+        y = np.zeros((n, oh, ow, cout), np.float32)
+        r = None if res is None else np.ascontiguousarray(res, np.float32)
+        o1, o2 = ctypes.c_int(), ctypes.c_int()
+        check(self._lib.vdt_conv2d(self._h, ptr(x), n, h, wd, cin, ptr(w), cout, kh, kw, stride, pad, ptr(scale),
+                                   ptr(shift), act, float(slope), ptr(r), res_mode, ptr(y), ctypes.byref(o1),
+                                   ctypes.byref(o2)))
+        return y

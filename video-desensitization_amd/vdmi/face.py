@@ -1,0 +1,107 @@
+"""Drop-in ``Retinaface`` (detect_face/face.py:14-150) backed by libvdmi.
+
+Same constructor keywords and defaults (face.py:15-23), same ``.device``
+attribute (read at combine_detect.py:866), same ``detect_images`` contract
+(face.py:120-150): a list of uint8 HxWx3 RGB arrays in, a list of
+``(image, [[x1, y1, x2, y2], ...])`` out, boxes as Python floats in source
+pixels, in NMS (descending score) order. Everything between — letterbox,
+ResNet-50/FPN/SSH forward, decode, NMS, correction — runs in HIP kernels.
+
+Differences, all deliberate:
+* ``cuda=False`` raises: the product path has no CPU fallback (the reference's
+  own CPU path crashes in retinaface_correct_boxes' ``.cuda()``, utils_bbox.py:118).
+* ``model_path`` missing on disk -> seeded random weights (reference keys), with a
+  warning, since the real checkpoint is not distributable here.
+* The returned image is the caller's array itself, not a copy (face.py:129 copies;
+  the driver never reads it, combine_detect.py:237).
+* Extra keywords: ``precision`` ("bf16" default, "fp32" parity mode),
+  ``max_batch``, ``device_index``, ``seed``, ``weights`` (a state_dict).
+"""
+import os
+import warnings
+
+import numpy as np
+
+from . import _lib
+from .context import Context
+from .weights import load_reference_checkpoint, retinaface_state_dict
+
+
+class Retinaface(object):
+    _defaults = {
+        "model_path": "model_data/Retinaface_resnet50.pth",
+        "backbone": "resnet50",
+        "confidence": 0.5,
+        "nms_iou": 0.45,
+        "input_shape": [1280, 1280, 3],
+        "letterbox_image": True,
+        "cuda": True,
+        # vdmi extras
+        "precision": "bf16",
+        "max_batch": 64,
+        "device_index": 0,
+        "seed": 0,
+        "weights": None,
+        "max_boxes": 256,
+    }
+
+    @classmethod
+    def get_defaults(cls, n):
+        return cls._defaults.get(n, f"Unrecognized attribute name '{n}'")
+
+    def __init__(self, **kwargs):
+        self.__dict__.update(self._defaults)
+        for name, value in kwargs.items():
+            setattr(self, name, value)
+        if self.backbone != "resnet50":
+            raise ValueError("only backbone='resnet50' (cfg_re50) is on the MI355X path "
+                             "(combine_detect.py:859 fixes it)")
+        if not self.letterbox_image:
+            raise ValueError("Batch inference requires letterbox_image=True for shape alignment.")  # face.py:80
+        if not self.cuda:
+            raise RuntimeError("vdmi.Retinaface runs on the GPU only (no CPU fallback)")
+        try:
+            import torch
+            self.device = torch.device(f"cuda:{self.device_index}")
+        except Exception:  # torch is optional plumbing
+            self.device = f"cuda:{self.device_index}"
+        self.ctx = Context(device=self.device_index, precision=self.precision, max_batch=self.max_batch,
+                           input_shape=self.input_shape[:2], confidence=self.confidence, nms_iou=self.nms_iou,
+                           max_boxes=self.max_boxes)
+        self.generate()
+
+    def generate(self):
+        """face.py:50-60: load weights once (device-resident; no DataParallel replicate)."""
+        if self.weights is not None:
+            sd = self.weights
+        elif self.model_path and os.path.exists(self.model_path):
+            sd = load_reference_checkpoint(self.model_path)
+        else:
+            warnings.warn(f"{self.model_path} not found: using seeded random RetinaFace weights (seed={self.seed})")
+            sd = retinaface_state_dict(self.seed)
+        self.ctx.load_weights(_lib.VD_NET_RETINAFACE, sd)
+
+    def detect_boxes(self, images):
+        """Per image: (float32 boxes [M,4], int boxes [M,4], scores [M]) in NMS order."""
+        if not isinstance(images, list):
+            images = [images]
+        out = [None] * len(images)
+        groups = {}
+        for i, img in enumerate(images):
+            groups.setdefault(img.shape[:2], []).append(i)
+        for (h, w), idx in groups.items():
+            for s in range(0, len(idx), self.max_batch):
+                chunk = idx[s:s + self.max_batch]
+                batch = np.stack([images[i] for i in chunk]) if len(chunk) > 1 else images[chunk[0]][None]
+                boxes = self.ctx.detect(np.ascontiguousarray(batch, np.uint8))
+                for j, i in enumerate(chunk):
+                    xi, xf, sc, _ = boxes.frame(j)
+                    out[i] = (xf.copy(), xi.copy(), sc.copy())
+        return out
+
+    def detect_images(self, images):
+        """face.py:120-150."""
+        if not isinstance(images, list):
+            images = [images]
+        res = self.detect_boxes(images)
+        return [(img, r[0].tolist()) for img, r in zip(images, res)]
