@@ -48,7 +48,8 @@ def cpu_baseline(frames, sd, seconds):
     import torch
     from oracle import anchors, bbox, letterbox, mosaic
     from oracle.retinaface import build_oracle_model
-    cores = len(os.sched_getaffinity(0))
+    # the GPU box shares its host: use the per-GPU CPU share (OMP_NUM_THREADS, 16 there)
+    cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
     torch.set_num_threads(cores)
     m = build_oracle_model(sd)
     pri = anchors.get_anchors((640, 640))

@@ -183,6 +183,7 @@ def test_postprocess_ties_and_capacity(gpu, face_ctx_factory):
     A = 16800
     loc = np.zeros((1, A, 4), F32)
     conf = np.zeros((1, A, 2), F32)
+    conf[0, :, 0] = 1.0             # background everywhere except the strided anchors
     conf[0, ::7, 1] = 2.0           # many exactly-equal scores: stable order decides
     conf[0, ::11, 1] = 3.0
     got = ctx.postprocess(loc, conf, (1080, 1920), cap=8192)

@@ -1,0 +1,58 @@
+"""Per-layer view of a rocprofv3 kernel trace of bench.py: maps the conv launches
+of the last step onto the RetinaFace plan (same order as face_net.cpp) and
+prints duration and achieved TFLOP/s per layer.
+
+    python tools/conv_layers.py gpurun_out/prof/run_kernel_trace.csv [batch]
+"""
+import csv
+import sys
+
+
+def face_plan(B=64, H=640, W=640):
+    """(name, M, N, K) of every conv in face_net.cpp order."""
+    L = []
+    h, w = H // 2, W // 2
+    L.append(("stem7x7", B * h * w, 64, 3 * 49))
+    h, w = h // 2, w // 2
+    cin = 64
+    for li, (planes, blocks, stride) in enumerate([(64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2)]):
+        for bi in range(blocks):
+            s = stride if bi == 0 else 1
+            L.append((f"l{li+1}.{bi}.c1", B * h * w, planes, cin))
+            oh, ow = h // s, w // s
+            L.append((f"l{li+1}.{bi}.c2", B * oh * ow, planes, planes * 9))
+            if bi == 0:
+                L.append((f"l{li+1}.{bi}.ds", B * oh * ow, planes * 4, cin))
+            L.append((f"l{li+1}.{bi}.c3", B * oh * ow, planes * 4, planes))
+            cin = planes * 4
+            h, w = oh, ow
+    s = [(H // 8, 512), (H // 16, 1024), (H // 32, 2048)]
+    L.append(("fpn.o3", B * s[2][0] ** 2, 256, 2048))
+    L.append(("fpn.o2", B * s[1][0] ** 2, 256, 1024))
+    L.append(("fpn.m2", B * s[1][0] ** 2, 256, 256 * 9))
+    L.append(("fpn.o1", B * s[0][0] ** 2, 256, 512))
+    L.append(("fpn.m1", B * s[0][0] ** 2, 256, 256 * 9))
+    for l, hh in enumerate((H // 8, H // 16, H // 32)):
+        m = B * hh * hh
+        L += [(f"ssh{l}.c3", m, 128, 2304), (f"ssh{l}.c51", m, 64, 2304), (f"ssh{l}.c52", m, 64, 576),
+              (f"ssh{l}.c72", m, 64, 576), (f"ssh{l}.c73", m, 64, 576), (f"head{l}", m, 32, 256)]
+    return L
+
+
+def main(path, B=64):
+    rows = [r for r in csv.DictReader(open(path)) if "conv_igemm" in r["Kernel_Name"]]
+    plan = face_plan(B)
+    last = rows[-len(plan):]
+    tot_t = tot_f = 0
+    for (name, M, N, K), r in zip(plan, last):
+        dt = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+        fl = 2.0 * M * N * K
+        tot_t += dt
+        tot_f += fl
+        kn = r["Kernel_Name"].split("conv_igemm_kernel")[1][:22]
+        print(f"{name:12s} M={M:8d} N={N:5d} K={K:5d} {dt*1e6:8.1f} us {fl/dt/1e12:7.1f} TF/s  {kn}")
+    print(f"total {tot_t*1e3:.2f} ms  {tot_f/tot_t/1e12:.1f} TF/s")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 64)

@@ -29,6 +29,8 @@
 
 namespace {
 
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));   // native vector (HIP's uint4 is a struct)
+
 template <typename T> struct Elem;
 template <> struct Elem<__bf16> { static constexpr int VEC = 8; };
 template <> struct Elem<float>  { static constexpr int VEC = 4; };
@@ -62,8 +64,10 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
     constexpr int KSTEP = std::is_same<T, float>::value ? 16 : 32;  // K per fragment step
     constexpr int NKS = BKE / KSTEP;                                 // = 2
     constexpr int BUF = (BM + BN) * 128;
+    constexpr int EPI = BM * (BN + 4) * 4;
+    constexpr int SMEM = (2 * BUF > EPI) ? 2 * BUF : EPI;
 
-    __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+    __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid / WAVES_N, wn = wid % WAVES_N;
@@ -95,48 +99,52 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
     }
     const T* wbase = (const T*)a.w + (size_t)(n0 + rbase) * a.kpad + chunk * VEC;
 
-    uint4 ra[A_IT], rb[B_IT];
+    u32x4 ra[A_IT], rb[B_IT];
     const int nk = a.kpad / BKE;
     const int cvec = a.cin_pad / VEC, ntap = a.kh * a.kw;
 
     // DENSE: whole tile inside one tap; track (kh, kw, c) incrementally.
     int t_kh = 0, t_kw = 0, t_c = 0;
+    const T* xsafe = (const T*)a.x;
 
-    auto load_tile = [&](int kt) {
-        int dy, dx, c;
-        bool kval = true;
-        if constexpr (DENSE) {
-            dy = t_kh; dx = t_kw; c = t_c + chunk * VEC;
-        } else {
-            int kv = kt * 8 + chunk;
-            int tap = kv / cvec;
-            c = (kv - tap * cvec) * VEC;
-            kval = tap < ntap;
-            dy = tap / a.kw; dx = tap - dy * a.kw;
-        }
-#pragma unroll
-        for (int i = 0; i < A_IT; ++i) {
-            int iy = iy0[i] + dy, ix = ix0[i] + dx;
-            bool ok = kval && (unsigned)iy < (unsigned)a.xh && (unsigned)ix < (unsigned)a.xw;
-            if (ok) ra[i] = *(const uint4*)(xrow[i] + ((size_t)iy * a.xw + ix) * a.ldx + c);
-            else ra[i] = make_uint4(0, 0, 0, 0);
-        }
-#pragma unroll
-        for (int i = 0; i < B_IT; ++i)
-            rb[i] = *(const uint4*)(wbase + (size_t)(32 * i) * a.kpad + (size_t)kt * BKE);
-        if constexpr (DENSE) {
-            t_c += BKE;
-            if (t_c >= a.cin_pad) { t_c = 0; if (++t_kw == a.kw) { t_kw = 0; ++t_kh; } }
-        }
-    };
-    auto store_tile = [&](int buf) {
-        char* As = smem + buf * BUF;
-        char* Bs = As + BM * 128;
-#pragma unroll
-        for (int i = 0; i < A_IT; ++i) *(uint4*)(As + lds_off(rbase + 32 * i, chunk)) = ra[i];
-#pragma unroll
-        for (int i = 0; i < B_IT; ++i) *(uint4*)(Bs + lds_off(rbase + 32 * i, chunk)) = rb[i];
-    };
+    // Global -> registers for K tile kt (padding taps read a valid address and
+    // are zeroed by a select, so the loads stay branch-free and in registers).
+#define VD_LOAD_TILE(kt)                                                                   \
+    do {                                                                                  \
+        int dy, dx, c;                                                                    \
+        bool kval = true;                                                                 \
+        if constexpr (DENSE) {                                                            \
+            dy = t_kh; dx = t_kw; c = t_c + chunk * VEC;                                  \
+        } else {                                                                          \
+            const int kv = (kt) * 8 + chunk;                                              \
+            const int tap = kv / cvec;                                                    \
+            c = (kv - tap * cvec) * VEC;                                                  \
+            kval = tap < ntap;                                                            \
+            dy = tap / a.kw; dx = tap - dy * a.kw;                                        \
+        }                                                                                 \
+        _Pragma("unroll") for (int i = 0; i < A_IT; ++i) {                                \
+            const int iy = iy0[i] + dy, ix = ix0[i] + dx;                                 \
+            const bool ok = kval && (unsigned)iy < (unsigned)a.xh && (unsigned)ix < (unsigned)a.xw; \
+            const T* src = ok ? xrow[i] + ((size_t)iy * a.xw + ix) * a.ldx + c : xsafe;  \
+            const u32x4 v = *(const u32x4*)src;                                           \
+            ra[i] = ok ? v : u32x4{0u, 0u, 0u, 0u};                                       \
+        }                                                                                 \
+        _Pragma("unroll") for (int i = 0; i < B_IT; ++i)                                  \
+            rb[i] = *(const u32x4*)(wbase + (size_t)(32 * i) * a.kpad + (size_t)(kt) * BKE); \
+        if constexpr (DENSE) {                                                            \
+            t_c += BKE;                                                                   \
+            if (t_c >= a.cin_pad) { t_c = 0; if (++t_kw == a.kw) { t_kw = 0; ++t_kh; } } \
+        }                                                                                 \
+    } while (0)
+#define VD_STORE_TILE(buf)                                                                 \
+    do {                                                                                  \
+        char* As_ = smem + (buf) * BUF;                                                   \
+        char* Bs_ = As_ + BM * 128;                                                       \
+        _Pragma("unroll") for (int i = 0; i < A_IT; ++i)                                  \
+            *(u32x4*)(As_ + lds_off(rbase + 32 * i, chunk)) = ra[i];                      \
+        _Pragma("unroll") for (int i = 0; i < B_IT; ++i)                                  \
+            *(u32x4*)(Bs_ + lds_off(rbase + 32 * i, chunk)) = rb[i];                      \
+    } while (0)
 
     f32x4_t acc[TM][TN];
 #pragma unroll
@@ -144,25 +152,25 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-    load_tile(0);
-    store_tile(0);
+    VD_LOAD_TILE(0);
+    VD_STORE_TILE(0);
     __syncthreads();
 
     for (int kt = 0; kt < nk; ++kt) {
         const int cur = kt & 1;
-        if (kt + 1 < nk) load_tile(kt + 1);
+        if (kt + 1 < nk) VD_LOAD_TILE(kt + 1);
         const char* As = smem + cur * BUF;
         const char* Bs = As + BM * 128;
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) {
             const int ch = ks * 4 + (lane >> 4);
-            uint4 af[TM], bfr[TN];
+            u32x4 af[TM], bfr[TN];
 #pragma unroll
             for (int i = 0; i < TM; ++i)
-                af[i] = *(const uint4*)(As + lds_off(wm * WTM + i * 16 + (lane & 15), ch));
+                af[i] = *(const u32x4*)(As + lds_off(wm * WTM + i * 16 + (lane & 15), ch));
 #pragma unroll
             for (int j = 0; j < TN; ++j)
-                bfr[j] = *(const uint4*)(Bs + lds_off(wn * WTN + j * 16 + (lane & 15), ch));
+                bfr[j] = *(const u32x4*)(Bs + lds_off(wn * WTN + j * 16 + (lane & 15), ch));
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -180,45 +188,100 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
                     }
                 }
         }
-        if (kt + 1 < nk) store_tile(cur ^ 1);
+        if (kt + 1 < nk) VD_STORE_TILE(cur ^ 1);
         __syncthreads();
     }
 
     // ---- fused epilogue ----
+    // Stage the f32 accumulator tile through LDS ([BM][BN+4], conflict-free
+    // 16x16 fragment writes), then each thread owns 8 consecutive channels of a
+    // row: 16-B residual loads and 16-B (bf16) / 32-B (f32) stores, coalesced
+    // along the NHWC channel dimension.
+    float* ep = (float*)smem;
+    constexpr int EPLD = BN + 4;
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        const int n = n0 + wn * WTN + j * 16 + (lane & 15);
-        if (n >= a.cout) continue;
-        const float sc = a.scale[n], sh = a.shift[n];
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int i = 0; i < TM; ++i) {
+        for (int j = 0; j < TN; ++j)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int m = m0 + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
-                if (m >= a.M) continue;
-                float v = acc[i][j][r] * sc + sh;
-                float rv = 0.f;
-                if (a.res_mode != VD_RES_NONE) {
-                    size_t roff;
-                    if (a.res_up) {
-                        int b = m / ohw, rem = m - b * ohw;
-                        int oy = rem / a.yw, ox = rem - oy * a.yw;
-                        roff = ((size_t)(b * a.rh + (oy >> 1)) * a.rw + (ox >> 1)) * a.res_ld;
-                    } else {
-                        roff = (size_t)m * a.res_ld;
-                    }
-                    rv = load_elem<T>(a.res, roff + a.res_coff + n);
+            for (int r = 0; r < 4; ++r)
+                ep[(wm * WTM + i * 16 + (lane >> 4) * 4 + r) * EPLD + wn * WTN + j * 16 + (lane & 15)] = acc[i][j][r];
+    __syncthreads();
+    const bool vec_ok = ((a.cout & 7) == 0) && ((a.ldy & 7) == 0) && ((a.ycoff & 7) == 0) &&
+                        (a.res_mode == VD_RES_NONE || (((a.res_ld | a.res_coff) & 7) == 0));
+    constexpr int CG = BN / 8;                     // 8-channel groups per row
+    for (int it = tid; it < BM * CG; it += 256) {
+        const int rr = it / CG, cg = it - rr * CG;
+        const int m = m0 + rr;
+        const int nb = n0 + cg * 8;
+        if (m >= a.M || nb >= a.cout) continue;
+        size_t roff = 0;
+        if (a.res_mode != VD_RES_NONE) {
+            if (a.res_up) {
+                const int b = m / ohw, rem = m - b * ohw;
+                const int oy = rem / a.yw, ox = rem - oy * a.yw;
+                roff = ((size_t)(b * a.rh + (oy >> 1)) * a.rw + (ox >> 1)) * a.res_ld + a.res_coff;
+            } else {
+                roff = (size_t)m * a.res_ld + a.res_coff;
+            }
+        }
+        const float* er = ep + rr * EPLD + cg * 8;
+        const size_t yo = (size_t)m * a.ldy + a.ycoff + nb;
+        if (vec_ok) {
+            float v[8], rv[8];
+            const float4 s0 = *(const float4*)(a.scale + nb), s1 = *(const float4*)(a.scale + nb + 4);
+            const float4 h0 = *(const float4*)(a.shift + nb), h1 = *(const float4*)(a.shift + nb + 4);
+            const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+            const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+            const float4 e0 = *(const float4*)er, e1 = *(const float4*)(er + 4);
+            const float ev[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+            if (a.res_mode != VD_RES_NONE) {
+                if constexpr (std::is_same<T, float>::value) {
+                    const float4 r0 = *(const float4*)((const float*)a.res + roff + nb);
+                    const float4 r1 = *(const float4*)((const float*)a.res + roff + nb + 4);
+                    rv[0] = r0.x; rv[1] = r0.y; rv[2] = r0.z; rv[3] = r0.w;
+                    rv[4] = r1.x; rv[5] = r1.y; rv[6] = r1.z; rv[7] = r1.w;
+                } else {
+                    const u32x4 u = *(const u32x4*)((const __bf16*)a.res + roff + nb);
+                    const __bf16* rb = (const __bf16*)&u;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) rv[e] = (float)rb[e];
                 }
-                if (a.res_mode == VD_RES_PRE_ACT) v += rv;
-                v = act_apply(v, a.act, a.slope);
-                if (a.res_mode == VD_RES_POST_ACT) v += rv;
-                const size_t yo = (size_t)m * a.ldy + a.ycoff + n;
-                if (a.out_f32 || std::is_same<T, float>::value) ((float*)a.y)[yo] = v;
-                else ((__bf16*)a.y)[yo] = (__bf16)v;
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                float t = ev[e] * sc[e] + sh[e];
+                if (a.res_mode == VD_RES_PRE_ACT) t += rv[e];
+                t = act_apply(t, a.act, a.slope);
+                if (a.res_mode == VD_RES_POST_ACT) t += rv[e];
+                v[e] = t;
+            }
+            if (a.out_f32 || std::is_same<T, float>::value) {
+                *(float4*)((float*)a.y + yo) = make_float4(v[0], v[1], v[2], v[3]);
+                *(float4*)((float*)a.y + yo + 4) = make_float4(v[4], v[5], v[6], v[7]);
+            } else {
+                bf16x8_t o;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) o[e] = (__bf16)v[e];
+                *(bf16x8_t*)((__bf16*)a.y + yo) = o;
+            }
+        } else {
+            for (int e = 0; e < 8 && nb + e < a.cout; ++e) {
+                const int n = nb + e;
+                float t = er[e] * a.scale[n] + a.shift[n];
+                const float rv = a.res_mode != VD_RES_NONE ? load_elem<T>(a.res, roff + n) : 0.f;
+                if (a.res_mode == VD_RES_PRE_ACT) t += rv;
+                t = act_apply(t, a.act, a.slope);
+                if (a.res_mode == VD_RES_POST_ACT) t += rv;
+                if (a.out_f32 || std::is_same<T, float>::value) ((float*)a.y)[yo + e] = t;
+                else ((__bf16*)a.y)[yo + e] = (__bf16)t;
             }
         }
     }
 }
+
+#undef VD_LOAD_TILE
+#undef VD_STORE_TILE
 
 template <typename T, int BM, int BN>
 hipError_t launch_bn(const ConvArgs& a0, bool dense, hipStream_t s) {

@@ -168,16 +168,24 @@ int vd_build_face(Ctx& c, const WMap& W) {
     F.A = A;
     if ((rc = c.dalloc((void**)&F.anchors, anc.size() * 4))) return rc;
     VD_CHECK_HIP(hipMemcpy(F.anchors, anc.data(), anc.size() * 4, hipMemcpyHostToDevice));
+    if ((rc = vd_alloc_post(c, F.post, A))) return rc;
+    F.loaded = true;
+    return VD_OK;
+}
+
+int vd_alloc_post(Ctx& c, PostScratch& ps, int A) {
     const size_t B = c.cfg.max_batch;
     int P = 1;
     while (P < A) P <<= 1;
-    F.sort_cap = P;
-    if ((rc = c.dalloc((void**)&F.cand_keys, B * A * 8))) return rc;
-    if ((rc = c.dalloc((void**)&F.cand_count, B * 4))) return rc;
-    if ((rc = c.dalloc((void**)&F.scratch_box, B * A * 16))) return rc;
-    if ((rc = c.dalloc((void**)&F.scratch_area, B * A * 4))) return rc;
-    if ((rc = c.dalloc((void**)&F.scratch_keys, B * (size_t)P * 8))) return rc;
-    if ((rc = c.dalloc((void**)&F.scratch_supp, B * A))) return rc;
-    F.loaded = true;
+    ps.sort_cap = P;
+    int rc;
+    if ((rc = c.dalloc((void**)&ps.keys, B * A * 8))) return rc;
+    if ((rc = c.dalloc((void**)&ps.count, B * 4))) return rc;
+    if ((rc = c.dalloc((void**)&ps.box, B * A * 16))) return rc;
+    if ((rc = c.dalloc((void**)&ps.cls, B * A * 4))) return rc;
+    if ((rc = c.dalloc((void**)&ps.nbox, B * A * 16))) return rc;
+    if ((rc = c.dalloc((void**)&ps.area, B * A * 4))) return rc;
+    if ((rc = c.dalloc((void**)&ps.sort, B * (size_t)P * 8))) return rc;
+    if ((rc = c.dalloc((void**)&ps.supp, B * A))) return rc;
     return VD_OK;
 }

@@ -8,21 +8,27 @@
 // contains p, then out(p) = in(p'). map_k = down(up(.)) per axis with OpenCV's
 // double-precision nearest index rule. This is a pure gather -> |delta| = 0.
 //
-// One workgroup per (frame, band of ROWS rows). The band's box list (boxes that
-// intersect the band, original order) is built in LDS; a 16-byte output chunk
-// that no band box touches is a vectorised copy, the rest walk per pixel. A
-// walk that leaves the band (points only move up/left) continues on the full
-// global list from where it left off, so the band list is an exact filter.
-// HBM traffic = read + write of each frame (2*W*H*3 bytes) + box-covered gathers.
+// Two kernels per call:
+//  mosaic_prep_kernel  one thread per box: clip to the frame and precompute the
+//                      four resizeNN factors into a per-frame table (boxes in
+//                      call order: faces first, then plates, combine_detect.py:242-244).
+//  mosaic_kernel       one workgroup per (frame, band of ROWS rows). The band's
+//                      box list (table entries intersecting the band, original
+//                      order) is staged in LDS; a 16-byte output chunk that no band
+//                      box touches is a vectorised copy, the rest walk per pixel.
+//                      A walk that leaves the band (points only move up/left)
+//                      continues on the frame's full table from where it left
+//                      off, so the band list is an exact filter.
+// HBM traffic = read + write of every frame (2*W*H*3 bytes) + ROI gathers (L2 hits).
 #include "vd_common.h"
 #include "vd_math.h"
 
 namespace {
 
 constexpr int ROWS = 8;
-constexpr int TB_CAP = 256;    // band-list capacity; larger bands fall back to the global walk
+constexpr int TB_CAP = 512;    // band-list capacity; larger bands walk the global table
 
-struct MBox { int x1, y1, x2, y2; int sw, sh, idx, pad; double fux, fdx, fuy, fdy; };
+struct MBox { int x1, y1, x2, y2; int sw, sh, idx, valid; double fux, fdx, fuy, fdy; };
 
 struct MosaicArgs {
     const uint8_t* in; uint8_t* out; int n, h, w; size_t pitch;
@@ -30,24 +36,34 @@ struct MosaicArgs {
     const int* cnt1; const int* xy1; int cap1;      // list 1 (plates, optional)
     int level;
     int vec_ok;                                      // 16-B aligned rows -> vector copies
+    MBox* table; int tcap;                           // [n][tcap] prepared boxes
 };
 
-__device__ __forceinline__ bool load_box(const MosaicArgs& a, int f, int k, int n0, MBox& m) {
+__global__ __launch_bounds__(256) void mosaic_prep_kernel(MosaicArgs a) {
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    const int f = blockIdx.y;
+    if (k >= a.tcap) return;
+    const int n0 = a.cnt0 ? min(a.cnt0[f], a.cap0) : 0;
+    const int n1 = a.cnt1 ? min(a.cnt1[f], a.cap1) : 0;
+    if (k >= n0 + n1) return;
     const int* src = k < n0 ? a.xy0 + ((size_t)f * a.cap0 + k) * 4 : a.xy1 + ((size_t)f * a.cap1 + (k - n0)) * 4;
-    int x1 = max(0, src[0]), y1 = max(0, src[1]);
-    int x2 = min(a.w, src[2]), y2 = min(a.h, src[3]);
-    if (x2 <= x1 || y2 <= y1) return false;
-    const int bw = x2 - x1, bh = y2 - y1;
-    m.x1 = x1; m.y1 = y1; m.x2 = x2; m.y2 = y2;
-    m.sw = max(1, bw / a.level);
-    m.sh = max(1, bh / a.level);
+    MBox m{};
+    // combine_detect.py:145-148 clip, :150-151 empty check
+    m.x1 = max(0, src[0]); m.y1 = max(0, src[1]);
+    m.x2 = min(a.w, src[2]); m.y2 = min(a.h, src[3]);
     m.idx = k;
-    // resizeNN: ifx = 1. / ((double)dst / src)
-    m.fux = __ddiv_rn(1.0, __ddiv_rn((double)bw, (double)m.sw));   // up:   dst=bw, src=sw
-    m.fdx = __ddiv_rn(1.0, __ddiv_rn((double)m.sw, (double)bw));   // down: dst=sw, src=bw
-    m.fuy = __ddiv_rn(1.0, __ddiv_rn((double)bh, (double)m.sh));
-    m.fdy = __ddiv_rn(1.0, __ddiv_rn((double)m.sh, (double)bh));
-    return true;
+    m.valid = (m.x2 > m.x1 && m.y2 > m.y1) ? 1 : 0;
+    if (m.valid) {
+        const int bw = m.x2 - m.x1, bh = m.y2 - m.y1;
+        m.sw = max(1, bw / a.level);              // :153-154
+        m.sh = max(1, bh / a.level);
+        // resizeNN [ext]: ifx = 1. / ((double)dst / src)
+        m.fux = __ddiv_rn(1.0, __ddiv_rn((double)bw, (double)m.sw));   // up:   dst=bw, src=sw
+        m.fdx = __ddiv_rn(1.0, __ddiv_rn((double)m.sw, (double)bw));   // down: dst=sw, src=bw
+        m.fuy = __ddiv_rn(1.0, __ddiv_rn((double)bh, (double)m.sh));
+        m.fdy = __ddiv_rn(1.0, __ddiv_rn((double)m.sh, (double)bh));
+    }
+    a.table[(size_t)f * a.tcap + k] = m;
 }
 
 __device__ __forceinline__ void apply(const MBox& m, int& y, int& x) {
@@ -66,52 +82,49 @@ __device__ __forceinline__ bool inside(const MBox& m, int y, int x) {
 __global__ __launch_bounds__(256) void mosaic_kernel(MosaicArgs a) {
     __shared__ MBox s_box[TB_CAP];
     __shared__ int s_n;
-    __shared__ int s_overflow;
+    __shared__ int s_wsum[4];
     const int f = blockIdx.y;
     const int y0 = blockIdx.x * ROWS;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int n0 = a.cnt0 ? min(a.cnt0[f], a.cap0) : 0;
     const int n1 = a.cnt1 ? min(a.cnt1[f], a.cap1) : 0;
     const int nb = n0 + n1;
-    if (tid == 0) { s_n = 0; s_overflow = 0; }
+    const MBox* table = a.table + (size_t)f * a.tcap;
+    if (tid == 0) s_n = 0;
     __syncthreads();
     // ordered compaction of the boxes intersecting rows [y0, y0+ROWS)
     for (int base = 0; base < nb; base += 256) {
         const int k = base + tid;
         MBox m;
         bool hit = false;
-        if (k < nb && load_box(a, f, k, n0, m)) hit = m.y1 < y0 + ROWS && m.y2 > y0;
-        // block-wide exclusive prefix over hits, in index order
-        __shared__ int s_wsum[4];
-        const int lane = tid & 63, wid = tid >> 6;
+        if (k < nb) {
+            m = table[k];
+            hit = m.valid && m.y1 < y0 + ROWS && m.y2 > y0;
+        }
         const uint64_t bal = __ballot(hit);
         const int wpre = __popcll(bal & ((1ULL << lane) - 1ULL));
         if (lane == 0) s_wsum[wid] = __popcll(bal);
         __syncthreads();
         int off = s_n;
         for (int i = 0; i < wid; ++i) off += s_wsum[i];
-        if (hit) {
-            const int pos = off + wpre;
-            if (pos < TB_CAP) s_box[pos] = m; else s_overflow = 1;
-        }
+        if (hit && off + wpre < TB_CAP) s_box[off + wpre] = m;
         __syncthreads();
         if (tid == 0) s_n += s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
         __syncthreads();
     }
+    const bool overflow = s_n > TB_CAP;
     const int nt = min(s_n, TB_CAP);
-    const bool overflow = s_overflow != 0;
 
     const uint8_t* src = a.in + (size_t)f * a.h * a.pitch;
     uint8_t* dst = a.out + (size_t)f * a.h * a.pitch;
     const int row_bytes = a.w * 3;
-    const int nchunk = row_bytes >> 4;
+    const int nchunk = (row_bytes + 15) >> 4;
 
     auto walk = [&](int y, int x, int& sy, int& sx) {
-        int t = nt - 1;
-        int next_global = nb - 1;       // global index still to consider
+        int next_global = nb - 1;       // table index still to consider
         bool in_band = !overflow;
         if (in_band) {
-            for (; t >= 0; --t) {
+            for (int t = nt - 1; t >= 0; --t) {
                 const MBox& m = s_box[t];
                 if (inside(m, y, x)) {
                     apply(m, y, x);
@@ -121,8 +134,8 @@ __global__ __launch_bounds__(256) void mosaic_kernel(MosaicArgs a) {
         }
         if (!in_band) {
             for (int k = next_global; k >= 0; --k) {
-                MBox m;
-                if (load_box(a, f, k, n0, m) && inside(m, y, x)) apply(m, y, x);
+                const MBox m = table[k];
+                if (m.valid && inside(m, y, x)) apply(m, y, x);
             }
         }
         sy = y; sx = x;
@@ -133,10 +146,9 @@ __global__ __launch_bounds__(256) void mosaic_kernel(MosaicArgs a) {
         if (y >= a.h) break;
         const uint8_t* srow = src + (size_t)y * a.pitch;
         uint8_t* drow = dst + (size_t)y * a.pitch;
-        for (int c = tid; c <= nchunk; c += 256) {
+        for (int c = tid; c < nchunk; c += 256) {
             const int b0 = c << 4;
             const int bend = min(b0 + 16, row_bytes);
-            if (b0 >= bend) continue;
             const int px0 = b0 / 3, px1 = (bend - 1) / 3;
             bool touched = overflow;
             for (int t = 0; t < nt && !touched; ++t) {
@@ -165,12 +177,17 @@ __global__ __launch_bounds__(256) void mosaic_kernel(MosaicArgs a) {
 
 }  // namespace
 
+size_t vd_mosaic_table_bytes(int n, int tcap) { return (size_t)n * tcap * sizeof(MBox); }
+
 hipError_t vd_launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w, size_t pitch,
                             const int* cnt0, const int* xy0, int cap0,
-                            const int* cnt1, const int* xy1, int cap1, int level, hipStream_t s) {
+                            const int* cnt1, const int* xy1, int cap1, int level, void* table,
+                            hipStream_t s) {
     const int vec_ok = (pitch % 16 == 0) && ((uintptr_t)in % 16 == 0) && ((uintptr_t)out % 16 == 0);
-    MosaicArgs a{in, out, n, h, w, pitch, cnt0, xy0, cap0, cnt1, xy1, cap1, level, vec_ok};
-    dim3 grid((h + ROWS - 1) / ROWS, n);
-    hipLaunchKernelGGL(mosaic_kernel, grid, dim3(256), 0, s, a);
+    const int tcap = (cnt0 ? cap0 : 0) + (cnt1 ? cap1 : 0);
+    MosaicArgs a{in, out, n, h, w, pitch, cnt0, xy0, cap0, cnt1, xy1, cap1, level, vec_ok, (MBox*)table, tcap};
+    if (tcap > 0)
+        hipLaunchKernelGGL(mosaic_prep_kernel, dim3((tcap + 255) / 256, n), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(mosaic_kernel, dim3((h + ROWS - 1) / ROWS, n), dim3(256), 0, s, a);
     return hipGetLastError();
 }

@@ -47,6 +47,18 @@ struct Net {
     std::vector<Op> ops;
 };
 
+struct PostScratch {   // per-net candidate / NMS scratch sized for max_batch x A
+    uint64_t* keys = nullptr;
+    int* count = nullptr;
+    float4* box = nullptr;
+    int* cls = nullptr;
+    float4* nbox = nullptr;
+    float* area = nullptr;
+    uint64_t* sort = nullptr;
+    uint8_t* supp = nullptr;
+    int sort_cap = 0;
+};
+
 struct FaceNet {
     bool loaded = false;
     int in_h = 640, in_w = 640;
@@ -56,31 +68,23 @@ struct FaceNet {
     int loff[3] = {0, 0, 0};
     int A = 0;
     float* anchors = nullptr;
-    uint64_t* cand_keys = nullptr;
-    int* cand_count = nullptr;
-    float4* scratch_box = nullptr;
-    float* scratch_area = nullptr;
-    uint64_t* scratch_keys = nullptr;
-    uint8_t* scratch_supp = nullptr;
-    int sort_cap = 0;
+    PostScratch post;
 };
 
 struct PlateNet {
     bool loaded = false;
     int nc = 1;
-    int in_h = 0, in_w = 0;         // letterboxed canvas planned for (max frame, auto stride padding)
     int imgsz = 640;
-    Act input;
-    Net net;
-    Act head[3];                    // per level [H][W][64+nc] f32 (box DFL logits | class logits)
-    int lh[3] = {0, 0, 0}, lw[3] = {0, 0, 0};
-    float* dfl = nullptr;           // scratch
-    // post scratch
-    float* cand = nullptr;          // [B][A][6]
-    int* cand_count = nullptr;
-    uint64_t* keys = nullptr;
-    int A = 0;
-    int cur_h = 0, cur_w = 0;       // canvas of the current call
+    int hstride = 0;                // head channel stride (64 DFL + nc, padded to 4)
+    Act input;                      // letterboxed canvas, allocated for imgsz x imgsz
+    std::vector<std::pair<std::string, Act>> bufs;   // named activation buffers (max canvas)
+    std::vector<std::pair<std::string, int>> conv_idx;
+    std::vector<std::pair<long long, Net>> plans;    // per canvas (h<<32|w)
+    Act head[3];
+    int A_max = 0;
+    PostScratch post;
+    // current call
+    int ch = 0, cw = 0, A = 0, lh[3] = {0, 0, 0}, lw[3] = {0, 0, 0}, loff[3] = {0, 0, 0};
 };
 
 struct BoxTargets {
@@ -112,6 +116,7 @@ struct Ctx {
     void* stage_out = nullptr; size_t stage_out_bytes = 0;
     void* stage_box = nullptr; size_t stage_box_bytes = 0;
     void* stage_box2 = nullptr; size_t stage_box2_bytes = 0;
+    void* mosaic_table = nullptr; size_t mosaic_table_bytes = 0;
     bool timing = false;
     std::vector<TimedEv> ev_pool;
     size_t ev_used = 0;
@@ -137,8 +142,11 @@ struct Ctx {
     int box_finish(vd_boxes* out, int n, const BoxTargets& t);
     int face_letterbox(const uint8_t* dframes, int n, int h, int w, size_t pitch);
     int face_post(int n, int img_h, int img_w, const BoxTargets& t);
+    int launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w, size_t pitch, const int* cnt0,
+                      const int* xy0, int cap0, const int* cnt1, const int* xy1, int cap1, int level);
 };
 
+int vd_alloc_post(Ctx& ctx, PostScratch& ps, int A);
 int vd_build_face(Ctx& ctx, const WMap& W);
 int vd_build_plate(Ctx& ctx, const WMap& W);
 int vd_plate_forward(Ctx& ctx, const uint8_t* dframes, int n, int h, int w, size_t pitch);

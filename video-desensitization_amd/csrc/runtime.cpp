@@ -388,25 +388,50 @@ int Ctx::face_letterbox(const uint8_t* dframes, int n, int h, int w, size_t pitc
 }
 
 int Ctx::face_post(int n, int img_h, int img_w, const BoxTargets& t) {
-    FacePostArgs p{};
+    PostArgs p{};
+    p.mode = POST_FACE;
     for (int l = 0; l < 3; ++l) {
         p.heads[l] = (const float*)face.heads[l].p;
         p.lh[l] = face.heads[l].h;
         p.lw[l] = face.heads[l].w;
         p.loff[l] = face.loff[l];
     }
+    p.hstride = face.heads[0].c;
     p.anchors = face.anchors; p.A = face.A; p.B = n;
-    p.conf = cfg.confidence; p.iou = cfg.nms_iou;
-    p.cand_keys = face.cand_keys; p.cand_count = face.cand_count;
-    p.scratch_box = face.scratch_box; p.scratch_area = face.scratch_area;
-    p.scratch_keys = face.scratch_keys; p.scratch_supp = face.scratch_supp; p.sort_cap = face.sort_cap;
-    p.img_h = img_h; p.img_w = img_w; p.in_h = face.in_h; p.in_w = face.in_w;
+    p.conf = cfg.confidence; p.iou = cfg.nms_iou; p.max_det = 0;
+    p.cand_keys = face.post.keys; p.cand_count = face.post.count;
+    p.scratch_box = face.post.box; p.scratch_cls = face.post.cls; p.scratch_nbox = face.post.nbox;
+    p.scratch_area = face.post.area; p.scratch_keys = face.post.sort; p.scratch_supp = face.post.supp;
+    p.sort_cap = face.post.sort_cap;
+    p.img_h = img_h; p.img_w = img_w;
+    // retinaface_correct_boxes factors (utils_bbox.py:118-132), float32 tensor arithmetic
+    const float inh = (float)face.in_h, inw = (float)face.in_w, ih = (float)img_h, iw = (float)img_w;
+    const float rh = inh / ih, rw = inw / iw;
+    const float mn = rh < rw ? rh : rw;
+    const float nh = ih * mn, nw = iw * mn;
+    p.offy = ((inh - nh) / 2.0f) / inh;
+    p.offx = ((inw - nw) / 2.0f) / inw;
+    p.scy = inh / nh;
+    p.scx = inw / nw;
     p.cap = t.cap; p.out_count = t.count; p.out_xyxy = t.xyxy; p.out_xyxy_f = t.xyxy_f;
     p.out_score = t.score; p.out_label = t.label;
-    t_begin(3, (double)n * face.A * 16 * 4);
-    hipError_t e = vd_launch_face_post(p, stream);
+    t_begin(3, (double)n * face.A * 32 * 4);
+    hipError_t e = vd_launch_post(p, stream);
     t_end();
     if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "face post: %s", hipGetErrorString(e));
+    return VD_OK;
+}
+
+int Ctx::launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w, size_t pitch, const int* cnt0,
+                       const int* xy0, int cap0, const int* cnt1, const int* xy1, int cap1, int level) {
+    const int tcap = (cnt0 ? cap0 : 0) + (cnt1 ? cap1 : 0);
+    int rc = ensure_staging(&mosaic_table, &mosaic_table_bytes, vd_mosaic_table_bytes(n, tcap) + 64);
+    if (rc) return rc;
+    t_begin(1, 2.0 * n * (double)h * w * 3);
+    hipError_t e = vd_launch_mosaic(in, out, n, h, w, pitch, cnt0, xy0, cap0, cnt1, xy1, cap1, level, mosaic_table,
+                                    stream);
+    t_end();
+    if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "mosaic: %s", hipGetErrorString(e));
     return VD_OK;
 }
 
@@ -479,6 +504,7 @@ int vd_destroy(vd_ctx* h) {
     if (ctx->stage_out) hipFree(ctx->stage_out);
     if (ctx->stage_box) hipFree(ctx->stage_box);
     if (ctx->stage_box2) hipFree(ctx->stage_box2);
+    if (ctx->mosaic_table) hipFree(ctx->mosaic_table);
     for (auto& t : ctx->ev_pool) { hipEventDestroy(t.a); hipEventDestroy(t.b); }
     hipStreamDestroy(ctx->own_stream);
     delete ctx;
@@ -586,11 +612,8 @@ int vd_mosaic(vd_ctx* h, const uint8_t* in, uint8_t* out, int n, int fh, int fw,
         cnt = dc;
         xy = dx;
     }
-    ctx->t_begin(1, 2.0 * n * (double)fh * fw * 3);
-    hipError_t e = vd_launch_mosaic(din, dout, n, fh, fw, pitch, cnt, xy, boxes->cap, nullptr, nullptr, 0, level,
-                                    ctx->stream);
-    ctx->t_end();
-    if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "mosaic: %s", hipGetErrorString(e));
+    if ((rc = ctx->launch_mosaic(din, dout, n, fh, fw, pitch, cnt, xy, boxes->cap, nullptr, nullptr, 0, level)))
+        return rc;
     if (where == VD_HOST) {
         VD_CHECK_HIP(hipMemcpyAsync(out, dout, bytes, hipMemcpyDeviceToHost, ctx->stream));
         VD_CHECK_HIP(hipStreamSynchronize(ctx->stream));
@@ -649,13 +672,11 @@ int vd_process(vd_ctx* h, const uint8_t* in, uint8_t* out, int n, int fh, int fw
             if ((rc = ctx->ensure_staging(&ctx->stage_out, &ctx->stage_out_bytes, bytes))) return rc;
             dout = (uint8_t*)ctx->stage_out;
         }
-        ctx->t_begin(1, 2.0 * n * (double)fh * fw * 3);
-        hipError_t e = vd_launch_mosaic(d, dout, n, fh, fw, pitch, do_faces ? tf.count : nullptr,
-                                        do_faces ? tf.xyxy : nullptr, do_faces ? tf.cap : 0,
-                                        mosaic_plates ? tp.count : nullptr, mosaic_plates ? tp.xyxy : nullptr,
-                                        mosaic_plates ? tp.cap : 0, ctx->cfg.mosaic_level, ctx->stream);
-        ctx->t_end();
-        if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "mosaic: %s", hipGetErrorString(e));
+        if ((rc = ctx->launch_mosaic(d, dout, n, fh, fw, pitch, do_faces ? tf.count : nullptr,
+                                     do_faces ? tf.xyxy : nullptr, do_faces ? tf.cap : 0,
+                                     mosaic_plates ? tp.count : nullptr, mosaic_plates ? tp.xyxy : nullptr,
+                                     mosaic_plates ? tp.cap : 0, ctx->cfg.mosaic_level)))
+            return rc;
         if (where == VD_HOST) VD_CHECK_HIP(hipMemcpyAsync(out, dout, bytes, hipMemcpyDeviceToHost, ctx->stream));
     }
     int rc2 = VD_OK;

@@ -29,25 +29,35 @@ struct ConvArgs {
     int ntiles_n;                                // ceil(cout / BN)
 };
 
-// Device buffers for one frame batch's face post-processing.
-struct FacePostArgs {
-    const float* heads[3];   // per level NHWC [B][H][W][32] f32: 0..7 bbox, 8..11 cls, 12..31 landm
+// Device buffers + parameters for one frame batch's detection post-processing.
+enum { POST_FACE = 0, POST_YOLO = 1 };
+struct PostArgs {
+    int mode;                // POST_FACE / POST_YOLO
+    const float* heads[3];   // per level NHWC [B][H][W][hstride] f32
+    int hstride;             // face: 32 (0..7 bbox, 8..11 cls, 12..31 landm); yolo: 64 DFL | nc cls (padded)
     int lh[3], lw[3];        // level dims
     int loff[3];             // first anchor index per level
-    const float* anchors;    // [A][4]
+    int strides[3];          // yolo: 8/16/32
+    const float* anchors;    // face: [A][4] priors
     int A;                   // anchors per frame
     int B;
+    int nc;                  // yolo classes
     float conf;
     double iou;
+    int max_det;             // yolo: 300 (0 = unlimited)
+    float max_wh;            // yolo class offset (7680)
     uint64_t* cand_keys;     // [B][A] candidate keys
     int* cand_count;         // [B]
-    float4* scratch_box;     // [B][A] global scratch for large candidate sets
+    float4* scratch_box;     // [B][A] decoded box by anchor (candidates only)
+    int* scratch_cls;        // [B][A] yolo class by anchor
+    float4* scratch_nbox;    // [B][A] NMS boxes for large candidate sets
     float* scratch_area;     // [B][A]
-    uint64_t* scratch_keys;  // [B][2^ceil(log2 A)] global sort scratch
+    uint64_t* scratch_keys;  // [B][sort_cap]
     uint8_t* scratch_supp;   // [B][A]
     int sort_cap;            // power of two >= A
     int img_h, img_w;        // source frame size (all frames of a call share it)
-    int in_h, in_w;          // net input size
+    float offx, offy, scx, scy;   // face correction (utils_bbox.py:118-132, float32)
+    int padx, pady; float inv_gain;  // yolo scale_boxes
     int cap;                 // output capacity per frame
     int* out_count;          // [B]
     int* out_xyxy;           // [B][cap][4]
@@ -80,10 +90,12 @@ hipError_t vd_launch_maxpool(bool f32, const void* x, int n, int xh, int xw, int
                              hipStream_t s);
 hipError_t vd_launch_upsample2x(bool f32, const void* x, int n, int xh, int xw, int ldx, int xcoff,
                                 void* y, int ldy, int ycoff, int c, hipStream_t s);
-hipError_t vd_launch_face_post(const FacePostArgs& p, hipStream_t s);
+hipError_t vd_launch_post(const PostArgs& p, hipStream_t s);
 hipError_t vd_launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w, size_t pitch,
                             const int* cnt0, const int* xy0, int cap0,
-                            const int* cnt1, const int* xy1, int cap1, int level, hipStream_t s);
+                            const int* cnt1, const int* xy1, int cap1, int level, void* table,
+                            hipStream_t s);
+size_t vd_mosaic_table_bytes(int n, int tcap);
 
 #define VD_CHECK_HIP(expr)                                                     \
     do {                                                                       \

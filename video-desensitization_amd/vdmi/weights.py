@@ -30,7 +30,7 @@ import numpy as np
 # level-0/1/2 anchors a score >= 0.5 (~40 candidates per frame, tens of kept boxes,
 # mostly small: a crowded street scene rather than one box per anchor).
 CLS_HEAD_STD = 0.02
-CLS_BIAS_DELTA = {0: -7.49, 1: -5.02, 2: -0.63}
+CLS_BIAS_DELTA = {0: -9.3, 1: -6.47, 2: -1.68}
 LOC_HEAD_STD = 0.01
 RESIDUAL_GAMMA = 0.25
 
