@@ -156,8 +156,9 @@ int vdt_conv2d(vd_ctx* ctx, const float* x, int n, int h, int w, int cin,
                const float* wgt, int cout, int kh, int kw, int stride, int pad,
                const float* scale, const float* shift, int act, float slope,
                const float* res, int res_mode, float* y, int* oh, int* ow);
-/* Raw YOLO outputs [n][4+nc][A] (decoded boxes xywh in letterbox pixels + class
- * sigmoid scores), host f32, A = anchors at the letterboxed size. */
+/* Raw YOLO Detect outputs [n][64+nc][A] (per-side DFL logits | class logits),
+ * host f32, anchors in level -> y -> x order at the letterboxed canvas; *anchors
+ * receives A. `out` may be NULL to query A. */
 int vdt_plate_raw(vd_ctx* ctx, const uint8_t* frames, int n, int h, int w, size_t pitch,
                   int where, float* out, int* anchors);
 

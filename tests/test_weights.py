@@ -52,3 +52,27 @@ def test_synthetic_frames_deterministic():
     assert not np.array_equal(synth.frame(16, 24, 0, seed=1), f1[0])
     b = synth.box_lists(4, 1080, 1920)
     assert b.shape == (4, 8, 4) and (b[..., 2] > b[..., 0]).all()
+
+
+def test_yolov8n_keys_match_ultralytics_tree():
+    from oracle.yolov8 import YOLOv8n
+    from vdmi import weights
+    sd = weights.yolov8n_state_dict(0, nc=1)
+    ref = {k: tuple(v.shape) for k, v in YOLOv8n(1).state_dict().items() if not k.endswith("num_batches_tracked")}
+    assert set(sd) == set(ref), set(sd) ^ set(ref)
+    for k, v in sd.items():
+        assert v.shape == ref[k], k
+    n = sum(v.size for k, v in sd.items())
+    assert 2.9e6 < n < 3.3e6          # YOLOv8n ~3.0-3.2 M parameters
+
+
+def test_oracle_yolo_runs_small():
+    from oracle.yolov8 import build_oracle_yolo, postprocess, raw_heads
+    from vdmi import weights
+    m = build_oracle_yolo(weights.yolov8n_state_dict(0))
+    with torch.no_grad():
+        lv = m(torch.zeros(1, 3, 64, 96))
+    assert [tuple(t.shape) for t in lv] == [(1, 65, 8, 12), (1, 65, 4, 6), (1, 65, 2, 3)]
+    raw = raw_heads(lv)
+    res = postprocess(raw, [(8, 12), (4, 6), (2, 3)], (64, 96), (64, 96))
+    assert len(res) == 1

@@ -49,6 +49,7 @@ int vd_build_face(Ctx& c, const WMap& W) {
         op.x = stem; op.y = pool; op.ch = 64; op.k = 3; op.s = 2; op.p = 1;
         F.net.ops.push_back(op);
     }
+    F.net.stage_end[0] = (int)F.net.ops.size();
 
     // ---- layer1..4 (Bottleneck x [3,4,6,3]) ----
     Act x = pool;
@@ -86,6 +87,7 @@ int vd_build_face(Ctx& c, const WMap& W) {
             x = out;
         }
         if (li >= 1) feats[li - 1] = x;   // layer2/3/4 -> C3/C4/C5 (config.py:26)
+        F.net.stage_end[li + 1] = (int)F.net.ops.size();
     }
 
     // ---- FPN ----

@@ -8,25 +8,35 @@
 // contains p, then out(p) = in(p'). map_k = down(up(.)) per axis with OpenCV's
 // double-precision nearest index rule. This is a pure gather -> |delta| = 0.
 //
-// Two kernels per call:
+// Kernels per call:
 //  mosaic_prep_kernel  one thread per box: clip to the frame and precompute the
 //                      four resizeNN factors into a per-frame table (boxes in
 //                      call order: faces first, then plates, combine_detect.py:242-244).
-//  mosaic_kernel       one workgroup per (frame, band of ROWS rows). The band's
-//                      box list (table entries intersecting the band, original
-//                      order) is staged in LDS; a 16-byte output chunk that no band
-//                      box touches is a vectorised copy, the rest walk per pixel.
-//                      A walk that leaves the band (points only move up/left)
-//                      continues on the frame's full table from where it left
-//                      off, so the band list is an exact filter.
+//  mosaic_copy_kernel  the img.copy() of :247 — a 64-B-per-thread streaming copy
+//                      of every frame with <= BOX_FAST boxes (HBM roofline).
+//  mosaic_box_kernel   one workgroup slice per (frame, box k): for each pixel of
+//                      box k that no LATER box contains (that box owns it), walk
+//                      k, k-1, ..., 0 and gather the 3 source bytes. Only covered
+//                      pixels are touched; the frame's box table sits in LDS.
+//  mosaic_kernel       fallback for frames with > BOX_FAST boxes: one workgroup
+//                      per (frame, band of ROWS rows). The band's box list (table
+//                      entries intersecting the band, original order) is staged
+//                      in LDS; a 16-byte chunk no band box touches is a vector
+//                      copy, the rest walk per pixel. A walk that leaves the band
+//                      (points only move up/left) continues on the frame's full
+//                      table, so the band list is an exact filter.
 // HBM traffic = read + write of every frame (2*W*H*3 bytes) + ROI gathers (L2 hits).
 #include "vd_common.h"
 #include "vd_math.h"
+
+#include <algorithm>
 
 namespace {
 
 constexpr int ROWS = 8;
 constexpr int TB_CAP = 512;    // band-list capacity; larger bands walk the global table
+constexpr int BOX_FAST = 256;  // frames with at most this many boxes take copy + box kernels
+constexpr int BOX_TILES = 8;   // workgroups per box
 
 struct MBox { int x1, y1, x2, y2; int sw, sh, idx, valid; double fux, fdx, fuy, fdy; };
 
@@ -37,6 +47,7 @@ struct MosaicArgs {
     int level;
     int vec_ok;                                      // 16-B aligned rows -> vector copies
     MBox* table; int tcap;                           // [n][tcap] prepared boxes
+    uint64_t* ovl;                                   // [n][BOX_FAST][4] overlap bitmasks (fast path)
 };
 
 __global__ __launch_bounds__(256) void mosaic_prep_kernel(MosaicArgs a) {
@@ -89,6 +100,7 @@ __global__ __launch_bounds__(256) void mosaic_kernel(MosaicArgs a) {
     const int n0 = a.cnt0 ? min(a.cnt0[f], a.cap0) : 0;
     const int n1 = a.cnt1 ? min(a.cnt1[f], a.cap1) : 0;
     const int nb = n0 + n1;
+    if (nb <= BOX_FAST) return;        // copy + box kernels own this frame
     const MBox* table = a.table + (size_t)f * a.tcap;
     if (tid == 0) s_n = 0;
     __syncthreads();
@@ -175,9 +187,133 @@ __global__ __launch_bounds__(256) void mosaic_kernel(MosaicArgs a) {
     }
 }
 
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// img.copy() for the frames of the fast path: 4 x 16 B per thread per iteration.
+__global__ __launch_bounds__(256) void mosaic_copy_kernel(MosaicArgs a) {
+    const int f = blockIdx.y;
+    const int n0 = a.cnt0 ? min(a.cnt0[f], a.cap0) : 0;
+    const int n1 = a.cnt1 ? min(a.cnt1[f], a.cap1) : 0;
+    if (n0 + n1 > BOX_FAST) return;
+    const size_t bytes = (size_t)a.h * a.pitch;
+    const uint8_t* src = a.in + (size_t)f * bytes;
+    uint8_t* dst = a.out + (size_t)f * bytes;
+    if (a.vec_ok) {
+        const size_t nv = bytes >> 4;
+        const u32x4* s4 = (const u32x4*)src;
+        u32x4* d4 = (u32x4*)dst;
+        const size_t stride = (size_t)gridDim.x * 256;
+        size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+        for (; i + 3 * stride < nv; i += 4 * stride) {
+            const u32x4 v0 = s4[i], v1 = s4[i + stride], v2 = s4[i + 2 * stride], v3 = s4[i + 3 * stride];
+            d4[i] = v0; d4[i + stride] = v1; d4[i + 2 * stride] = v2; d4[i + 3 * stride] = v3;
+        }
+        for (; i < nv; i += stride) d4[i] = s4[i];
+        for (size_t t = (nv << 4) + (size_t)blockIdx.x * 256 + threadIdx.x; t < bytes; t += stride) dst[t] = src[t];
+    } else {
+        for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t < bytes; t += (size_t)gridDim.x * 256) dst[t] = src[t];
+    }
+}
+
+// Overlap graph of the fast-path frames: bit j of ovl[k] <=> boxes j and k intersect.
+__global__ __launch_bounds__(256) void mosaic_overlap_kernel(MosaicArgs a) {
+    const int f = blockIdx.y;
+    const int k = threadIdx.x;
+    const int n0 = a.cnt0 ? min(a.cnt0[f], a.cap0) : 0;
+    const int n1 = a.cnt1 ? min(a.cnt1[f], a.cap1) : 0;
+    const int nb = n0 + n1;
+    if (nb > BOX_FAST || k >= nb) return;
+    const MBox* t = a.table + (size_t)f * a.tcap;
+    uint64_t m[4] = {0, 0, 0, 0};
+    const MBox bk = t[k];
+    if (bk.valid)
+        for (int j = 0; j < nb; ++j) {
+            const MBox bj = t[j];
+            if (j != k && bj.valid && bj.x1 < bk.x2 && bk.x1 < bj.x2 && bj.y1 < bk.y2 && bk.y1 < bj.y2)
+                m[j >> 6] |= 1ULL << (j & 63);
+        }
+    uint64_t* o = a.ovl + ((size_t)f * BOX_FAST + k) * 4;
+    o[0] = m[0]; o[1] = m[1]; o[2] = m[2]; o[3] = m[3];
+}
+
+// Highest set bit index < lim in a 256-bit mask, or -1.
+__device__ __forceinline__ int top_below(const uint64_t* m, int lim) {
+    for (int w = (lim - 1) >> 6; w >= 0; --w) {
+        uint64_t v = m[w];
+        const int hi = lim - (w << 6);               // bits [0, hi) of this word are eligible
+        if (hi < 64) v &= (1ULL << hi) - 1ULL;
+        if (v) return (w << 6) + 63 - __clzll((long long)v);
+    }
+    return -1;
+}
+
+// Pixels of box k that no LATER box contains: walk k, then earlier boxes along the
+// overlap graph (a box containing a point of box j overlaps j), gather 3 bytes.
+__global__ __launch_bounds__(256) void mosaic_box_kernel(MosaicArgs a) {
+    __shared__ MBox s_tab[BOX_FAST];
+    __shared__ uint64_t s_ovl[BOX_FAST][4];
+    const int f = blockIdx.z;
+    const int k = blockIdx.y;
+    const int n0 = a.cnt0 ? min(a.cnt0[f], a.cap0) : 0;
+    const int n1 = a.cnt1 ? min(a.cnt1[f], a.cap1) : 0;
+    const int nb = n0 + n1;
+    if (nb > BOX_FAST || k >= nb) return;
+    const MBox* table = a.table + (size_t)f * a.tcap;
+    if (!table[k].valid) return;
+    const uint64_t* ovl = a.ovl + (size_t)f * BOX_FAST * 4;
+    for (int i = threadIdx.x; i < nb; i += 256) {
+        s_tab[i] = table[i];
+        s_ovl[i][0] = ovl[4 * i + 0]; s_ovl[i][1] = ovl[4 * i + 1];
+        s_ovl[i][2] = ovl[4 * i + 2]; s_ovl[i][3] = ovl[4 * i + 3];
+    }
+    __syncthreads();
+    const MBox bk = s_tab[k];
+    const int bw = bk.x2 - bk.x1;
+    const int area = bw * (bk.y2 - bk.y1);
+    const uint8_t* src = a.in + (size_t)f * a.h * a.pitch;
+    uint8_t* dst = a.out + (size_t)f * a.h * a.pitch;
+    // later boxes overlapping k (the only ones that can own a pixel of k)
+    uint64_t later[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const int lo = k + 1 - (w << 6);   // keep bits >= k+1
+        uint64_t v = s_ovl[k][w];
+        if (lo >= 64) v = 0; else if (lo > 0) v &= ~((1ULL << lo) - 1ULL);
+        later[w] = v;
+    }
+    for (int p = blockIdx.x * 256 + threadIdx.x; p < area; p += BOX_TILES * 256) {
+        const int y0 = bk.y1 + p / bw, x0 = bk.x1 + p % bw;
+        bool owned = true;
+#pragma unroll
+        for (int w = 0; w < 4 && owned; ++w) {
+            uint64_t v = later[w];
+            while (v && owned) {
+                const int j = (w << 6) + __ffsll((long long)v) - 1;
+                v &= v - 1;
+                owned = !inside(s_tab[j], y0, x0);
+            }
+        }
+        if (!owned) continue;
+        int y = y0, x = x0;
+        apply(bk, y, x);
+        int cur = k;
+        for (;;) {   // next (highest-index, earlier) box containing the point, along the overlap graph
+            int lim = cur, j;
+            while ((j = top_below(s_ovl[cur], lim)) >= 0 && !inside(s_tab[j], y, x)) lim = j;
+            if (j < 0) break;
+            apply(s_tab[j], y, x);
+            cur = j;
+        }
+        const uint8_t* sp = src + (size_t)y * a.pitch + x * 3;
+        uint8_t* dp = dst + (size_t)y0 * a.pitch + x0 * 3;
+        const uint8_t c0 = sp[0], c1 = sp[1], c2 = sp[2];
+        dp[0] = c0; dp[1] = c1; dp[2] = c2;
+    }
+}
+
 }  // namespace
 
-size_t vd_mosaic_table_bytes(int n, int tcap) { return (size_t)n * tcap * sizeof(MBox); }
+size_t vd_mosaic_table_bytes(int n, int tcap) { return (size_t)n * tcap * sizeof(MBox) + (size_t)n * BOX_FAST * 32; }
 
 hipError_t vd_launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w, size_t pitch,
                             const int* cnt0, const int* xy0, int cap0,
@@ -185,9 +321,19 @@ hipError_t vd_launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w
                             hipStream_t s) {
     const int vec_ok = (pitch % 16 == 0) && ((uintptr_t)in % 16 == 0) && ((uintptr_t)out % 16 == 0);
     const int tcap = (cnt0 ? cap0 : 0) + (cnt1 ? cap1 : 0);
-    MosaicArgs a{in, out, n, h, w, pitch, cnt0, xy0, cap0, cnt1, xy1, cap1, level, vec_ok, (MBox*)table, tcap};
+    MosaicArgs a{in, out, n, h, w, pitch, cnt0, xy0, cap0, cnt1, xy1, cap1, level, vec_ok, (MBox*)table, tcap,
+                 (uint64_t*)((char*)table + vd_mosaic_table_bytes(n, tcap) - (size_t)n * BOX_FAST * 32)};
     if (tcap > 0)
         hipLaunchKernelGGL(mosaic_prep_kernel, dim3((tcap + 255) / 256, n), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(mosaic_kernel, dim3((h + ROWS - 1) / ROWS, n), dim3(256), 0, s, a);
+    // fast path: copy (~1 MiB per workgroup row of the grid) then owned-pixel gathers
+    const size_t fbytes = (size_t)h * pitch;
+    const int cblocks = (int)std::min<size_t>(1024, std::max<size_t>(1, fbytes / (64 * 256 * 4)));
+    hipLaunchKernelGGL(mosaic_copy_kernel, dim3(cblocks, n), dim3(256), 0, s, a);
+    if (tcap > 0) {
+        hipLaunchKernelGGL(mosaic_overlap_kernel, dim3(1, n), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(mosaic_box_kernel, dim3(BOX_TILES, std::min(tcap, BOX_FAST), n), dim3(256), 0, s, a);
+        // frames with more boxes than the fast path holds
+        hipLaunchKernelGGL(mosaic_kernel, dim3((h + ROWS - 1) / ROWS, n), dim3(256), 0, s, a);
+    }
     return hipGetLastError();
 }

@@ -45,6 +45,7 @@ struct Op {
 
 struct Net {
     std::vector<Op> ops;
+    int stage_end[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // op index after each backbone stage (face: 0=stem,1..4=layerN)
 };
 
 struct PostScratch {   // per-net candidate / NMS scratch sized for max_batch x A
@@ -134,13 +135,15 @@ struct Ctx {
                  int rcoff = 0, int rmode = 0, int rup = 0);
     void t_begin(int fam, double work);
     void t_end();
-    int run_conv_op(const Op& op, int n);
-    int run_net(const Net& net, int n);
+    int run_conv_op(const Op& op, int f0, int n);
+    int run_ops(const Net& net, int b, int e, int f0, int n);
+    int run_net(const Net& net, int n, int mb = 0, int split = 0);
     const uint8_t* frames_to_device(const uint8_t* frames, int n, int h, size_t pitch, int where, int* rc);
     int check_frames(int n, int h, int w, size_t pitch);
     int box_targets(vd_boxes* out, int n, BoxTargets& t);
     int box_finish(vd_boxes* out, int n, const BoxTargets& t);
     int face_letterbox(const uint8_t* dframes, int n, int h, int w, size_t pitch);
+    int face_forward(int n);
     int face_post(int n, int img_h, int img_w, const BoxTargets& t);
     int launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w, size_t pitch, const int* cnt0,
                       const int* xy0, int cap0, const int* cnt1, const int* xy1, int cap1, int level);

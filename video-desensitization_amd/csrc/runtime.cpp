@@ -10,6 +10,7 @@
 #include "vd_math.h"
 #include "nets.h"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -224,7 +225,7 @@ int Ctx::add_conv(Net& net, int ci, const Act& x, int xcoff, Act& y, int ycoff, 
     if (res) { op.r = *res; op.rcoff = rcoff; op.rmode = rmode; op.rup = rup; }
     const int oh = (x.h + 2 * cv.pad - cv.kh) / cv.stride + 1;
     const int ow = (x.w + 2 * cv.pad - cv.kw) / cv.stride + 1;
-    if (oh != y.h || ow != y.w || ycoff + cv.cout > y.c || xcoff + cv.cin > x.c)
+    if (oh != y.h || ow != y.w || ycoff + cv.cout > y.c || xcoff + cv.cin_pad > x.c)
         return vd_set_error(VD_ERR_ARG, "conv plan shape mismatch (%dx%d vs %dx%d)", oh, ow, y.h, y.w);
     net.ops.push_back(op);
     return VD_OK;
@@ -253,14 +254,18 @@ void Ctx::t_end() {
     ++ev_used;
 }
 
-int Ctx::run_conv_op(const Op& op, int n) {
+static inline const void* foff(const Act& a, int f0) {
+    return a.p ? (const char*)a.p + (size_t)f0 * a.h * a.w * a.c * (a.f32 ? 4 : 2) : nullptr;
+}
+
+int Ctx::run_conv_op(const Op& op, int f0, int n) {
     const Conv& cv = convs[op.conv];
     ConvArgs a{};
-    a.x = op.x.p; a.xh = op.x.h; a.xw = op.x.w; a.ldx = op.x.c; a.xcoff = op.xcoff;
+    a.x = foff(op.x, f0); a.xh = op.x.h; a.xw = op.x.w; a.ldx = op.x.c; a.xcoff = op.xcoff;
     a.w = cv.w; a.scale = cv.scale; a.shift = cv.shift;
-    a.res = op.r.p; a.res_ld = op.r.c; a.res_coff = op.rcoff; a.res_up = op.rup; a.rh = op.r.h; a.rw = op.r.w;
+    a.res = foff(op.r, f0); a.res_ld = op.r.c; a.res_coff = op.rcoff; a.res_up = op.rup; a.rh = op.r.h; a.rw = op.r.w;
     a.res_mode = op.r.p ? op.rmode : VD_RES_NONE;
-    a.y = op.y.p; a.yh = op.y.h; a.yw = op.y.w; a.ldy = op.y.c; a.ycoff = op.ycoff;
+    a.y = (void*)foff(op.y, f0); a.yh = op.y.h; a.yw = op.y.w; a.ldy = op.y.c; a.ycoff = op.ycoff;
     a.B = n; a.cin_pad = cv.cin_pad; a.cout = cv.cout; a.kpad = cv.kpad;
     a.kh = cv.kh; a.kw = cv.kw; a.stride = cv.stride; a.pad = cv.pad;
     a.M = n * op.y.h * op.y.w;
@@ -272,27 +277,43 @@ int Ctx::run_conv_op(const Op& op, int n) {
     return VD_OK;
 }
 
-int Ctx::run_net(const Net& net, int n) {
-    for (const Op& op : net.ops) {
+int Ctx::run_ops(const Net& net, int b, int e, int f0, int n) {
+    for (int i = b; i < e; ++i) {
+        const Op& op = net.ops[i];
         int rc = VD_OK;
         if (op.kind == OP_CONV) {
-            rc = run_conv_op(op, n);
+            rc = run_conv_op(op, f0, n);
         } else if (op.kind == OP_MAXPOOL) {
             t_begin(4, 0);
-            hipError_t e = vd_launch_maxpool(f32, op.x.p, n, op.x.h, op.x.w, op.x.c, op.xcoff, op.y.p, op.y.h,
-                                             op.y.w, op.y.c, op.ycoff, op.ch, op.k, op.s, op.p, stream);
+            hipError_t er = vd_launch_maxpool(f32, foff(op.x, f0), n, op.x.h, op.x.w, op.x.c, op.xcoff,
+                                              (void*)foff(op.y, f0), op.y.h, op.y.w, op.y.c, op.ycoff, op.ch, op.k,
+                                              op.s, op.p, stream);
             t_end();
-            if (e != hipSuccess) rc = vd_set_error(VD_ERR_HIP, "maxpool: %s", hipGetErrorString(e));
+            if (er != hipSuccess) rc = vd_set_error(VD_ERR_HIP, "maxpool: %s", hipGetErrorString(er));
         } else if (op.kind == OP_UPSAMPLE) {
             t_begin(4, 0);
-            hipError_t e = vd_launch_upsample2x(f32, op.x.p, n, op.x.h, op.x.w, op.x.c, op.xcoff, op.y.p, op.y.c,
-                                                op.ycoff, op.ch, stream);
+            hipError_t er = vd_launch_upsample2x(f32, foff(op.x, f0), n, op.x.h, op.x.w, op.x.c, op.xcoff,
+                                                 (void*)foff(op.y, f0), op.y.c, op.ycoff, op.ch, stream);
             t_end();
-            if (e != hipSuccess) rc = vd_set_error(VD_ERR_HIP, "upsample: %s", hipGetErrorString(e));
+            if (er != hipSuccess) rc = vd_set_error(VD_ERR_HIP, "upsample: %s", hipGetErrorString(er));
         }
         if (rc) return rc;
     }
     return VD_OK;
+}
+
+// Depth-first over micro-batches of `mb` frames for ops [0, split) -- each
+// micro-batch's stem/layer1/layer2 intermediates (~100-200 MB) then stay in the
+// 256 MiB Infinity Cache between producer and consumer -- then ops [split, end)
+// over the whole batch (the small late layers need the whole batch to fill 256 CUs).
+int Ctx::run_net(const Net& net, int n, int mb, int split) {
+    const int ne = (int)net.ops.size();
+    if (mb <= 0 || mb >= n || split <= 0) return run_ops(net, 0, ne, 0, n);
+    for (int f0 = 0; f0 < n; f0 += mb) {
+        int rc = run_ops(net, 0, split, f0, std::min(mb, n - f0));
+        if (rc) return rc;
+    }
+    return run_ops(net, split, ne, 0, n);
 }
 
 // cv2.resize mode selection (resize.cpp hal::resize [ext]; oracle/letterbox.py)
@@ -385,6 +406,13 @@ int Ctx::face_letterbox(const uint8_t* dframes, int n, int h, int w, size_t pitc
     t_end();
     if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "letterbox: %s", hipGetErrorString(e));
     return VD_OK;
+}
+
+int Ctx::face_forward(int n) {
+    const int mb = cfg.reserved[0];                       // frames per micro-batch (0 = off)
+    const int stage = cfg.reserved[1] > 0 ? cfg.reserved[1] : 2;   // micro-batch through layer<stage>
+    const int split = face.net.stage_end[std::min(std::max(stage, 0), 4)];
+    return run_net(face.net, n, mb, split);
 }
 
 int Ctx::face_post(int n, int img_h, int img_w, const BoxTargets& t) {
@@ -558,7 +586,7 @@ int vd_detect(vd_ctx* h, const uint8_t* frames, int n, int fh, int fw, size_t pi
     const uint8_t* d = ctx->frames_to_device(frames, n, fh, pitch, where, &rc);
     if (rc) return rc;
     if ((rc = ctx->face_letterbox(d, n, fh, fw, pitch))) return rc;
-    if ((rc = ctx->run_net(ctx->face.net, n))) return rc;
+    if ((rc = ctx->face_forward(n))) return rc;
     if ((rc = ctx->face_post(n, fh, fw, t))) return rc;
     return ctx->box_finish(faces, n, t);
 }
@@ -587,6 +615,8 @@ int vd_mosaic(vd_ctx* h, const uint8_t* in, uint8_t* out, int n, int fh, int fw,
     if (mode != VD_MOSAIC_OUT_OF_PLACE) return vd_set_error(VD_ERR_ARG, "unsupported mosaic mode %d", mode);
     if (!in || !out || !boxes || !boxes->count || !boxes->xyxy || boxes->cap <= 0)
         return vd_set_error(VD_ERR_ARG, "vd_mosaic: null argument");
+    if ((const void*)in == (const void*)out)
+        return vd_set_error(VD_ERR_ARG, "vd_mosaic: out-of-place only (out must not alias in)");
     if (n <= 0 || fh <= 0 || fw <= 0 || pitch < (size_t)fw * 3 || level <= 0)
         return vd_set_error(VD_ERR_ARG, "vd_mosaic: bad geometry");
     int rc = VD_OK;
@@ -658,7 +688,7 @@ int vd_process(vd_ctx* h, const uint8_t* in, uint8_t* out, int n, int fh, int fw
     if (rc) return rc;
     if (do_faces) {
         if ((rc = ctx->face_letterbox(d, n, fh, fw, pitch))) return rc;
-        if ((rc = ctx->run_net(ctx->face.net, n))) return rc;
+        if ((rc = ctx->face_forward(n))) return rc;
         if ((rc = ctx->face_post(n, fh, fw, tf))) return rc;
     }
     if (do_plates) {
@@ -770,7 +800,7 @@ int vdt_forward_heads(vd_ctx* h, const uint8_t* frames, int n, int fh, int fw, s
     const uint8_t* d = ctx->frames_to_device(frames, n, fh, pitch, where, &rc);
     if (rc) return rc;
     if ((rc = ctx->face_letterbox(d, n, fh, fw, pitch))) return rc;
-    if ((rc = ctx->run_net(ctx->face.net, n))) return rc;
+    if ((rc = ctx->face_forward(n))) return rc;
     VD_CHECK_HIP(hipStreamSynchronize(ctx->stream));
     const int A = ctx->face.A;
     for (int l = 0; l < 3; ++l) {

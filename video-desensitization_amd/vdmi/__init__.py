@@ -13,6 +13,7 @@ from ._lib import VdCapacityError, VdError, load  # noqa: F401
 from .context import Context, DeviceBoxes  # noqa: F401
 from .face import Retinaface  # noqa: F401
 from .mosaic import mosaic_frames, mosaic_rectangle_region_single  # noqa: F401
+from .plate import YOLO, PlateDetector  # noqa: F401
 
-__all__ = ["Context", "DeviceBoxes", "Retinaface", "mosaic_rectangle_region_single", "mosaic_frames",
-           "VdError", "VdCapacityError", "load"]
+__all__ = ["Context", "DeviceBoxes", "Retinaface", "YOLO", "PlateDetector", "mosaic_rectangle_region_single",
+           "mosaic_frames", "VdError", "VdCapacityError", "load"]

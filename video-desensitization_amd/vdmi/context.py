@@ -57,7 +57,7 @@ class Context:
 
     def __init__(self, device=0, precision="bf16", max_batch=64, input_shape=(640, 640), confidence=0.5,
                  nms_iou=0.4, max_boxes=256, mosaic_level=8, plate_nc=1, plate_conf=0.5, plate_iou=0.7,
-                 plate_max_det=300, plate_imgsz=640):
+                 plate_max_det=300, plate_imgsz=640, microbatch=0, microbatch_stage=2):
         lib = _lib.load()
         cfg = _lib.default_cfg()
         cfg.input_h, cfg.input_w = int(input_shape[0]), int(input_shape[1])
@@ -69,6 +69,8 @@ class Context:
         cfg.mosaic_level = int(mosaic_level)
         cfg.plate_nc, cfg.plate_conf, cfg.plate_iou = int(plate_nc), float(plate_conf), float(plate_iou)
         cfg.plate_max_det, cfg.plate_imgsz = int(plate_max_det), int(plate_imgsz)
+        # depth-first micro-batching of the backbone through layer<stage> (reserved[0..1])
+        cfg.reserved[0], cfg.reserved[1] = int(microbatch), int(microbatch_stage)
         self.cfg = cfg
         self.device = int(device)
         self.precision = "fp32" if cfg.precision == _lib.VD_PREC_FP32 else "bf16"
@@ -213,6 +215,15 @@ class Context:
         s = boxes.struct()
         check(self._lib.vdt_postprocess(self._h, ptr(loc), ptr(conf), n, ptr(hw), ctypes.byref(s)))
         return boxes
+
+    def plate_raw(self, frames):
+        """Raw YOLO head outputs [n][64+nc][A] (DFL logits | class logits), f32."""
+        p, n, h, w, pitch, where, keep = _frames_arg(frames)
+        A = ctypes.c_int()
+        check(self._lib.vdt_plate_raw(self._h, p, n, h, w, pitch, where, None, ctypes.byref(A)))
+        out = np.zeros((n, 64 + self.cfg.plate_nc, A.value), np.float32)
+        check(self._lib.vdt_plate_raw(self._h, p, n, h, w, pitch, where, ptr(out), ctypes.byref(A)))
+        return out
 
     def conv2d(self, x, w, stride=1, pad=0, scale=None, shift=None, act=0, slope=0.0, res=None, res_mode=0):
         """x: f32 NHWC [n,h,w,cin]; w: f32 [cout,cin,kh,kw] -> f32 NHWC."""

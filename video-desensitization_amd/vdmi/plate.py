@@ -1,0 +1,110 @@
+"""Drop-in for the ultralytics plate detector the reference drives
+(``YOLO(plate_model_path).cuda()`` at combine_detect.py:872, called as
+``plate_detector(batch_images, verbose=False, conf=0.5)`` at :217 and probed with
+``next(plate_detector.model.parameters()).device`` at :876).
+
+``__call__`` returns one ``Results``-like object per image whose ``.boxes``
+carries ``xyxy`` / ``conf`` / ``cls`` (numpy, source pixels, NMS order), as
+ultralytics does [ext]. Note the reference never uses them: its tuple check at
+combine_detect.py:239 always yields [] for Results objects. ``vdmi.pipeline``
+reproduces that by default and offers the intended behaviour as an option.
+
+Architecture: YOLOv8n. The weights (best.pt) are a
+pickled ultralytics object that cannot be loaded here without executing it; a
+converted state_dict (``model.<i>...`` keys) or seeded random weights are used.
+"""
+import os
+import warnings
+
+import numpy as np
+
+from . import _lib
+from .context import Context
+from .weights import yolov8n_state_dict
+
+
+class Boxes:
+    def __init__(self, xyxy, conf, cls):
+        self.xyxy, self.conf, self.cls = xyxy, conf, cls
+        self.data = np.concatenate([xyxy, conf[:, None], cls[:, None].astype(np.float32)], 1) if len(xyxy) else \
+            np.zeros((0, 6), np.float32)
+
+    def __len__(self):
+        return len(self.xyxy)
+
+
+class Results:
+    def __init__(self, orig_img, boxes, names):
+        self.orig_img = orig_img
+        self.orig_shape = orig_img.shape[:2]
+        self.boxes = boxes
+        self.names = names
+
+    def __len__(self):
+        return len(self.boxes)
+
+
+class _ModelProxy:
+    """``.parameters()`` for combine_detect.py:876."""
+
+    def __init__(self, device):
+        self._device = device
+
+    def parameters(self):
+        try:
+            import torch
+            yield torch.nn.Parameter(torch.empty(0, device=self._device))
+        except Exception:   # torch absent: a stand-in with .device
+            yield type("P", (), {"device": self._device})()
+
+
+class YOLO:
+    """ultralytics-style plate detector on libvdmi."""
+
+    def __init__(self, model="best.pt", nc=1, weights=None, precision="bf16", max_batch=64, device_index=0,
+                 seed=0, imgsz=640, iou=0.7, max_det=300, names=None):
+        self.nc = nc
+        self.names = names or {i: f"plate{i}" if nc > 1 else "plate" for i in range(nc)}
+        self.device_index = device_index
+        self.max_batch = max_batch
+        self.ctx = Context(device=device_index, precision=precision, max_batch=max_batch, plate_nc=nc,
+                           plate_iou=iou, plate_max_det=max_det, plate_imgsz=imgsz)
+        if weights is None:
+            if model and os.path.exists(model) and not model.endswith(".pt"):
+                from .weights import unpack_vdw
+                weights = unpack_vdw(open(model, "rb").read())
+            else:
+                if model and os.path.exists(model):
+                    warnings.warn(f"{model}: pickled ultralytics checkpoints are not loaded (they execute code); "
+                                  "convert to a state_dict / VDW1 file. Using seeded random weights.")
+                weights = yolov8n_state_dict(seed, nc)
+        self.ctx.load_weights(_lib.VD_NET_YOLOV8N, weights)
+        self.model = _ModelProxy(f"cuda:{device_index}")
+        self._conf = 0.5
+
+    def cuda(self):
+        return self
+
+    def predict(self, source, conf=0.5, verbose=False, **_):
+        return self(source, conf=conf, verbose=verbose)
+
+    def __call__(self, source, verbose=False, conf=0.5, **_):
+        imgs = source if isinstance(source, list) else [source]
+        if abs(conf - self.ctx.cfg.plate_conf) > 1e-12:
+            raise ValueError(f"conf={conf} differs from the context's plate_conf={self.ctx.cfg.plate_conf}")
+        out = [None] * len(imgs)
+        groups = {}
+        for i, im in enumerate(imgs):
+            groups.setdefault(im.shape[:2], []).append(i)
+        for (h, w), idx in groups.items():
+            for s in range(0, len(idx), self.max_batch):
+                chunk = idx[s:s + self.max_batch]
+                batch = np.stack([imgs[i] for i in chunk]) if len(chunk) > 1 else imgs[chunk[0]][None]
+                bx = self.ctx.detect_plates(np.ascontiguousarray(batch, np.uint8))
+                for j, i in enumerate(chunk):
+                    _, xf, sc, lab = bx.frame(j)
+                    out[i] = Results(imgs[i], Boxes(xf.copy(), sc.copy(), lab.astype(np.float32)), self.names)
+        return out
+
+
+PlateDetector = YOLO
