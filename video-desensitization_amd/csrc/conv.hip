@@ -25,6 +25,8 @@
 //   Block -> tile mapping is XCD-aware: blocks that share an A (pixel) panel
 //   are placed on one XCD so the panel is fetched into that XCD's L2 once.
 #include "vd_common.h"
+#include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 namespace {
@@ -52,7 +54,12 @@ __device__ __forceinline__ float load_elem(const void* p, size_t off) {
     else return (float)((const __bf16*)p)[off];
 }
 
-template <typename T, int BM, int BN, bool DENSE>
+// 16 zero bytes: the LDS-DMA source of padding taps (conv zero padding, K padding).
+__device__ __attribute__((aligned(16))) unsigned vd_zero16[4] = {0u, 0u, 0u, 0u};
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+template <typename T, int BM, int BN, bool DENSE, bool GLDS>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
     constexpr int VEC = Elem<T>::VEC;
     constexpr int BKE = 8 * VEC;                 // K elements per 128-byte tile row
@@ -64,10 +71,12 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
     constexpr int KSTEP = std::is_same<T, float>::value ? 16 : 32;  // K per fragment step
     constexpr int NKS = BKE / KSTEP;                                 // = 2
     constexpr int BUF = (BM + BN) * 128;
-    constexpr int EPI = BM * (BN + 4) * 4;
-    constexpr int SMEM = (2 * BUF > EPI) ? 2 * BUF : EPI;
+    constexpr int EPLD = BN + 4;                 // f32 epilogue row stride (conflict-free fragment writes)
+    constexpr int CG = BN / 8;                   // 8-channel groups per output row
+    constexpr int ITEMS = BM * CG / 256;         // epilogue items (row, 8 channels) per thread
 
-    __shared__ __attribute__((aligned(16))) char smem[SMEM];
+    // dynamic LDS: 2 K buffers (1 when K fits one tile) | the f32 epilogue tile, half at a time
+    extern __shared__ __attribute__((aligned(16))) char smem[];
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid / WAVES_N, wn = wid % WAVES_N;
@@ -146,135 +155,225 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
             *(u32x4*)(Bs_ + lds_off(rbase + 32 * i, chunk)) = rb[i];                      \
     } while (0)
 
+    // LDS-DMA form: every lane DMAs its 16-B chunk straight into the K buffer.
+    // The destination is lane-linear (wave w, instruction i -> rows w*8+32i ..
+    // +7, slot = lane&7), so the XOR swizzle moves to the SOURCE: the lane
+    // fetches logical chunk (lane&7) ^ swz(row) (rule: swizzle both sides or
+    // neither). Padding taps read the zero page.
+    const int lchunk = (tid & 7) ^ ((rbase >> 1) & 7);
+    const T* wbase_g = (const T*)a.w + (size_t)(n0 + rbase) * a.kpad + lchunk * VEC;
+#define VD_GLDS_TILE(kt, buf)                                                              \
+    do {                                                                                  \
+        int dy, dx, c;                                                                    \
+        bool kval = true;                                                                 \
+        if constexpr (DENSE) {                                                            \
+            dy = t_kh; dx = t_kw; c = t_c + lchunk * VEC;                                 \
+        } else {                                                                          \
+            const int kv = (kt) * 8 + lchunk;                                             \
+            const int tap = kv / cvec;                                                    \
+            c = (kv - tap * cvec) * VEC;                                                  \
+            kval = tap < ntap;                                                            \
+            dy = tap / a.kw; dx = tap - dy * a.kw;                                        \
+        }                                                                                 \
+        char* As_ = smem + (buf) * BUF;                                                   \
+        char* Bs_ = As_ + BM * 128;                                                       \
+        _Pragma("unroll") for (int i = 0; i < A_IT; ++i) {                                \
+            const int iy = iy0[i] + dy, ix = ix0[i] + dx;                                 \
+            const bool ok = kval && (unsigned)iy < (unsigned)a.xh && (unsigned)ix < (unsigned)a.xw; \
+            const void* src = ok ? (const void*)(xrow[i] + ((size_t)iy * a.xw + ix) * a.ldx + c) \
+                                 : (const void*)vd_zero16;                                \
+            __builtin_amdgcn_global_load_lds(src, (lds_void_t*)(As_ + (wid * 8 + 32 * i) * 128), 16, 0, 0); \
+        }                                                                                 \
+        _Pragma("unroll") for (int i = 0; i < B_IT; ++i)                                  \
+            __builtin_amdgcn_global_load_lds(                                             \
+                (const void*)(wbase_g + (size_t)(32 * i) * a.kpad + (size_t)(kt) * BKE),   \
+                (lds_void_t*)(Bs_ + (wid * 8 + 32 * i) * 128), 16, 0, 0);                  \
+        if constexpr (DENSE) {                                                            \
+            t_c += BKE;                                                                   \
+            if (t_c >= a.cin_pad) { t_c = 0; if (++t_kw == a.kw) { t_kw = 0; ++t_kh; } } \
+        }                                                                                 \
+    } while (0)
+
     f32x4_t acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-    VD_LOAD_TILE(0);
-    VD_STORE_TILE(0);
-    __syncthreads();
+    // one K tile of fragment reads + MFMAs from LDS buffer `buf`
+#define VD_COMPUTE(buf)                                                                     \
+    do {                                                                                  \
+        const char* As = smem + (buf) * BUF;                                              \
+        const char* Bs = As + BM * 128;                                                   \
+        _Pragma("unroll") for (int ks = 0; ks < NKS; ++ks) {                              \
+            const int ch = ks * 4 + (lane >> 4);                                          \
+            u32x4 af[TM], bfr[TN];                                                        \
+            _Pragma("unroll") for (int i = 0; i < TM; ++i)                                \
+                af[i] = *(const u32x4*)(As + lds_off(wm * WTM + i * 16 + (lane & 15), ch)); \
+            _Pragma("unroll") for (int j = 0; j < TN; ++j)                                \
+                bfr[j] = *(const u32x4*)(Bs + lds_off(wn * WTN + j * 16 + (lane & 15), ch)); \
+            _Pragma("unroll") for (int i = 0; i < TM; ++i)                                \
+            _Pragma("unroll") for (int j = 0; j < TN; ++j) {                              \
+                if constexpr (std::is_same<T, float>::value) {                            \
+                    const float* fa = (const float*)&af[i];                               \
+                    const float* fb = (const float*)&bfr[j];                              \
+                    _Pragma("unroll") for (int e = 0; e < 4; ++e)                         \
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[e], fb[e], acc[i][j], 0, 0, 0); \
+                } else {                                                                  \
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(                  \
+                        __builtin_bit_cast(bf16x8_t, af[i]), __builtin_bit_cast(bf16x8_t, bfr[j]), \
+                        acc[i][j], 0, 0, 0);                                              \
+                }                                                                         \
+            }                                                                             \
+        }                                                                                 \
+    } while (0)
 
-    for (int kt = 0; kt < nk; ++kt) {
-        const int cur = kt & 1;
-        if (kt + 1 < nk) VD_LOAD_TILE(kt + 1);
-        const char* As = smem + cur * BUF;
-        const char* Bs = As + BM * 128;
-#pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) {
-            const int ch = ks * 4 + (lane >> 4);
-            u32x4 af[TM], bfr[TN];
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-                af[i] = *(const u32x4*)(As + lds_off(wm * WTM + i * 16 + (lane & 15), ch));
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-                bfr[j] = *(const u32x4*)(Bs + lds_off(wn * WTN + j * 16 + (lane & 15), ch));
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j) {
-                    if constexpr (std::is_same<T, float>::value) {
-                        const float* fa = (const float*)&af[i];
-                        const float* fb = (const float*)&bfr[j];
-#pragma unroll
-                        for (int e = 0; e < 4; ++e)
-                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[e], fb[e], acc[i][j], 0, 0, 0);
-                    } else {
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                            __builtin_bit_cast(bf16x8_t, af[i]), __builtin_bit_cast(bf16x8_t, bfr[j]),
-                            acc[i][j], 0, 0, 0);
-                    }
-                }
-        }
-        if (kt + 1 < nk) VD_STORE_TILE(cur ^ 1);
-        __syncthreads();
-    }
-
-    // ---- fused epilogue ----
-    // Stage the f32 accumulator tile through LDS ([BM][BN+4], conflict-free
-    // 16x16 fragment writes), then each thread owns 8 consecutive channels of a
-    // row: 16-B residual loads and 16-B (bf16) / 32-B (f32) stores, coalesced
-    // along the NHWC channel dimension.
-    float* ep = (float*)smem;
-    constexpr int EPLD = BN + 4;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                ep[(wm * WTM + i * 16 + (lane >> 4) * 4 + r) * EPLD + wn * WTN + j * 16 + (lane & 15)] = acc[i][j][r];
-    __syncthreads();
+    // Residual prefetch: the epilogue's 16-B residual vectors are loaded now, so
+    // their latency overlaps the K loop instead of following it (c3 / FPN convs).
     const bool vec_ok = ((a.cout & 7) == 0) && ((a.ldy & 7) == 0) && ((a.ycoff & 7) == 0) &&
                         (a.res_mode == VD_RES_NONE || (((a.res_ld | a.res_coff) & 7) == 0));
-    constexpr int CG = BN / 8;                     // 8-channel groups per row
-    for (int it = tid; it < BM * CG; it += 256) {
-        const int rr = it / CG, cg = it - rr * CG;
-        const int m = m0 + rr;
-        const int nb = n0 + cg * 8;
-        if (m >= a.M || nb >= a.cout) continue;
+    // (bf16 only; the exact-f32 parity mode reads its residual in the epilogue)
+    const bool pf = vec_ok && a.res_mode != VD_RES_NONE && !std::is_same<T, float>::value;
+    u32x4 rpf[ITEMS];
+#pragma unroll
+    for (int q = 0; q < ITEMS; ++q) {
+        const int it = tid + 256 * q;
+        const int m = m0 + it / CG, nb = n0 + (it % CG) * 8;
+        const bool ok = pf && m < a.M && nb < a.cout;
         size_t roff = 0;
-        if (a.res_mode != VD_RES_NONE) {
+        if (ok) {
             if (a.res_up) {
                 const int b = m / ohw, rem = m - b * ohw;
                 const int oy = rem / a.yw, ox = rem - oy * a.yw;
-                roff = ((size_t)(b * a.rh + (oy >> 1)) * a.rw + (ox >> 1)) * a.res_ld + a.res_coff;
+                roff = ((size_t)(b * a.rh + (oy >> 1)) * a.rw + (ox >> 1)) * a.res_ld + a.res_coff + nb;
             } else {
-                roff = (size_t)m * a.res_ld + a.res_coff;
+                roff = (size_t)m * a.res_ld + a.res_coff + nb;
             }
         }
-        const float* er = ep + rr * EPLD + cg * 8;
-        const size_t yo = (size_t)m * a.ldy + a.ycoff + nb;
-        if (vec_ok) {
-            float v[8], rv[8];
-            const float4 s0 = *(const float4*)(a.scale + nb), s1 = *(const float4*)(a.scale + nb + 4);
-            const float4 h0 = *(const float4*)(a.shift + nb), h1 = *(const float4*)(a.shift + nb + 4);
-            const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-            const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-            const float4 e0 = *(const float4*)er, e1 = *(const float4*)(er + 4);
-            const float ev[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
-            if (a.res_mode != VD_RES_NONE) {
-                if constexpr (std::is_same<T, float>::value) {
-                    const float4 r0 = *(const float4*)((const float*)a.res + roff + nb);
-                    const float4 r1 = *(const float4*)((const float*)a.res + roff + nb + 4);
-                    rv[0] = r0.x; rv[1] = r0.y; rv[2] = r0.z; rv[3] = r0.w;
-                    rv[4] = r1.x; rv[5] = r1.y; rv[6] = r1.z; rv[7] = r1.w;
-                } else {
-                    const u32x4 u = *(const u32x4*)((const __bf16*)a.res + roff + nb);
-                    const __bf16* rb = (const __bf16*)&u;
+        const T* rp = ok ? (const T*)a.res + roff : xsafe;
+        rpf[q] = *(const u32x4*)rp;
+    }
+
+    if constexpr (GLDS) {
+        // Two LDS buffers, tile kt+1 in flight while kt is consumed. Raw barriers
+        // with counted vmcnt: __syncthreads() would add vmcnt(0) and drain the DMA.
+        constexpr int LPT = A_IT + B_IT;                 // DMA instructions per lane per tile
+        VD_GLDS_TILE(0, 0);
+        if (nk > 1) VD_GLDS_TILE(1, 1);
+        for (int kt = 0; kt < nk; ++kt) {
+            if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPT) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            VD_COMPUTE(kt & 1);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            if (kt + 2 < nk) VD_GLDS_TILE(kt + 2, kt & 1);
+        }
+    } else {
+        VD_LOAD_TILE(0);
+        VD_STORE_TILE(0);
+        __syncthreads();
+        for (int kt = 0; kt < nk; ++kt) {
+            const int cur = kt & 1;
+            if (kt + 1 < nk) VD_LOAD_TILE(kt + 1);
+            VD_COMPUTE(cur);
+            if (kt + 1 < nk) VD_STORE_TILE(cur ^ 1);
+            __syncthreads();
+        }
+    }
+
+    // ---- fused epilogue ----
+    // The f32 accumulator tile goes through LDS one half (BM/2 rows) at a time
+    // ([BM/2][BN+4], conflict-free fragment writes); each thread then owns 8
+    // consecutive channels of a row: 16-B (bf16) / 32-B (f32) stores coalesced
+    // along the NHWC channel dimension, with the prefetched residual.
+    float* ep = (float*)smem;
 #pragma unroll
-                    for (int e = 0; e < 8; ++e) rv[e] = (float)rb[e];
+    for (int h = 0; h < 2; ++h) {
+        if (h) __syncthreads();
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int row0 = wm * WTM + i * 16;
+            if (row0 / (BM / 2) != h) continue;
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    ep[(row0 - h * (BM / 2) + (lane >> 4) * 4 + r) * EPLD + wn * WTN + j * 16 + (lane & 15)] =
+                        acc[i][j][r];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = h * (ITEMS / 2); q < (h + 1) * (ITEMS / 2); ++q) {
+            const int it = tid + 256 * q;
+            const int rr = it / CG, cg = it % CG;
+            const int m = m0 + rr;
+            const int nb = n0 + cg * 8;
+            if (m >= a.M || nb >= a.cout) continue;
+            const float* er = ep + (rr - h * (BM / 2)) * EPLD + cg * 8;
+            const size_t yo = (size_t)m * a.ldy + a.ycoff + nb;
+            if (vec_ok) {
+                float v[8], rv[8];
+                const float4 s0 = *(const float4*)(a.scale + nb), s1 = *(const float4*)(a.scale + nb + 4);
+                const float4 h0 = *(const float4*)(a.shift + nb), h1 = *(const float4*)(a.shift + nb + 4);
+                const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+                const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+                const float4 e0 = *(const float4*)er, e1 = *(const float4*)(er + 4);
+                const float ev[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+                if (pf) {
+                    const bf16x8_t rb8 = __builtin_bit_cast(bf16x8_t, rpf[q]);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) rv[e] = (float)rb8[e];
+                } else if (a.res_mode != VD_RES_NONE) {   // f32 residual, read here
+                    size_t roff;
+                    if (a.res_up) {
+                        const int b = m / ohw, rem = m - b * ohw;
+                        const int oy = rem / a.yw, ox = rem - oy * a.yw;
+                        roff = ((size_t)(b * a.rh + (oy >> 1)) * a.rw + (ox >> 1)) * a.res_ld + a.res_coff + nb;
+                    } else {
+                        roff = (size_t)m * a.res_ld + a.res_coff + nb;
+                    }
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) rv[e] = load_elem<T>(a.res, roff + e);
                 }
-            }
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                float t = ev[e] * sc[e] + sh[e];
-                if (a.res_mode == VD_RES_PRE_ACT) t += rv[e];
-                t = act_apply(t, a.act, a.slope);
-                if (a.res_mode == VD_RES_POST_ACT) t += rv[e];
-                v[e] = t;
-            }
-            if (a.out_f32 || std::is_same<T, float>::value) {
-                *(float4*)((float*)a.y + yo) = make_float4(v[0], v[1], v[2], v[3]);
-                *(float4*)((float*)a.y + yo + 4) = make_float4(v[4], v[5], v[6], v[7]);
+                for (int e = 0; e < 8; ++e) {
+                    float t = ev[e] * sc[e] + sh[e];
+                    if (a.res_mode == VD_RES_PRE_ACT) t += rv[e];
+                    t = act_apply(t, a.act, a.slope);
+                    if (a.res_mode == VD_RES_POST_ACT) t += rv[e];
+                    v[e] = t;
+                }
+                if (a.out_f32 || std::is_same<T, float>::value) {
+                    *(float4*)((float*)a.y + yo) = make_float4(v[0], v[1], v[2], v[3]);
+                    *(float4*)((float*)a.y + yo + 4) = make_float4(v[4], v[5], v[6], v[7]);
+                } else {
+                    bf16x8_t o;
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) o[e] = (__bf16)v[e];
+                    *(bf16x8_t*)((__bf16*)a.y + yo) = o;
+                }
             } else {
-                bf16x8_t o;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) o[e] = (__bf16)v[e];
-                *(bf16x8_t*)((__bf16*)a.y + yo) = o;
-            }
-        } else {
-            for (int e = 0; e < 8 && nb + e < a.cout; ++e) {
-                const int n = nb + e;
-                float t = er[e] * a.scale[n] + a.shift[n];
-                const float rv = a.res_mode != VD_RES_NONE ? load_elem<T>(a.res, roff + n) : 0.f;
-                if (a.res_mode == VD_RES_PRE_ACT) t += rv;
-                t = act_apply(t, a.act, a.slope);
-                if (a.res_mode == VD_RES_POST_ACT) t += rv;
-                if (a.out_f32 || std::is_same<T, float>::value) ((float*)a.y)[yo + e] = t;
-                else ((__bf16*)a.y)[yo + e] = (__bf16)t;
+                size_t roff = 0;
+                if (a.res_mode != VD_RES_NONE) {
+                    if (a.res_up) {
+                        const int b = m / ohw, rem = m - b * ohw;
+                        const int oy = rem / a.yw, ox = rem - oy * a.yw;
+                        roff = ((size_t)(b * a.rh + (oy >> 1)) * a.rw + (ox >> 1)) * a.res_ld + a.res_coff;
+                    } else {
+                        roff = (size_t)m * a.res_ld + a.res_coff;
+                    }
+                }
+                for (int e = 0; e < 8 && nb + e < a.cout; ++e) {
+                    const int n = nb + e;
+                    float t = er[e] * a.scale[n] + a.shift[n];
+                    const float rv = a.res_mode != VD_RES_NONE ? load_elem<T>(a.res, roff + n) : 0.f;
+                    if (a.res_mode == VD_RES_PRE_ACT) t += rv;
+                    t = act_apply(t, a.act, a.slope);
+                    if (a.res_mode == VD_RES_POST_ACT) t += rv;
+                    if (a.out_f32 || std::is_same<T, float>::value) ((float*)a.y)[yo + e] = t;
+                    else ((__bf16*)a.y)[yo + e] = (__bf16)t;
+                }
             }
         }
     }
@@ -282,15 +381,27 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
 
 #undef VD_LOAD_TILE
 #undef VD_STORE_TILE
+#undef VD_GLDS_TILE
+#undef VD_COMPUTE
 
 template <typename T, int BM, int BN>
 hipError_t launch_bn(const ConvArgs& a0, bool dense, hipStream_t s) {
+    static const bool glds = [] { const char* e = getenv("VD_CONV_GLDS"); return !e || atoi(e) != 0; }();
     ConvArgs a = a0;
     a.ntiles_n = (a.cout + BN - 1) / BN;
     const int mt = (a.M + BM - 1) / BM;
     dim3 grid(mt * a.ntiles_n), block(256);
-    if (dense) hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, true>), grid, block, 0, s, a);
-    else hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, false>), grid, block, 0, s, a);
+    constexpr int VEC = Elem<T>::VEC;
+    constexpr size_t BUF = (size_t)(BM + BN) * 128, EPI = (size_t)(BM / 2) * (BN + 4) * 4;
+    const int nk = a.kpad / (8 * VEC);
+    const size_t lds = std::max((nk > 1 ? 2 : 1) * BUF, EPI);
+    if (glds) {
+        if (dense) hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, true, true>), grid, block, lds, s, a);
+        else hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, false, true>), grid, block, lds, s, a);
+    } else {
+        if (dense) hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, true, false>), grid, block, lds, s, a);
+        else hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, false, false>), grid, block, lds, s, a);
+    }
     return hipGetLastError();
 }
 
