@@ -112,15 +112,13 @@ def main():
     pboxes = vdmi.DeviceBoxes(B, cap, dev) if plates else None
     stream = torch.cuda.current_stream(dev)
     ctx.set_stream(stream.cuda_stream)
-    rec = torch.empty((B, 1 + 4 * cap), dtype=torch.int32, device=dev)
-    gathered = torch.empty((world * B, 1 + 4 * cap), dtype=torch.int32, device=dev) if world > 1 else None
+    from vdmi.dist import all_gather_records, pack_records
+    rec_cap = 64                      # box record: count + 64 boxes per frame
 
     def step():
         ctx.process(frames, out, faces=faces, plates=pboxes, flags=flags)
         if world > 1:   # per-frame box records -> every rank (RCCL all-gather over xGMI)
-            rec[:, 0] = faces.count
-            rec[:, 1:] = faces.xyxy.view(B, -1)
-            dist.all_gather_into_tensor(gathered, rec)
+            all_gather_records(pack_records(faces.count, faces.xyxy, rec_cap))
 
     for _ in range(a.warmup):
         step()

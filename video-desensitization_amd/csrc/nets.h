@@ -108,6 +108,8 @@ struct Ctx {
     int device = 0;
     bool f32 = false;
     hipStream_t stream = nullptr, own_stream = nullptr;
+    hipStream_t stream2 = nullptr;               // plate branch runs beside the face branch
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::mutex mu;
     std::vector<void*> allocs;
     std::vector<Conv> convs;

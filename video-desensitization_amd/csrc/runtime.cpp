@@ -518,6 +518,13 @@ int vd_create(const vd_cfg* cfg, int device, vd_ctx** out) {
         return vd_set_error(VD_ERR_HIP, "hipStreamCreate failed");
     }
     ctx->stream = ctx->own_stream;
+    if (hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming) != hipSuccess) {
+        hipStreamDestroy(ctx->own_stream);
+        delete ctx;
+        return vd_set_error(VD_ERR_HIP, "stream/event creation failed");
+    }
     *out = (vd_ctx*)ctx;
     return VD_OK;
 }
@@ -534,6 +541,10 @@ int vd_destroy(vd_ctx* h) {
     if (ctx->stage_box2) hipFree(ctx->stage_box2);
     if (ctx->mosaic_table) hipFree(ctx->mosaic_table);
     for (auto& t : ctx->ev_pool) { hipEventDestroy(t.a); hipEventDestroy(t.b); }
+    hipStreamSynchronize(ctx->stream2);
+    hipEventDestroy(ctx->ev_fork);
+    hipEventDestroy(ctx->ev_join);
+    hipStreamDestroy(ctx->stream2);
     hipStreamDestroy(ctx->own_stream);
     delete ctx;
     return VD_OK;
@@ -686,14 +697,29 @@ int vd_process(vd_ctx* h, const uint8_t* in, uint8_t* out, int n, int fh, int fw
     }
     const uint8_t* d = ctx->frames_to_device(in, n, fh, pitch, where, &rc);
     if (rc) return rc;
+    // Face and plate branches run concurrently (the reference submits them to two
+    // threads, combine_detect.py:214-217): plates on stream2, forked/joined by events.
+    const bool fork = do_faces && do_plates;
+    if (fork) {
+        VD_CHECK_HIP(hipEventRecord(ctx->ev_fork, ctx->stream));
+        VD_CHECK_HIP(hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
+    }
     if (do_faces) {
         if ((rc = ctx->face_letterbox(d, n, fh, fw, pitch))) return rc;
         if ((rc = ctx->face_forward(n))) return rc;
         if ((rc = ctx->face_post(n, fh, fw, tf))) return rc;
     }
     if (do_plates) {
-        if ((rc = vd_plate_forward(*ctx, d, n, fh, fw, pitch))) return rc;
-        if ((rc = vd_plate_post(*ctx, n, fh, fw, tp))) return rc;
+        hipStream_t main = ctx->stream;
+        if (fork) ctx->stream = ctx->stream2;
+        rc = vd_plate_forward(*ctx, d, n, fh, fw, pitch);
+        if (!rc) rc = vd_plate_post(*ctx, n, fh, fw, tp);
+        ctx->stream = main;
+        if (rc) return rc;
+    }
+    if (fork) {
+        VD_CHECK_HIP(hipEventRecord(ctx->ev_join, ctx->stream2));
+        VD_CHECK_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
     }
     if (do_mosaic) {
         uint8_t* dout = out;
