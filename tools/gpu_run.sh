@@ -11,6 +11,7 @@ STEPS=("$@")
 [ ${#STEPS[@]} -eq 0 ] && STEPS=(tests smoke bench)
 BENCH_ARGS=${BENCH_ARGS:-"--steps 10 --warmup 3"}
 PYTEST_ARGS=${PYTEST_ARGS:-"tests -m gpu -x -q"}
+PYTEST_K=${PYTEST_K:-}   # optional -k expression (may contain spaces)
 
 run() {  # name timeout cmd...
     local name=$1 t=$2; shift 2
@@ -27,7 +28,8 @@ run() {  # name timeout cmd...
 
 for s in "${STEPS[@]}"; do
     case $s in
-        tests) run pytest_gpu 700 python -m pytest $PYTEST_ARGS ;;
+        tests) if [ -n "$PYTEST_K" ]; then run pytest_gpu 700 python -m pytest $PYTEST_ARGS -k "$PYTEST_K"
+               else run pytest_gpu 700 python -m pytest $PYTEST_ARGS; fi ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 400 python bench.py $BENCH_ARGS ;;
         prof)  run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;

@@ -36,7 +36,7 @@ namespace {
 constexpr int ROWS = 8;
 constexpr int TB_CAP = 512;    // band-list capacity; larger bands walk the global table
 constexpr int BOX_FAST = 256;  // frames with at most this many boxes take copy + box kernels
-constexpr int BOX_TILES = 8;   // workgroups per box
+constexpr int BOX_BLOCKS = 256; // workgroups per frame sharing its box pixels
 
 struct MBox { int x1, y1, x2, y2; int sw, sh, idx, valid; double fux, fdx, fuy, fdy; };
 
@@ -48,6 +48,7 @@ struct MosaicArgs {
     int vec_ok;                                      // 16-B aligned rows -> vector copies
     MBox* table; int tcap;                           // [n][tcap] prepared boxes
     uint64_t* ovl;                                   // [n][BOX_FAST][4] overlap bitmasks (fast path)
+    int* pref;                                       // [n][BOX_FAST+1] prefix sums of box areas (fast path)
 };
 
 __global__ __launch_bounds__(256) void mosaic_prep_kernel(MosaicArgs a) {
@@ -236,6 +237,31 @@ __global__ __launch_bounds__(256) void mosaic_overlap_kernel(MosaicArgs a) {
     o[0] = m[0]; o[1] = m[1]; o[2] = m[2]; o[3] = m[3];
 }
 
+// Per frame: exclusive prefix sum of the valid boxes' pixel counts (one block per frame).
+__global__ __launch_bounds__(256) void mosaic_prefix_kernel(MosaicArgs a) {
+    __shared__ int s[256];
+    const int f = blockIdx.x, k = threadIdx.x;
+    const int n0 = a.cnt0 ? min(a.cnt0[f], a.cap0) : 0;
+    const int n1 = a.cnt1 ? min(a.cnt1[f], a.cap1) : 0;
+    const int nb = n0 + n1;
+    int* pref = a.pref + (size_t)f * (BOX_FAST + 1);
+    if (nb > BOX_FAST) { if (k == 0) pref[0] = 0; return; }
+    int v = 0;
+    if (k < nb) {
+        const MBox b = a.table[(size_t)f * a.tcap + k];
+        if (b.valid) v = (b.x2 - b.x1) * (b.y2 - b.y1);
+    }
+    s[k] = v;
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {      // Hillis-Steele inclusive scan
+        const int t = k >= off ? s[k - off] : 0;
+        __syncthreads();
+        s[k] += t;
+        __syncthreads();
+    }
+    if (k <= nb) pref[k] = k == 0 ? 0 : s[k - 1];
+}
+
 // Highest set bit index < lim in a 256-bit mask, or -1.
 __device__ __forceinline__ int top_below(const uint64_t* m, int lim) {
     for (int w = (lim - 1) >> 6; w >= 0; --w) {
@@ -249,44 +275,49 @@ __device__ __forceinline__ int top_below(const uint64_t* m, int lim) {
 
 // Pixels of box k that no LATER box contains: walk k, then earlier boxes along the
 // overlap graph (a box containing a point of box j overlaps j), gather 3 bytes.
+// Work is balanced over the frame's flattened box-pixel index space
+// [0, sum of box areas): workgroup g of BOX_BLOCKS takes a strided share, and a
+// binary search over the area prefix sums maps an index to (box, pixel).
 __global__ __launch_bounds__(256) void mosaic_box_kernel(MosaicArgs a) {
     __shared__ MBox s_tab[BOX_FAST];
     __shared__ uint64_t s_ovl[BOX_FAST][4];
-    const int f = blockIdx.z;
-    const int k = blockIdx.y;
+    __shared__ int s_pref[BOX_FAST + 1];
+    const int f = blockIdx.y;
     const int n0 = a.cnt0 ? min(a.cnt0[f], a.cap0) : 0;
     const int n1 = a.cnt1 ? min(a.cnt1[f], a.cap1) : 0;
     const int nb = n0 + n1;
-    if (nb > BOX_FAST || k >= nb) return;
+    if (nb > BOX_FAST || nb == 0) return;
+    const int* pref = a.pref + (size_t)f * (BOX_FAST + 1);
+    const int total = pref[nb];
+    if (blockIdx.x * 256 >= total) return;
     const MBox* table = a.table + (size_t)f * a.tcap;
-    if (!table[k].valid) return;
     const uint64_t* ovl = a.ovl + (size_t)f * BOX_FAST * 4;
     for (int i = threadIdx.x; i < nb; i += 256) {
         s_tab[i] = table[i];
         s_ovl[i][0] = ovl[4 * i + 0]; s_ovl[i][1] = ovl[4 * i + 1];
         s_ovl[i][2] = ovl[4 * i + 2]; s_ovl[i][3] = ovl[4 * i + 3];
     }
+    for (int i = threadIdx.x; i <= nb; i += 256) s_pref[i] = pref[i];
     __syncthreads();
-    const MBox bk = s_tab[k];
-    const int bw = bk.x2 - bk.x1;
-    const int area = bw * (bk.y2 - bk.y1);
     const uint8_t* src = a.in + (size_t)f * a.h * a.pitch;
     uint8_t* dst = a.out + (size_t)f * a.h * a.pitch;
-    // later boxes overlapping k (the only ones that can own a pixel of k)
-    uint64_t later[4];
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-        const int lo = k + 1 - (w << 6);   // keep bits >= k+1
-        uint64_t v = s_ovl[k][w];
-        if (lo >= 64) v = 0; else if (lo > 0) v &= ~((1ULL << lo) - 1ULL);
-        later[w] = v;
-    }
-    for (int p = blockIdx.x * 256 + threadIdx.x; p < area; p += BOX_TILES * 256) {
-        const int y0 = bk.y1 + p / bw, x0 = bk.x1 + p % bw;
+    for (int t = blockIdx.x * 256 + threadIdx.x; t < total; t += gridDim.x * 256) {
+        int lo = 0, hi = nb - 1;                    // largest k with s_pref[k] <= t
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_pref[mid] <= t) lo = mid; else hi = mid - 1;
+        }
+        const int k = lo;
+        const MBox& bk = s_tab[k];
+        const int bw = bk.x2 - bk.x1;
+        const int p = t - s_pref[k];
+        const int py = p / bw;
+        const int y0 = bk.y1 + py, x0 = bk.x1 + (p - py * bw);
         bool owned = true;
-#pragma unroll
-        for (int w = 0; w < 4 && owned; ++w) {
-            uint64_t v = later[w];
+        for (int w = (k + 1) >> 6; w < 4 && owned; ++w) {       // later boxes overlapping k
+            uint64_t v = s_ovl[k][w];
+            const int lo_bit = k + 1 - (w << 6);
+            if (lo_bit > 0) v &= ~((1ULL << lo_bit) - 1ULL);
             while (v && owned) {
                 const int j = (w << 6) + __ffsll((long long)v) - 1;
                 v &= v - 1;
@@ -313,7 +344,9 @@ __global__ __launch_bounds__(256) void mosaic_box_kernel(MosaicArgs a) {
 
 }  // namespace
 
-size_t vd_mosaic_table_bytes(int n, int tcap) { return (size_t)n * tcap * sizeof(MBox) + (size_t)n * BOX_FAST * 32; }
+size_t vd_mosaic_table_bytes(int n, int tcap) {
+    return (size_t)n * tcap * sizeof(MBox) + (size_t)n * BOX_FAST * 32 + (size_t)n * (BOX_FAST + 1) * 4;
+}
 
 hipError_t vd_launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w, size_t pitch,
                             const int* cnt0, const int* xy0, int cap0,
@@ -321,8 +354,9 @@ hipError_t vd_launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w
                             hipStream_t s) {
     const int vec_ok = (pitch % 16 == 0) && ((uintptr_t)in % 16 == 0) && ((uintptr_t)out % 16 == 0);
     const int tcap = (cnt0 ? cap0 : 0) + (cnt1 ? cap1 : 0);
+    char* tail = (char*)table + (size_t)n * tcap * sizeof(MBox);
     MosaicArgs a{in, out, n, h, w, pitch, cnt0, xy0, cap0, cnt1, xy1, cap1, level, vec_ok, (MBox*)table, tcap,
-                 (uint64_t*)((char*)table + vd_mosaic_table_bytes(n, tcap) - (size_t)n * BOX_FAST * 32)};
+                 (uint64_t*)tail, (int*)(tail + (size_t)n * BOX_FAST * 32)};
     if (tcap > 0)
         hipLaunchKernelGGL(mosaic_prep_kernel, dim3((tcap + 255) / 256, n), dim3(256), 0, s, a);
     // fast path: copy (~1 MiB per workgroup row of the grid) then owned-pixel gathers
@@ -331,7 +365,8 @@ hipError_t vd_launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w
     hipLaunchKernelGGL(mosaic_copy_kernel, dim3(cblocks, n), dim3(256), 0, s, a);
     if (tcap > 0) {
         hipLaunchKernelGGL(mosaic_overlap_kernel, dim3(1, n), dim3(256), 0, s, a);
-        hipLaunchKernelGGL(mosaic_box_kernel, dim3(BOX_TILES, std::min(tcap, BOX_FAST), n), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(mosaic_prefix_kernel, dim3(n), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(mosaic_box_kernel, dim3(BOX_BLOCKS, n), dim3(256), 0, s, a);
         // frames with more boxes than the fast path holds
         hipLaunchKernelGGL(mosaic_kernel, dim3((h + ROWS - 1) / ROWS, n), dim3(256), 0, s, a);
     }
