@@ -41,24 +41,21 @@ def face_plan(B=64, H=640, W=640):
 
 def main(path, B=64):
     allk = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-    lb = [i for i, r in enumerate(allk) if "letterbox_kernel" in r["Kernel_Name"]]
     plan = face_plan(B)
-    # the face forward of the last step: conv launches after the last face letterbox
-    # (when plates run, the last letterbox is the plate one; take the one before it)
-    face_lb = lb[-1]
-    after = [r for r in allk[face_lb:] if "conv_igemm" in r["Kernel_Name"]]
-    if len(after) > len(plan) + 8:
-        face_lb = lb[-1]
-    elif len(lb) > 1 and len(after) < len(plan):
-        face_lb = lb[-2]
-    last = [r for r in allk[face_lb:] if "conv_igemm" in r["Kernel_Name"]][:len(plan)]
+    # The face forward may share the GPU with the plate network on a second
+    # stream: find the last stem launch (its grid is M/128 workgroups of 256)
+    # and take the conv launches that follow it on the same stream.
+    stem_grid = str((plan[0][1] + 127) // 128 * 256)
+    convs = [r for r in allk if "conv_igemm" in r["Kernel_Name"] or "conv1x1_stream" in r["Kernel_Name"]]
+    si = max(i for i, r in enumerate(convs) if r["Grid_Size_X"] == stem_grid)
+    last = [r for r in convs[si:] if r["Stream_Id"] == convs[si]["Stream_Id"]][:len(plan)]
     tot_t = tot_f = 0
     for (name, M, N, K), r in zip(plan, last):
         dt = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
         fl = 2.0 * M * N * K
         tot_t += dt
         tot_f += fl
-        kn = r["Kernel_Name"].split("conv_igemm_kernel")[1][:22]
+        kn = r["Kernel_Name"].replace("conv1x1_stream_kernel", "S:").replace("conv_igemm_kernel", "G:").split("_1")[-1][:26]
         print(f"{name:12s} M={M:8d} N={N:5d} K={K:5d} {dt*1e6:8.1f} us {fl/dt/1e12:7.1f} TF/s  {kn}")
     print(f"total {tot_t*1e3:.2f} ms  {tot_f/tot_t/1e12:.1f} TF/s")
 

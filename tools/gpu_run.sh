@@ -10,6 +10,8 @@ export TMPDIR=/tmp
 STEPS=("$@")
 [ ${#STEPS[@]} -eq 0 ] && STEPS=(tests smoke bench)
 BENCH_ARGS=${BENCH_ARGS:-"--steps 10 --warmup 3"}
+PROF_ARGS=${PROF_ARGS:-"--steps 5 --warmup 2 --no-cpu-baseline"}
+PMC_ARGS=${PMC_ARGS:-"--steps 3 --warmup 1 --no-cpu-baseline --no-timing"}
 PYTEST_ARGS=${PYTEST_ARGS:-"tests -m gpu -x -q"}
 PYTEST_K=${PYTEST_K:-}   # optional -k expression (may contain spaces)
 
@@ -32,9 +34,9 @@ for s in "${STEPS[@]}"; do
                else run pytest_gpu 700 python -m pytest $PYTEST_ARGS; fi ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 400 python bench.py $BENCH_ARGS ;;
-        prof)  run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
-        pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-timing &&
-               run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-timing ;;
+        prof)  run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py $PROF_ARGS ;;
+        pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py $PMC_ARGS &&
+               run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py $PMC_ARGS ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done

@@ -59,23 +59,29 @@ __device__ __attribute__((aligned(16))) unsigned vd_zero16[4] = {0u, 0u, 0u, 0u}
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-template <typename T, int BM, int BN, bool DENSE, bool GLDS>
-__global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
+// NT threads (4 or 8 waves); STAGES = 2: one tile in flight, two barriers per
+// K tile; STAGES = 3 (LDS-DMA only): two tiles in flight, one barrier per K tile.
+template <typename T, int BM, int BN, int NT, int STAGES, bool DENSE, bool GLDS>
+__global__ __launch_bounds__(NT) void conv_igemm_kernel(ConvArgs a) {
     constexpr int VEC = Elem<T>::VEC;
     constexpr int BKE = 8 * VEC;                 // K elements per 128-byte tile row
+    constexpr int WAVES = NT / 64;
     constexpr int WAVES_N = (BN >= 64) ? 2 : 1;
-    constexpr int WAVES_M = 4 / WAVES_N;
+    constexpr int WAVES_M = WAVES / WAVES_N;
     constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
     constexpr int TM = WTM / 16, TN = WTN / 16;
-    constexpr int A_IT = BM / 32, B_IT = BN / 32;
+    constexpr int ROWS = NT / 8;                 // tile rows covered by one pass of 16-B chunks
+    constexpr int A_IT = BM / ROWS, B_IT = BN / ROWS;
+    static_assert(BM % ROWS == 0 && BN % ROWS == 0 && (STAGES == 2 || GLDS), "tile shape");
     constexpr int KSTEP = std::is_same<T, float>::value ? 16 : 32;  // K per fragment step
     constexpr int NKS = BKE / KSTEP;                                 // = 2
     constexpr int BUF = (BM + BN) * 128;
     constexpr int EPLD = BN + 4;                 // f32 epilogue row stride (conflict-free fragment writes)
     constexpr int CG = BN / 8;                   // 8-channel groups per output row
-    constexpr int ITEMS = BM * CG / 256;         // epilogue items (row, 8 channels) per thread
+    constexpr int ITEMS = BM * CG / NT;          // epilogue items (row, 8 channels) per thread
+    constexpr int EP = (ITEMS % 4 == 0) ? 4 : 2; // epilogue passes (BM/EP rows staged per pass)
 
-    // dynamic LDS: 2 K buffers (1 when K fits one tile) | the f32 epilogue tile, half at a time
+    // dynamic LDS: STAGES K buffers (1 when K fits one tile) | the f32 epilogue tile, BM/EP rows at a time
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -95,7 +101,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
     const int ohw = a.yh * a.yw;
 #pragma unroll
     for (int i = 0; i < A_IT; ++i) {
-        int m = m0 + rbase + 32 * i;
+        int m = m0 + rbase + ROWS * i;
         if (m < a.M) {
             int b = m / ohw, rem = m - b * ohw;
             int oy = rem / a.yw, ox = rem - oy * a.yw;
@@ -139,7 +145,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
             ra[i] = ok ? v : u32x4{0u, 0u, 0u, 0u};                                       \
         }                                                                                 \
         _Pragma("unroll") for (int i = 0; i < B_IT; ++i)                                  \
-            rb[i] = *(const u32x4*)(wbase + (size_t)(32 * i) * a.kpad + (size_t)(kt) * BKE); \
+            rb[i] = *(const u32x4*)(wbase + (size_t)(ROWS * i) * a.kpad + (size_t)(kt) * BKE); \
         if constexpr (DENSE) {                                                            \
             t_c += BKE;                                                                   \
             if (t_c >= a.cin_pad) { t_c = 0; if (++t_kw == a.kw) { t_kw = 0; ++t_kh; } } \
@@ -150,9 +156,9 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
         char* As_ = smem + (buf) * BUF;                                                   \
         char* Bs_ = As_ + BM * 128;                                                       \
         _Pragma("unroll") for (int i = 0; i < A_IT; ++i)                                  \
-            *(u32x4*)(As_ + lds_off(rbase + 32 * i, chunk)) = ra[i];                      \
+            *(u32x4*)(As_ + lds_off(rbase + ROWS * i, chunk)) = ra[i];                    \
         _Pragma("unroll") for (int i = 0; i < B_IT; ++i)                                  \
-            *(u32x4*)(Bs_ + lds_off(rbase + 32 * i, chunk)) = rb[i];                      \
+            *(u32x4*)(Bs_ + lds_off(rbase + ROWS * i, chunk)) = rb[i];                    \
     } while (0)
 
     // LDS-DMA form: every lane DMAs its 16-B chunk straight into the K buffer.
@@ -182,12 +188,12 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
             const bool ok = kval && (unsigned)iy < (unsigned)a.xh && (unsigned)ix < (unsigned)a.xw; \
             const void* src = ok ? (const void*)(xrow[i] + ((size_t)iy * a.xw + ix) * a.ldx + c) \
                                  : (const void*)vd_zero16;                                \
-            __builtin_amdgcn_global_load_lds(src, (lds_void_t*)(As_ + (wid * 8 + 32 * i) * 128), 16, 0, 0); \
+            __builtin_amdgcn_global_load_lds(src, (lds_void_t*)(As_ + (wid * 8 + ROWS * i) * 128), 16, 0, 0); \
         }                                                                                 \
         _Pragma("unroll") for (int i = 0; i < B_IT; ++i)                                  \
             __builtin_amdgcn_global_load_lds(                                             \
-                (const void*)(wbase_g + (size_t)(32 * i) * a.kpad + (size_t)(kt) * BKE),   \
-                (lds_void_t*)(Bs_ + (wid * 8 + 32 * i) * 128), 16, 0, 0);                  \
+                (const void*)(wbase_g + (size_t)(ROWS * i) * a.kpad + (size_t)(kt) * BKE), \
+                (lds_void_t*)(Bs_ + (wid * 8 + ROWS * i) * 128), 16, 0, 0);                \
         if constexpr (DENSE) {                                                            \
             t_c += BKE;                                                                   \
             if (t_c >= a.cin_pad) { t_c = 0; if (++t_kw == a.kw) { t_kw = 0; ++t_kh; } } \
@@ -237,7 +243,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
     u32x4 rpf[ITEMS];
 #pragma unroll
     for (int q = 0; q < ITEMS; ++q) {
-        const int it = tid + 256 * q;
+        const int it = tid + NT * q;
         const int m = m0 + it / CG, nb = n0 + (it % CG) * 8;
         const bool ok = pf && m < a.M && nb < a.cout;
         size_t roff = 0;
@@ -254,7 +260,24 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
         rpf[q] = *(const u32x4*)rp;
     }
 
-    if constexpr (GLDS) {
+    if constexpr (GLDS && STAGES == 3) {
+        // Three LDS buffers, tiles kt+1 and kt+2 in flight while kt is consumed;
+        // one raw barrier per K tile (it also retires the reads of kt-1, whose
+        // buffer is then refilled with kt+2).
+        constexpr int LPT = A_IT + B_IT;
+        VD_GLDS_TILE(0, 0);
+        if (nk > 1) VD_GLDS_TILE(1, 1);
+        for (int kt = 0; kt < nk; ++kt) {
+            if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(LPT) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            if (kt + 2 < nk) VD_GLDS_TILE(kt + 2, (kt + 2) % 3);
+            VD_COMPUTE(kt % 3);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    } else if constexpr (GLDS) {
         // Two LDS buffers, tile kt+1 in flight while kt is consumed. Raw barriers
         // with counted vmcnt: __syncthreads() would add vmcnt(0) and drain the DMA.
         constexpr int LPT = A_IT + B_IT;                 // DMA instructions per lane per tile
@@ -283,34 +306,34 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
     }
 
     // ---- fused epilogue ----
-    // The f32 accumulator tile goes through LDS one half (BM/2 rows) at a time
-    // ([BM/2][BN+4], conflict-free fragment writes); each thread then owns 8
+    // The f32 accumulator tile goes through LDS BM/EP rows at a time
+    // ([BM/EP][BN+4], conflict-free fragment writes); each thread then owns 8
     // consecutive channels of a row: 16-B (bf16) / 32-B (f32) stores coalesced
     // along the NHWC channel dimension, with the prefetched residual.
     float* ep = (float*)smem;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < EP; ++h) {
         if (h) __syncthreads();
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
             const int row0 = wm * WTM + i * 16;
-            if (row0 / (BM / 2) != h) continue;
+            if (row0 / (BM / EP) != h) continue;
 #pragma unroll
             for (int j = 0; j < TN; ++j)
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    ep[(row0 - h * (BM / 2) + (lane >> 4) * 4 + r) * EPLD + wn * WTN + j * 16 + (lane & 15)] =
+                    ep[(row0 - h * (BM / EP) + (lane >> 4) * 4 + r) * EPLD + wn * WTN + j * 16 + (lane & 15)] =
                         acc[i][j][r];
         }
         __syncthreads();
 #pragma unroll
-        for (int q = h * (ITEMS / 2); q < (h + 1) * (ITEMS / 2); ++q) {
-            const int it = tid + 256 * q;
+        for (int q = h * (ITEMS / EP); q < (h + 1) * (ITEMS / EP); ++q) {
+            const int it = tid + NT * q;
             const int rr = it / CG, cg = it % CG;
             const int m = m0 + rr;
             const int nb = n0 + cg * 8;
             if (m >= a.M || nb >= a.cout) continue;
-            const float* er = ep + (rr - h * (BM / 2)) * EPLD + cg * 8;
+            const float* er = ep + (rr - h * (BM / EP)) * EPLD + cg * 8;
             const size_t yo = (size_t)m * a.ldy + a.ycoff + nb;
             if (vec_ok) {
                 float v[8], rv[8];
@@ -384,35 +407,50 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs a) {
 #undef VD_GLDS_TILE
 #undef VD_COMPUTE
 
-template <typename T, int BM, int BN>
+template <typename T, int BM, int BN, int NT = 256, int STAGES = 2>
 hipError_t launch_bn(const ConvArgs& a0, bool dense, hipStream_t s) {
     static const bool glds = [] { const char* e = getenv("VD_CONV_GLDS"); return !e || atoi(e) != 0; }();
     ConvArgs a = a0;
     a.ntiles_n = (a.cout + BN - 1) / BN;
     const int mt = (a.M + BM - 1) / BM;
-    dim3 grid(mt * a.ntiles_n), block(256);
+    dim3 grid(mt * a.ntiles_n), block(NT);
     constexpr int VEC = Elem<T>::VEC;
-    constexpr size_t BUF = (size_t)(BM + BN) * 128, EPI = (size_t)(BM / 2) * (BN + 4) * 4;
+    constexpr int ITEMS = BM * (BN / 8) / NT, EP = (ITEMS % 4 == 0) ? 4 : 2;   // as in the kernel
+    constexpr size_t BUF = (size_t)(BM + BN) * 128, EPI = (size_t)(BM / EP) * (BN + 4) * 4;
     const int nk = a.kpad / (8 * VEC);
-    const size_t lds = std::max((nk > 1 ? 2 : 1) * BUF, EPI);
-    if (glds) {
-        if (dense) hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, true, true>), grid, block, lds, s, a);
-        else hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, false, true>), grid, block, lds, s, a);
+    const size_t lds = std::max((nk > 1 ? STAGES : 1) * BUF, EPI);
+    if constexpr (STAGES == 3) {
+        static const bool attr = [] {   // > 64 KB of dynamic LDS must be opted into
+            (void)hipFuncSetAttribute((const void*)conv_igemm_kernel<T, BM, BN, NT, 3, true, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)(3 * BUF));
+            return true;
+        }();
+        (void)attr;
+        hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, NT, 3, true, true>), grid, block, lds, s, a);
+    } else if (glds) {
+        if (dense) hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, NT, 2, true, true>), grid, block, lds, s, a);
+        else hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, NT, 2, false, true>), grid, block, lds, s, a);
     } else {
-        if (dense) hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, true, false>), grid, block, lds, s, a);
-        else hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, false, false>), grid, block, lds, s, a);
+        if (dense) hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, NT, 2, true, false>), grid, block, lds, s, a);
+        else hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, NT, 2, false, false>), grid, block, lds, s, a);
     }
     return hipGetLastError();
 }
 
 }  // namespace
 
-// Tile selection: BN follows Cout (32 heads / 64 / 128), BM = 128.
+// Tile selection: BN follows Cout (32 heads / 64 / 128), BM = 128; large dense
+// bf16 layers with Cout >= 128 take the 256 x 128, 8-wave, 3-stage form.
 // Weights must be packed with Npad a multiple of the chosen BN (runtime pads to 128).
 hipError_t vd_launch_conv(const ConvArgs& a, bool f32, hipStream_t s) {
+    static const int big_min = [] { const char* e = getenv("VD_CONV_BIG_MIN"); return e ? atoi(e) : 0; }();
     const int vec = f32 ? 4 : 8;
     const int bke = 8 * vec;
     const bool dense = (a.cin_pad % bke) == 0;
+    if (!f32 && vd_conv1x1_stream_ok(a)) return vd_launch_conv1x1_stream(a, s);
+    if (!f32 && dense && a.cout >= 128 && big_min > 0 && a.kpad / bke > 1 &&
+        (long)((a.M + 255) / 256) * ((a.cout + 127) / 128) >= big_min)
+        return launch_bn<__bf16, 256, 128, 512, 3>(a, dense, s);
     if (f32) {
         if (a.cout <= 32) return launch_bn<float, 128, 32>(a, dense, s);
         if (a.cout <= 64) return launch_bn<float, 128, 64>(a, dense, s);
