@@ -60,6 +60,21 @@ def test_mosaic_nested_chain_and_levels(gpu, face_ctx_factory):
             np.testing.assert_array_equal(got[i], omosaic.mosaic_frame(frames[i], boxes[i], level))
 
 
+def test_mosaic_cell_table_overflow(gpu, face_ctx_factory):
+    """Level 1 on large boxes: more mosaic cells than the per-frame cell table
+    holds (2^18), so the frame takes the per-pixel walk; mixed with a frame that
+    uses the table."""
+    from vdmi import mosaic_frames, synth
+    ctx = face_ctx_factory("bf16", 8)
+    frames = synth.frames(2, 480, 720, seed=9)
+    boxes = [[(0, 0, 720, 480), (100, 50, 600, 400), (30, 20, 700, 470)],
+             [(10, 10, 90, 70), (50, 40, 200, 160)]]
+    for level in (1, 3):
+        got = mosaic_frames(frames, boxes, level, ctx=ctx)
+        for i in range(2):
+            np.testing.assert_array_equal(got[i], omosaic.mosaic_frame(frames[i], boxes[i], level))
+
+
 def test_mosaic_many_boxes_band_overflow(gpu, face_ctx_factory):
     from vdmi import mosaic_frames, synth
     ctx = face_ctx_factory("bf16", 8)

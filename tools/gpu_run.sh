@@ -2,7 +2,7 @@
 # One gpurun session: GPU tests, smoke, bench, optional rocprof. Each GPU step
 # has its own time limit; a crash/abort/timeout (anything but exit 0/1) stops
 # the script before the next GPU step.
-#   bash tools/gpu_run.sh [tests|smoke|bench|prof|pmc ...]
+#   bash tools/gpu_run.sh [tests|smoke|bench|prof|profp|pmc ...]   (profp: plate net alone)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -35,6 +35,7 @@ for s in "${STEPS[@]}"; do
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 400 python bench.py $BENCH_ARGS ;;
         prof)  run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py $PROF_ARGS ;;
+        profp) run profp 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profp -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --faces 0 --plates 1 ;;
         pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py $PMC_ARGS &&
                run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py $PMC_ARGS ;;
         *) echo "unknown step $s"; exit 2 ;;

@@ -25,6 +25,47 @@ int conv_bn(Ctx& c, const WMap& W, const std::string& conv, const std::string& b
             int* idx) {
     return c.make_conv_bn(W, conv, bn, BN_EPS, stride, pad, act, 0.f, idx);
 }
+
+// The stem conv1 (7x7, stride 2, pad 3, 3 -> 64) rewritten over the space-to-depth
+// input X'[Y][X][(py*2+px)*4 + c] = x[2Y+py-1][2X+px-1][c]: a 4x4, stride-1, pad-1
+// conv with 16 input channels, W'[n][(py*2+px)*4+c][ta][tb] = W[n][c][2ta+py][2tb+px]
+// (zero where 2ta+py or 2tb+px is 7, and for the 4th channel of each sub-pixel).
+// Same products and the same sum (K 147 real terms of 256 instead of 147 of 448).
+int stem_s2d(Ctx& c, const WMap& W, int* idx) {
+    const HT* w = find_t(W, "body.conv1.weight");
+    const HT* g = find_t(W, "body.bn1.weight");
+    const HT* b = find_t(W, "body.bn1.bias");
+    const HT* m = find_t(W, "body.bn1.running_mean");
+    const HT* v = find_t(W, "body.bn1.running_var");
+    if (!w || w->shape.size() != 4 || w->shape[1] != 3 || w->shape[2] != 7 || w->shape[3] != 7)
+        return vd_set_error(VD_ERR_WEIGHTS, "missing/bad body.conv1.weight");
+    if (!g || !b || !m || !v) return vd_set_error(VD_ERR_WEIGHTS, "missing BatchNorm tensors under body.bn1");
+    Conv cv{};
+    cv.cout = w->shape[0]; cv.cin = 16; cv.kh = 4; cv.kw = 4;
+    cv.stride = 1; cv.pad = 1; cv.act = VD_ACT_RELU; cv.slope = 0.f;
+    std::vector<float> wt((size_t)cv.cout * 16 * 16, 0.f), sc(cv.cout), sh(cv.cout);
+    for (int n = 0; n < cv.cout; ++n) {
+        for (int ta = 0; ta < 4; ++ta)
+            for (int tb = 0; tb < 4; ++tb)
+                for (int py = 0; py < 2; ++py)
+                    for (int px = 0; px < 2; ++px)
+                        for (int ch = 0; ch < 3; ++ch) {
+                            const int dy = 2 * ta + py, dx = 2 * tb + px;
+                            if (dy > 6 || dx > 6) continue;
+                            const int ci = (py * 2 + px) * 4 + ch;
+                            wt[(((size_t)n * 16 + ci) * 4 + ta) * 4 + tb] = w->data[(((size_t)n * 3 + ch) * 7 + dy) * 7 + dx];
+                        }
+        const float alpha = g->data[n] / std::sqrt(v->data[n] + BN_EPS);
+        sc[n] = alpha;
+        sh[n] = b->data[n] - m->data[n] * alpha;
+    }
+    int rc = c.upload_conv(cv, wt, sc, sh);
+    if (rc) return rc;
+    cv.flops_per_px = 2.0 * cv.cout * 3 * 49;   // algorithmic work of the original 7x7 conv
+    c.convs.push_back(cv);
+    *idx = (int)c.convs.size() - 1;
+    return VD_OK;
+}
 }  // namespace
 
 int vd_build_face(Ctx& c, const WMap& W) {
@@ -34,11 +75,16 @@ int vd_build_face(Ctx& c, const WMap& W) {
     const int H = F.in_h, Wd = F.in_w;
     const int cpad = c.f32 ? 4 : 8;
     int rc;
-    if ((rc = c.act(F.input, H, Wd, cpad))) return rc;
+    F.s2d = !c.f32 && H % 2 == 0 && Wd % 2 == 0;
+    if (F.s2d) rc = c.act(F.input, H / 2 + 1, Wd / 2 + 1, 16);
+    else rc = c.act(F.input, H, Wd, cpad);
+    if (rc) return rc;
 
     // ---- stem: conv1 7x7/2 + bn1 + relu, maxpool 3x3/2 pad 1 ----
     int ci;
-    if ((rc = conv_bn(c, W, "body.conv1.weight", "body.bn1", 2, 3, VD_ACT_RELU, &ci))) return rc;
+    if (F.s2d) rc = stem_s2d(c, W, &ci);
+    else rc = conv_bn(c, W, "body.conv1.weight", "body.bn1", 2, 3, VD_ACT_RELU, &ci);
+    if (rc) return rc;
     Act stem, pool;
     if ((rc = c.act(stem, H / 2, Wd / 2, 64))) return rc;
     if ((rc = c.add_conv(F.net, ci, F.input, 0, stem, 0))) return rc;

@@ -14,10 +14,16 @@
 //                      call order: faces first, then plates, combine_detect.py:242-244).
 //  mosaic_copy_kernel  the img.copy() of :247 — a 64-B-per-thread streaming copy
 //                      of every frame with <= BOX_FAST boxes (HBM roofline).
-//  mosaic_box_kernel   one workgroup slice per (frame, box k): for each pixel of
-//                      box k that no LATER box contains (that box owns it), walk
-//                      k, k-1, ..., 0 and gather the 3 source bytes. Only covered
-//                      pixels are touched; the frame's box table sits in LDS.
+//  mosaic_prefix_kernel per frame: prefix sums of the boxes' pixel counts and of
+//                      their mosaic cell counts (sw*sh), for balanced flat grids.
+//  mosaic_cell_kernel  one thread per mosaic CELL (ux, uy) of every box: all the
+//                      pixels of a cell map to the same point, so the backward
+//                      walk over earlier boxes and the 3-byte gather run once per
+//                      cell (level^2 fewer times than per pixel) into a cell table.
+//  mosaic_box_kernel   every pixel of box k that no LATER box contains (box k owns
+//                      it) takes its cell's colour. Work is flat over the frame's
+//                      box pixels; the frame's box table sits in LDS. (Frames whose
+//                      cells exceed the table walk per pixel instead.)
 //  mosaic_kernel       fallback for frames with > BOX_FAST boxes: one workgroup
 //                      per (frame, band of ROWS rows). The band's box list (table
 //                      entries intersecting the band, original order) is staged
@@ -37,6 +43,8 @@ constexpr int ROWS = 8;
 constexpr int TB_CAP = 512;    // band-list capacity; larger bands walk the global table
 constexpr int BOX_FAST = 256;  // frames with at most this many boxes take copy + box kernels
 constexpr int BOX_BLOCKS = 256; // workgroups per frame sharing its box pixels
+constexpr int CELL_BLOCKS = 32; // workgroups per frame sharing its mosaic cells
+constexpr int CELL_CAP = 1 << 18;   // cell-table entries per frame (packed RGB)
 
 struct MBox { int x1, y1, x2, y2; int sw, sh, idx, valid; double fux, fdx, fuy, fdy; };
 
@@ -48,7 +56,9 @@ struct MosaicArgs {
     int vec_ok;                                      // 16-B aligned rows -> vector copies
     MBox* table; int tcap;                           // [n][tcap] prepared boxes
     uint64_t* ovl;                                   // [n][BOX_FAST][4] overlap bitmasks (fast path)
-    int* pref;                                       // [n][BOX_FAST+1] prefix sums of box areas (fast path)
+    int* pref;                                       // [n][BOX_FAST+1] prefix sums of box quads (fast path)
+    int* cpref;                                      // [n][BOX_FAST+1] prefix sums of box cells sw*sh
+    uint32_t* cells;                                 // [n][CELL_CAP] walked colour per cell
 };
 
 __global__ __launch_bounds__(256) void mosaic_prep_kernel(MosaicArgs a) {
@@ -245,21 +255,25 @@ __global__ __launch_bounds__(256) void mosaic_prefix_kernel(MosaicArgs a) {
     const int n1 = a.cnt1 ? min(a.cnt1[f], a.cap1) : 0;
     const int nb = n0 + n1;
     int* pref = a.pref + (size_t)f * (BOX_FAST + 1);
-    if (nb > BOX_FAST) { if (k == 0) pref[0] = 0; return; }
-    int v = 0;
-    if (k < nb) {
-        const MBox b = a.table[(size_t)f * a.tcap + k];
-        if (b.valid) v = (b.x2 - b.x1) * (b.y2 - b.y1);
-    }
-    s[k] = v;
-    __syncthreads();
-    for (int off = 1; off < 256; off <<= 1) {      // Hillis-Steele inclusive scan
-        const int t = k >= off ? s[k - off] : 0;
+    int* cpref = a.cpref + (size_t)f * (BOX_FAST + 1);
+    if (nb > BOX_FAST) { if (k == 0) { pref[0] = 0; cpref[0] = 0; } return; }
+    MBox b{};
+    if (k < nb) b = a.table[(size_t)f * a.tcap + k];
+    for (int pass = 0; pass < 2; ++pass) {
+        int v = 0;
+        // pass 0: 4-pixel quads (aligned to absolute x % 4) per box; pass 1: mosaic cells
+        if (k < nb && b.valid) v = pass == 0 ? (((b.x2 - 1) >> 2) - (b.x1 >> 2) + 1) * (b.y2 - b.y1) : b.sw * b.sh;
+        s[k] = v;
         __syncthreads();
-        s[k] += t;
+        for (int off = 1; off < 256; off <<= 1) {      // Hillis-Steele inclusive scan
+            const int t = k >= off ? s[k - off] : 0;
+            __syncthreads();
+            s[k] += t;
+            __syncthreads();
+        }
+        if (k <= nb) (pass == 0 ? pref : cpref)[k] = k == 0 ? 0 : s[k - 1];
         __syncthreads();
     }
-    if (k <= nb) pref[k] = k == 0 ? 0 : s[k - 1];
 }
 
 // Highest set bit index < lim in a 256-bit mask, or -1.
@@ -273,15 +287,77 @@ __device__ __forceinline__ int top_below(const uint64_t* m, int lim) {
     return -1;
 }
 
-// Pixels of box k that no LATER box contains: walk k, then earlier boxes along the
-// overlap graph (a box containing a point of box j overlaps j), gather 3 bytes.
-// Work is balanced over the frame's flattened box-pixel index space
-// [0, sum of box areas): workgroup g of BOX_BLOCKS takes a strided share, and a
-// binary search over the area prefix sums maps an index to (box, pixel).
+__device__ __forceinline__ int find_box(const int* pref, int nb, int t) {   // largest k with pref[k] <= t
+    int lo = 0, hi = nb - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (pref[mid] <= t) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+// Walk a point already mapped by box `cur` back through the earlier boxes that
+// contain it (the highest-index earlier box first, along the overlap graph).
+__device__ __forceinline__ void walk_back(const MBox* tab, const uint64_t (*ovl)[4], int cur, int& y, int& x) {
+    for (;;) {
+        int lim = cur, j;
+        while ((j = top_below(ovl[cur], lim)) >= 0 && !inside(tab[j], y, x)) lim = j;
+        if (j < 0) break;
+        apply(tab[j], y, x);
+        cur = j;
+    }
+}
+
+// One thread per mosaic cell of every box of a fast-path frame (flat over the
+// frame's cells): map, walk, gather the colour into the cell table.
+__global__ __launch_bounds__(256) void mosaic_cell_kernel(MosaicArgs a) {
+    __shared__ MBox s_tab[BOX_FAST];
+    __shared__ uint64_t s_ovl[BOX_FAST][4];
+    __shared__ int s_cpref[BOX_FAST + 1];
+    const int f = blockIdx.y;
+    const int n0 = a.cnt0 ? min(a.cnt0[f], a.cap0) : 0;
+    const int n1 = a.cnt1 ? min(a.cnt1[f], a.cap1) : 0;
+    const int nb = n0 + n1;
+    if (nb > BOX_FAST || nb == 0) return;
+    const int* cpref = a.cpref + (size_t)f * (BOX_FAST + 1);
+    const int total = cpref[nb];
+    if (total > CELL_CAP || blockIdx.x * 256 >= total) return;
+    const MBox* table = a.table + (size_t)f * a.tcap;
+    const uint64_t* ovl = a.ovl + (size_t)f * BOX_FAST * 4;
+    for (int i = threadIdx.x; i < nb; i += 256) {
+        s_tab[i] = table[i];
+        s_ovl[i][0] = ovl[4 * i + 0]; s_ovl[i][1] = ovl[4 * i + 1];
+        s_ovl[i][2] = ovl[4 * i + 2]; s_ovl[i][3] = ovl[4 * i + 3];
+    }
+    for (int i = threadIdx.x; i <= nb; i += 256) s_cpref[i] = cpref[i];
+    __syncthreads();
+    const uint8_t* src = a.in + (size_t)f * a.h * a.pitch;
+    uint32_t* cells = a.cells + (size_t)f * CELL_CAP;
+    for (int t = blockIdx.x * 256 + threadIdx.x; t < total; t += gridDim.x * 256) {
+        const int k = find_box(s_cpref, nb, t);
+        const MBox& bk = s_tab[k];
+        const int c = t - s_cpref[k];
+        const int uy = c / bk.sw, ux = c - uy * bk.sw;
+        // apply(bk) of any pixel of this cell: the down-mapped point of (ux, uy)
+        int x = bk.x1 + min((int)floor(VD_DMUL((double)ux, bk.fdx)), bk.x2 - bk.x1 - 1);
+        int y = bk.y1 + min((int)floor(VD_DMUL((double)uy, bk.fdy)), bk.y2 - bk.y1 - 1);
+        walk_back(s_tab, s_ovl, k, y, x);
+        const uint8_t* sp = src + (size_t)y * a.pitch + x * 3;
+        cells[t] = (uint32_t)sp[0] | ((uint32_t)sp[1] << 8) | ((uint32_t)sp[2] << 16);
+    }
+}
+
+// Pixels of box k that no LATER box contains take the colour of their cell
+// (or, when the frame's cells overflow the table, walk per pixel).
+// Work is balanced over the frame's flattened index space of box QUADS (4
+// pixels x .. x+3 of one row, x % 4 == 0, clipped to the box): workgroup g of
+// BOX_BLOCKS takes a strided share, and a binary search over the quad prefix sums
+// maps an index to (box, row, quad). A fully owned quad is one 12-B store.
 __global__ __launch_bounds__(256) void mosaic_box_kernel(MosaicArgs a) {
     __shared__ MBox s_tab[BOX_FAST];
     __shared__ uint64_t s_ovl[BOX_FAST][4];
     __shared__ int s_pref[BOX_FAST + 1];
+    __shared__ int s_cpref[BOX_FAST + 1];
     const int f = blockIdx.y;
     const int n0 = a.cnt0 ? min(a.cnt0[f], a.cap0) : 0;
     const int n1 = a.cnt1 ? min(a.cnt1[f], a.cap1) : 0;
@@ -290,6 +366,7 @@ __global__ __launch_bounds__(256) void mosaic_box_kernel(MosaicArgs a) {
     const int* pref = a.pref + (size_t)f * (BOX_FAST + 1);
     const int total = pref[nb];
     if (blockIdx.x * 256 >= total) return;
+    const bool use_cells = a.cpref[(size_t)f * (BOX_FAST + 1) + nb] <= CELL_CAP;
     const MBox* table = a.table + (size_t)f * a.tcap;
     const uint64_t* ovl = a.ovl + (size_t)f * BOX_FAST * 4;
     for (int i = threadIdx.x; i < nb; i += 256) {
@@ -297,55 +374,79 @@ __global__ __launch_bounds__(256) void mosaic_box_kernel(MosaicArgs a) {
         s_ovl[i][0] = ovl[4 * i + 0]; s_ovl[i][1] = ovl[4 * i + 1];
         s_ovl[i][2] = ovl[4 * i + 2]; s_ovl[i][3] = ovl[4 * i + 3];
     }
-    for (int i = threadIdx.x; i <= nb; i += 256) s_pref[i] = pref[i];
+    for (int i = threadIdx.x; i <= nb; i += 256) {
+        s_pref[i] = pref[i];
+        s_cpref[i] = a.cpref[(size_t)f * (BOX_FAST + 1) + i];
+    }
     __syncthreads();
     const uint8_t* src = a.in + (size_t)f * a.h * a.pitch;
     uint8_t* dst = a.out + (size_t)f * a.h * a.pitch;
+    const uint32_t* cells = a.cells + (size_t)f * CELL_CAP;
+    const bool al4 = ((a.pitch & 3) == 0) && (((uintptr_t)a.out & 3) == 0);
     for (int t = blockIdx.x * 256 + threadIdx.x; t < total; t += gridDim.x * 256) {
-        int lo = 0, hi = nb - 1;                    // largest k with s_pref[k] <= t
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (s_pref[mid] <= t) lo = mid; else hi = mid - 1;
-        }
-        const int k = lo;
+        const int k = find_box(s_pref, nb, t);
         const MBox& bk = s_tab[k];
-        const int bw = bk.x2 - bk.x1;
+        const int q0 = bk.x1 >> 2, nq = ((bk.x2 - 1) >> 2) - q0 + 1;
         const int p = t - s_pref[k];
-        const int py = p / bw;
-        const int y0 = bk.y1 + py, x0 = bk.x1 + (p - py * bw);
-        bool owned = true;
-        for (int w = (k + 1) >> 6; w < 4 && owned; ++w) {       // later boxes overlapping k
+        const int r = p / nq;
+        const int y = bk.y1 + r, xq = (q0 + (p - r * nq)) * 4;
+        // pixels of the quad inside box k, minus those a LATER overlapping box contains
+        const int lo0 = max(bk.x1 - xq, 0), hi0 = min(bk.x2 - xq, 4);
+        unsigned own = ((1u << hi0) - 1u) & ~((1u << lo0) - 1u);
+        for (int w = (k + 1) >> 6; w < 4 && own; ++w) {
             uint64_t v = s_ovl[k][w];
             const int lo_bit = k + 1 - (w << 6);
             if (lo_bit > 0) v &= ~((1ULL << lo_bit) - 1ULL);
-            while (v && owned) {
+            while (v && own) {
                 const int j = (w << 6) + __ffsll((long long)v) - 1;
                 v &= v - 1;
-                owned = !inside(s_tab[j], y0, x0);
+                const MBox& bj = s_tab[j];
+                if (y < bj.y1 || y >= bj.y2) continue;
+                const int lo = max(bj.x1 - xq, 0), hi = min(bj.x2 - xq, 4);
+                if (lo < hi) own &= ~(((1u << hi) - 1u) & ~((1u << lo) - 1u));
             }
         }
-        if (!owned) continue;
-        int y = y0, x = x0;
-        apply(bk, y, x);
-        int cur = k;
-        for (;;) {   // next (highest-index, earlier) box containing the point, along the overlap graph
-            int lim = cur, j;
-            while ((j = top_below(s_ovl[cur], lim)) >= 0 && !inside(s_tab[j], y, x)) lim = j;
-            if (j < 0) break;
-            apply(s_tab[j], y, x);
-            cur = j;
+        uint32_t col[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            if (!(own & (1u << e))) continue;
+            const int x = xq + e;
+            if (use_cells) {
+                const int ux = min((int)floor(VD_DMUL((double)(x - bk.x1), bk.fux)), bk.sw - 1);
+                const int uy = min((int)floor(VD_DMUL((double)(y - bk.y1), bk.fuy)), bk.sh - 1);
+                col[e] = cells[s_cpref[k] + uy * bk.sw + ux];
+            } else {
+                int yy = y, xx = x;
+                apply(bk, yy, xx);
+                walk_back(s_tab, s_ovl, k, yy, xx);
+                const uint8_t* sp = src + (size_t)yy * a.pitch + xx * 3;
+                col[e] = (uint32_t)sp[0] | ((uint32_t)sp[1] << 8) | ((uint32_t)sp[2] << 16);
+            }
         }
-        const uint8_t* sp = src + (size_t)y * a.pitch + x * 3;
-        uint8_t* dp = dst + (size_t)y0 * a.pitch + x0 * 3;
-        const uint8_t c0 = sp[0], c1 = sp[1], c2 = sp[2];
-        dp[0] = c0; dp[1] = c1; dp[2] = c2;
+        if (!own) continue;
+        uint8_t* dp = dst + (size_t)y * a.pitch + xq * 3;
+        if (own == 15u && al4) {   // 12 bytes = 4 packed RGB pixels
+            const uint32_t w0 = col[0] | (col[1] << 24);
+            const uint32_t w1 = (col[1] >> 8) | (col[2] << 16);
+            const uint32_t w2 = (col[2] >> 16) | (col[3] << 8);
+            uint32_t* d32 = (uint32_t*)dp;
+            d32[0] = w0; d32[1] = w1; d32[2] = w2;
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (own & (1u << e)) {
+                    dp[3 * e] = (uint8_t)col[e]; dp[3 * e + 1] = (uint8_t)(col[e] >> 8);
+                    dp[3 * e + 2] = (uint8_t)(col[e] >> 16);
+                }
+        }
     }
 }
 
 }  // namespace
 
 size_t vd_mosaic_table_bytes(int n, int tcap) {
-    return (size_t)n * tcap * sizeof(MBox) + (size_t)n * BOX_FAST * 32 + (size_t)n * (BOX_FAST + 1) * 4;
+    return (size_t)n * tcap * sizeof(MBox) + (size_t)n * BOX_FAST * 32 + 2 * (size_t)n * (BOX_FAST + 1) * 4 + 16 +
+           (size_t)n * CELL_CAP * 4;
 }
 
 hipError_t vd_launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w, size_t pitch,
@@ -355,8 +456,12 @@ hipError_t vd_launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w
     const int vec_ok = (pitch % 16 == 0) && ((uintptr_t)in % 16 == 0) && ((uintptr_t)out % 16 == 0);
     const int tcap = (cnt0 ? cap0 : 0) + (cnt1 ? cap1 : 0);
     char* tail = (char*)table + (size_t)n * tcap * sizeof(MBox);
+    char* pre = tail + (size_t)n * BOX_FAST * 32;
+    char* cpre = pre + (size_t)n * (BOX_FAST + 1) * 4;
+    char* cel = cpre + (size_t)n * (BOX_FAST + 1) * 4;
+    cel += (16 - ((uintptr_t)cel & 15)) & 15;
     MosaicArgs a{in, out, n, h, w, pitch, cnt0, xy0, cap0, cnt1, xy1, cap1, level, vec_ok, (MBox*)table, tcap,
-                 (uint64_t*)tail, (int*)(tail + (size_t)n * BOX_FAST * 32)};
+                 (uint64_t*)tail, (int*)pre, (int*)cpre, (uint32_t*)cel};
     if (tcap > 0)
         hipLaunchKernelGGL(mosaic_prep_kernel, dim3((tcap + 255) / 256, n), dim3(256), 0, s, a);
     // fast path: copy (~1 MiB per workgroup row of the grid) then owned-pixel gathers
@@ -366,6 +471,7 @@ hipError_t vd_launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w
     if (tcap > 0) {
         hipLaunchKernelGGL(mosaic_overlap_kernel, dim3(1, n), dim3(256), 0, s, a);
         hipLaunchKernelGGL(mosaic_prefix_kernel, dim3(n), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(mosaic_cell_kernel, dim3(CELL_BLOCKS, n), dim3(256), 0, s, a);
         hipLaunchKernelGGL(mosaic_box_kernel, dim3(BOX_BLOCKS, n), dim3(256), 0, s, a);
         // frames with more boxes than the fast path holds
         hipLaunchKernelGGL(mosaic_kernel, dim3((h + ROWS - 1) / ROWS, n), dim3(256), 0, s, a);

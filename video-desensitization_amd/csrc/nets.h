@@ -46,6 +46,7 @@ struct Op {
 struct Net {
     std::vector<Op> ops;
     int stage_end[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // op index after each backbone stage (face: 0=stem,1..4=layerN)
+    int conv_fam = 0;                                // timing family of its convs (0 face, 5 plate)
 };
 
 struct PostScratch {   // per-net candidate / NMS scratch sized for max_batch x A
@@ -63,6 +64,7 @@ struct PostScratch {   // per-net candidate / NMS scratch sized for max_batch x 
 struct FaceNet {
     bool loaded = false;
     int in_h = 640, in_w = 640;
+    bool s2d = false;               // bf16: stem input in space-to-depth form (pre.hip letterbox_s2d_kernel)
     Act input;
     Net net;
     Act heads[3];
@@ -137,7 +139,7 @@ struct Ctx {
                  int rcoff = 0, int rmode = 0, int rup = 0);
     void t_begin(int fam, double work);
     void t_end();
-    int run_conv_op(const Op& op, int f0, int n);
+    int run_conv_op(const Op& op, int f0, int n, int fam = 0);
     int run_ops(const Net& net, int b, int e, int f0, int n);
     int run_net(const Net& net, int n, int mb = 0, int split = 0);
     const uint8_t* frames_to_device(const uint8_t* frames, int n, int h, size_t pitch, int where, int* rc);

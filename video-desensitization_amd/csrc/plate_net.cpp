@@ -296,6 +296,7 @@ int vd_plate_forward(Ctx& c, const uint8_t* d, int n, int h, int w, size_t pitch
         if (pl.first == key) net = &pl.second;
     if (!net) {
         P.plans.push_back({key, Net{}});
+        P.plans.back().second.conv_fam = 5;
         net = &P.plans.back().second;
         int rc = build_plan(c, oh, ow, *net);
         if (rc) { P.plans.pop_back(); return rc; }

@@ -33,20 +33,66 @@ __device__ __forceinline__ Tap linear_tap(int d, int ssize, double scale) {
     return t;
 }
 
-__device__ __forceinline__ int resized_px(const LetterboxArgs& a, const uint8_t* img, int y, int x, int c) {
-    if (a.mode == LB_COPY) return img[(size_t)y * a.pitch + x * 3 + c];
-    if (a.mode == LB_AREA2) {
-        const uint8_t* p = img + (size_t)(2 * y) * a.pitch + (2 * x) * 3 + c;
-        return (p[0] + p[3] + p[a.pitch] + p[a.pitch + 3] + 2) >> 2;
+// The 3 channels of resized pixel (y, x) (interpolation taps computed once).
+__device__ __forceinline__ void resized_px3(const LetterboxArgs& a, const uint8_t* img, int y, int x, int out[3]) {
+    if (a.mode == LB_COPY) {
+        const uint8_t* p = img + (size_t)y * a.pitch + x * 3;
+        out[0] = p[0]; out[1] = p[1]; out[2] = p[2];
+        return;
     }
-    Tap tx = linear_tap(x, a.iw, a.scale_x);
-    Tap ty = linear_tap(y, a.ih, a.scale_y);
+    if (a.mode == LB_AREA2) {
+        const uint8_t* p = img + (size_t)(2 * y) * a.pitch + (2 * x) * 3;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) out[c] = (p[c] + p[c + 3] + p[a.pitch + c] + p[a.pitch + c + 3] + 2) >> 2;
+        return;
+    }
+    const Tap tx = linear_tap(x, a.iw, a.scale_x);
+    const Tap ty = linear_tap(y, a.ih, a.scale_y);
     const uint8_t* r0 = img + (size_t)ty.s0 * a.pitch;
     const uint8_t* r1 = img + (size_t)ty.s1 * a.pitch;
-    int d0 = r0[tx.s0 * 3 + c] * tx.a0 + r0[tx.s1 * 3 + c] * tx.a1;
-    int d1 = r1[tx.s0 * 3 + c] * tx.a0 + r1[tx.s1 * 3 + c] * tx.a1;
-    int v = ((((d0 >> 4) * ty.a0) >> 16) + (((d1 >> 4) * ty.a1) >> 16) + 2) >> 2;
-    return v < 0 ? 0 : (v > 255 ? 255 : v);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        int d0 = r0[tx.s0 * 3 + c] * tx.a0 + r0[tx.s1 * 3 + c] * tx.a1;
+        int d1 = r1[tx.s0 * 3 + c] * tx.a0 + r1[tx.s1 * 3 + c] * tx.a1;
+        int v = ((((d0 >> 4) * ty.a0) >> 16) + (((d1 >> 4) * ty.a1) >> 16) + 2) >> 2;
+        out[c] = v < 0 ? 0 : (v > 255 ? 255 : v);
+    }
+}
+
+// Normalised canvas pixel (y, x) (resized image or pad value), 3 channels.
+__device__ __forceinline__ void canvas_px(const LetterboxArgs& a, const uint8_t* img, int y, int x, float v[3]) {
+    const int ry = y - a.top, rx = x - a.left;
+    const bool inside = (unsigned)ry < (unsigned)a.nh && (unsigned)rx < (unsigned)a.nw;
+    int p3[3] = {0, 0, 0};
+    if (inside) resized_px3(a, img, ry, rx, p3);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const int pv = a.flip ? p3[2 - c] : p3[c];
+        const float px = inside ? (float)pv : a.pad_value;
+        v[c] = VD_FDIV(VD_FSUB(px, a.mean[c]), a.div);
+    }
+}
+
+// Space-to-depth form (a.s2d): one thread per 2x2 canvas block, 32 B out.
+__global__ __launch_bounds__(256) void letterbox_s2d_kernel(LetterboxArgs a) {
+    const int X = blockIdx.x * 256 + threadIdx.x;
+    const int Y = blockIdx.y;
+    const int f = blockIdx.z;
+    const int OW = a.ow / 2 + 1, OH = a.oh / 2 + 1;
+    if (X >= OW) return;
+    const uint8_t* img = a.src + (size_t)f * a.ih * a.pitch;
+    __bf16 t[16];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int y = 2 * Y + (s >> 1) - 1, x = 2 * X + (s & 1) - 1;
+        float v[3] = {0.f, 0.f, 0.f};   // conv zero padding outside the canvas
+        if ((unsigned)y < (unsigned)a.oh && (unsigned)x < (unsigned)a.ow) canvas_px(a, img, y, x, v);
+        t[4 * s + 0] = (__bf16)v[0]; t[4 * s + 1] = (__bf16)v[1]; t[4 * s + 2] = (__bf16)v[2];
+        t[4 * s + 3] = (__bf16)0.f;
+    }
+    __bf16* out = (__bf16*)a.out + (((size_t)f * OH + Y) * OW + X) * 16;
+    *(uint4*)out = *(const uint4*)t;
+    *(uint4*)(out + 8) = *(const uint4*)(t + 8);
 }
 
 __global__ __launch_bounds__(256) void letterbox_kernel(LetterboxArgs a) {
@@ -56,14 +102,7 @@ __global__ __launch_bounds__(256) void letterbox_kernel(LetterboxArgs a) {
     if (x >= a.ow) return;
     const uint8_t* img = a.src + (size_t)f * a.ih * a.pitch;
     float v[3];
-    const int ry = y - a.top, rx = x - a.left;
-    const bool inside = (unsigned)ry < (unsigned)a.nh && (unsigned)rx < (unsigned)a.nw;
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        int sc = a.flip ? 2 - c : c;
-        float px = inside ? (float)resized_px(a, img, ry, rx, sc) : a.pad_value;
-        v[c] = VD_FDIV(VD_FSUB(px, a.mean[c]), a.div);
-    }
+    canvas_px(a, img, y, x, v);
     const size_t o = (((size_t)f * a.oh + y) * a.ow + x) * a.cpad;
     if (a.out_f32) {
         float* out = (float*)a.out + o;
@@ -136,6 +175,11 @@ __global__ __launch_bounds__(256) void upsample2x_kernel(const T* x, int xh, int
 }  // namespace
 
 hipError_t vd_launch_letterbox(const LetterboxArgs& a, hipStream_t s) {
+    if (a.s2d) {
+        dim3 grid((a.ow / 2 + 1 + 255) / 256, a.oh / 2 + 1, a.n);
+        hipLaunchKernelGGL(letterbox_s2d_kernel, grid, dim3(256), 0, s, a);
+        return hipGetLastError();
+    }
     dim3 grid((a.ow + 255) / 256, a.oh, a.n);
     hipLaunchKernelGGL(letterbox_kernel, grid, dim3(256), 0, s, a);
     return hipGetLastError();

@@ -14,6 +14,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -258,7 +259,7 @@ static inline const void* foff(const Act& a, int f0) {
     return a.p ? (const char*)a.p + (size_t)f0 * a.h * a.w * a.c * (a.f32 ? 4 : 2) : nullptr;
 }
 
-int Ctx::run_conv_op(const Op& op, int f0, int n) {
+int Ctx::run_conv_op(const Op& op, int f0, int n, int fam) {
     const Conv& cv = convs[op.conv];
     ConvArgs a{};
     a.x = foff(op.x, f0); a.xh = op.x.h; a.xw = op.x.w; a.ldx = op.x.c; a.xcoff = op.xcoff;
@@ -270,7 +271,7 @@ int Ctx::run_conv_op(const Op& op, int f0, int n) {
     a.kh = cv.kh; a.kw = cv.kw; a.stride = cv.stride; a.pad = cv.pad;
     a.M = n * op.y.h * op.y.w;
     a.act = cv.act; a.slope = cv.slope; a.out_f32 = op.y.f32 ? 1 : 0;
-    t_begin(0, cv.flops_per_px * a.M);
+    t_begin(fam, cv.flops_per_px * a.M);
     hipError_t e = vd_launch_conv(a, f32, stream);
     t_end();
     if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "conv launch: %s", hipGetErrorString(e));
@@ -282,7 +283,7 @@ int Ctx::run_ops(const Net& net, int b, int e, int f0, int n) {
         const Op& op = net.ops[i];
         int rc = VD_OK;
         if (op.kind == OP_CONV) {
-            rc = run_conv_op(op, f0, n);
+            rc = run_conv_op(op, f0, n, net.conv_fam);
         } else if (op.kind == OP_MAXPOOL) {
             t_begin(4, 0);
             hipError_t er = vd_launch_maxpool(f32, foff(op.x, f0), n, op.x.h, op.x.w, op.x.c, op.xcoff,
@@ -401,6 +402,7 @@ int Ctx::face_letterbox(const uint8_t* dframes, int n, int h, int w, size_t pitc
     a.div = 1.f;
     a.flip = 0;
     a.out = face.input.p; a.cpad = face.input.c; a.out_f32 = f32 ? 1 : 0;
+    a.s2d = face.s2d ? 1 : 0;
     t_begin(2, (double)n * (a.nh * (double)w * 3 + (double)a.oh * a.ow * a.cpad * (f32 ? 4 : 2)));
     hipError_t e = vd_launch_letterbox(a, stream);
     t_end();
@@ -518,7 +520,13 @@ int vd_create(const vd_cfg* cfg, int device, vd_ctx** out) {
         return vd_set_error(VD_ERR_HIP, "hipStreamCreate failed");
     }
     ctx->stream = ctx->own_stream;
-    if (hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess ||
+    // VD_PLATE_PRIO=1 puts the plate branch on a high-priority stream (so its small
+    // launches would take CUs the face convs leave idle first); measured neutral.
+    int prio_lo = 0, prio_hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    const char* pe = getenv("VD_PLATE_PRIO");
+    const int prio = (pe && atoi(pe) != 0) ? prio_hi : prio_lo;   // measured: no gain, default normal
+    if (hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking, prio) != hipSuccess ||
         hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming) != hipSuccess) {
         hipStreamDestroy(ctx->own_stream);
@@ -803,6 +811,23 @@ int vdt_letterbox(vd_ctx* h, const uint8_t* frames, int n, int fh, int fw, size_
     } else {
         hb.resize(px * in.c);
         VD_CHECK_HIP(hipMemcpy(hb.data(), in.p, hb.size() * 2, hipMemcpyDeviceToHost));
+    }
+    if (ctx->face.s2d) {   // unpack the space-to-depth canvas back to [n][H][W][cpad]
+        const int H = ctx->face.in_h, W = ctx->face.in_w;
+        for (int f = 0; f < n; ++f)
+            for (int y = 0; y < H; ++y)
+                for (int x = 0; x < W; ++x)
+                    for (int c = 0; c < cpad; ++c) {
+                        float v = 0.f;
+                        if (c < 3) {
+                            const int Y = (y + 1) >> 1, X = (x + 1) >> 1, s = ((y + 1) & 1) * 2 + ((x + 1) & 1);
+                            const size_t i = (((size_t)f * in.h + Y) * in.w + X) * in.c + s * 4 + c;
+                            uint32_t u = (uint32_t)hb[i] << 16;
+                            memcpy(&v, &u, 4);
+                        }
+                        out[(((size_t)f * H + y) * W + x) * cpad + c] = v;
+                    }
+        return VD_OK;
     }
     for (size_t i = 0; i < px; ++i)
         for (int c = 0; c < cpad; ++c) {

@@ -80,6 +80,9 @@ struct LetterboxArgs {
     float div;             // divisor after mean (1, or 255 for ultralytics' im /= 255)
     int flip;              // 1: output channel c takes source channel 2-c
     void* out; int cpad; int out_f32;
+    int s2d;               // 1: space-to-depth canvas for the stride-2 stem (bf16, 16 channels):
+                           //    out[Y][X][(py*2+px)*4 + c] = canvas[2Y+py-1][2X+px-1][c], 0 off-canvas,
+                           //    Y in [0, oh/2], X in [0, ow/2]
 };
 
 // ---- kernel launchers (one translation unit each) ----
