@@ -125,12 +125,23 @@ CONV_CASES = [
     (1, 10, 14, 128, 512, 1, 1, 0, 1, 1),
     (2, 9, 7, 256, 128, 1, 1, 0, 3, 0),       # SiLU
     (1, 13, 11, 128, 192, 1, 1, 0, 0, 2),     # residual after (no) activation, 64-channel slices
+    # streaming taps kernel (K <= 320, Cout % 16 == 0): YOLO C2f bottleneck / 1x1 / stride-2 shapes
+    (2, 14, 18, 16, 16, 3, 1, 1, 3, 2),       # 16-channel slice, SiLU, shortcut after activation
+    (1, 20, 22, 32, 48, 1, 1, 0, 3, 0),       # 1x1 with K 32 (< one k-tile), three 16-channel slices
+    (1, 31, 29, 32, 64, 3, 2, 1, 3, 0),       # stride 2, K 288, odd spatial dims
 ]
 
 
-@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("prec", ["fp32", "bf16", "bf16-gemm64", "bf16-gemm128"])
 @pytest.mark.parametrize("case", CONV_CASES)
-def test_conv_matches_torch(gpu, face_ctx_factory, prec, case):
+def test_conv_matches_torch(gpu, face_ctx_factory, monkeypatch, prec, case):
+    """bf16: the default dispatch (streaming 1x1 / streaming taps / GEMM); bf16-gemm64 and
+    bf16-gemm128: the implicit-GEMM kernel with 64- and 128-row tiles."""
+    if prec.startswith("bf16-gemm"):
+        monkeypatch.setenv("VD_CONV_TAPS", "0")
+        monkeypatch.setenv("VD_CONV_STREAM", "0")
+        monkeypatch.setenv("VD_CONV_SMALL", "100000000" if prec == "bf16-gemm64" else "0")
+        prec = "bf16"
     n, h, w, cin, cout, k, s, p, act, res_mode = case
     ctx = face_ctx_factory(prec, 8)
     rng = np.random.default_rng(cin * 7 + cout)
@@ -158,6 +169,26 @@ def test_conv_matches_torch(gpu, face_ctx_factory, prec, case):
     err = np.abs(got - y).max() / (np.abs(y).max() + 1e-6)
     assert got.shape == y.shape
     assert err < tol, f"rel err {err}"
+
+
+BIG_CASES = [
+    # 256 x 256-tile phased kernel (conv_big.hip): Cout % 256 == 0, Cin % 64 == 0
+    (2, 20, 24, 128, 256, 3, 1, 1, 1, 1),     # 3x3 + residual before ReLU, M tail (960 rows)
+    (1, 26, 30, 64, 256, 3, 2, 1, 1, 0),      # stride 2, two K tiles per tap row
+    (1, 33, 31, 256, 512, 1, 1, 0, 0, 2),     # 1x1, two N tiles, residual after activation
+    (2, 9, 11, 512, 256, 3, 1, 1, 2, 0),      # K = 4608 (72 K tiles), leaky
+]
+
+
+@pytest.mark.parametrize("ph", ["2", "4", "8"])
+@pytest.mark.parametrize("case", BIG_CASES)
+def test_conv_big_matches_torch(gpu, face_ctx_factory, monkeypatch, case, ph):
+    """Force the phased 256x256 kernel on small shapes (VD_CONV_BIG = min tiles),
+    in each of its schedules (VD_CONV_BIG_PH: 2 / 4 phases, 8 = staggered)."""
+    monkeypatch.setenv("VD_CONV_BIG", "1")
+    monkeypatch.setenv("VD_CONV_BIG_PH", ph)
+    monkeypatch.setenv("VD_CONV_STREAM", "0")
+    test_conv_matches_torch(gpu, face_ctx_factory, monkeypatch, "bf16", case)
 
 
 # ------------------------------------------------------------------ post-processing

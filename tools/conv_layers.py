@@ -46,7 +46,7 @@ def main(path, B=64):
     # stream: find the last stem launch (its grid is M/128 workgroups of 256)
     # and take the conv launches that follow it on the same stream.
     stem_grid = str((plan[0][1] + 127) // 128 * 256)
-    convs = [r for r in allk if "conv_igemm" in r["Kernel_Name"] or "conv1x1_stream" in r["Kernel_Name"]]
+    convs = [r for r in allk if any(k in r["Kernel_Name"] for k in ("conv_igemm", "conv1x1_stream", "conv_big"))]
     si = max(i for i, r in enumerate(convs) if r["Grid_Size_X"] == stem_grid)
     last = [r for r in convs[si:] if r["Stream_Id"] == convs[si]["Stream_Id"]][:len(plan)]
     tot_t = tot_f = 0
@@ -55,7 +55,7 @@ def main(path, B=64):
         fl = 2.0 * M * N * K
         tot_t += dt
         tot_f += fl
-        kn = r["Kernel_Name"].replace("conv1x1_stream_kernel", "S:").replace("conv_igemm_kernel", "G:").split("_1")[-1][:26]
+        kn = ("BIG" if "conv_big" in r["Kernel_Name"] else "S:" + r["Kernel_Name"].split("<")[1][:12] if "conv1x1_stream" in r["Kernel_Name"] else "G:" + r["Kernel_Name"].split("conv_igemm_kernel")[1][:22])
         print(f"{name:12s} M={M:8d} N={N:5d} K={K:5d} {dt*1e6:8.1f} us {fl/dt/1e12:7.1f} TF/s  {kn}")
     print(f"total {tot_t*1e3:.2f} ms  {tot_f/tot_t/1e12:.1f} TF/s")
 

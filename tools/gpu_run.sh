@@ -34,7 +34,7 @@ for s in "${STEPS[@]}"; do
                else run pytest_gpu 700 python -m pytest $PYTEST_ARGS; fi ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 400 python bench.py $BENCH_ARGS ;;
-        prof)  run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py $PROF_ARGS ;;
+        prof)  run prof${PROF_TAG:-} 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof${PROF_TAG:-} -o run --output-format csv -- python3 bench.py $PROF_ARGS ;;
         profp) run profp 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profp -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --faces 0 --plates 1 ;;
         pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py $PMC_ARGS &&
                run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py $PMC_ARGS ;;

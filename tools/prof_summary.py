@@ -8,7 +8,7 @@ numbers (roofline.avg_launch_ms).
 import csv
 import sys
 
-FAMILIES = [("conv", ("conv_igemm_kernel", "conv1x1_stream_kernel")), ("mosaic", ("mosaic_",)), ("letterbox", ("letterbox_kernel", "letterbox_s2d_kernel")),
+FAMILIES = [("conv", ("conv_igemm_kernel", "conv1x1_stream_kernel", "conv_big_kernel")), ("mosaic", ("mosaic_",)), ("letterbox", ("letterbox_kernel", "letterbox_s2d_kernel")),
             ("post", ("candidates_kernel", "nms_kernel")), ("other", ("maxpool", "upsample"))]
 
 

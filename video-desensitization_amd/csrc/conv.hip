@@ -59,8 +59,7 @@ __device__ __attribute__((aligned(16))) unsigned vd_zero16[4] = {0u, 0u, 0u, 0u}
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-// NT threads (4 or 8 waves); STAGES = 2: one tile in flight, two barriers per
-// K tile; STAGES = 3 (LDS-DMA only): two tiles in flight, one barrier per K tile.
+// NT threads (4 waves); two LDS stages: one K tile in flight, two barriers per K tile.
 template <typename T, int BM, int BN, int NT, int STAGES, bool DENSE, bool GLDS>
 __global__ __launch_bounds__(NT) void conv_igemm_kernel(ConvArgs a) {
     constexpr int VEC = Elem<T>::VEC;
@@ -72,14 +71,14 @@ __global__ __launch_bounds__(NT) void conv_igemm_kernel(ConvArgs a) {
     constexpr int TM = WTM / 16, TN = WTN / 16;
     constexpr int ROWS = NT / 8;                 // tile rows covered by one pass of 16-B chunks
     constexpr int A_IT = BM / ROWS, B_IT = BN / ROWS;
-    static_assert(BM % ROWS == 0 && BN % ROWS == 0 && (STAGES == 2 || GLDS), "tile shape");
+    static_assert(BM % ROWS == 0 && BN % ROWS == 0 && STAGES == 2, "tile shape");
     constexpr int KSTEP = std::is_same<T, float>::value ? 16 : 32;  // K per fragment step
     constexpr int NKS = BKE / KSTEP;                                 // = 2
     constexpr int BUF = (BM + BN) * 128;
     constexpr int EPLD = BN + 4;                 // f32 epilogue row stride (conflict-free fragment writes)
     constexpr int CG = BN / 8;                   // 8-channel groups per output row
     constexpr int ITEMS = BM * CG / NT;          // epilogue items (row, 8 channels) per thread
-    constexpr int EP = (ITEMS % 4 == 0) ? 4 : 2; // epilogue passes (BM/EP rows staged per pass)
+    constexpr int EP = (ITEMS % 4 == 0) ? 4 : ((ITEMS % 2 == 0) ? 2 : 1);   // epilogue passes (BM/EP rows each)
 
     // dynamic LDS: STAGES K buffers (1 when K fits one tile) | the f32 epilogue tile, BM/EP rows at a time
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -260,24 +259,7 @@ __global__ __launch_bounds__(NT) void conv_igemm_kernel(ConvArgs a) {
         rpf[q] = *(const u32x4*)rp;
     }
 
-    if constexpr (GLDS && STAGES == 3) {
-        // Three LDS buffers, tiles kt+1 and kt+2 in flight while kt is consumed;
-        // one raw barrier per K tile (it also retires the reads of kt-1, whose
-        // buffer is then refilled with kt+2).
-        constexpr int LPT = A_IT + B_IT;
-        VD_GLDS_TILE(0, 0);
-        if (nk > 1) VD_GLDS_TILE(1, 1);
-        for (int kt = 0; kt < nk; ++kt) {
-            if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(LPT) : "memory");
-            else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            asm volatile("" ::: "memory");
-            if (kt + 2 < nk) VD_GLDS_TILE(kt + 2, (kt + 2) % 3);
-            VD_COMPUTE(kt % 3);
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-    } else if constexpr (GLDS) {
+    if constexpr (GLDS) {
         // Two LDS buffers, tile kt+1 in flight while kt is consumed. Raw barriers
         // with counted vmcnt: __syncthreads() would add vmcnt(0) and drain the DMA.
         constexpr int LPT = A_IT + B_IT;                 // DMA instructions per lane per tile
@@ -415,19 +397,11 @@ hipError_t launch_bn(const ConvArgs& a0, bool dense, hipStream_t s) {
     const int mt = (a.M + BM - 1) / BM;
     dim3 grid(mt * a.ntiles_n), block(NT);
     constexpr int VEC = Elem<T>::VEC;
-    constexpr int ITEMS = BM * (BN / 8) / NT, EP = (ITEMS % 4 == 0) ? 4 : 2;   // as in the kernel
+    constexpr int ITEMS = BM * (BN / 8) / NT, EP = (ITEMS % 4 == 0) ? 4 : ((ITEMS % 2 == 0) ? 2 : 1);   // as in the kernel
     constexpr size_t BUF = (size_t)(BM + BN) * 128, EPI = (size_t)(BM / EP) * (BN + 4) * 4;
     const int nk = a.kpad / (8 * VEC);
     const size_t lds = std::max((nk > 1 ? STAGES : 1) * BUF, EPI);
-    if constexpr (STAGES == 3) {
-        static const bool attr = [] {   // > 64 KB of dynamic LDS must be opted into
-            (void)hipFuncSetAttribute((const void*)conv_igemm_kernel<T, BM, BN, NT, 3, true, true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)(3 * BUF));
-            return true;
-        }();
-        (void)attr;
-        hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, NT, 3, true, true>), grid, block, lds, s, a);
-    } else if (glds) {
+    if (glds) {
         if (dense) hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, NT, 2, true, true>), grid, block, lds, s, a);
         else hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, NT, 2, false, true>), grid, block, lds, s, a);
     } else {
@@ -443,20 +417,29 @@ hipError_t launch_bn(const ConvArgs& a0, bool dense, hipStream_t s) {
 // bf16 layers with Cout >= 128 take the 256 x 128, 8-wave, 3-stage form.
 // Weights must be packed with Npad a multiple of the chosen BN (runtime pads to 128).
 hipError_t vd_launch_conv(const ConvArgs& a, bool f32, hipStream_t s) {
-    static const int big_min = [] { const char* e = getenv("VD_CONV_BIG_MIN"); return e ? atoi(e) : 0; }();
     const int vec = f32 ? 4 : 8;
     const int bke = 8 * vec;
     const bool dense = (a.cin_pad % bke) == 0;
     if (!f32 && vd_conv1x1_stream_ok(a)) return vd_launch_conv1x1_stream(a, s);
-    if (!f32 && dense && a.cout >= 128 && big_min > 0 && a.kpad / bke > 1 &&
-        (long)((a.M + 255) / 256) * ((a.cout + 127) / 128) >= big_min)
-        return launch_bn<__bf16, 256, 128, 512, 3>(a, dense, s);
+    if (!f32 && vd_conv_big_ok(a)) return vd_launch_conv_big(a, s);
+    if (!f32 && vd_conv_taps_ok(a)) return vd_launch_conv_taps(a, s);
     if (f32) {
         if (a.cout <= 32) return launch_bn<float, 128, 32>(a, dense, s);
         if (a.cout <= 64) return launch_bn<float, 128, 64>(a, dense, s);
         return launch_bn<float, 128, 128>(a, dense, s);
     }
-    if (a.cout <= 32) return launch_bn<__bf16, 128, 32>(a, dense, s);
-    if (a.cout <= 64) return launch_bn<__bf16, 128, 64>(a, dense, s);
+    // Small grids (YOLO's deep levels, RetinaFace level 3): 64-row tiles give
+    // twice the workgroups, so the launch covers more of the 256 CUs.
+    const int bn = a.cout <= 32 ? 32 : (a.cout <= 64 ? 64 : 128);
+    const long tiles128 = (long)((a.M + 127) / 128) * ((a.cout + bn - 1) / bn);
+    const char* e = getenv("VD_CONV_SMALL");
+    const long small_lim = e ? atol(e) : 512;
+    if (tiles128 < small_lim) {
+        if (bn == 32) return launch_bn<__bf16, 64, 32>(a, dense, s);
+        if (bn == 64) return launch_bn<__bf16, 64, 64>(a, dense, s);
+        return launch_bn<__bf16, 64, 128>(a, dense, s);
+    }
+    if (bn == 32) return launch_bn<__bf16, 128, 32>(a, dense, s);
+    if (bn == 64) return launch_bn<__bf16, 128, 64>(a, dense, s);
     return launch_bn<__bf16, 128, 128>(a, dense, s);
 }

@@ -42,7 +42,10 @@ __device__ __forceinline__ float bf_hi(unsigned u) { return __uint_as_float(u & 
 
 // KS: K / 32 (k-steps), NTT: 16-channel tiles per wave (NCH = 16 * NTT channels per
 // workgroup), ACT / RES: activation and residual mode (compile-time: no per-element branches).
-template <int KS, int NTT, int ACT, int RES>
+// TAPS: general KxK / strided / padded taps with any Cin (multiple of 8): each lane's
+// 16-B fragment of k-step ks is (tap, 8 channels) = K elements (4ks + q)*8 .. +8 in the
+// (kh, kw, c) order, gathered per pixel with zero padding (and zero past the last tap).
+template <int KS, int NTT, int ACT, int RES, bool TAPS>
 __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvArgs a, int nchunks, int groups) {
     constexpr int NCH = 16 * NTT;
     constexpr int KT = (KS + 1) / 2;                      // 128-byte K tiles per weight row
@@ -66,7 +69,7 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvArgs a, int nch
         for (int i = tid; i < NCH * CPR; i += 512) {
             const int row = i / CPR, c = i - row * CPR;
             const int j = row >> 4, ii = row & 15;
-            const int chn = 32 * (j >> 1) + 8 * (ii >> 2) + 4 * (j & 1) + (ii & 3);
+            const int chn = NTT == 1 ? row : 32 * (j >> 1) + 8 * (ii >> 2) + 4 * (j & 1) + (ii & 3);
             const u32x4 v = *(const u32x4*)(w + (size_t)(n0 + chn) * a.kpad + c * 8);
             *(u32x4*)(smem + (c >> 3) * (NCH * 128) + lds_off(row, c & 7)) = v;
         }
@@ -79,6 +82,20 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvArgs a, int nch
 
     const int p_lane = lane & 15, q = lane >> 4;          // pixel within group, channel quad / k chunk
     const int ohw = a.yh * a.yw;
+    // TAPS: per-lane tap table (the lane's K chunk of every k-step is fixed)
+    int toff[TAPS ? KS : 1], tdy[TAPS ? KS : 1], tdx[TAPS ? KS : 1];
+    if constexpr (TAPS) {
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const int ko = (ks * 4 + q) * 8;
+            const int tap = ko / a.cin_pad, c = ko - tap * a.cin_pad;
+            const int dy = tap / a.kw, dx = tap - dy * a.kw;
+            const bool real = tap < a.kh * a.kw;
+            toff[ks] = (dy * a.xw + dx) * a.ldx + c;
+            tdy[ks] = real ? dy : -(1 << 20);               // past the last tap: always "outside"
+            tdx[ks] = dx;
+        }
+    }
     const int wstride = nmblk * 8;
     for (int g = mblk * 8 + wid; g < groups; g += wstride) {
         // keep the weight-fragment LDS reads inside the loop (hoisting them all
@@ -91,22 +108,40 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvArgs a, int nch
         const int rem = m - b * ohw;
         const int oy = rem / a.yw;
         const int ox = rem - oy * a.yw;
-        // input fragments: pixel p_lane, channels ks*32 + 8q .. +8
-        const __bf16* xp = (const __bf16*)a.x +
-                           (((size_t)b * a.xh + oy * a.stride) * a.xw + ox * a.stride) * a.ldx + a.xcoff + q * 8;
         u32x4 xf[KS];
+        if constexpr (TAPS) {
+            const int iy0 = oy * a.stride - a.pad, ix0 = ox * a.stride - a.pad;
+            const long base = (((long)b * a.xh + iy0) * a.xw + ix0) * a.ldx + a.xcoff;
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks)
-            xf[ks] = *(const u32x4*)(xp + ks * 32);
-        // residual: pixel p_lane, channels n0 + 32i + 8q .. +8 (16 B each)
-        u32x4 rf[NTT / 2];
+            for (int ks = 0; ks < KS; ++ks) {
+                const int iy = iy0 + tdy[ks], ix = ix0 + tdx[ks];
+                const bool in = (unsigned)iy < (unsigned)a.xh && (unsigned)ix < (unsigned)a.xw;
+                const __bf16* src = (const __bf16*)a.x + (in ? base + toff[ks] : 0);
+                const u32x4 v = *(const u32x4*)src;
+                xf[ks] = in ? v : u32x4{0u, 0u, 0u, 0u};
+            }
+        } else {
+            // input fragments: pixel p_lane, channels ks*32 + 8q .. +8
+            const __bf16* xp = (const __bf16*)a.x +
+                               (((size_t)b * a.xh + oy * a.stride) * a.xw + ox * a.stride) * a.ldx + a.xcoff + q * 8;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+                xf[ks] = *(const u32x4*)(xp + ks * 32);
+        }
+        // residual: pixel p_lane, channels n0 + 32i + 8q .. +8 (16 B each; NTT 1: 4q .. +4, 8 B)
+        u32x4 rf[NTT > 1 ? NTT / 2 : 1];
         if constexpr (RES != VD_RES_NONE) {
             size_t roff;
             if (a.res_up) roff = ((size_t)(b * a.rh + (oy >> 1)) * a.rw + (ox >> 1)) * a.res_ld;
             else roff = (size_t)m * a.res_ld;
-            const __bf16* rp = (const __bf16*)a.res + roff + a.res_coff + n0 + q * 8;
+            if constexpr (NTT == 1) {
+                const unsigned* rp = (const unsigned*)((const __bf16*)a.res + roff + a.res_coff + n0 + q * 4);
+                rf[0] = u32x4{rp[0], rp[1], 0u, 0u};
+            } else {
+                const __bf16* rp = (const __bf16*)a.res + roff + a.res_coff + n0 + q * 8;
 #pragma unroll
-            for (int i = 0; i < NTT / 2; ++i) rf[i] = *(const u32x4*)(rp + 32 * i);
+                for (int i = 0; i < NTT / 2; ++i) rf[i] = *(const u32x4*)(rp + 32 * i);
+            }
         }
         f32x4_t acc[NTT];
 #pragma unroll
@@ -122,8 +157,34 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvArgs a, int nch
                                                                  __builtin_bit_cast(bf16x8_t, xf[ks]), acc[j], 0, 0, 0);
             }
         }
-        // lane holds channels n0 + 32i + 8q + (0..3 from tile 2i, 4..7 from tile 2i+1) of pixel m
         if (!ok) continue;
+        if constexpr (NTT == 1) {   // lane holds channels n0 + 4q .. +4 of pixel m
+            const size_t yo = (size_t)m * a.ldy + a.ycoff + n0 + q * 4;
+            const float4 sc = *(const float4*)(s_scale + q * 4), sh = *(const float4*)(s_shift + q * 4);
+            float v[4] = {acc[0][0] * sc.x + sh.x, acc[0][1] * sc.y + sh.y, acc[0][2] * sc.z + sh.z,
+                          acc[0][3] * sc.w + sh.w};
+            float rv[4] = {0.f, 0.f, 0.f, 0.f};
+            if constexpr (RES != VD_RES_NONE) {
+                rv[0] = bf_lo(rf[0][0]); rv[1] = bf_hi(rf[0][0]); rv[2] = bf_lo(rf[0][1]); rv[3] = bf_hi(rf[0][1]);
+            }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float t = v[e];
+                if constexpr (RES == VD_RES_PRE_ACT) t += rv[e];
+                t = act_apply<ACT>(t, a.slope);
+                if constexpr (RES == VD_RES_POST_ACT) t += rv[e];
+                v[e] = t;
+            }
+            if (a.out_f32) {
+                *(float4*)((float*)a.y + yo) = make_float4(v[0], v[1], v[2], v[3]);
+            } else {
+                typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+                const bf16x4_t o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+                *(bf16x4_t*)((__bf16*)a.y + yo) = o;
+            }
+            continue;
+        }
+        // lane holds channels n0 + 32i + 8q + (0..3 from tile 2i, 4..7 from tile 2i+1) of pixel m
         const size_t yo = (size_t)m * a.ldy + a.ycoff + n0 + q * 8;
 #pragma unroll
         for (int i = 0; i < NTT / 2; ++i) {
@@ -160,12 +221,12 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvArgs a, int nch
     }
 }
 
-template <int KS, int NTT, int ACT, int RES>
+template <int KS, int NTT, int ACT, int RES, bool TAPS>
 hipError_t launch_stream(const ConvArgs& a, hipStream_t s) {
     constexpr int NCH = 16 * NTT, KT = (KS + 1) / 2;
     constexpr size_t lds = (size_t)KT * NCH * 128 + 2 * NCH * sizeof(float);
     static const bool attr = [] {
-        (void)hipFuncSetAttribute((const void*)conv1x1_stream_kernel<KS, NTT, ACT, RES>,
+        (void)hipFuncSetAttribute((const void*)conv1x1_stream_kernel<KS, NTT, ACT, RES, TAPS>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         return true;
     }();
@@ -176,7 +237,7 @@ hipError_t launch_stream(const ConvArgs& a, hipStream_t s) {
         int dev = 0, cus = 256, per_cu = 1;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv1x1_stream_kernel<KS, NTT, ACT, RES>, 512, lds);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv1x1_stream_kernel<KS, NTT, ACT, RES, TAPS>, 512, lds);
         return std::max(1, cus * std::max(1, per_cu));
     }();
     const int nchunks = a.cout / NCH;
@@ -184,23 +245,31 @@ hipError_t launch_stream(const ConvArgs& a, hipStream_t s) {
     int k = std::max(1, resident / (8 * nchunks));
     k = std::min(k, std::max(1, (groups + 63) / 64));
     dim3 grid(8 * nchunks * k), block(512);
-    hipLaunchKernelGGL((conv1x1_stream_kernel<KS, NTT, ACT, RES>), grid, block, lds, s, a, nchunks, groups);
+    hipLaunchKernelGGL((conv1x1_stream_kernel<KS, NTT, ACT, RES, TAPS>), grid, block, lds, s, a, nchunks, groups);
     return hipGetLastError();
 }
 
-template <int KS, int NTT>
+template <int KS, int NTT, bool TAPS>
 hipError_t launch_mode(const ConvArgs& a, hipStream_t s) {
     if (a.act == VD_ACT_RELU) {
-        if (a.res_mode == VD_RES_PRE_ACT) return launch_stream<KS, NTT, VD_ACT_RELU, VD_RES_PRE_ACT>(a, s);
-        if (a.res_mode == VD_RES_POST_ACT) return launch_stream<KS, NTT, VD_ACT_RELU, VD_RES_POST_ACT>(a, s);
-        return launch_stream<KS, NTT, VD_ACT_RELU, VD_RES_NONE>(a, s);
+        if (a.res_mode == VD_RES_PRE_ACT) return launch_stream<KS, NTT, VD_ACT_RELU, VD_RES_PRE_ACT, TAPS>(a, s);
+        if (a.res_mode == VD_RES_POST_ACT) return launch_stream<KS, NTT, VD_ACT_RELU, VD_RES_POST_ACT, TAPS>(a, s);
+        return launch_stream<KS, NTT, VD_ACT_RELU, VD_RES_NONE, TAPS>(a, s);
     }
     if (a.act == VD_ACT_NONE) {
-        if (a.res_mode == VD_RES_POST_ACT) return launch_stream<KS, NTT, VD_ACT_NONE, VD_RES_POST_ACT>(a, s);
-        if (a.res_mode == VD_RES_NONE) return launch_stream<KS, NTT, VD_ACT_NONE, VD_RES_NONE>(a, s);
+        if (a.res_mode == VD_RES_POST_ACT) return launch_stream<KS, NTT, VD_ACT_NONE, VD_RES_POST_ACT, TAPS>(a, s);
+        if (a.res_mode == VD_RES_NONE) return launch_stream<KS, NTT, VD_ACT_NONE, VD_RES_NONE, TAPS>(a, s);
     }
-    if (a.act == VD_ACT_SILU && a.res_mode == VD_RES_NONE) return launch_stream<KS, NTT, VD_ACT_SILU, VD_RES_NONE>(a, s);
-    return hipErrorInvalidValue;   // excluded by vd_conv1x1_stream_ok
+    if (a.act == VD_ACT_SILU) {
+        if (a.res_mode == VD_RES_POST_ACT) return launch_stream<KS, NTT, VD_ACT_SILU, VD_RES_POST_ACT, TAPS>(a, s);
+        if (a.res_mode == VD_RES_NONE) return launch_stream<KS, NTT, VD_ACT_SILU, VD_RES_NONE, TAPS>(a, s);
+    }
+    return hipErrorInvalidValue;   // excluded by the eligibility checks
+}
+
+bool mode_ok(const ConvArgs& a) {
+    return (a.act == VD_ACT_RELU) || (a.act == VD_ACT_NONE && a.res_mode != VD_RES_PRE_ACT) ||
+           (a.act == VD_ACT_SILU && a.res_mode != VD_RES_PRE_ACT);
 }
 
 }  // namespace
@@ -208,23 +277,57 @@ hipError_t launch_mode(const ConvArgs& a, hipStream_t s) {
 // Eligible: bf16, 1x1 taps without padding, K in {64,128,256}, Cout a multiple of
 // the channel slice, 16-B aligned channel offsets/strides for the residual and output.
 bool vd_conv1x1_stream_ok(const ConvArgs& a) {
-    static const bool on = [] { const char* e = getenv("VD_CONV_STREAM"); return !e || atoi(e) != 0; }();
-    if (!on || a.kh != 1 || a.kw != 1 || a.pad != 0) return false;
+    const char* e = getenv("VD_CONV_STREAM");   // read per call (A/B and tests)
+    if ((e && atoi(e) == 0) || a.kh != 1 || a.kw != 1 || a.pad != 0) return false;
     if (a.cin_pad != 64 && a.cin_pad != 128 && a.cin_pad != 256) return false;
     if (a.kpad < a.cin_pad || (a.cout % 64) != 0) return false;
     if ((a.ldx | a.xcoff) & 7) return false;
     if ((a.ldy | a.ycoff) & 7) return false;
     if (a.res_mode != VD_RES_NONE && ((a.res_ld | a.res_coff) & 7)) return false;
-    const bool mode_ok = (a.act == VD_ACT_RELU) ||
-                         (a.act == VD_ACT_NONE && a.res_mode != VD_RES_PRE_ACT) ||
-                         (a.act == VD_ACT_SILU && a.res_mode == VD_RES_NONE);
-    return mode_ok;
+    return mode_ok(a);
 }
 
 hipError_t vd_launch_conv1x1_stream(const ConvArgs& a, hipStream_t s) {
     // 128-channel slices (64 when Cout is not a multiple of 128); K 64/128/256
     const bool wide = a.cout % 128 == 0;
-    if (a.cin_pad == 64) return wide ? launch_mode<2, 8>(a, s) : launch_mode<2, 4>(a, s);
-    if (a.cin_pad == 128) return wide ? launch_mode<4, 8>(a, s) : launch_mode<4, 4>(a, s);
-    return wide ? launch_mode<8, 8>(a, s) : launch_mode<8, 4>(a, s);
+    if (a.cin_pad == 64) return wide ? launch_mode<2, 8, false>(a, s) : launch_mode<2, 4, false>(a, s);
+    if (a.cin_pad == 128) return wide ? launch_mode<4, 8, false>(a, s) : launch_mode<4, 4, false>(a, s);
+    return wide ? launch_mode<8, 8, false>(a, s) : launch_mode<8, 4, false>(a, s);
+}
+
+// General taps (any kh x kw, stride, pad; Cin a multiple of 8) for small layers:
+// K (padded to 64) <= TAPS_KMAX and Cout a multiple of 16 up to 128. Measured
+// (tools/convbench yolo): 1.2-2.4x the implicit GEMM at K <= 288 (YOLO's 16-64
+// channel layers), 0.6x at K = 576, hence the cut. VD_CONV_TAPS=0 disables.
+constexpr int TAPS_KMAX = 320;
+bool vd_conv_taps_ok(const ConvArgs& a) {
+    const char* e = getenv("VD_CONV_TAPS");
+    if (e && atoi(e) == 0) return false;
+    if ((a.cin_pad & 7) || a.kpad > TAPS_KMAX || (a.kpad & 63) || (a.cout & 15) || a.cout > 128) return false;
+    if ((a.ldx | a.xcoff) & 7) return false;
+    const int align = (a.cout % 32 == 0) ? 7 : 3;        // 16-B (or 8-B for 16-channel slices) stores
+    if ((a.ldy | a.ycoff) & align) return false;
+    if (a.res_mode != VD_RES_NONE && ((a.res_ld | a.res_coff) & align)) return false;
+    if (a.res_mode != VD_RES_NONE && a.res_up) return false;
+    return mode_ok(a);
+}
+
+template <int KS>
+hipError_t launch_taps_n(const ConvArgs& a, hipStream_t s) {
+    // channel slice: 16 * NTT, largest that divides Cout with the slice weights <= 64 KB
+    const int kb = a.kpad * 2;
+    if (a.cout % 64 == 0 && 64 * kb <= 65536) return launch_mode<KS, 4, true>(a, s);
+    if (a.cout % 32 == 0 && 32 * kb <= 65536) return launch_mode<KS, 2, true>(a, s);
+    return launch_mode<KS, 1, true>(a, s);
+}
+
+hipError_t vd_launch_conv_taps(const ConvArgs& a, hipStream_t s) {
+    switch (a.kpad / 32) {
+        case 2: return launch_taps_n<2>(a, s);
+        case 4: return launch_taps_n<4>(a, s);
+        case 6: return launch_taps_n<6>(a, s);
+        case 8: return launch_taps_n<8>(a, s);
+        case 10: return launch_taps_n<10>(a, s);
+        default: return hipErrorInvalidValue;
+    }
 }

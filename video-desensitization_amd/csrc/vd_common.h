@@ -87,7 +87,11 @@ struct LetterboxArgs {
 
 // ---- kernel launchers (one translation unit each) ----
 bool vd_conv1x1_stream_ok(const ConvArgs& a);
+bool vd_conv_big_ok(const ConvArgs& a);
+hipError_t vd_launch_conv_big(const ConvArgs& a, hipStream_t s);
 hipError_t vd_launch_conv1x1_stream(const ConvArgs& a, hipStream_t s);
+bool vd_conv_taps_ok(const ConvArgs& a);
+hipError_t vd_launch_conv_taps(const ConvArgs& a, hipStream_t s);
 hipError_t vd_launch_conv(const ConvArgs& a, bool f32, hipStream_t s);
 hipError_t vd_launch_letterbox(const LetterboxArgs& a, hipStream_t s);
 hipError_t vd_launch_maxpool(bool f32, const void* x, int n, int xh, int xw, int ldx, int xcoff,
