@@ -186,6 +186,7 @@ def test_conv_big_matches_torch(gpu, face_ctx_factory, monkeypatch, case, ph):
     """Force the phased 256x256 kernel on small shapes (VD_CONV_BIG = min tiles),
     in each of its schedules (VD_CONV_BIG_PH: 2 / 4 phases, 8 = staggered)."""
     monkeypatch.setenv("VD_CONV_BIG", "1")
+    monkeypatch.setenv("VD_CONV_BIG_KMIN", "0")
     monkeypatch.setenv("VD_CONV_BIG_PH", ph)
     monkeypatch.setenv("VD_CONV_STREAM", "0")
     test_conv_matches_torch(gpu, face_ctx_factory, monkeypatch, "bf16", case)

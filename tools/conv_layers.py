@@ -43,12 +43,14 @@ def main(path, B=64):
     allk = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     plan = face_plan(B)
     # The face forward may share the GPU with the plate network on a second
-    # stream: find the last stem launch (its grid is M/128 workgroups of 256)
+    # stream: anchor on the last face letterbox (space-to-depth form in bf16)
     # and take the conv launches that follow it on the same stream.
-    stem_grid = str((plan[0][1] + 127) // 128 * 256)
-    convs = [r for r in allk if any(k in r["Kernel_Name"] for k in ("conv_igemm", "conv1x1_stream", "conv_big"))]
-    si = max(i for i, r in enumerate(convs) if r["Grid_Size_X"] == stem_grid)
-    last = [r for r in convs[si:] if r["Stream_Id"] == convs[si]["Stream_Id"]][:len(plan)]
+    conv_keys = ("conv_igemm", "conv1x1_stream", "conv_big")
+    li = max(i for i, r in enumerate(allk) if "letterbox_s2d_kernel" in r["Kernel_Name"]
+             or ("letterbox_kernel" in r["Kernel_Name"] and int(r["Grid_Size_Y"]) == 640))
+    stream = allk[li]["Stream_Id"]
+    last = [r for r in allk[li:] if r["Stream_Id"] == stream and any(k in r["Kernel_Name"] for k in conv_keys)]
+    last = last[:len(plan)]
     tot_t = tot_f = 0
     for (name, M, N, K), r in zip(plan, last):
         dt = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9

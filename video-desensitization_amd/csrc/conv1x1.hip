@@ -97,52 +97,60 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvArgs a, int nch
         }
     }
     const int wstride = nmblk * 8;
-    for (int g = mblk * 8 + wid; g < groups; g += wstride) {
+    constexpr int NR = NTT > 1 ? NTT / 2 : 1;
+    // Load group G's input fragments into XF and its residual into RF.
+#define VD_SLOAD(G, XF, RF)                                                                    \
+    do {                                                                                       \
+        const int mu_ = (G) * 16 + p_lane;                                                     \
+        const int m_ = mu_ < a.M ? mu_ : a.M - 1;   /* tail lanes load a valid pixel */        \
+        const int b_ = m_ / ohw;                                                               \
+        const int rem_ = m_ - b_ * ohw;                                                        \
+        const int oy_ = rem_ / a.yw;                                                           \
+        const int ox_ = rem_ - oy_ * a.yw;                                                     \
+        if constexpr (TAPS) {                                                                  \
+            const int iy0 = oy_ * a.stride - a.pad, ix0 = ox_ * a.stride - a.pad;              \
+            const long base = (((long)b_ * a.xh + iy0) * a.xw + ix0) * a.ldx + a.xcoff;        \
+            _Pragma("unroll") for (int ks = 0; ks < KS; ++ks) {                                \
+                const int iy = iy0 + tdy[ks], ix = ix0 + tdx[ks];                              \
+                const bool in = (unsigned)iy < (unsigned)a.xh && (unsigned)ix < (unsigned)a.xw;\
+                const __bf16* src = (const __bf16*)a.x + (in ? base + toff[ks] : 0);           \
+                const u32x4 v = *(const u32x4*)src;                                            \
+                XF[ks] = in ? v : u32x4{0u, 0u, 0u, 0u};                                       \
+            }                                                                                  \
+        } else {                                                                               \
+            const __bf16* xp = (const __bf16*)a.x +                                            \
+                (((size_t)b_ * a.xh + oy_ * a.stride) * a.xw + ox_ * a.stride) * a.ldx + a.xcoff + q * 8; \
+            _Pragma("unroll") for (int ks = 0; ks < KS; ++ks) XF[ks] = *(const u32x4*)(xp + ks * 32); \
+        }                                                                                      \
+        if constexpr (RES != VD_RES_NONE) {                                                    \
+            size_t roff;                                                                       \
+            if (a.res_up) roff = ((size_t)(b_ * a.rh + (oy_ >> 1)) * a.rw + (ox_ >> 1)) * a.res_ld; \
+            else roff = (size_t)m_ * a.res_ld;                                                 \
+            if constexpr (NTT == 1) {                                                          \
+                const unsigned* rp = (const unsigned*)((const __bf16*)a.res + roff + a.res_coff + n0 + q * 4); \
+                RF[0] = u32x4{rp[0], rp[1], 0u, 0u};                                           \
+            } else {                                                                           \
+                const __bf16* rp = (const __bf16*)a.res + roff + a.res_coff + n0 + q * 8;      \
+                _Pragma("unroll") for (int i = 0; i < NR; ++i) RF[i] = *(const u32x4*)(rp + 32 * i); \
+            }                                                                                  \
+        }                                                                                      \
+    } while (0)
+
+    // Software-pipelined over the wave's groups: group g+1's loads are issued
+    // before group g's MFMAs and stores, so every wave keeps reads in flight.
+    u32x4 xf[KS], rf[NR];
+    int g = mblk * 8 + wid;
+    if (g < groups) VD_SLOAD(g, xf, rf);
+    for (; g < groups; g += wstride) {
         // keep the weight-fragment LDS reads inside the loop (hoisting them all
         // would pin NTT*KS*4 VGPRs and cut the number of resident waves)
         asm volatile("" ::: "memory");
+        u32x4 xn[KS], rn[NR];
+        const int gn = g + wstride;
+        if (gn < groups) VD_SLOAD(gn, xn, rn);
         const int mu = g * 16 + p_lane;
         const bool ok = mu < a.M;
-        const int m = ok ? mu : a.M - 1;          // tail lanes load a valid pixel, store nothing
-        const int b = m / ohw;
-        const int rem = m - b * ohw;
-        const int oy = rem / a.yw;
-        const int ox = rem - oy * a.yw;
-        u32x4 xf[KS];
-        if constexpr (TAPS) {
-            const int iy0 = oy * a.stride - a.pad, ix0 = ox * a.stride - a.pad;
-            const long base = (((long)b * a.xh + iy0) * a.xw + ix0) * a.ldx + a.xcoff;
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-                const int iy = iy0 + tdy[ks], ix = ix0 + tdx[ks];
-                const bool in = (unsigned)iy < (unsigned)a.xh && (unsigned)ix < (unsigned)a.xw;
-                const __bf16* src = (const __bf16*)a.x + (in ? base + toff[ks] : 0);
-                const u32x4 v = *(const u32x4*)src;
-                xf[ks] = in ? v : u32x4{0u, 0u, 0u, 0u};
-            }
-        } else {
-            // input fragments: pixel p_lane, channels ks*32 + 8q .. +8
-            const __bf16* xp = (const __bf16*)a.x +
-                               (((size_t)b * a.xh + oy * a.stride) * a.xw + ox * a.stride) * a.ldx + a.xcoff + q * 8;
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks)
-                xf[ks] = *(const u32x4*)(xp + ks * 32);
-        }
-        // residual: pixel p_lane, channels n0 + 32i + 8q .. +8 (16 B each; NTT 1: 4q .. +4, 8 B)
-        u32x4 rf[NTT > 1 ? NTT / 2 : 1];
-        if constexpr (RES != VD_RES_NONE) {
-            size_t roff;
-            if (a.res_up) roff = ((size_t)(b * a.rh + (oy >> 1)) * a.rw + (ox >> 1)) * a.res_ld;
-            else roff = (size_t)m * a.res_ld;
-            if constexpr (NTT == 1) {
-                const unsigned* rp = (const unsigned*)((const __bf16*)a.res + roff + a.res_coff + n0 + q * 4);
-                rf[0] = u32x4{rp[0], rp[1], 0u, 0u};
-            } else {
-                const __bf16* rp = (const __bf16*)a.res + roff + a.res_coff + n0 + q * 8;
-#pragma unroll
-                for (int i = 0; i < NTT / 2; ++i) rf[i] = *(const u32x4*)(rp + 32 * i);
-            }
-        }
+        const int m = ok ? mu : a.M - 1;
         f32x4_t acc[NTT];
 #pragma unroll
         for (int j = 0; j < NTT; ++j) acc[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -157,7 +165,7 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvArgs a, int nch
                                                                  __builtin_bit_cast(bf16x8_t, xf[ks]), acc[j], 0, 0, 0);
             }
         }
-        if (!ok) continue;
+        if (ok) {
         if constexpr (NTT == 1) {   // lane holds channels n0 + 4q .. +4 of pixel m
             const size_t yo = (size_t)m * a.ldy + a.ycoff + n0 + q * 4;
             const float4 sc = *(const float4*)(s_scale + q * 4), sh = *(const float4*)(s_shift + q * 4);
@@ -182,8 +190,7 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvArgs a, int nch
                 const bf16x4_t o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
                 *(bf16x4_t*)((__bf16*)a.y + yo) = o;
             }
-            continue;
-        }
+        } else {
         // lane holds channels n0 + 32i + 8q + (0..3 from tile 2i, 4..7 from tile 2i+1) of pixel m
         const size_t yo = (size_t)m * a.ldy + a.ycoff + n0 + q * 8;
 #pragma unroll
@@ -218,7 +225,14 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvArgs a, int nch
                 *(bf16x8_t*)((__bf16*)a.y + yo + 32 * i) = o;
             }
         }
+        }
+        }
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) xf[ks] = xn[ks];
+#pragma unroll
+        for (int i = 0; i < NR; ++i) rf[i] = rn[i];
     }
+#undef VD_SLOAD
 }
 
 template <int KS, int NTT, int ACT, int RES, bool TAPS>
