@@ -66,6 +66,26 @@ def test_heads_bf16_close(gpu, face_ctx_factory):
     assert _rel(loc, eloc) < 6e-2 and _rel(conf, econf) < 6e-2
 
 
+def test_heads_bf16_fused_downsample_matches_unfused(gpu, monkeypatch):
+    """bf16 plans fuse each bottleneck's conv3 + downsample into one streaming pass
+    (layer1.0, layer2.0); VD_CONV_DUAL=0 at weight load keeps them separate. The
+    only numeric difference is the bf16 rounding of the downsample output that the
+    unfused plan stores, so the heads agree far tighter than the oracle bound."""
+    import vdmi
+    fr = _frames(2, 1080, 1920, seed=3)
+    out = {}
+    for dual in ("1", "0"):
+        monkeypatch.setenv("VD_CONV_DUAL", dual)
+        ctx = vdmi.Context(precision="bf16", max_batch=2)
+        try:
+            ctx.load_weights(0, face_weights("default"))
+            out[dual] = ctx.forward_heads(fr)
+        finally:
+            ctx.close()
+    for a, b in zip(out["1"], out["0"]):
+        assert _rel(a, b) < 2e-2
+
+
 def _near_decision(conf_b, boxes_norm, thr=0.5, iou=0.4, eps=1e-4):
     """Anchors whose score is within eps of thr, or whose IoU with another candidate
     is within eps of the NMS threshold: decisions there are ulp-sensitive."""

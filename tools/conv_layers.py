@@ -8,7 +8,7 @@ import csv
 import sys
 
 
-def face_plan(B=64, H=640, W=640):
+def face_plan(B=64, H=640, W=640, fused=True):
     """(name, M, N, K) of every conv in face_net.cpp order."""
     L = []
     h, w = H // 2, W // 2
@@ -21,9 +21,12 @@ def face_plan(B=64, H=640, W=640):
             L.append((f"l{li+1}.{bi}.c1", B * h * w, planes, cin))
             oh, ow = h // s, w // s
             L.append((f"l{li+1}.{bi}.c2", B * oh * ow, planes, planes * 9))
-            if bi == 0:
-                L.append((f"l{li+1}.{bi}.ds", B * oh * ow, planes * 4, cin))
-            L.append((f"l{li+1}.{bi}.c3", B * oh * ow, planes * 4, planes))
+            if bi == 0 and fused and li < 2:     # bf16 plan: conv3 + downsample in one pass
+                L.append((f"l{li+1}.{bi}.c3+ds", B * oh * ow, planes * 4, planes + cin))
+            else:
+                if bi == 0:
+                    L.append((f"l{li+1}.{bi}.ds", B * oh * ow, planes * 4, cin))
+                L.append((f"l{li+1}.{bi}.c3", B * oh * ow, planes * 4, planes))
             cin = planes * 4
             h, w = oh, ow
     s = [(H // 8, 512), (H // 16, 1024), (H // 32, 2048)]

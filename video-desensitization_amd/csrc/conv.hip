@@ -65,7 +65,8 @@ __global__ __launch_bounds__(NT) void conv_igemm_kernel(ConvArgs a) {
     constexpr int VEC = Elem<T>::VEC;
     constexpr int BKE = 8 * VEC;                 // K elements per 128-byte tile row
     constexpr int WAVES = NT / 64;
-    constexpr int WAVES_N = (BN >= 64) ? 2 : 1;
+    // tall tiles (BM >= 4*BN) stack the waves along M: 64x64 wave tiles for BN = 64
+    constexpr int WAVES_N = (BN >= 64 && BM < 4 * BN) ? 2 : 1;
     constexpr int WAVES_M = WAVES / WAVES_N;
     constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
     constexpr int TM = WTM / 16, TN = WTN / 16;
@@ -420,6 +421,10 @@ hipError_t vd_launch_conv(const ConvArgs& a, bool f32, hipStream_t s) {
     const int vec = f32 ? 4 : 8;
     const int bke = 8 * vec;
     const bool dense = (a.cin_pad % bke) == 0;
+    if (a.x2) {   // fused conv3 + downsample: planned only where the dual streaming kernel applies
+        if (f32 || !vd_conv1x1_dual_ok(a)) return hipErrorInvalidValue;
+        return vd_launch_conv1x1_stream(a, s);
+    }
     if (!f32 && vd_conv1x1_stream_ok(a)) return vd_launch_conv1x1_stream(a, s);
     if (!f32 && vd_conv_big_ok(a)) return vd_launch_conv_big(a, s);
     if (!f32 && vd_conv_taps_ok(a)) return vd_launch_conv_taps(a, s);
@@ -440,6 +445,11 @@ hipError_t vd_launch_conv(const ConvArgs& a, bool f32, hipStream_t s) {
         return launch_bn<__bf16, 64, 128>(a, dense, s);
     }
     if (bn == 32) return launch_bn<__bf16, 128, 32>(a, dense, s);
-    if (bn == 64) return launch_bn<__bf16, 128, 64>(a, dense, s);
+    if (bn == 64) {
+        const char* t = getenv("VD_CONV_TALL");          // min 128-row tiles for 256-row tiles (0: off)
+        const long tall_min = t ? atol(t) : 0;   // measured slower than 128x64 (1 workgroup/CU): off
+        if (dense && tall_min > 0 && tiles128 >= tall_min) return launch_bn<__bf16, 256, 64>(a, dense, s);
+        return launch_bn<__bf16, 128, 64>(a, dense, s);
+    }
     return launch_bn<__bf16, 128, 128>(a, dense, s);
 }

@@ -45,14 +45,21 @@ __device__ __forceinline__ float bf_hi(unsigned u) { return __uint_as_float(u & 
 // TAPS: general KxK / strided / padded taps with any Cin (multiple of 8): each lane's
 // 16-B fragment of k-step ks is (tap, 8 channels) = K elements (4ks + q)*8 .. +8 in the
 // (kh, kw, c) order, gathered per pixel with zero padding (and zero past the last tap).
-template <int KS, int NTT, int ACT, int RES, bool TAPS>
+// KS2 > 0: DUAL — a second 1x1 conv (K2 = 32*KS2, weights w2, its own BN) over x2
+// at stride2 is summed before the activation (bottleneck conv3 + downsample).
+template <int KS, int NTT, int ACT, int RES, bool TAPS, int KS2 = 0>
 __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvArgs a, int nchunks, int groups) {
     constexpr int NCH = 16 * NTT;
     constexpr int KT = (KS + 1) / 2;                      // 128-byte K tiles per weight row
+    constexpr int KT2 = (KS2 + 1) / 2;
     constexpr int WBYTES = KT * NCH * 128;
+    constexpr int WBYTES2 = KT2 * NCH * 128;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    float* s_scale = (float*)(smem + WBYTES);
+    char* smem2 = smem + WBYTES;                          // second weight image (DUAL)
+    float* s_scale = (float*)(smem + WBYTES + WBYTES2);
     float* s_shift = s_scale + NCH;
+    float* s_scale2 = s_shift + NCH;
+    float* s_shift2 = s_scale2 + NCH;
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int bid = blockIdx.x, xcd = bid & 7, local = bid >> 3;
@@ -77,6 +84,21 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvArgs a, int nch
             s_scale[i] = a.scale[n0 + i];
             s_shift[i] = a.shift[n0 + i];
         }
+        if constexpr (KS2 > 0) {
+            const __bf16* w2 = (const __bf16*)a.w2;
+            constexpr int CPR2 = KS2 * 4;
+            for (int i = tid; i < NCH * CPR2; i += 512) {
+                const int row = i / CPR2, c = i - row * CPR2;
+                const int j = row >> 4, ii = row & 15;
+                const int chn = NTT == 1 ? row : 32 * (j >> 1) + 8 * (ii >> 2) + 4 * (j & 1) + (ii & 3);
+                const u32x4 v = *(const u32x4*)(w2 + (size_t)(n0 + chn) * a.kpad2 + c * 8);
+                *(u32x4*)(smem2 + (c >> 3) * (NCH * 128) + lds_off(row, c & 7)) = v;
+            }
+            for (int i = tid; i < NCH; i += 512) {
+                s_scale2[i] = a.scale2[n0 + i];
+                s_shift2[i] = a.shift2[n0 + i];
+            }
+        }
     }
     __syncthreads();
 
@@ -99,7 +121,7 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvArgs a, int nch
     const int wstride = nmblk * 8;
     constexpr int NR = NTT > 1 ? NTT / 2 : 1;
     // Load group G's input fragments into XF and its residual into RF.
-#define VD_SLOAD(G, XF, RF)                                                                    \
+#define VD_SLOAD(G, XF, RF, XF2)                                                               \
     do {                                                                                       \
         const int mu_ = (G) * 16 + p_lane;                                                     \
         const int m_ = mu_ < a.M ? mu_ : a.M - 1;   /* tail lanes load a valid pixel */        \
@@ -122,6 +144,11 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvArgs a, int nch
                 (((size_t)b_ * a.xh + oy_ * a.stride) * a.xw + ox_ * a.stride) * a.ldx + a.xcoff + q * 8; \
             _Pragma("unroll") for (int ks = 0; ks < KS; ++ks) XF[ks] = *(const u32x4*)(xp + ks * 32); \
         }                                                                                      \
+        if constexpr (KS2 > 0) {                                                               \
+            const __bf16* xp2 = (const __bf16*)a.x2 +                                          \
+                (((size_t)b_ * a.xh2 + oy_ * a.stride2) * a.xw2 + ox_ * a.stride2) * a.ldx2 + a.xcoff2 + q * 8; \
+            _Pragma("unroll") for (int ks = 0; ks < (KS2 > 0 ? KS2 : 1); ++ks) XF2[ks] = *(const u32x4*)(xp2 + ks * 32); \
+        }                                                                                      \
         if constexpr (RES != VD_RES_NONE) {                                                    \
             size_t roff;                                                                       \
             if (a.res_up) roff = ((size_t)(b_ * a.rh + (oy_ >> 1)) * a.rw + (ox_ >> 1)) * a.res_ld; \
@@ -138,22 +165,38 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvArgs a, int nch
 
     // Software-pipelined over the wave's groups: group g+1's loads are issued
     // before group g's MFMAs and stores, so every wave keeps reads in flight.
-    u32x4 xf[KS], rf[NR];
+    constexpr int KX2 = KS2 > 0 ? KS2 : 1;
+    u32x4 xf[KS], rf[NR], xf2[KX2];
     int g = mblk * 8 + wid;
-    if (g < groups) VD_SLOAD(g, xf, rf);
+    if (g < groups) VD_SLOAD(g, xf, rf, xf2);
     for (; g < groups; g += wstride) {
         // keep the weight-fragment LDS reads inside the loop (hoisting them all
         // would pin NTT*KS*4 VGPRs and cut the number of resident waves)
         asm volatile("" ::: "memory");
-        u32x4 xn[KS], rn[NR];
+        u32x4 xn[KS], rn[NR], xn2[KX2];
         const int gn = g + wstride;
-        if (gn < groups) VD_SLOAD(gn, xn, rn);
+        if (gn < groups) VD_SLOAD(gn, xn, rn, xn2);
         const int mu = g * 16 + p_lane;
         const bool ok = mu < a.M;
         const int m = ok ? mu : a.M - 1;
-        f32x4_t acc[NTT];
+        f32x4_t acc[NTT], acc2[KS2 > 0 ? NTT : 1];
 #pragma unroll
         for (int j = 0; j < NTT; ++j) acc[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        if constexpr (KS2 > 0) {
+#pragma unroll
+            for (int j = 0; j < NTT; ++j) acc2[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < KS2; ++ks) {
+                const char* wt = smem2 + (ks >> 1) * (NCH * 128);
+                const int ch = (ks & 1) * 4 + q;
+#pragma unroll
+                for (int j = 0; j < NTT; ++j) {
+                    const u32x4 wf = *(const u32x4*)(wt + lds_off(16 * j + p_lane, ch));
+                    acc2[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, wf),
+                                                                      __builtin_bit_cast(bf16x8_t, xf2[ks]), acc2[j], 0, 0, 0);
+                }
+            }
+        }
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
             const char* wt = smem + (ks >> 1) * (NCH * 128);
@@ -202,6 +245,16 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvArgs a, int nch
             const f32x4_t& hi = acc[2 * i + 1];
             float v[8] = {lo[0] * s0.x + h0.x, lo[1] * s0.y + h0.y, lo[2] * s0.z + h0.z, lo[3] * s0.w + h0.w,
                           hi[0] * s1.x + h1.x, hi[1] * s1.y + h1.y, hi[2] * s1.z + h1.z, hi[3] * s1.w + h1.w};
+            if constexpr (KS2 > 0) {   // + bn(downsample): the branch sum, then the activation
+                const float4 t0 = *(const float4*)(s_scale2 + c), t1 = *(const float4*)(s_scale2 + c + 4);
+                const float4 g0 = *(const float4*)(s_shift2 + c), g1 = *(const float4*)(s_shift2 + c + 4);
+                const f32x4_t& l2 = acc2[2 * i];
+                const f32x4_t& h2 = acc2[2 * i + 1];
+                const float u[8] = {l2[0] * t0.x + g0.x, l2[1] * t0.y + g0.y, l2[2] * t0.z + g0.z, l2[3] * t0.w + g0.w,
+                                    h2[0] * t1.x + g1.x, h2[1] * t1.y + g1.y, h2[2] * t1.z + g1.z, h2[3] * t1.w + g1.w};
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] += u[e];
+            }
             float rv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
             if constexpr (RES != VD_RES_NONE) {
 #pragma unroll
@@ -231,16 +284,20 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvArgs a, int nch
         for (int ks = 0; ks < KS; ++ks) xf[ks] = xn[ks];
 #pragma unroll
         for (int i = 0; i < NR; ++i) rf[i] = rn[i];
+        if constexpr (KS2 > 0) {
+#pragma unroll
+            for (int ks = 0; ks < KS2; ++ks) xf2[ks] = xn2[ks];
+        }
     }
 #undef VD_SLOAD
 }
 
-template <int KS, int NTT, int ACT, int RES, bool TAPS>
+template <int KS, int NTT, int ACT, int RES, bool TAPS, int KS2 = 0>
 hipError_t launch_stream(const ConvArgs& a, hipStream_t s) {
-    constexpr int NCH = 16 * NTT, KT = (KS + 1) / 2;
-    constexpr size_t lds = (size_t)KT * NCH * 128 + 2 * NCH * sizeof(float);
+    constexpr int NCH = 16 * NTT, KT = (KS + 1) / 2, KT2 = (KS2 + 1) / 2;
+    constexpr size_t lds = (size_t)(KT + KT2) * NCH * 128 + 4 * NCH * sizeof(float);
     static const bool attr = [] {
-        (void)hipFuncSetAttribute((const void*)conv1x1_stream_kernel<KS, NTT, ACT, RES, TAPS>,
+        (void)hipFuncSetAttribute((const void*)conv1x1_stream_kernel<KS, NTT, ACT, RES, TAPS, KS2>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         return true;
     }();
@@ -251,7 +308,7 @@ hipError_t launch_stream(const ConvArgs& a, hipStream_t s) {
         int dev = 0, cus = 256, per_cu = 1;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv1x1_stream_kernel<KS, NTT, ACT, RES, TAPS>, 512, lds);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv1x1_stream_kernel<KS, NTT, ACT, RES, TAPS, KS2>, 512, lds);
         return std::max(1, cus * std::max(1, per_cu));
     }();
     const int nchunks = a.cout / NCH;
@@ -259,7 +316,7 @@ hipError_t launch_stream(const ConvArgs& a, hipStream_t s) {
     int k = std::max(1, resident / (8 * nchunks));
     k = std::min(k, std::max(1, (groups + 63) / 64));
     dim3 grid(8 * nchunks * k), block(512);
-    hipLaunchKernelGGL((conv1x1_stream_kernel<KS, NTT, ACT, RES, TAPS>), grid, block, lds, s, a, nchunks, groups);
+    hipLaunchKernelGGL((conv1x1_stream_kernel<KS, NTT, ACT, RES, TAPS, KS2>), grid, block, lds, s, a, nchunks, groups);
     return hipGetLastError();
 }
 
@@ -301,7 +358,23 @@ bool vd_conv1x1_stream_ok(const ConvArgs& a) {
     return mode_ok(a);
 }
 
+// DUAL (conv3 + downsample): instantiated for ResNet layer1.0 (K 64 + 64) and
+// layer2.0 (K 128 + 256 at stride 2), 128-channel slices, ReLU.
+bool vd_conv1x1_dual_ok(const ConvArgs& a) {
+    const char* e = getenv("VD_CONV_DUAL");
+    if ((e && atoi(e) == 0) || !a.x2) return false;
+    if (a.kh != 1 || a.kw != 1 || a.pad != 0 || a.stride != 1 || a.act != VD_ACT_RELU || a.res_mode != VD_RES_NONE)
+        return false;
+    if (a.cout % 128 || a.kpad != a.cin_pad || a.kpad2 != a.cin2_pad) return false;
+    if ((a.ldx | a.xcoff | a.ldy | a.ycoff | a.ldx2 | a.xcoff2) & 7) return false;
+    return (a.cin_pad == 64 && a.cin2_pad == 64) || (a.cin_pad == 128 && a.cin2_pad == 256);
+}
+
 hipError_t vd_launch_conv1x1_stream(const ConvArgs& a, hipStream_t s) {
+    if (a.x2) {
+        if (a.cin_pad == 64) return launch_stream<2, 8, VD_ACT_RELU, VD_RES_NONE, false, 2>(a, s);
+        return launch_stream<4, 8, VD_ACT_RELU, VD_RES_NONE, false, 8>(a, s);
+    }
     // 128-channel slices (64 when Cout is not a multiple of 128); K 64/128/256
     const bool wide = a.cout % 128 == 0;
     if (a.cin_pad == 64) return wide ? launch_mode<2, 8, false>(a, s) : launch_mode<2, 4, false>(a, s);

@@ -123,6 +123,13 @@ int vd_build_face(Ctx& c, const WMap& W) {
             if ((rc = c.add_conv(F.net, c1, x, 0, t1, 0))) return rc;
             if ((rc = c.add_conv(F.net, c2, t1, 0, t2, 0))) return rc;
             const Act* idt = &x;
+            if (has_ds && c.dual_ok(c3, cd, out)) {
+                // relu(bn3(conv3(t2)) + bn(downsample(x))) in one streaming pass: the
+                // downsample output never goes through HBM (bf16 fast path only)
+                if ((rc = c.add_conv_dual(F.net, c3, t2, cd, x, out))) return rc;
+                x = out;
+                continue;
+            }
             if (has_ds) {
                 if ((rc = c.act(ds, oh, ow, planes * 4))) return rc;
                 if ((rc = c.add_conv(F.net, cd, x, 0, ds, 0))) return rc;

@@ -40,6 +40,7 @@ struct Op {
     Act x; int xcoff = 0;
     Act y; int ycoff = 0;
     Act r; int rcoff = 0; int rmode = 0; int rup = 0;
+    int conv2 = -1; Act x2;            // fused second 1x1 conv (downsample branch), summed pre-activation
     int ch = 0, k = 0, s = 0, p = 0;   // maxpool / upsample
 };
 
@@ -135,6 +136,8 @@ struct Ctx {
                      int act, float slope, int* out_idx);
     int make_conv_cat(const WMap& W, const std::vector<std::string>& wkeys, const std::vector<std::string>& bkeys,
                       int act, int* out_idx);
+    int add_conv_dual(Net& net, int ci, const Act& x, int c2, const Act& x2, Act& y);
+    bool dual_ok(int ci, int c2, const Act& y) const;
     int add_conv(Net& net, int ci, const Act& x, int xcoff, Act& y, int ycoff, const Act* res = nullptr,
                  int rcoff = 0, int rmode = 0, int rup = 0);
     void t_begin(int fam, double work);

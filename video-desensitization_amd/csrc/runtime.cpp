@@ -215,6 +215,29 @@ int Ctx::make_conv_cat(const WMap& W, const std::vector<std::string>& wkeys, con
     return VD_OK;
 }
 
+// Bottleneck conv3 (ci on x) + downsample (c2 on x2, strided 1x1) in one op.
+bool Ctx::dual_ok(int ci, int c2, const Act& y) const {
+    if (f32) return false;
+    const Conv& a = convs[ci];
+    const Conv& b = convs[c2];
+    ConvArgs t{};
+    t.kh = a.kh; t.kw = a.kw; t.pad = a.pad; t.stride = a.stride; t.cin_pad = a.cin_pad; t.kpad = a.kpad;
+    t.cout = a.cout; t.act = a.act; t.res_mode = VD_RES_NONE; t.ldx = a.cin_pad; t.ldy = y.c; t.x2 = (const void*)1;
+    t.cin2_pad = b.cin_pad; t.kpad2 = b.kpad; t.ldx2 = b.cin_pad;
+    return b.kh == 1 && b.kw == 1 && b.pad == 0 && b.cout == a.cout && b.act == VD_ACT_NONE && vd_conv1x1_dual_ok(t);
+}
+
+int Ctx::add_conv_dual(Net& net, int ci, const Act& x, int c2, const Act& x2, Act& y) {
+    int rc = add_conv(net, ci, x, 0, y, 0);
+    if (rc) return rc;
+    const Conv& b = convs[c2];
+    if ((x2.h - 1) / b.stride + 1 != y.h || (x2.w - 1) / b.stride + 1 != y.w || b.cin_pad > x2.c)
+        return vd_set_error(VD_ERR_ARG, "dual conv plan shape mismatch");
+    net.ops.back().conv2 = c2;
+    net.ops.back().x2 = x2;
+    return VD_OK;
+}
+
 int Ctx::add_conv(Net& net, int ci, const Act& x, int xcoff, Act& y, int ycoff, const Act* res, int rcoff, int rmode,
                   int rup) {
     const Conv& cv = convs[ci];
@@ -271,7 +294,15 @@ int Ctx::run_conv_op(const Op& op, int f0, int n, int fam) {
     a.kh = cv.kh; a.kw = cv.kw; a.stride = cv.stride; a.pad = cv.pad;
     a.M = n * op.y.h * op.y.w;
     a.act = cv.act; a.slope = cv.slope; a.out_f32 = op.y.f32 ? 1 : 0;
-    t_begin(fam, cv.flops_per_px * a.M);
+    double flops = cv.flops_per_px * a.M;
+    if (op.conv2 >= 0) {
+        const Conv& c2 = convs[op.conv2];
+        a.x2 = foff(op.x2, f0); a.xh2 = op.x2.h; a.xw2 = op.x2.w; a.ldx2 = op.x2.c; a.xcoff2 = 0;
+        a.stride2 = c2.stride; a.w2 = c2.w; a.scale2 = c2.scale; a.shift2 = c2.shift;
+        a.cin2_pad = c2.cin_pad; a.kpad2 = c2.kpad;
+        flops += c2.flops_per_px * a.M;
+    }
+    t_begin(fam, flops);
     hipError_t e = vd_launch_conv(a, f32, stream);
     t_end();
     if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "conv launch: %s", hipGetErrorString(e));

@@ -27,6 +27,10 @@ struct ConvArgs {
     int M;                                       // B*yh*yw
     int act; float slope; int res_mode; int out_f32;
     int ntiles_n;                                // ceil(cout / BN)
+    // optional second 1x1 conv summed before the activation (bottleneck conv3 +
+    // downsample in one pass): y = act(acc*scale + shift + acc2*scale2 + shift2)
+    const void* x2; int xh2, xw2, ldx2, xcoff2, stride2;
+    const void* w2; const float* scale2; const float* shift2; int cin2_pad, kpad2;
 };
 
 // Device buffers + parameters for one frame batch's detection post-processing.
@@ -91,6 +95,7 @@ bool vd_conv_big_ok(const ConvArgs& a);
 hipError_t vd_launch_conv_big(const ConvArgs& a, hipStream_t s);
 hipError_t vd_launch_conv1x1_stream(const ConvArgs& a, hipStream_t s);
 bool vd_conv_taps_ok(const ConvArgs& a);
+bool vd_conv1x1_dual_ok(const ConvArgs& a);
 hipError_t vd_launch_conv_taps(const ConvArgs& a, hipStream_t s);
 hipError_t vd_launch_conv(const ConvArgs& a, bool f32, hipStream_t s);
 hipError_t vd_launch_letterbox(const LetterboxArgs& a, hipStream_t s);
