@@ -73,6 +73,19 @@ def cpu_baseline(frames, sd, seconds):
                       f"(torch-CPU fp32 RetinaFace-R50 + numpy decode/NMS/mosaic), {dt:.1f} s"}
 
 
+def pmc_traffic():
+    """HBM bytes per face-conv launch measured by the committed rocprofv3 PMC passes
+    of this same command (profiles/rNN_pmc_traffic.json, tools/pmc_traffic.py);
+    (None, None) when no such profile exists."""
+    import glob
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                                          "r*_pmc_traffic.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    return d.get("traffic_bytes_per_launch"), os.path.join("profiles", os.path.basename(files[-1]))
+
+
 def main():
     a = parse()
     import torch
@@ -155,11 +168,14 @@ def main():
         oms, on_, _ = ctx.timing_read(_lib.FAM_OTHER)
         yms, yn, yflop = ctx.timing_read(_lib.FAM_PLATE_CONV)
         ach = cflop / (cms * 1e-3) / 1e12 if cms > 0 else 0.0
+        traffic, tsrc = pmc_traffic()
         roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_TFLOPS[a.precision], "unit": "TFLOP/s",
-                "frac": round(ach / PEAK_TFLOPS[a.precision], 4), "traffic": None,
+                "frac": round(ach / PEAK_TFLOPS[a.precision], 4), "traffic": traffic,
                 "kernel": "RetinaFace convs: conv_igemm_kernel + conv1x1_stream_kernel (all face conv launches "
                           "of a step; the plate net runs concurrently on a second stream)",
-                "avg_launch_ms": round(cms / max(cn, 1), 4), "launches": cn}
+                "avg_launch_ms": round(cms / max(cn, 1), 4), "launches": cn,
+                "flop_per_launch": round(cflop / max(cn, 1)), "traffic_unit": "bytes per launch (HBM, PMC)",
+                "traffic_source": tsrc}
         bach = mbytes / (mms * 1e-3) / 1e9 if mms > 0 else 0.0
         blur = {"bound": "hbm", "achieved": round(bach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(bach / PEAK_HBM_GBS, 4), "avg_launch_ms": round(mms / max(mn, 1), 4),

@@ -1,15 +1,46 @@
-"""Summarise a rocprofv3 --kernel-trace --stats run of bench.py into a markdown
-table per kernel family (conv / mosaic / letterbox / post / other), so the
+"""Summarise a rocprofv3 --kernel-trace --stats run of bench.py into markdown:
+per kernel (from the stats CSV) and per family (conv / mosaic / letterbox / post /
+other), and — from the kernel trace next to it — the RetinaFace conv family on
+its own stream (the plate network's convs run on a second stream), so the
 per-launch averages can be checked against bench.py's in-process HIP-event
-numbers (roofline.avg_launch_ms).
+numbers (`roofline.avg_launch_ms` is the face conv family).
 
     python tools/prof_summary.py gpurun_out/prof/run_kernel_stats.csv [out.md]
 """
 import csv
+import os
 import sys
 
-FAMILIES = [("conv", ("conv_igemm_kernel", "conv1x1_stream_kernel", "conv_big_kernel")), ("mosaic", ("mosaic_",)), ("letterbox", ("letterbox_kernel", "letterbox_s2d_kernel")),
+FAMILIES = [("conv", ("conv_igemm_kernel", "conv1x1_stream_kernel", "conv_big_kernel")),
+            ("mosaic", ("mosaic_",)), ("letterbox", ("letterbox_kernel", "letterbox_s2d_kernel")),
             ("post", ("candidates_kernel", "nms_kernel")), ("other", ("maxpool", "upsample"))]
+CONV = FAMILIES[0][1]
+
+
+def family(name):
+    return next((f for f, keys in FAMILIES if any(k in name for k in keys)), None)
+
+
+def face_stream(rows):
+    """Stream id(s) of the RetinaFace branch: the stream of the face letterbox
+    (space-to-depth form in bf16, the 640-row canvas in fp32)."""
+    face = {r["Stream_Id"] for r in rows if "letterbox_s2d_kernel" in r["Kernel_Name"]}
+    if not face:
+        face = {r["Stream_Id"] for r in rows if "letterbox_kernel" in r["Kernel_Name"] and r["Grid_Size_Y"] == "640"}
+    return face
+
+
+def face_stream_convs(trace_path):
+    """[count, total ns] of conv launches on the face stream, and on the others."""
+    rows = list(csv.DictReader(open(trace_path)))
+    face = face_stream(rows)
+    f, o = [0, 0], [0, 0]
+    for r in rows:
+        if any(k in r["Kernel_Name"] for k in CONV):
+            acc = f if r["Stream_Id"] in face else o
+            acc[0] += 1
+            acc[1] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    return f, o
 
 
 def main(path, out=None):
@@ -18,7 +49,7 @@ def main(path, out=None):
     fam_tot = {}
     for r in rows:
         name = r["Name"]
-        fam = next((f for f, keys in FAMILIES if any(k in name for k in keys)), None)
+        fam = family(name)
         if fam is None:
             continue
         calls, tot = int(r["Calls"]), float(r["TotalDurationNs"]) / 1e6
@@ -32,6 +63,16 @@ def main(path, out=None):
     lines.append("|---|---:|---:|---:|")
     for fam, (c, t) in fam_tot.items():
         lines.append(f"| {fam} | {c} | {t:.3f} | {t / c * 1e3:.1f} |")
+    trace = os.path.join(os.path.dirname(path), os.path.basename(path).replace("kernel_stats", "kernel_trace"))
+    if os.path.exists(trace):
+        (fc, ft), (oc, ot) = face_stream_convs(trace)
+        lines.append("")
+        lines.append("| conv launches by stream | calls | total ms | avg us per launch |")
+        lines.append("|---|---:|---:|---:|")
+        if fc:
+            lines.append(f"| RetinaFace (face stream) | {fc} | {ft / 1e6:.3f} | {ft / fc / 1e3:.1f} |")
+        if oc:
+            lines.append(f"| YOLOv8n (plate stream) | {oc} | {ot / 1e6:.3f} | {ot / oc / 1e3:.1f} |")
     txt = "\n".join(lines) + "\n"
     if out:
         open(out, "w").write(txt)
