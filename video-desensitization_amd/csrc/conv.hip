@@ -96,7 +96,9 @@ __global__ __launch_bounds__(NT) void conv_igemm_kernel(ConvArgs a) {
 
     // ---- per-thread A-row decomposition (fixed across K) ----
     const int chunk = tid & 7, rbase = tid >> 3;
-    const T* xrow[A_IT];
+    // per A row: input position at tap (0,0) and its element offset there (may
+    // point before the image; dereferenced only when the tap is inside)
+    long pix0[A_IT];
     int iy0[A_IT], ix0[A_IT];
     const int ohw = a.yh * a.yw;
 #pragma unroll
@@ -107,11 +109,12 @@ __global__ __launch_bounds__(NT) void conv_igemm_kernel(ConvArgs a) {
             int oy = rem / a.yw, ox = rem - oy * a.yw;
             iy0[i] = oy * a.stride - a.pad;
             ix0[i] = ox * a.stride - a.pad;
-            xrow[i] = (const T*)a.x + (size_t)b * a.xh * a.xw * a.ldx + a.xcoff;
+            pix0[i] = (((long)b * a.xh + iy0[i]) * a.xw + ix0[i]) * a.ldx + a.xcoff;
         } else {
-            iy0[i] = -(1 << 28); ix0[i] = 0; xrow[i] = (const T*)a.x;
+            iy0[i] = -(1 << 28); ix0[i] = 0; pix0[i] = 0;
         }
     }
+    const long tap_dy = (long)a.xw * a.ldx;   // element offset of one tap row
     const T* wbase = (const T*)a.w + (size_t)(n0 + rbase) * a.kpad + chunk * VEC;
 
     u32x4 ra[A_IT], rb[B_IT];
@@ -137,10 +140,11 @@ __global__ __launch_bounds__(NT) void conv_igemm_kernel(ConvArgs a) {
             kval = tap < ntap;                                                            \
             dy = tap / a.kw; dx = tap - dy * a.kw;                                        \
         }                                                                                 \
+        const long toff = dy * tap_dy + (long)dx * a.ldx + c;                             \
         _Pragma("unroll") for (int i = 0; i < A_IT; ++i) {                                \
             const int iy = iy0[i] + dy, ix = ix0[i] + dx;                                 \
             const bool ok = kval && (unsigned)iy < (unsigned)a.xh && (unsigned)ix < (unsigned)a.xw; \
-            const T* src = ok ? xrow[i] + ((size_t)iy * a.xw + ix) * a.ldx + c : xsafe;  \
+            const T* src = ok ? (const T*)a.x + (pix0[i] + toff) : xsafe;                 \
             const u32x4 v = *(const u32x4*)src;                                           \
             ra[i] = ok ? v : u32x4{0u, 0u, 0u, 0u};                                       \
         }                                                                                 \
@@ -183,10 +187,11 @@ __global__ __launch_bounds__(NT) void conv_igemm_kernel(ConvArgs a) {
         }                                                                                 \
         char* As_ = smem + (buf) * BUF;                                                   \
         char* Bs_ = As_ + BM * 128;                                                       \
+        const long toff = dy * tap_dy + (long)dx * a.ldx + c;                             \
         _Pragma("unroll") for (int i = 0; i < A_IT; ++i) {                                \
             const int iy = iy0[i] + dy, ix = ix0[i] + dx;                                 \
             const bool ok = kval && (unsigned)iy < (unsigned)a.xh && (unsigned)ix < (unsigned)a.xw; \
-            const void* src = ok ? (const void*)(xrow[i] + ((size_t)iy * a.xw + ix) * a.ldx + c) \
+            const void* src = ok ? (const void*)((const T*)a.x + (pix0[i] + toff))       \
                                  : (const void*)vd_zero16;                                \
             __builtin_amdgcn_global_load_lds(src, (lds_void_t*)(As_ + (wid * 8 + ROWS * i) * 128), 16, 0, 0); \
         }                                                                                 \

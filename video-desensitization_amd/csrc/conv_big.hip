@@ -83,8 +83,10 @@ __global__ __launch_bounds__(512) void conv_big_kernel(ConvArgs a) {
     const int rbase = tid >> 3;
     const int lchunk = (tid & 7) ^ ((rbase >> 1) & 7);
     const int ohw = a.yh * a.yw;
+    // Per A row: the pixel's input position at tap (0,0) and its element offset
+    // there (may point before the image; used only when the tap is inside).
     int iy0[4], ix0[4];
-    const __bf16* xrow[4];
+    long pix0[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int m = m0 + rbase + 64 * i;
@@ -93,11 +95,16 @@ __global__ __launch_bounds__(512) void conv_big_kernel(ConvArgs a) {
             const int oy = rem / a.yw, ox = rem - oy * a.yw;
             iy0[i] = oy * a.stride - a.pad;
             ix0[i] = ox * a.stride - a.pad;
-            xrow[i] = (const __bf16*)a.x + (size_t)b * a.xh * a.xw * a.ldx + a.xcoff + lchunk * 8;
+            pix0[i] = (((long)b * a.xh + iy0[i]) * a.xw + ix0[i]) * a.ldx + a.xcoff + lchunk * 8;
         } else {
-            iy0[i] = -(1 << 28); ix0[i] = 0; xrow[i] = (const __bf16*)a.x;
+            iy0[i] = -(1 << 28); ix0[i] = 0; pix0[i] = 0;
         }
     }
+    // A K tiles are issued in order (A0 of tile t before A0 of t+1, likewise A1):
+    // two incremental (dy, dx, c) trackers replace per-issue divisions. The
+    // element offset of tap (dy, dx), channel c relative to tap (0,0) is uniform.
+    int a0_dy = 0, a0_dx = 0, a0_c = 0, a1_dy = 0, a1_dx = 0, a1_c = 0;
+    const long tap_dy = (long)a.xw * a.ldx;
     const __bf16* wrow = (const __bf16*)a.w + (size_t)(n0 + rbase) * a.kpad + lchunk * 8;
     const int nk = a.kpad / 64;
     const int nh_total = 4 * nk;                      // half-tiles in the K loop
@@ -110,18 +117,21 @@ __global__ __launch_bounds__(512) void conv_big_kernel(ConvArgs a) {
         char* dst_ = smem + ((t_ & 1) * 4 + j_) * HT + wid * 8 * 128;                          \
         const int kpos = t_ * 64;                                                              \
         if (j_ == 0 || j_ == 3) {                                                              \
-            const int tap = kpos / a.cin_pad;                                                  \
-            const int c_ = kpos - tap * a.cin_pad;                                             \
-            const int dy = tap / a.kw, dx = tap - dy * a.kw;                                   \
+            int& dy = j_ == 3 ? a1_dy : a0_dy;                                                 \
+            int& dx = j_ == 3 ? a1_dx : a0_dx;                                                 \
+            int& cc = j_ == 3 ? a1_c : a0_c;                                                   \
+            const long toff = dy * tap_dy + (long)dx * a.ldx + cc;                             \
             const int i0 = j_ == 3 ? 2 : 0;                                                    \
             _Pragma("unroll") for (int ii = 0; ii < 2; ++ii) {                                 \
                 const int i = i0 + ii;                                                         \
-                const int iy = iy0[i] + dy, ix = ix0[i] + dx;                                  \
-                const bool ok = (unsigned)iy < (unsigned)a.xh && (unsigned)ix < (unsigned)a.xw;\
-                const void* src = ok ? (const void*)(xrow[i] + ((size_t)iy * a.xw + ix) * a.ldx + c_) \
-                                     : (const void*)vdb_zero16;                                \
+                const bool ok = (unsigned)(iy0[i] + dy) < (unsigned)a.xh &&                   \
+                                (unsigned)(ix0[i] + dx) < (unsigned)a.xw;                      \
+                const __bf16* p_ = (const __bf16*)a.x + (pix0[i] + toff);                      \
+                const void* src = ok ? (const void*)p_ : (const void*)vdb_zero16;              \
                 __builtin_amdgcn_global_load_lds(src, (lds_void_t*)(dst_ + ii * 64 * 128), 16, 0, 0); \
             }                                                                                  \
+            cc += 64;                                                                          \
+            if (cc >= a.cin_pad) { cc = 0; if (++dx == a.kw) { dx = 0; ++dy; } }              \
         } else {                                                                               \
             const int i0 = j_ == 2 ? 2 : 0;                                                    \
             _Pragma("unroll") for (int ii = 0; ii < 2; ++ii)                                   \
@@ -198,18 +208,17 @@ __global__ __launch_bounds__(512) void conv_big_kernel(ConvArgs a) {
         if (2 * P + 6 < nh_total) VDB_ISSUE(2 * P + 6);                                        \
         if (2 * P + 7 < nh_total) VDB_ISSUE(2 * P + 7);                                        \
         const char* st_ = smem + (t & 1) * 4 * HT;                                             \
-        {                                                                                      \
+        /* k-step-major read order: the k-step 0 MFMAs can start while k-step 1 reads land */ \
+        _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) {                                     \
             const char* As_ = st_ + ((R) ? 3 : 0) * HT;                                        \
             _Pragma("unroll") for (int i = 0; i < 4; ++i)                                      \
-            _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                   \
                 af[i][ks] = *(const u32x4*)(As_ + lds_off(wr * 64 + i * 16 + (lane & 15), ks * 4 + (lane >> 4))); \
-        }                                                                                      \
-        if ((R) == 0) {                                                                        \
-            _Pragma("unroll") for (int nh = 0; nh < 2; ++nh) {                                 \
-                const char* Bs_ = st_ + (nh ? 2 : 1) * HT;                                     \
-                _Pragma("unroll") for (int j = 0; j < 2; ++j)                                  \
-                _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                               \
-                    bq[nh][j][ks] = *(const u32x4*)(Bs_ + lds_off(wc * 32 + j * 16 + (lane & 15), ks * 4 + (lane >> 4))); \
+            if ((R) == 0) {                                                                    \
+                _Pragma("unroll") for (int nh = 0; nh < 2; ++nh) {                             \
+                    const char* Bs_ = st_ + (nh ? 2 : 1) * HT;                                 \
+                    _Pragma("unroll") for (int j = 0; j < 2; ++j)                              \
+                        bq[nh][j][ks] = *(const u32x4*)(Bs_ + lds_off(wc * 32 + j * 16 + (lane & 15), ks * 4 + (lane >> 4))); \
+                }                                                                              \
             }                                                                                  \
         }                                                                                      \
         __builtin_amdgcn_s_setprio(1);                                                         \
@@ -391,7 +400,7 @@ __global__ __launch_bounds__(512) void conv_big_kernel(ConvArgs a) {
 // output with 16-B aligned channel offsets, at least `min_tiles` 256 x 256 tiles.
 bool vd_conv_big_ok(const ConvArgs& a) {
     const char* e = getenv("VD_CONV_BIG");   // read per call: tests lower it to reach small shapes
-    const int min_tiles = e ? atoi(e) : 384;
+    const int min_tiles = e ? atoi(e) : 100;
     if (min_tiles <= 0 || a.out_f32) return false;
     // measured (tools/conv_layers.py A/B): ahead of the 128x128 GEMM only with long K loops
     const char* ek = getenv("VD_CONV_BIG_KMIN");
@@ -418,8 +427,9 @@ hipError_t vd_launch_conv_big(const ConvArgs& a0, hipStream_t s) {
     a.ntiles_n = a.cout / 256;
     dim3 grid(((a.M + 255) / 256) * a.ntiles_n), block(512);
     const char* e = getenv("VD_CONV_BIG_PH");
+    // default: the staggered schedule (measured best once the A-address issue was made cheap)
     if (e && atoi(e) == 4) hipLaunchKernelGGL(conv_big_kernel<4>, grid, block, LDS_BYTES, s, a);
-    else if (e && atoi(e) == 8) hipLaunchKernelGGL(conv_big_kernel<8>, grid, block, LDS_BYTES, s, a);
-    else hipLaunchKernelGGL(conv_big_kernel<2>, grid, block, LDS_BYTES, s, a);
+    else if (e && atoi(e) == 2) hipLaunchKernelGGL(conv_big_kernel<2>, grid, block, LDS_BYTES, s, a);
+    else hipLaunchKernelGGL(conv_big_kernel<8>, grid, block, LDS_BYTES, s, a);
     return hipGetLastError();
 }
