@@ -193,6 +193,26 @@ def test_conv_big_matches_torch(gpu, face_ctx_factory, monkeypatch, case, ph):
     test_conv_matches_torch(gpu, face_ctx_factory, monkeypatch, "bf16", case)
 
 
+BIG128_CASES = [
+    # 256 x 128-tile staggered kernel (conv_big.hip conv_big128_kernel): Cout % 128 == 0
+    (2, 20, 24, 128, 128, 3, 1, 1, 1, 1),     # 3x3 + residual before ReLU, M tail
+    (1, 26, 30, 64, 384, 3, 2, 1, 1, 0),      # stride 2, three N tiles
+    (1, 33, 31, 256, 128, 1, 1, 0, 0, 2),     # 1x1, residual after activation
+    (2, 9, 11, 512, 128, 3, 1, 1, 2, 0),      # K = 4608, leaky
+    (1, 7, 5, 64, 128, 1, 1, 0, 1, 0),        # a single K tile
+]
+
+
+@pytest.mark.parametrize("case", BIG128_CASES)
+def test_conv_big128_matches_torch(gpu, face_ctx_factory, monkeypatch, case):
+    monkeypatch.setenv("VD_CONV_BIG", "0")
+    monkeypatch.setenv("VD_CONV_BIG128", "1")
+    monkeypatch.setenv("VD_CONV_BIG_KMIN", "0")
+    monkeypatch.setenv("VD_CONV_STREAM", "0")
+    monkeypatch.setenv("VD_CONV_TAPS", "0")
+    test_conv_matches_torch(gpu, face_ctx_factory, monkeypatch, "bf16", case)
+
+
 # ------------------------------------------------------------------ post-processing
 def _heads(rng, n, A, bias):
     loc = (rng.standard_normal((n, A, 4)) * 1.5).astype(F32)

@@ -432,6 +432,7 @@ hipError_t vd_launch_conv(const ConvArgs& a, bool f32, hipStream_t s) {
     }
     if (!f32 && vd_conv1x1_stream_ok(a)) return vd_launch_conv1x1_stream(a, s);
     if (!f32 && vd_conv_big_ok(a)) return vd_launch_conv_big(a, s);
+    if (!f32 && vd_conv_big128_ok(a)) return vd_launch_conv_big128(a, s);
     if (!f32 && vd_conv_taps_ok(a)) return vd_launch_conv_taps(a, s);
     if (f32) {
         if (a.cout <= 32) return launch_bn<float, 128, 32>(a, dense, s);

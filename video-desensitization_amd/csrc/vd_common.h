@@ -93,6 +93,8 @@ struct LetterboxArgs {
 bool vd_conv1x1_stream_ok(const ConvArgs& a);
 bool vd_conv_big_ok(const ConvArgs& a);
 hipError_t vd_launch_conv_big(const ConvArgs& a, hipStream_t s);
+bool vd_conv_big128_ok(const ConvArgs& a);
+hipError_t vd_launch_conv_big128(const ConvArgs& a, hipStream_t s);
 hipError_t vd_launch_conv1x1_stream(const ConvArgs& a, hipStream_t s);
 bool vd_conv_taps_ok(const ConvArgs& a);
 bool vd_conv1x1_dual_ok(const ConvArgs& a);
