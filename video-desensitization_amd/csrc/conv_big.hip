@@ -29,6 +29,22 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 
 __device__ __attribute__((aligned(16))) unsigned vdb_zero16[4] = {0u, 0u, 0u, 0u};
 
+#ifdef VD_STAMPS   // diagnostic build only (tools/stamps.cpp): s_memtime at segment edges
+__device__ unsigned long long vd_stamps[8][2048];
+#define VDB_STAMP()                                                                            \
+    do {                                                                                       \
+        if (blockIdx.x == 0 && lane == 0 && sidx < 2048) vd_stamps[wid][sidx++] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define VDB_STAMP() do { } while (0)
+#endif
+#ifndef VDB_DIAG_DMA          // diagnostic builds (tools/stamps.cpp) may drop the DMA or the
+#define VDB_DIAG_DMA 1        // fragment reads to price them; results are then meaningless
+#endif
+#ifndef VDB_DIAG_READ
+#define VDB_DIAG_READ 1
+#endif
+
 constexpr int HT = 16384;          // half-tile bytes: 128 rows x 128 B
 constexpr int LDS_BYTES = 8 * HT;  // 2 stages x {A0, B0, B1, A1}
 constexpr int EPLD = 256 + 4;      // f32 epilogue row stride
@@ -105,9 +121,16 @@ __global__ __launch_bounds__(512) void conv_big_kernel(ConvArgs a) {
     // element offset of tap (dy, dx), channel c relative to tap (0,0) is uniform.
     int a0_dy = 0, a0_dx = 0, a0_c = 0, a1_dy = 0, a1_dx = 0, a1_c = 0;
     const long tap_dy = (long)a.xw * a.ldx;
-    const __bf16* wrow = (const __bf16*)a.w + (size_t)(n0 + rbase) * a.kpad + lchunk * 8;
     const int nk = a.kpad / 64;
     const int nh_total = 4 * nk;                      // half-tiles in the K loop
+    // LDS-DMA through buffer descriptors (buffer_load_dwordx4 ... lds): 32-bit per-lane
+    // byte offsets, and out-of-range offsets return zeros (conv padding). Built from
+    // kernel arguments only, so the descriptors are scalar.
+    const __amdgpu_buffer_rsrc_t rsrc_x = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)a.x, 0, (int)((long)a.B * a.xh * a.xw * a.ldx * 2 < 0x7fffffffL ? (long)a.B * a.xh * a.xw * a.ldx * 2
+                                                                                 : 0x7fffffffL), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsrc_w = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7fffffff, 0x00020000);
+    const unsigned woff = (unsigned)(((long)(n0 + rbase) * a.kpad + lchunk * 8) * 2);
 
     // Issue half-tile h (K tile h>>2, part h&3 in {A0, B0, B1, A1}) into its slot.
 #define VDB_ISSUE(h_)                                                                          \
@@ -126,18 +149,19 @@ __global__ __launch_bounds__(512) void conv_big_kernel(ConvArgs a) {
                 const int i = i0 + ii;                                                         \
                 const bool ok = (unsigned)(iy0[i] + dy) < (unsigned)a.xh &&                   \
                                 (unsigned)(ix0[i] + dx) < (unsigned)a.xw;                      \
-                const __bf16* p_ = (const __bf16*)a.x + (pix0[i] + toff);                      \
-                const void* src = ok ? (const void*)p_ : (const void*)vdb_zero16;              \
-                __builtin_amdgcn_global_load_lds(src, (lds_void_t*)(dst_ + ii * 64 * 128), 16, 0, 0); \
+                /* padding taps: an offset past num_records, which the buffer unit reads as 0 */ \
+                const unsigned off = ok ? (unsigned)((pix0[i] + toff) * 2) : 0x80000000u;      \
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_x, (lds_void_t*)(dst_ + ii * 64 * 128), 16, \
+                                                         off, 0, 0, 0);                        \
             }                                                                                  \
             cc += 64;                                                                          \
             if (cc >= a.cin_pad) { cc = 0; if (++dx == a.kw) { dx = 0; ++dy; } }              \
         } else {                                                                               \
             const int i0 = j_ == 2 ? 2 : 0;                                                    \
             _Pragma("unroll") for (int ii = 0; ii < 2; ++ii)                                   \
-                __builtin_amdgcn_global_load_lds(                                              \
-                    (const void*)(wrow + (size_t)(64 * (i0 + ii)) * a.kpad + kpos),            \
-                    (lds_void_t*)(dst_ + ii * 64 * 128), 16, 0, 0);                            \
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_w, (lds_void_t*)(dst_ + ii * 64 * 128), 16, \
+                                                         woff + (unsigned)(64 * (i0 + ii) * a.kpad * 2), \
+                                                         (unsigned)(kpos * 2), 0, 0);          \
         }                                                                                      \
     } while (0)
 
@@ -243,23 +267,26 @@ __global__ __launch_bounds__(512) void conv_big_kernel(ConvArgs a) {
     do {                                                                                       \
         const int p = 4 * t + (R);                                                             \
         const char* st_ = smem + (t & 1) * 4 * HT;                                             \
-        if (RA) {                                                                              \
+        VDB_STAMP();                                                                           \
+        /* DMA issue first: its cost overlaps the fragment reads' latency */                  \
+        if (VDB_DIAG_DMA && p + 6 < nh_total) VDB_ISSUE(p + 6);                                \
+        if ((RA) && VDB_DIAG_READ) {                                                           \
             const char* As_ = st_ + ((MH) ? 3 : 0) * HT;                                       \
             _Pragma("unroll") for (int i = 0; i < 4; ++i)                                      \
             _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                   \
                 af[i][ks] = *(const u32x4*)(As_ + lds_off(wr * 64 + i * 16 + (lane & 15), ks * 4 + (lane >> 4))); \
         }                                                                                      \
-        if (RB0) {                                                                             \
+        if ((RB0) && VDB_DIAG_READ) {                                                          \
             _Pragma("unroll") for (int j = 0; j < 2; ++j)                                      \
             _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                   \
                 b0[j][ks] = *(const u32x4*)(st_ + HT + lds_off(wc * 32 + j * 16 + (lane & 15), ks * 4 + (lane >> 4))); \
         }                                                                                      \
-        if (RB1) {                                                                             \
+        if ((RB1) && VDB_DIAG_READ) {                                                          \
             _Pragma("unroll") for (int j = 0; j < 2; ++j)                                      \
             _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                   \
                 b1[j][ks] = *(const u32x4*)(st_ + 2 * HT + lds_off(wc * 32 + j * 16 + (lane & 15), ks * 4 + (lane >> 4))); \
         }                                                                                      \
-        if (p + 6 < nh_total) VDB_ISSUE(p + 6);                                                \
+        VDB_STAMP();                                                                           \
         if (STEADY) {                                                                          \
             if ((R) == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");                     \
             else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");                              \
@@ -268,8 +295,11 @@ __global__ __launch_bounds__(512) void conv_big_kernel(ConvArgs a) {
             const int need = 4 * (q >> 2) + ((q & 3) == 0 ? 1 : ((q & 3) == 1 ? 2 : 3));       \
             wait_vm(min(p + 5, nh_total - 1) - need);                                          \
         }                                                                                      \
+        VDB_STAMP();                                                                           \
         __builtin_amdgcn_s_barrier();                                                          \
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                     \
+        VDB_STAMP();                                                                           \
+        /* no lgkmcnt(0) here: hipcc waits per MFMA operand, and every read of this */         \
+        /* phase is consumed (so complete) before the second barrier */                       \
         __builtin_amdgcn_s_setprio(1);                                                         \
         _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                       \
         _Pragma("unroll") for (int i = 0; i < 4; ++i)                                          \
@@ -279,11 +309,15 @@ __global__ __launch_bounds__(512) void conv_big_kernel(ConvArgs a) {
                 __builtin_bit_cast(bf16x8_t, (NH) ? b1[j][ks] : b0[j][ks]), acc[MH][NH][i][j], 0, 0, 0); \
         __builtin_amdgcn_s_setprio(0);                                                         \
         asm volatile("" ::: "memory");                                                         \
+        VDB_STAMP();                                                                           \
         __builtin_amdgcn_s_barrier();                                                          \
         asm volatile("" ::: "memory");                                                         \
     } while (0)
 
     int t = 0;
+#ifdef VD_STAMPS
+    int sidx = 0;
+#endif
     if constexpr (PH == 8) {
         for (int h = 0; h < 6 && h < nh_total; ++h) VDB_ISSUE(h);   // prologue: half-tiles 0..5
         wait_vm(min(5, nh_total - 1) - 1);                          // A0(0), B0(0) landed
