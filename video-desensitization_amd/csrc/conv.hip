@@ -171,7 +171,14 @@ __global__ __launch_bounds__(NT) void conv_igemm_kernel(ConvArgs a) {
     // fetches logical chunk (lane&7) ^ swz(row) (rule: swizzle both sides or
     // neither). Padding taps read the zero page.
     const int lchunk = (tid & 7) ^ ((rbase >> 1) & 7);
-    const T* wbase_g = (const T*)a.w + (size_t)(n0 + rbase) * a.kpad + lchunk * VEC;
+    // LDS-DMA through buffer descriptors (buffer_load_dwordx4 ... lds): 32-bit
+    // per-lane byte offsets; an offset past num_records reads zeros (conv padding).
+    constexpr int ESZ = (int)sizeof(T);
+    const long xbytes = (long)a.B * a.xh * a.xw * a.ldx * ESZ;
+    const __amdgpu_buffer_rsrc_t rsrc_x =
+        __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, (int)(xbytes < 0x7fffffffL ? xbytes : 0x7fffffffL), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsrc_w = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7fffffff, 0x00020000);
+    const unsigned woff_g = (unsigned)(((long)(n0 + rbase) * a.kpad + lchunk * VEC) * ESZ);
 #define VD_GLDS_TILE(kt, buf)                                                              \
     do {                                                                                  \
         int dy, dx, c;                                                                    \
@@ -191,14 +198,14 @@ __global__ __launch_bounds__(NT) void conv_igemm_kernel(ConvArgs a) {
         _Pragma("unroll") for (int i = 0; i < A_IT; ++i) {                                \
             const int iy = iy0[i] + dy, ix = ix0[i] + dx;                                 \
             const bool ok = kval && (unsigned)iy < (unsigned)a.xh && (unsigned)ix < (unsigned)a.xw; \
-            const void* src = ok ? (const void*)((const T*)a.x + (pix0[i] + toff))       \
-                                 : (const void*)vd_zero16;                                \
-            __builtin_amdgcn_global_load_lds(src, (lds_void_t*)(As_ + (wid * 8 + ROWS * i) * 128), 16, 0, 0); \
+            const unsigned off = ok ? (unsigned)((pix0[i] + toff) * ESZ) : 0x80000000u;  \
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_x, (lds_void_t*)(As_ + (wid * 8 + ROWS * i) * 128), 16, \
+                                                     off, 0, 0, 0);                      \
         }                                                                                 \
         _Pragma("unroll") for (int i = 0; i < B_IT; ++i)                                  \
-            __builtin_amdgcn_global_load_lds(                                             \
-                (const void*)(wbase_g + (size_t)(ROWS * i) * a.kpad + (size_t)(kt) * BKE), \
-                (lds_void_t*)(Bs_ + (wid * 8 + ROWS * i) * 128), 16, 0, 0);                \
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_w, (lds_void_t*)(Bs_ + (wid * 8 + ROWS * i) * 128), 16, \
+                                                     woff_g + (unsigned)(ROWS * i * a.kpad * ESZ), \
+                                                     (unsigned)((kt) * BKE * ESZ), 0, 0);  \
         if constexpr (DENSE) {                                                            \
             t_c += BKE;                                                                   \
             if (t_c >= a.cin_pad) { t_c = 0; if (++t_kw == a.kw) { t_kw = 0; ++t_kh; } } \
