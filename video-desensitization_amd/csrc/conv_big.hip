@@ -469,8 +469,12 @@ __global__ __launch_bounds__(512) void conv_big128_kernel(ConvArgs a) {
             iy0[i] = -(1 << 28); ix0[i] = 0; pix0[i] = 0;
         }
     }
-    const __bf16* wrow = (const __bf16*)a.w + (size_t)(n0 + rbase) * a.kpad + lchunk * 8;
     const int nk = a.kpad / 64;
+    const __amdgpu_buffer_rsrc_t rsrc_x = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)a.x, 0, (int)((long)a.B * a.xh * a.xw * a.ldx * 2 < 0x7fffffffL ? (long)a.B * a.xh * a.xw * a.ldx * 2
+                                                                                 : 0x7fffffffL), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsrc_w = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7fffffff, 0x00020000);
+    const unsigned woff = (unsigned)(((long)(n0 + rbase) * a.kpad + lchunk * 8) * 2);
     int a0_dy = 0, a0_dx = 0, a0_c = 0, a1_dy = 0, a1_dx = 0, a1_c = 0;
     const long tap_dy = (long)a.xw * a.ldx;
 
@@ -489,17 +493,17 @@ __global__ __launch_bounds__(512) void conv_big128_kernel(ConvArgs a) {
                 const int i = i0 + ii;                                                         \
                 const bool ok = (unsigned)(iy0[i] + dy) < (unsigned)a.xh &&                   \
                                 (unsigned)(ix0[i] + dx) < (unsigned)a.xw;                      \
-                const __bf16* p_ = (const __bf16*)a.x + (pix0[i] + toff);                      \
-                const void* src = ok ? (const void*)p_ : (const void*)vdb_zero16;              \
-                __builtin_amdgcn_global_load_lds(src, (lds_void_t*)(dst_ + ii * 64 * 128), 16, 0, 0); \
+                const unsigned off = ok ? (unsigned)((pix0[i] + toff) * 2) : 0x80000000u;      \
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_x, (lds_void_t*)(dst_ + ii * 64 * 128), 16, \
+                                                         off, 0, 0, 0);                        \
             }                                                                                  \
             cc += 64;                                                                          \
             if (cc >= a.cin_pad) { cc = 0; if (++dx == a.kw) { dx = 0; ++dy; } }              \
         } else {                                                                               \
             _Pragma("unroll") for (int ii = 0; ii < 2; ++ii)                                   \
-                __builtin_amdgcn_global_load_lds(                                              \
-                    (const void*)(wrow + (size_t)(64 * ii) * a.kpad + t_ * 64),                \
-                    (lds_void_t*)(dst_ + ii * 64 * 128), 16, 0, 0);                            \
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_w, (lds_void_t*)(dst_ + ii * 64 * 128), 16, \
+                                                         woff + (unsigned)(64 * ii * a.kpad * 2), \
+                                                         (unsigned)(t_ * 64 * 2), 0, 0);       \
         }                                                                                      \
     } while (0)
 
@@ -515,6 +519,10 @@ __global__ __launch_bounds__(512) void conv_big128_kernel(ConvArgs a) {
 #define VDC_PHASE(R, STEADY)                                                                   \
     do {                                                                                       \
         const char* st_ = smem + (t % 3) * STAGE3;                                             \
+        if (t + 2 < nk) {                                                                      \
+            if ((R) == 0) { VDC_ISSUE(t + 2, 0); VDC_ISSUE(t + 2, 1); }                        \
+            else VDC_ISSUE(t + 2, 2);                                                          \
+        }                                                                                      \
         _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) {                                     \
             const char* As_ = st_ + ((R) ? 2 : 0) * HT;                                        \
             _Pragma("unroll") for (int i = 0; i < 4; ++i)                                      \
@@ -524,10 +532,6 @@ __global__ __launch_bounds__(512) void conv_big128_kernel(ConvArgs a) {
                     bf[j][ks] = *(const u32x4*)(st_ + HT + lds_off(wc * 32 + j * 16 + (lane & 15), ks * 4 + (lane >> 4))); \
             }                                                                                  \
         }                                                                                      \
-        if (t + 2 < nk) {                                                                      \
-            if ((R) == 0) { VDC_ISSUE(t + 2, 0); VDC_ISSUE(t + 2, 1); }                        \
-            else VDC_ISSUE(t + 2, 2);                                                          \
-        }                                                                                      \
         if (STEADY) {                                                                          \
             if ((R) == 0) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");                    \
             else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");                              \
@@ -535,7 +539,6 @@ __global__ __launch_bounds__(512) void conv_big128_kernel(ConvArgs a) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                   \
         }                                                                                      \
         __builtin_amdgcn_s_barrier();                                                          \
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                     \
         __builtin_amdgcn_s_setprio(1);                                                         \
         _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                       \
         _Pragma("unroll") for (int i = 0; i < 4; ++i)                                          \
