@@ -156,6 +156,15 @@ int vdt_conv2d(vd_ctx* ctx, const float* x, int n, int h, int w, int cin,
                const float* wgt, int cout, int kh, int kw, int stride, int pad,
                const float* scale, const float* shift, int act, float slope,
                const float* res, int res_mode, float* y, int* oh, int* ow);
+/* One ResNet layer1 bottleneck on host f32 NHWC x [n][h][w][cin] -> y [n][h][w][256]
+ * (bf16 context): conv1 1x1 cin->64, conv2 3x3 64->64 pad 1, conv3 1x1 64->256, each
+ * OIHW weights + BN as bn = [scale[cout] | shift[cout]]; ReLU after each, the residual
+ * (x, or bn(downsample(x)) when wd != NULL, cin 64) added before the last ReLU.
+ * fused = 1: the one-kernel fused block (block.hip); 0: the conv-by-conv chain. */
+int vdt_bottleneck(vd_ctx* ctx, const float* x, int n, int h, int w, int cin,
+                   const float* w1, const float* bn1, const float* w2, const float* bn2,
+                   const float* w3, const float* bn3, const float* wd, const float* bnd,
+                   int fused, float* y);
 /* Raw YOLO Detect outputs [n][64+nc][A] (per-side DFL logits | class logits),
  * host f32, anchors in level -> y -> x order at the letterboxed canvas; *anchors
  * receives A. `out` may be NULL to query A. */

@@ -86,6 +86,25 @@ def test_heads_bf16_fused_downsample_matches_unfused(gpu, monkeypatch):
         assert _rel(a, b) < 2e-2
 
 
+def test_heads_bf16_fused_block_matches_unfused(gpu, monkeypatch):
+    """bf16 plans run each layer1 bottleneck as one kernel (block.hip: t1/t2 in LDS);
+    VD_BLOCK_FUSE=0 at weight load keeps the conv-by-conv chain. Same bf16 weights
+    and the same bf16 rounding points, only the f32 summation order differs."""
+    import vdmi
+    fr = _frames(2, 1080, 1920, seed=5)
+    out = {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("VD_BLOCK_FUSE", fuse)
+        ctx = vdmi.Context(precision="bf16", max_batch=2)
+        try:
+            ctx.load_weights(0, face_weights("default"))
+            out[fuse] = ctx.forward_heads(fr)
+        finally:
+            ctx.close()
+    for a, b in zip(out["1"], out["0"]):
+        assert _rel(a, b) < 2e-2
+
+
 def _near_decision(conf_b, boxes_norm, thr=0.5, iou=0.4, eps=1e-4):
     """Anchors whose score is within eps of thr, or whose IoU with another candidate
     is within eps of the NMS threshold: decisions there are ulp-sensitive."""

@@ -213,6 +213,55 @@ def test_conv_big128_matches_torch(gpu, face_ctx_factory, monkeypatch, case):
     test_conv_matches_torch(gpu, face_ctx_factory, monkeypatch, "bf16", case)
 
 
+# ------------------------------------------------------------------ fused bottleneck
+BLOCK_CASES = [
+    # (n, h, w, cin, downsample)
+    (2, 16, 32, 256, False),     # whole 8x16 tiles
+    (1, 21, 37, 256, False),     # ragged tiles on both axes
+    (2, 13, 18, 64, True),       # layer1.0: cin 64 + downsample branch
+    (1, 8, 5, 64, True),         # narrower than one tile
+    (1, 40, 40, 256, False),     # 3x3 halo across interior tile seams
+]
+
+
+def _bn(rng, c):
+    return np.concatenate([rng.uniform(0.5, 1.5, c), rng.standard_normal(c) * 0.1]).astype(F32)
+
+
+@pytest.mark.parametrize("case", BLOCK_CASES)
+def test_bottleneck_fused_matches_torch_and_chain(gpu, face_ctx_factory, case):
+    """block.hip (one kernel per bottleneck) against (a) a torch fp32 bottleneck on the
+    same bf16-rounded operands with t1/t2 rounded to bf16 as the kernels store them
+    (2e-2 relative, the bf16 bar), and (b) the conv-by-conv chain of the same library
+    (same bf16 weights, only the f32 summation order differs: 1e-2 relative)."""
+    n, h, w, cin, ds = case
+    ctx = face_ctx_factory("bf16", 8)
+    rng = np.random.default_rng(h * 100 + w + cin)
+    bf = lambda a: torch.from_numpy(np.ascontiguousarray(a, F32)).bfloat16().float().numpy()
+    he = lambda co, ci, k: (rng.standard_normal((co, ci, k, k)) * np.sqrt(2.0 / (ci * k * k))).astype(F32)
+    x = bf(rng.standard_normal((n, h, w, cin)).astype(F32))
+    w1, w2, w3 = bf(he(64, cin, 1)), bf(he(64, 64, 3)), bf(he(256, 64, 1))
+    b1, b2, b3 = _bn(rng, 64), _bn(rng, 64), _bn(rng, 256)
+    wd, bd = (bf(he(256, cin, 1)), _bn(rng, 256)) if ds else (None, None)
+    got = ctx.bottleneck(x, w1, b1, w2, b2, w3, b3, wd, bd, fused=True)
+    chain = ctx.bottleneck(x, w1, b1, w2, b2, w3, b3, wd, bd, fused=False)
+
+    T = lambda a: torch.from_numpy(a)
+    conv = lambda v, wt, p: torch.nn.functional.conv2d(v, T(wt), padding=p)
+    aff = lambda v, b, c: v * T(b[:c]).view(1, c, 1, 1) + T(b[c:]).view(1, c, 1, 1)
+    rb = lambda v: v.bfloat16().float()
+    xt = T(x).permute(0, 3, 1, 2)
+    t1 = rb(torch.relu(aff(conv(xt, w1, 0), b1, 64)))
+    t2 = rb(torch.relu(aff(conv(t1, w2, 1), b2, 64)))
+    idt = aff(conv(xt, wd, 0), bd, 256) if ds else xt
+    ref = torch.relu(aff(conv(t2, w3, 0), b3, 256) + idt).permute(0, 2, 3, 1).numpy()
+    scale = np.abs(ref).max() + 1e-6
+    assert got.shape == ref.shape
+    assert np.abs(got - ref).max() / scale < 2e-2
+    assert np.abs(got - chain).max() / scale < 1e-2
+    assert np.mean(got == chain) > 0.95        # mostly bit-identical after bf16 rounding
+
+
 # ------------------------------------------------------------------ post-processing
 def _heads(rng, n, A, bias):
     loc = (rng.standard_normal((n, A, 4)) * 1.5).astype(F32)

@@ -75,8 +75,66 @@ static double run(const Layer& L, int reps) {
     return us;
 }
 
+// fused layer1 bottleneck (block.hip) on random bf16 data: B x H x W x cin -> 256
+static void run_block(int reps, int B, int H, int W, int cin, bool ds) {
+    auto rnd_buf = [](size_t n, float sc) {
+        std::vector<uint16_t> h(n);
+        uint32_t st = 777u + (uint32_t)n;
+        for (auto& v : h) { st = st * 1664525u + 1013904223u; v = f2bf((((st >> 8) & 0xffff) / 32768.0f - 1.0f) * sc); }
+        void* d;
+        CK(hipMalloc(&d, n * 2));
+        CK(hipMemcpy(d, h.data(), n * 2, hipMemcpyHostToDevice));
+        return d;
+    };
+    BlockArgs a{};
+    a.x = rnd_buf((size_t)B * H * W * cin, 1.0f);
+    CK(hipMalloc(&a.y, (size_t)B * H * W * 256 * 2));
+    a.B = B; a.H = H; a.W = W; a.cin = cin; a.ds = ds;
+    a.tiles_x = (W + 15) / 16; a.tiles_y = (H + 7) / 8;
+    a.w1 = rnd_buf((size_t)cin * 64, 0.05f);
+    a.w2 = rnd_buf((size_t)4 * 18 * 64 * 8, 0.05f);
+    a.w3 = rnd_buf((size_t)4 * 4 * 2 * 64 * 8, 0.05f);
+    a.wd = rnd_buf((size_t)4 * 4 * (cin / 32) * 64 * 8, 0.05f);
+    std::vector<float> bn(1280, 0.5f);
+    float* dbn;
+    CK(hipMalloc(&dbn, bn.size() * 4));
+    CK(hipMemcpy(dbn, bn.data(), bn.size() * 4, hipMemcpyHostToDevice));
+    a.bn = dbn;
+    unsigned long long* ddiag;
+    CK(hipMalloc(&ddiag, 8 * sizeof(unsigned long long)));
+    a.diag = getenv("VD_DIAG") ? ddiag : nullptr;
+    a.mode = getenv("VD_BLOCK_MODE") ? atoi(getenv("VD_BLOCK_MODE")) : 0;
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    for (int i = 0; i < 3; ++i) CK(vd_launch_block(a, 0));
+    CK(hipEventRecord(e0, 0));
+    for (int i = 0; i < reps; ++i) CK(vd_launch_block(a, 0));
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    const double us = ms * 1e3 / reps, px = (double)B * H * W;
+    const double fl = 2.0 * px * (cin * 64 + 576 * 64 + 64 * 256 + (ds ? cin * 256 : 0));
+    const double by = px * (cin + 256) * 2.0;
+    printf("block cin=%d ds=%d %dx%dx%d  %8.1f us  %7.1f TF/s  %7.1f GB/s (x + y)\n", cin, (int)ds, B, H, W, us,
+           fl / us * 1e-6, by / us * 1e-3);
+    if (a.diag) {   // last launch's per-segment cycle sums (workgroup 0, wave 0)
+        unsigned long long d[8];
+        CK(hipMemcpy(d, ddiag, sizeof d, hipMemcpyDeviceToHost));
+        const char* nm[8] = {"wait x", "barrier0", "stage1", "barrier1", "stage2", "barrier2", "stage3", "loop"};
+        unsigned long long tot = 0;
+        for (int i = 0; i < 8; ++i) tot += d[i];
+        for (int i = 0; i < 8; ++i) printf("   %-9s %10llu cycles %5.1f%%\n", nm[i], d[i], 100.0 * d[i] / (tot ? tot : 1));
+    }
+}
+
 int main(int argc, char** argv) {
     const int reps = argc > 1 ? atoi(argv[1]) : 20;
+    if (argc == 3 && std::string(argv[2]) == "block") {
+        run_block(reps, 64, 160, 160, 64, true);
+        run_block(reps, 64, 160, 160, 256, false);
+        return 0;
+    }
     std::vector<Layer> layers;
     if (argc == 3 && std::string(argv[2]) == "yolo") {   // YOLOv8n-like small-channel layers, 640x384 canvas
         layers = {

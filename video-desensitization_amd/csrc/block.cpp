@@ -1,0 +1,237 @@
+// block.cpp — plans for the fused layer1 bottleneck (block.hip): eligibility,
+// weight repacking from the per-conv bf16 weights (so the fused op multiplies
+// exactly the same bf16 values as the conv-by-conv chain), execution, and the
+// vdt_bottleneck test entry (fused and conv-by-conv on the same inputs).
+#include "../../include/vdmi.h"
+#include "nets.h"
+
+#include <cstring>
+#include <vector>
+
+namespace {
+
+// LDS row R of a 64-row weight image (MFMA tile j = R/16, row i = R%16) holds
+// channel 32(j>>1) + 8(i>>2) + 4(j&1) + (i&3): tiles 2p and 2p+1 then give a lane
+// 8 consecutive output channels (block.hip stage-1 / stage-3 epilogues).
+int perm_row(int R) {
+    const int j = R >> 4, i = R & 15;
+    return 32 * (j >> 1) + 8 * (i >> 2) + 4 * (j & 1) + (i & 3);
+}
+
+int fetch(const Conv& cv, std::vector<uint16_t>& w, std::vector<float>& sc, std::vector<float>& sh) {
+    w.resize((size_t)cv.npad * cv.kpad);
+    sc.resize(cv.npad);
+    sh.resize(cv.npad);
+    VD_CHECK_HIP(hipMemcpy(w.data(), cv.w, w.size() * 2, hipMemcpyDeviceToHost));
+    VD_CHECK_HIP(hipMemcpy(sc.data(), cv.scale, sc.size() * 4, hipMemcpyDeviceToHost));
+    VD_CHECK_HIP(hipMemcpy(sh.data(), cv.shift, sh.size() * 4, hipMemcpyDeviceToHost));
+    return VD_OK;
+}
+
+bool is_conv(const Conv& c, int cin, int cout, int k, int stride, int pad, int act) {
+    return c.cin == cin && c.cin_pad == cin && c.cout == cout && c.kh == k && c.kw == k && c.stride == stride &&
+           c.pad == pad && c.act == act;
+}
+
+}  // namespace
+
+bool Ctx::block_ok(int c1, int c2, int c3, int cd, const Act& x) const {
+    if (f32 || x.f32) return false;
+    const bool ds = cd >= 0;
+    const int cin = x.c;
+    if (!vd_block_ok(cin, ds, x.h, x.w)) return false;
+    if (!is_conv(convs[c1], cin, 64, 1, 1, 0, VD_ACT_RELU)) return false;
+    if (!is_conv(convs[c2], 64, 64, 3, 1, 1, VD_ACT_RELU)) return false;
+    if (!is_conv(convs[c3], 64, 256, 1, 1, 0, VD_ACT_RELU)) return false;
+    if (ds && !is_conv(convs[cd], cin, 256, 1, 1, 0, VD_ACT_NONE)) return false;
+    return true;
+}
+
+int Ctx::make_block(int c1, int c2, int c3, int cd, int* idx) {
+    Block bk;
+    bk.cin = convs[c1].cin;
+    bk.ds = cd >= 0;
+    bk.c1 = c1; bk.c2 = c2; bk.c3 = c3; bk.cd = cd;
+    const int cin = bk.cin;
+    std::vector<uint16_t> w1, w2, w3, wd;
+    std::vector<float> s1, h1, s2, h2, s3, h3, sd, hd;
+    int rc;
+    if ((rc = fetch(convs[c1], w1, s1, h1))) return rc;
+    if ((rc = fetch(convs[c2], w2, s2, h2))) return rc;
+    if ((rc = fetch(convs[c3], w3, s3, h3))) return rc;
+    if (bk.ds && (rc = fetch(convs[cd], wd, sd, hd))) return rc;
+    const int k1 = convs[c1].kpad, k2 = convs[c2].kpad, k3 = convs[c3].kpad, kd = bk.ds ? convs[cd].kpad : 0;
+
+    // MFMA A-operand fragments [group][k-step][lane][8]: lane l holds output channel
+    // row(group, l%16) and K elements 32s + 8(l/16) .. +8 (block.hip register layout)
+    auto frags = [](const std::vector<uint16_t>& src, int kpad, int groups, int ks, auto row) {
+        std::vector<uint16_t> f((size_t)groups * ks * 64 * 8);
+        for (int q = 0; q < groups; ++q)
+            for (int s = 0; s < ks; ++s)
+                for (int l = 0; l < 64; ++l)
+                    for (int e = 0; e < 8; ++e)
+                        f[(((size_t)q * ks + s) * 64 + l) * 8 + e] = src[(size_t)row(q, l & 15) * kpad + 32 * s + 8 * (l >> 4) + e];
+        return f;
+    };
+    // conv1 / conv2: 16-channel groups (stage 1 / 2 wave columns); conv2's K order is
+    // (tap, c) with 64 channels per tap, so k-step s = 32-channel half s&1 of tap s>>1
+    const auto id16 = [](int q, int i) { return 16 * q + i; };
+    std::vector<uint16_t> f1 = frags(w1, k1, 4, cin / 32, id16);
+    std::vector<uint16_t> f2 = frags(w2, k2, 4, 18, id16);
+    // conv3 / downsample: 32-channel groups of two tiles, rows permuted so a lane
+    // ends with 8 consecutive output channels
+    const auto perm32 = [](int q, int i) { return 32 * (q >> 1) + perm_row(16 * (q & 1) + i); };
+    std::vector<uint16_t> f3 = frags(w3, k3, 16, 2, perm32), fd;
+    if (bk.ds) fd = frags(wd, kd, 16, cin / 32, perm32);
+    std::vector<float> bn(1280, 0.f);
+    for (int c = 0; c < 64; ++c) {
+        bn[c] = s1[c]; bn[64 + c] = h1[c]; bn[128 + c] = s2[c]; bn[192 + c] = h2[c];
+    }
+    for (int c = 0; c < 256; ++c) {
+        bn[256 + c] = s3[c]; bn[512 + c] = h3[c];
+        if (bk.ds) { bn[768 + c] = sd[c]; bn[1024 + c] = hd[c]; }
+    }
+    auto up = [&](void** dst, const void* src, size_t bytes) {
+        int r = dalloc(dst, bytes);
+        if (r) return r;
+        VD_CHECK_HIP(hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice));
+        return VD_OK;
+    };
+    if ((rc = up(&bk.w1, f1.data(), f1.size() * 2))) return rc;
+    if ((rc = up(&bk.w2, f2.data(), f2.size() * 2))) return rc;
+    if ((rc = up(&bk.w3, f3.data(), f3.size() * 2))) return rc;
+    if (bk.ds && (rc = up(&bk.wd, fd.data(), fd.size() * 2))) return rc;
+    if ((rc = up((void**)&bk.bn, bn.data(), bn.size() * 4))) return rc;
+    blocks.push_back(bk);
+    *idx = (int)blocks.size() - 1;
+    return VD_OK;
+}
+
+int Ctx::add_block(Net& net, int bi, const Act& x, Act& y) {
+    const Block& bk = blocks[bi];
+    if (x.c != bk.cin || y.c != 256 || y.h != x.h || y.w != x.w || x.f32 || y.f32)
+        return vd_set_error(VD_ERR_ARG, "fused bottleneck plan shape mismatch");
+    Op op{};
+    op.kind = OP_BLOCK;
+    op.blk = bi;
+    op.x = x;
+    op.y = y;
+    net.ops.push_back(op);
+    return VD_OK;
+}
+
+static inline const void* foff_b(const Act& a, int f0) {
+    return (const char*)a.p + (size_t)f0 * a.h * a.w * a.c * 2;
+}
+
+int Ctx::run_block_op(const Op& op, int f0, int n, int fam) {
+    const Block& bk = blocks[op.blk];
+    BlockArgs a{};
+    a.x = foff_b(op.x, f0);
+    a.y = (void*)foff_b(op.y, f0);
+    a.B = n; a.H = op.x.h; a.W = op.x.w; a.cin = bk.cin; a.ds = bk.ds;
+    a.tiles_x = (a.W + 15) / 16;
+    a.tiles_y = (a.H + 7) / 8;
+    a.w1 = bk.w1; a.w2 = bk.w2; a.w3 = bk.w3; a.wd = bk.wd; a.bn = bk.bn;
+    double fpp = convs[bk.c1].flops_per_px + convs[bk.c2].flops_per_px + convs[bk.c3].flops_per_px;
+    if (bk.ds) fpp += convs[bk.cd].flops_per_px;
+    t_begin(fam, fpp * n * a.H * a.W);
+    hipError_t e = vd_launch_block(a, stream);
+    t_end();
+    if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "fused bottleneck launch: %s", hipGetErrorString(e));
+    return VD_OK;
+}
+
+static uint16_t bf16_rne(float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+
+extern "C" int vdt_bottleneck(vd_ctx* h, const float* x, int n, int hh, int ww, int cin, const float* w1,
+                              const float* bn1, const float* w2, const float* bn2, const float* w3, const float* bn3,
+                              const float* wd, const float* bnd, int fused, float* y) {
+    Ctx* ctx = (Ctx*)h;
+    if (!ctx) return vd_set_error(VD_ERR_ARG, "null context");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (hipSetDevice(ctx->device) != hipSuccess) return vd_set_error(VD_ERR_HIP, "hipSetDevice failed");
+    if (ctx->f32) return vd_set_error(VD_ERR_ARG, "vdt_bottleneck: bf16 contexts only");
+    if (n <= 0 || hh <= 0 || ww <= 0 || !x || !w1 || !w2 || !w3 || !bn1 || !bn2 || !bn3 || !y ||
+        (cin != 64 && cin != 256) || (wd && !bnd) || (!wd && cin != 256))
+        return vd_set_error(VD_ERR_ARG, "vdt_bottleneck: bad arguments");
+    const size_t nalloc = ctx->allocs.size(), nconv = ctx->convs.size(), nblk = ctx->blocks.size();
+    auto cleanup = [&]() {
+        for (size_t i = nalloc; i < ctx->allocs.size(); ++i) hipFree(ctx->allocs[i]);
+        ctx->allocs.resize(nalloc);
+        ctx->convs.resize(nconv);
+        ctx->blocks.resize(nblk);
+    };
+    auto mk = [&](const float* wt, const float* bn, int ci, int co, int k, int pad, int act, int* idx) {
+        Conv cv{};
+        cv.cin = ci; cv.cout = co; cv.kh = k; cv.kw = k; cv.stride = 1; cv.pad = pad; cv.act = act;
+        std::vector<float> wv(wt, wt + (size_t)co * ci * k * k), sc(bn, bn + co), sh(bn + co, bn + 2 * co);
+        int r = ctx->upload_conv(cv, wv, sc, sh);
+        if (r) return r;
+        ctx->convs.push_back(cv);
+        *idx = (int)ctx->convs.size() - 1;
+        return VD_OK;
+    };
+    int c1, c2, c3, cd = -1, rc;
+    if ((rc = mk(w1, bn1, cin, 64, 1, 0, VD_ACT_RELU, &c1)) || (rc = mk(w2, bn2, 64, 64, 3, 1, VD_ACT_RELU, &c2)) ||
+        (rc = mk(w3, bn3, 64, 256, 1, 0, VD_ACT_RELU, &c3)) || (wd && (rc = mk(wd, bnd, cin, 256, 1, 0, VD_ACT_NONE, &cd)))) {
+        cleanup();
+        return rc;
+    }
+    auto buf = [&](Act& a, int c) {
+        a.h = hh; a.w = ww; a.c = c; a.f32 = false;
+        const size_t bytes = (size_t)n * hh * ww * c * 2;
+        int r = ctx->dalloc(&a.p, bytes);
+        if (!r && hipMemset(a.p, 0, bytes) != hipSuccess) r = vd_set_error(VD_ERR_HIP, "hipMemset");
+        return r;
+    };
+    Act ax, at1, at2, aout, ads;
+    if ((rc = buf(ax, cin)) || (rc = buf(aout, 256))) { cleanup(); return rc; }
+    {
+        std::vector<uint16_t> xb((size_t)n * hh * ww * cin);
+        for (size_t i = 0; i < xb.size(); ++i) xb[i] = bf16_rne(x[i]);
+        if (hipMemcpy(ax.p, xb.data(), xb.size() * 2, hipMemcpyHostToDevice) != hipSuccess) {
+            cleanup();
+            return vd_set_error(VD_ERR_HIP, "vdt_bottleneck: upload");
+        }
+    }
+    Net net;
+    if (fused) {
+        int bi;
+        if (!ctx->block_ok(c1, c2, c3, cd, ax)) { cleanup(); return vd_set_error(VD_ERR_ARG, "vdt_bottleneck: fused path not eligible"); }
+        if ((rc = ctx->make_block(c1, c2, c3, cd, &bi)) || (rc = ctx->add_block(net, bi, ax, aout))) { cleanup(); return rc; }
+    } else {
+        if ((rc = buf(at1, 64)) || (rc = buf(at2, 64))) { cleanup(); return rc; }
+        if ((rc = ctx->add_conv(net, c1, ax, 0, at1, 0)) || (rc = ctx->add_conv(net, c2, at1, 0, at2, 0))) { cleanup(); return rc; }
+        if (cd >= 0 && ctx->dual_ok(c3, cd, aout)) {
+            rc = ctx->add_conv_dual(net, c3, at2, cd, ax, aout);
+        } else if (cd >= 0) {
+            if (!(rc = buf(ads, 256)) && !(rc = ctx->add_conv(net, cd, ax, 0, ads, 0)))
+                rc = ctx->add_conv(net, c3, at2, 0, aout, 0, &ads, 0, VD_RES_PRE_ACT, 0);
+        } else {
+            rc = ctx->add_conv(net, c3, at2, 0, aout, 0, &ax, 0, VD_RES_PRE_ACT, 0);
+        }
+        if (rc) { cleanup(); return rc; }
+    }
+    rc = ctx->run_ops(net, 0, (int)net.ops.size(), 0, n);
+    if (!rc && hipStreamSynchronize(ctx->stream) != hipSuccess) rc = vd_set_error(VD_ERR_HIP, "vdt_bottleneck: sync");
+    if (!rc) {
+        std::vector<uint16_t> yb((size_t)n * hh * ww * 256);
+        if (hipMemcpy(yb.data(), aout.p, yb.size() * 2, hipMemcpyDeviceToHost) != hipSuccess) {
+            rc = vd_set_error(VD_ERR_HIP, "vdt_bottleneck: download");
+        } else {
+            for (size_t i = 0; i < yb.size(); ++i) {
+                const uint32_t u = (uint32_t)yb[i] << 16;
+                memcpy(&y[i], &u, 4);
+            }
+        }
+    }
+    cleanup();
+    return rc;
+}

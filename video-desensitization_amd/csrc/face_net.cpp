@@ -117,6 +117,15 @@ int vd_build_face(Ctx& c, const WMap& W) {
                 return vd_set_error(VD_ERR_WEIGHTS, "%s: missing downsample", pre.c_str());
             const int oh = x.h / s, ow = x.w / s;
             Act t1, t2, out, ds;
+            if (s == 1 && c.block_ok(c1, c2, c3, cd, x)) {
+                // the whole bottleneck in one kernel (block.hip): t1/t2 stay in LDS
+                int bk;
+                if ((rc = c.act(out, oh, ow, planes * 4))) return rc;
+                if ((rc = c.make_block(c1, c2, c3, cd, &bk))) return rc;
+                if ((rc = c.add_block(F.net, bk, x, out))) return rc;
+                x = out;
+                continue;
+            }
             if ((rc = c.act(t1, x.h, x.w, planes))) return rc;
             if ((rc = c.act(t2, oh, ow, planes))) return rc;
             if ((rc = c.act(out, oh, ow, planes * 4))) return rc;

@@ -32,7 +32,19 @@ struct Conv {
     double flops_per_px = 0;   // algorithmic FLOPs per output pixel (real Cin, no padding)
 };
 
-enum { OP_CONV = 0, OP_MAXPOOL = 1, OP_UPSAMPLE = 2 };
+// One fused layer1 bottleneck (block.hip, block.cpp): the per-conv bf16 weights
+// of conv1/conv2/conv3(/downsample) repacked for the fused kernel.
+struct Block {
+    int cin = 0, ds = 0;
+    int c1 = -1, c2 = -1, c3 = -1, cd = -1;   // the per-conv plans (flops, unfused fallback)
+    void* w1 = nullptr;
+    void* w2 = nullptr;
+    void* w3 = nullptr;
+    void* wd = nullptr;
+    float* bn = nullptr;
+};
+
+enum { OP_CONV = 0, OP_MAXPOOL = 1, OP_UPSAMPLE = 2, OP_BLOCK = 3 };
 
 struct Op {
     int kind = OP_CONV;
@@ -42,6 +54,7 @@ struct Op {
     Act r; int rcoff = 0; int rmode = 0; int rup = 0;
     int conv2 = -1; Act x2;            // fused second 1x1 conv (downsample branch), summed pre-activation
     int ch = 0, k = 0, s = 0, p = 0;   // maxpool / upsample
+    int blk = -1;                      // OP_BLOCK: index into Ctx::blocks (x -> y)
 };
 
 struct Net {
@@ -116,6 +129,7 @@ struct Ctx {
     std::mutex mu;
     std::vector<void*> allocs;
     std::vector<Conv> convs;
+    std::vector<Block> blocks;
     FaceNet face;
     PlateNet plate;
     void* stage_in = nullptr;  size_t stage_in_bytes = 0;
@@ -140,6 +154,10 @@ struct Ctx {
     bool dual_ok(int ci, int c2, const Act& y) const;
     int add_conv(Net& net, int ci, const Act& x, int xcoff, Act& y, int ycoff, const Act* res = nullptr,
                  int rcoff = 0, int rmode = 0, int rup = 0);
+    bool block_ok(int c1, int c2, int c3, int cd, const Act& x) const;
+    int make_block(int c1, int c2, int c3, int cd, int* idx);
+    int add_block(Net& net, int bi, const Act& x, Act& y);
+    int run_block_op(const Op& op, int f0, int n, int fam = 0);
     void t_begin(int fam, double work);
     void t_end();
     int run_conv_op(const Op& op, int f0, int n, int fam = 0);

@@ -33,6 +33,21 @@ struct ConvArgs {
     const void* w2; const float* scale2; const float* shift2; int cin2_pad, kpad2;
 };
 
+// One fused layer1 bottleneck (block.hip): x [B][H][W][cin] -> y [B][H][W][256],
+// weights pre-packed by the runtime (Ctx::make_block) from the per-conv bf16 weights.
+struct BlockArgs {
+    const void* x; void* y;
+    int B, H, W, cin, ds;        // ds: identity = bn(downsample(x)) (cin 64), else x (cin 256)
+    int tiles_x, tiles_y;        // 16-wide x 8-high output tiles
+    const void* w1;              // conv1 MFMA fragments [4 groups of 16 ch][cin/32 k-steps][64 lanes][8]
+    const void* w2;              // conv2 fragments [4][18][64][8]
+    const void* w3;              // conv3 fragments [8 groups of 32 ch][2 tiles][2 k-steps][64][8]
+    const void* wd;              // downsample fragments [8][2][cin/32][64][8] (ds)
+    const float* bn;             // s1 t1 s2 t2 (64 each) s3 t3 sd td (256 each)
+    unsigned long long* diag;    // optional: per-stage cycle sums of workgroup 0, wave 0 (tools/convbench)
+    int mode;                    // experiments (tools/convbench VD_BLOCK_MODE); 0 in production
+};
+
 // Device buffers + parameters for one frame batch's detection post-processing.
 enum { POST_FACE = 0, POST_YOLO = 1 };
 struct PostArgs {
@@ -100,6 +115,8 @@ bool vd_conv_taps_ok(const ConvArgs& a);
 bool vd_conv1x1_dual_ok(const ConvArgs& a);
 hipError_t vd_launch_conv_taps(const ConvArgs& a, hipStream_t s);
 hipError_t vd_launch_conv(const ConvArgs& a, bool f32, hipStream_t s);
+bool vd_block_ok(int cin, bool ds, int h, int w);
+hipError_t vd_launch_block(const BlockArgs& a, hipStream_t s);
 hipError_t vd_launch_letterbox(const LetterboxArgs& a, hipStream_t s);
 hipError_t vd_launch_maxpool(bool f32, const void* x, int n, int xh, int xw, int ldx, int xcoff,
                              void* y, int yh, int yw, int ldy, int ycoff, int c, int k, int st, int p,

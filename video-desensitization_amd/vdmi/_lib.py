@@ -82,6 +82,7 @@ SIGNATURES = [
     ("vdt_postprocess", _I, [_P, _P, _P, _I, _P, ctypes.POINTER(vd_boxes)]),
     ("vdt_conv2d", _I, [_P, _P, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _P, _P, _I, _F, _P, _I, _P,
                         ctypes.POINTER(_I), ctypes.POINTER(_I)]),
+    ("vdt_bottleneck", _I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
     ("vdt_plate_raw", _I, [_P, _P, _I, _I, _I, _SZ, _I, _P, ctypes.POINTER(_I)]),
 ]
 

@@ -225,6 +225,19 @@ class Context:
         check(self._lib.vdt_plate_raw(self._h, p, n, h, w, pitch, where, ptr(out), ctypes.byref(A)))
         return out
 
+    def bottleneck(self, x, w1, bn1, w2, bn2, w3, bn3, wd=None, bnd=None, fused=True):
+        """One ResNet layer1 bottleneck (bf16 context): x f32 NHWC [n,h,w,cin] -> f32 NHWC
+        [n,h,w,256]; bnK = concat(scale, shift). fused: the one-kernel block, else the
+        conv-by-conv chain."""
+        f = lambda a: None if a is None else np.ascontiguousarray(a, np.float32)
+        x = f(x)
+        n, h, wd_, cin = x.shape
+        y = np.zeros((n, h, wd_, 256), np.float32)
+        args = [f(a) for a in (w1, bn1, w2, bn2, w3, bn3, wd, bnd)]
+        check(self._lib.vdt_bottleneck(self._h, ptr(x), n, h, wd_, cin, *[ptr(a) for a in args], int(bool(fused)),
+                                       ptr(y)))
+        return y
+
     def conv2d(self, x, w, stride=1, pad=0, scale=None, shift=None, act=0, slope=0.0, res=None, res_mode=0):
         """x: f32 NHWC [n,h,w,cin]; w: f32 [cout,cin,kh,kw] -> f32 NHWC."""
         x = np.ascontiguousarray(x, np.float32)
