@@ -271,21 +271,28 @@ __global__ __launch_bounds__(512, 1) void bottleneck_kernel(BlockArgs a) {
             f32x4_t acc[4];
 #pragma unroll
             for (int m = 0; m < 4; ++m) acc[m] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-            u32x4 tf[2][4];   // the reads of k-step s+1 go out before the MFMAs of s
-#define VD_T1READ(S, BUF)                                                                          \
+            // Each t1 window (halo row 4*half + hh, shift dx, channel half hf) is read once
+            // and feeds every output row it touches (m = hh - dy for the three kernel rows
+            // dy): 36 reads for the 72 MFMAs. Reads run 3 windows ahead of their MFMAs.
+            constexpr int PD = 3;
+            u32x4 tf[PD + 1];
+#define VD_T1READ(Q)                                                                               \
             do {                                                                                   \
-                const int tap_ = (S) >> 1, dy_ = tap_ / 3, dx_ = tap_ - dy_ * 3;                   \
-                _Pragma("unroll") for (int m = 0; m < 4; ++m)                                      \
-                    tf[BUF][m] = *(const u32x4*)(lt1 + lds_off((4 * half + m + dy_) * HWD + li + dx_, \
-                                                               ((S) & 1) * 4 + g));                \
+                const int hh_ = (Q) / 6, hf_ = ((Q) / 3) & 1, dx_ = (Q) % 3;                       \
+                tf[(Q) % (PD + 1)] = *(const u32x4*)(lt1 + lds_off((4 * half + hh_) * HWD + li + dx_, 4 * hf_ + g)); \
             } while (0)
-            VD_T1READ(0, 0);
 #pragma unroll
-            for (int s = 0; s < 18; ++s) {
+            for (int q = 0; q < PD; ++q) VD_T1READ(q);
+#pragma unroll
+            for (int q = 0; q < 36; ++q) {
                 asm volatile("" ::: "memory");
-                if (s + 1 < 18) VD_T1READ(s + 1, (s + 1) & 1);
+                if (q + PD < 36) VD_T1READ(q + PD);
+                const int hh = q / 6, hf = (q / 3) & 1, dx = q % 3;
 #pragma unroll
-                for (int m = 0; m < 4; ++m) acc[m] = mfma(w2f[s], tf[s & 1][m], acc[m]);
+                for (int dy = 0; dy < 3; ++dy) {
+                    const int m = hh - dy;
+                    if (m >= 0 && m < 4) acc[m] = mfma(w2f[2 * (3 * dy + dx) + hf], tf[q % (PD + 1)], acc[m]);
+                }
             }
 #undef VD_T1READ
             if constexpr (!W1_STAT) {   // next tile's W1 (consumed after the next top-of-tile vmcnt(0))
