@@ -105,6 +105,26 @@ def test_heads_bf16_fused_block_matches_unfused(gpu, monkeypatch):
         assert _rel(a, b) < 2e-2
 
 
+def test_heads_bf16_fused_stem_pool_matches_unfused(gpu, monkeypatch):
+    """bf16 plans run conv1 + bn1 + relu + maxpool as one kernel (stem.hip: the stem map
+    stays in LDS); VD_STEM_POOL=0 at weight load keeps the taps conv + maxpool kernels.
+    Same products in the same K order and the same bf16 rounding, max pooling is
+    exact: the heads are identical."""
+    import vdmi
+    fr = _frames(2, 720, 1280, seed=9)
+    out = {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("VD_STEM_POOL", fuse)
+        ctx = vdmi.Context(precision="bf16", max_batch=2)
+        try:
+            ctx.load_weights(0, face_weights("default"))
+            out[fuse] = ctx.forward_heads(fr)
+        finally:
+            ctx.close()
+    for a, b in zip(out["1"], out["0"]):
+        np.testing.assert_array_equal(a, b)
+
+
 def _near_decision(conf_b, boxes_norm, thr=0.5, iou=0.4, eps=1e-4):
     """Anchors whose score is within eps of thr, or whose IoU with another candidate
     is within eps of the NMS threshold: decisions there are ulp-sensitive."""

@@ -8,8 +8,10 @@ import csv
 import sys
 
 
-def face_plan(B=64, H=640, W=640, fused=True):
-    """(name, M, N, K) of every conv in face_net.cpp order."""
+def face_plan(B=64, H=640, W=640, fused=True, block=True):
+    """(name, M, N, K) of every conv launch in face_net.cpp order; with `block` the
+    three layer1 bottlenecks are one launch each (block.hip), K = their summed
+    reduction depth per output channel of 256 (same FLOPs)."""
     L = []
     h, w = H // 2, W // 2
     L.append(("stem7x7", B * h * w, 64, 3 * 49))
@@ -18,6 +20,11 @@ def face_plan(B=64, H=640, W=640, fused=True):
     for li, (planes, blocks, stride) in enumerate([(64, 3, 1), (128, 4, 2), (256, 6, 2), (512, 3, 2)]):
         for bi in range(blocks):
             s = stride if bi == 0 else 1
+            if block and li == 0:
+                k = (cin * 64 + 576 * 64 + 64 * 256 + (cin * 256 if bi == 0 else 0)) // 256
+                L.append((f"l1.{bi}.block", B * h * w, 256, k))
+                cin = planes * 4
+                continue
             L.append((f"l{li+1}.{bi}.c1", B * h * w, planes, cin))
             oh, ow = h // s, w // s
             L.append((f"l{li+1}.{bi}.c2", B * oh * ow, planes, planes * 9))
@@ -48,7 +55,9 @@ def main(path, B=64):
     # The face forward may share the GPU with the plate network on a second
     # stream: anchor on the last face letterbox (space-to-depth form in bf16)
     # and take the conv launches that follow it on the same stream.
-    conv_keys = ("conv_igemm", "conv1x1_stream", "conv_big")
+    conv_keys = ("conv_igemm", "conv1x1_stream", "conv_big", "bottleneck_kernel", "stem_pool_kernel")
+    if not any("bottleneck_kernel" in r["Kernel_Name"] for r in allk):
+        plan = face_plan(B, block=False)
     li = max(i for i, r in enumerate(allk) if "letterbox_s2d_kernel" in r["Kernel_Name"]
              or ("letterbox_kernel" in r["Kernel_Name"] and int(r["Grid_Size_Y"]) == 640))
     stream = allk[li]["Stream_Id"]
@@ -60,7 +69,7 @@ def main(path, B=64):
         fl = 2.0 * M * N * K
         tot_t += dt
         tot_f += fl
-        kn = ("BIG" if "conv_big" in r["Kernel_Name"] else "S:" + r["Kernel_Name"].split("<")[1][:12] if "conv1x1_stream" in r["Kernel_Name"] else "G:" + r["Kernel_Name"].split("conv_igemm_kernel")[1][:22])
+        kn = ("STEM+POOL" if "stem_pool" in r["Kernel_Name"] else "BLOCK" if "bottleneck" in r["Kernel_Name"] else "BIG" if "conv_big" in r["Kernel_Name"] else "S:" + r["Kernel_Name"].split("<")[1][:12] if "conv1x1_stream" in r["Kernel_Name"] else "G:" + r["Kernel_Name"].split("conv_igemm_kernel")[1][:22])
         print(f"{name:12s} M={M:8d} N={N:5d} K={K:5d} {dt*1e6:8.1f} us {fl/dt/1e12:7.1f} TF/s  {kn}")
     print(f"total {tot_t*1e3:.2f} ms  {tot_f/tot_t/1e12:.1f} TF/s")
 

@@ -11,7 +11,8 @@ import csv
 import os
 import sys
 
-FAMILIES = [("conv", ("conv_igemm_kernel", "conv1x1_stream_kernel", "conv_big_kernel")),
+FAMILIES = [("conv", ("conv_igemm_kernel", "conv1x1_stream_kernel", "conv_big_kernel", "bottleneck_kernel",
+                       "stem_pool_kernel")),
             ("mosaic", ("mosaic_",)), ("letterbox", ("letterbox_kernel", "letterbox_s2d_kernel")),
             ("post", ("candidates_kernel", "nms_kernel")), ("other", ("maxpool", "upsample"))]
 CONV = FAMILIES[0][1]

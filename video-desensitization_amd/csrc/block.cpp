@@ -28,6 +28,23 @@ int fetch(const Conv& cv, std::vector<uint16_t>& w, std::vector<float>& sc, std:
     return VD_OK;
 }
 
+// MFMA A-operand fragments [group][k-step][lane][8]: lane l holds output channel
+// row(group, l%16) and K elements 32s + 8(l/16) .. +8 (block.hip / stem.hip layout)
+template <class Row>
+std::vector<uint16_t> frags(const std::vector<uint16_t>& src, int kpad, int groups, int ks, Row row) {
+    std::vector<uint16_t> f((size_t)groups * ks * 64 * 8);
+    for (int q = 0; q < groups; ++q)
+        for (int s = 0; s < ks; ++s)
+            for (int l = 0; l < 64; ++l)
+                for (int e = 0; e < 8; ++e)
+                    f[(((size_t)q * ks + s) * 64 + l) * 8 + e] = src[(size_t)row(q, l & 15) * kpad + 32 * s + 8 * (l >> 4) + e];
+    return f;
+}
+
+// 32-channel groups of two MFMA tiles, rows permuted so a lane ends with 8
+// consecutive output channels
+int perm32(int q, int i) { return 32 * (q >> 1) + perm_row(16 * (q & 1) + i); }
+
 bool is_conv(const Conv& c, int cin, int cout, int k, int stride, int pad, int act) {
     return c.cin == cin && c.cin_pad == cin && c.cout == cout && c.kh == k && c.kw == k && c.stride == stride &&
            c.pad == pad && c.act == act;
@@ -62,17 +79,6 @@ int Ctx::make_block(int c1, int c2, int c3, int cd, int* idx) {
     if (bk.ds && (rc = fetch(convs[cd], wd, sd, hd))) return rc;
     const int k1 = convs[c1].kpad, k2 = convs[c2].kpad, k3 = convs[c3].kpad, kd = bk.ds ? convs[cd].kpad : 0;
 
-    // MFMA A-operand fragments [group][k-step][lane][8]: lane l holds output channel
-    // row(group, l%16) and K elements 32s + 8(l/16) .. +8 (block.hip register layout)
-    auto frags = [](const std::vector<uint16_t>& src, int kpad, int groups, int ks, auto row) {
-        std::vector<uint16_t> f((size_t)groups * ks * 64 * 8);
-        for (int q = 0; q < groups; ++q)
-            for (int s = 0; s < ks; ++s)
-                for (int l = 0; l < 64; ++l)
-                    for (int e = 0; e < 8; ++e)
-                        f[(((size_t)q * ks + s) * 64 + l) * 8 + e] = src[(size_t)row(q, l & 15) * kpad + 32 * s + 8 * (l >> 4) + e];
-        return f;
-    };
     // conv1 / conv2: 16-channel groups (stage 1 / 2 wave columns); conv2's K order is
     // (tap, c) with 64 channels per tap, so k-step s = 32-channel half s&1 of tap s>>1
     const auto id16 = [](int q, int i) { return 16 * q + i; };
@@ -80,7 +86,6 @@ int Ctx::make_block(int c1, int c2, int c3, int cd, int* idx) {
     std::vector<uint16_t> f2 = frags(w2, k2, 4, 18, id16);
     // conv3 / downsample: 32-channel groups of two tiles, rows permuted so a lane
     // ends with 8 consecutive output channels
-    const auto perm32 = [](int q, int i) { return 32 * (q >> 1) + perm_row(16 * (q & 1) + i); };
     std::vector<uint16_t> f3 = frags(w3, k3, 16, 2, perm32), fd;
     if (bk.ds) fd = frags(wd, kd, 16, cin / 32, perm32);
     std::vector<float> bn(1280, 0.f);
@@ -120,6 +125,29 @@ int Ctx::add_block(Net& net, int bi, const Act& x, Act& y) {
     return VD_OK;
 }
 
+// stem conv (space-to-depth 4x4, 16 -> 64) + maxpool 3x3/2 (stem.hip)
+int Ctx::add_stem_pool(Net& net, int ci, const Act& x, Act& y) {
+    const Conv& cv = convs[ci];
+    if (f32 || x.f32 || y.f32 || cv.cin != 16 || cv.cin_pad != 16 || cv.cout != 64 || cv.kh != 4 || cv.kw != 4 ||
+        cv.stride != 1 || cv.pad != 1 || cv.act != VD_ACT_RELU || cv.kpad != 256 || x.c != 16 || y.c != 64 ||
+        !vd_stem_pool_ok(x.h, x.w, y.h, y.w))
+        return vd_set_error(VD_ERR_ARG, "fused stem plan shape mismatch");
+    std::vector<uint16_t> w;
+    std::vector<float> sc, sh;
+    int rc = fetch(cv, w, sc, sh);
+    if (rc) return rc;
+    std::vector<uint16_t> f = frags(w, cv.kpad, 4, 8, perm32);
+    Op op{};
+    op.kind = OP_STEMPOOL;
+    op.conv = ci;
+    op.x = x;
+    op.y = y;
+    if ((rc = dalloc(&op.wf, f.size() * 2))) return rc;
+    VD_CHECK_HIP(hipMemcpy(op.wf, f.data(), f.size() * 2, hipMemcpyHostToDevice));
+    net.ops.push_back(op);
+    return VD_OK;
+}
+
 static inline const void* foff_b(const Act& a, int f0) {
     return (const char*)a.p + (size_t)f0 * a.h * a.w * a.c * 2;
 }
@@ -139,6 +167,19 @@ int Ctx::run_block_op(const Op& op, int f0, int n, int fam) {
     hipError_t e = vd_launch_block(a, stream);
     t_end();
     if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "fused bottleneck launch: %s", hipGetErrorString(e));
+    return VD_OK;
+}
+
+int Ctx::run_stem_pool_op(const Op& op, int f0, int n, int fam) {
+    const Conv& cv = convs[op.conv];
+    StemPoolArgs a{};
+    a.x = foff_b(op.x, f0); a.B = n; a.xh = op.x.h; a.xw = op.x.w;
+    a.y = (void*)foff_b(op.y, f0); a.ph = op.y.h; a.pw = op.y.w;
+    a.wf = op.wf; a.scale = cv.scale; a.shift = cv.shift;
+    t_begin(fam, cv.flops_per_px * n * (double)(op.x.h - 1) * (op.x.w - 1));
+    hipError_t e = vd_launch_stem_pool(a, stream);
+    t_end();
+    if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "fused stem launch: %s", hipGetErrorString(e));
     return VD_OK;
 }
 

@@ -86,10 +86,13 @@ int vd_build_face(Ctx& c, const WMap& W) {
     else rc = conv_bn(c, W, "body.conv1.weight", "body.bn1", 2, 3, VD_ACT_RELU, &ci);
     if (rc) return rc;
     Act stem, pool;
-    if ((rc = c.act(stem, H / 2, Wd / 2, 64))) return rc;
-    if ((rc = c.add_conv(F.net, ci, F.input, 0, stem, 0))) return rc;
     if ((rc = c.act(pool, H / 4, Wd / 4, 64))) return rc;
-    {
+    if (F.s2d && vd_stem_pool_ok(F.input.h, F.input.w, pool.h, pool.w)) {
+        // conv1 + bn1 + relu + maxpool in one kernel (stem.hip): the stem map stays on chip
+        if ((rc = c.add_stem_pool(F.net, ci, F.input, pool))) return rc;
+    } else {
+        if ((rc = c.act(stem, H / 2, Wd / 2, 64))) return rc;
+        if ((rc = c.add_conv(F.net, ci, F.input, 0, stem, 0))) return rc;
         Op op;
         op.kind = OP_MAXPOOL;
         op.x = stem; op.y = pool; op.ch = 64; op.k = 3; op.s = 2; op.p = 1;

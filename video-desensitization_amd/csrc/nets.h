@@ -44,7 +44,7 @@ struct Block {
     float* bn = nullptr;
 };
 
-enum { OP_CONV = 0, OP_MAXPOOL = 1, OP_UPSAMPLE = 2, OP_BLOCK = 3 };
+enum { OP_CONV = 0, OP_MAXPOOL = 1, OP_UPSAMPLE = 2, OP_BLOCK = 3, OP_STEMPOOL = 4 };
 
 struct Op {
     int kind = OP_CONV;
@@ -55,6 +55,7 @@ struct Op {
     int conv2 = -1; Act x2;            // fused second 1x1 conv (downsample branch), summed pre-activation
     int ch = 0, k = 0, s = 0, p = 0;   // maxpool / upsample
     int blk = -1;                      // OP_BLOCK: index into Ctx::blocks (x -> y)
+    void* wf = nullptr;                // OP_STEMPOOL: conv's weight fragments (conv = the stem conv)
 };
 
 struct Net {
@@ -158,6 +159,8 @@ struct Ctx {
     int make_block(int c1, int c2, int c3, int cd, int* idx);
     int add_block(Net& net, int bi, const Act& x, Act& y);
     int run_block_op(const Op& op, int f0, int n, int fam = 0);
+    int add_stem_pool(Net& net, int ci, const Act& x, Act& y);
+    int run_stem_pool_op(const Op& op, int f0, int n, int fam = 0);
     void t_begin(int fam, double work);
     void t_end();
     int run_conv_op(const Op& op, int f0, int n, int fam = 0);

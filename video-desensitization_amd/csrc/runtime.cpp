@@ -317,6 +317,8 @@ int Ctx::run_ops(const Net& net, int b, int e, int f0, int n) {
             rc = run_conv_op(op, f0, n, net.conv_fam);
         } else if (op.kind == OP_BLOCK) {
             rc = run_block_op(op, f0, n, net.conv_fam);
+        } else if (op.kind == OP_STEMPOOL) {
+            rc = run_stem_pool_op(op, f0, n, net.conv_fam);
         } else if (op.kind == OP_MAXPOOL) {
             t_begin(4, 0);
             hipError_t er = vd_launch_maxpool(f32, foff(op.x, f0), n, op.x.h, op.x.w, op.x.c, op.xcoff,

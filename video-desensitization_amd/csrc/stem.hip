@@ -1,0 +1,211 @@
+// stem.hip — the ResNet-50 stem of RetinaFace in one kernel: conv1 7x7/2 + bn1 +
+// relu, then maxpool 3x3/2 pad 1 (torchvision resnet50 [ext] as loaded from the
+// reference's body.conv1 / body.bn1 / body.maxpool, detect_face/retinaface.py:53-60).
+//
+// The conv runs in its space-to-depth form (face_net.cpp stem_s2d: a 4x4 stride-1
+// pad-1 conv over X'[Y][X][16] = the letterboxed canvas in 2x2 sub-pixel blocks),
+// the same bf16 products and K order as the streaming taps kernel, so the stem
+// activations are identical; they are rounded to bf16 and pooled in LDS, and only
+// the pooled map (1/4 of the stem's bytes) reaches HBM -- the 64x320x320x64 stem
+// map of a 640x640 batch (839 MB at B = 64) is never written or read back.
+//
+// Persistent workgroups of 4 waves walk 8x8 tiles of pool outputs:
+//   - the 20x20 X' tile (13 KB) arrives by LDS-DMA, double-buffered: the next tile's
+//     is in flight while this one computes;
+//   - stage A: the 17x17 stem outputs under the pool windows (19 groups of 16
+//     pixels) as D^T = W . X^T with v_mfma_f32_16x16x32_bf16; wave w holds the
+//     weight fragments of channels 32(w&1) .. +32 in VGPRs for good and takes every
+//     other group; BN + ReLU, bf16, 16-B LDS writes of 8 consecutive channels;
+//   - stage B: the 3x3/2 max of 64 pool pixels x 8 channel chunks (bf16 values >= 0
+//     after the ReLU compare as their bit patterns; zero padding = the -inf padding
+//     of the pool over non-negative inputs), 16-B stores.
+#include "vd_common.h"
+
+#include <cstdlib>
+
+namespace {
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+constexpr int PT = 8;                     // pool tile (PT x PT outputs)
+constexpr int SE = 2 * PT + 1;            // stem tile edge (17)
+constexpr int SP = SE * SE;               // 289 stem pixels
+constexpr int NG = (SP + 15) / 16;        // 19 groups of 16
+constexpr int XE = SE + 3;                // X' tile edge (20): 4x4 taps, pad 1
+constexpr int XP = XE * XE;               // 400 X' pixels x 32 B
+constexpr int NDMA = (XP * 32 + 1023) / 1024;
+constexpr int DPW = (NDMA + 3) / 4;       // DMA instructions per wave (padded, see block.hip)
+constexpr int XBUF = NDMA * 1024;
+constexpr int STB = NG * 16 * 128;        // stem tile image: 304 rows x 64 channels bf16
+constexpr int VMCNT0 = 0x0F70;
+
+__device__ __forceinline__ int st_off(int row, int chunk) {
+    return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
+}
+
+__device__ __forceinline__ f32x4_t mfma(const u32x4& a, const u32x4& b, const f32x4_t& c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
+                                                   c, 0, 0, 0);
+}
+
+__device__ __forceinline__ unsigned max_bf16x2(unsigned a, unsigned b) {   // non-negative bf16 pairs
+    const unsigned lo = (a & 0xffffu) > (b & 0xffffu) ? (a & 0xffffu) : (b & 0xffffu);
+    const unsigned hi = (a >> 16) > (b >> 16) ? (a >> 16) : (b >> 16);
+    return lo | (hi << 16);
+}
+
+__global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemPoolArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* lx = smem;                       // 2 x XBUF
+    char* lst = smem + 2 * XBUF;           // STB
+    char* lscratch = lst + STB;            // 1 KB sink of the padding DMA slots
+
+    const int tid = threadIdx.x, lane = tid & 63, li0 = lane & 15, g0 = lane >> 4;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int np = w & 1, gh = w >> 1;
+    const int SH = a.xh - 1, SW = a.xw - 1;                   // stem output (4x4, pad 1)
+    const int tpr = (a.ph + PT - 1) / PT, tpc = (a.pw + PT - 1) / PT, tpf = tpr * tpc;
+    const int T = a.B * tpf;
+    const int G = gridDim.x, bid = blockIdx.x;
+    int t0, tstep, tend;
+    if (G >= 8) {   // XCD-contiguous tile ranges
+        const int x8 = bid & 7;
+        t0 = (int)((long)x8 * T / 8) + (bid >> 3);
+        tstep = G / 8 + (x8 < G % 8 ? 1 : 0);
+        tend = (int)((long)(x8 + 1) * T / 8);
+    } else {
+        t0 = bid; tstep = G; tend = T;
+    }
+    if (t0 >= tend) return;
+    const size_t fx = (size_t)a.xh * a.xw * 16;              // X' elements per frame
+
+    auto issue_x = [&](int t, int buf) {
+        const int b = t / tpf, r0 = t - b * tpf;
+        const int ty = r0 / tpc, tx = r0 - ty * tpc;
+        const int xr0 = 2 * PT * ty - 2, xc0 = 2 * PT * tx - 2;   // X' origin of the tile
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)((const __bf16*)a.x + (size_t)b * fx), 0, (int)(fx * 2), 0x00020000);
+        char* dst = lx + buf * XBUF;
+#pragma unroll
+        for (int k = 0; k < DPW; ++k) {
+            const int i = w + 4 * k;
+            const bool real = i < NDMA;
+            const int xp = 32 * i + (lane >> 1), ch = lane & 1;
+            const int xr = xp / XE, xc = xp - xr * XE;
+            const int iy = xr0 + xr, ix = xc0 + xc;
+            const bool in = real && xp < XP && (unsigned)iy < (unsigned)a.xh && (unsigned)ix < (unsigned)a.xw;
+            const unsigned off = in ? (unsigned)(((iy * a.xw + ix) * 16 + ch * 8) * 2) : 0x80000000u;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(real ? dst + i * 1024 : lscratch), 16, off, 0, 0,
+                                                     0);
+        }
+    };
+    issue_x(t0, 0);
+
+    // stationary: weight fragments of this wave's 32 channels (2 tiles x 8 k-steps) and BN
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)a.wf, 0, 0x7fffffff, 0x00020000);
+    u32x4 wf[2][8];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+            wf[j][s] = __builtin_amdgcn_raw_buffer_load_b128(rw, (unsigned)lane * 16u, ((2 * np + j) * 8 + s) * 1024, 0);
+    float sc[8], sh[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        sc[e] = a.scale[32 * np + 8 * g0 + e];
+        sh[e] = a.shift[32 * np + 8 * g0 + e];
+    }
+
+    int buf = 0;
+#pragma unroll 1
+    for (int t = t0; t < tend; t += tstep) {
+        const int b = t / tpf, r0 = t - b * tpf;
+        const int ty = r0 / tpc, tx = r0 - ty * tpc;
+        const int sy0 = 2 * PT * ty - 1, sx0 = 2 * PT * tx - 1;   // stem origin of the tile
+        const char* lxc = lx + buf * XBUF;
+        __builtin_amdgcn_s_waitcnt(VMCNT0);                         // this tile's X' (DMA)
+        __syncthreads();
+        if (t + tstep < tend) issue_x(t + tstep, buf ^ 1);          // no register loads follow
+        int li = li0, g = g0;
+        asm volatile("" : "+v"(li), "+v"(g));
+
+        // ---- stage A: stem outputs of this wave's groups, channels 32np .. +32 ----
+#pragma unroll 1
+        for (int G16 = gh; G16 < NG; G16 += 2) {
+            const int p = 16 * G16 + li;
+            const int r = p / SE, c = p - r * SE;
+            f32x4_t acc[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+            u32x4 xf[8];
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                const int tap = 2 * s + (g >> 1), ta = tap >> 2, tb = tap & 3;
+                xf[s] = *(const u32x4*)(lxc + ((r + ta) * XE + c + tb) * 32 + (g & 1) * 16);
+            }
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                acc[0] = mfma(wf[0][s], xf[s], acc[0]);
+                acc[1] = mfma(wf[1][s], xf[s], acc[1]);
+            }
+            const int sy = sy0 + r, sx = sx0 + c;
+            const bool in = p < SP && (unsigned)sy < (unsigned)SH && (unsigned)sx < (unsigned)SW;
+            bf16x8_t o;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float v = acc[e >> 2][e & 3] * sc[e] + sh[e];
+                o[e] = (__bf16)(in && v > 0.f ? v : 0.f);
+            }
+            *(bf16x8_t*)(lst + st_off(p, 4 * np + g)) = o;
+        }
+        __syncthreads();
+
+        // ---- stage B: 3x3/2 max pool of the tile, 8 channels per thread ----
+        {
+            __bf16* yb = (__bf16*)a.y + (size_t)b * a.ph * a.pw * 64;
+#pragma unroll
+            for (int pass = 0; pass < 2; ++pass) {
+                const int q = pass * 32 + (tid >> 3), ch = tid & 7;
+                const int pi = q >> 3, pj = q & 7;
+                u32x4 m = {0u, 0u, 0u, 0u};
+#pragma unroll
+                for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+                    for (int dx = 0; dx < 3; ++dx) {
+                        const u32x4 v = *(const u32x4*)(lst + st_off((2 * pi + dy) * SE + 2 * pj + dx, ch));
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) m[e] = max_bf16x2(m[e], v[e]);
+                    }
+                const int py = PT * ty + pi, px = PT * tx + pj;
+                if (py < a.ph && px < a.pw) *(u32x4*)(yb + ((size_t)py * a.pw + px) * 64 + 8 * ch) = m;
+            }
+        }
+        buf ^= 1;
+    }
+}
+
+}  // namespace
+
+bool vd_stem_pool_ok(int xh, int xw, int ph, int pw) {
+    const char* e = getenv("VD_STEM_POOL");
+    if (e && atoi(e) == 0) return false;
+    const int sh = xh - 1, sw = xw - 1;
+    return xh >= 2 && xw >= 2 && ph == (sh - 1) / 2 + 1 && pw == (sw - 1) / 2 + 1 &&
+           (double)xh * xw * 16 * 2 < 2147483647.0;
+}
+
+hipError_t vd_launch_stem_pool(const StemPoolArgs& a, hipStream_t s) {
+    if (a.B <= 0) return hipSuccess;
+    constexpr size_t lds = 2 * XBUF + STB + 1024;
+    static const int cus = [] {
+        (void)hipFuncSetAttribute((const void*)stem_pool_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+        int dev = 0, n = 256;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        return n > 0 ? n : 256;
+    }();
+    const int tiles = a.B * ((a.ph + PT - 1) / PT) * ((a.pw + PT - 1) / PT);
+    const int grid = tiles < 2 * cus ? tiles : 2 * cus;   // persistent, two workgroups per CU
+    hipLaunchKernelGGL(stem_pool_kernel, dim3(grid), dim3(256), lds, s, a);
+    return hipGetLastError();
+}

@@ -48,6 +48,15 @@ struct BlockArgs {
     int mode;                    // experiments (tools/convbench VD_BLOCK_MODE); 0 in production
 };
 
+// RetinaFace stem conv (space-to-depth form) + maxpool in one kernel (stem.hip):
+// x = X' [B][xh][xw][16] -> y = pooled [B][ph][pw][64].
+struct StemPoolArgs {
+    const void* x; int B, xh, xw;
+    void* y; int ph, pw;
+    const void* wf;              // MFMA fragments [4 groups of 16 ch, pairs permuted][8 k-steps][64 lanes][8]
+    const float* scale; const float* shift;
+};
+
 // Device buffers + parameters for one frame batch's detection post-processing.
 enum { POST_FACE = 0, POST_YOLO = 1 };
 struct PostArgs {
@@ -116,6 +125,8 @@ bool vd_conv1x1_dual_ok(const ConvArgs& a);
 hipError_t vd_launch_conv_taps(const ConvArgs& a, hipStream_t s);
 hipError_t vd_launch_conv(const ConvArgs& a, bool f32, hipStream_t s);
 bool vd_block_ok(int cin, bool ds, int h, int w);
+bool vd_stem_pool_ok(int xh, int xw, int ph, int pw);
+hipError_t vd_launch_stem_pool(const StemPoolArgs& a, hipStream_t s);
 hipError_t vd_launch_block(const BlockArgs& a, hipStream_t s);
 hipError_t vd_launch_letterbox(const LetterboxArgs& a, hipStream_t s);
 hipError_t vd_launch_maxpool(bool f32, const void* x, int n, int xh, int xw, int ldx, int xcoff,
