@@ -38,7 +38,7 @@ constexpr int NDMA = (XP * 32 + 1023) / 1024;
 constexpr int DPW = (NDMA + 3) / 4;       // DMA instructions per wave (padded, see block.hip)
 constexpr int XBUF = NDMA * 1024;
 constexpr int STB = NG * 16 * 128;        // stem tile image: 304 rows x 64 channels bf16
-constexpr int VMCNT0 = 0x0F70;
+constexpr int VMCNT2 = 0x0F72;            // s_waitcnt vmcnt(2) (expcnt / lgkmcnt: no wait)
 
 __device__ __forceinline__ int st_off(int row, int chunk) {
     return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
@@ -124,7 +124,9 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemPoolArgs a) {
         const int ty = r0 / tpc, tx = r0 - ty * tpc;
         const int sy0 = 2 * PT * ty - 1, sx0 = 2 * PT * tx - 1;   // stem origin of the tile
         const char* lxc = lx + buf * XBUF;
-        __builtin_amdgcn_s_waitcnt(VMCNT0);                         // this tile's X' (DMA)
+        // this tile's X' (DMA): vmcnt counts loads, stores and LDS-DMA together in issue
+        // order, and the previous tile's 2 stores per thread are the only younger ops
+        __builtin_amdgcn_s_waitcnt(VMCNT2);
         __syncthreads();
         if (t + tstep < tend) issue_x(t + tstep, buf ^ 1);          // no register loads follow
         int li = li0, g = g0;
@@ -161,7 +163,10 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemPoolArgs a) {
 
         // ---- stage B: 3x3/2 max pool of the tile, 8 channels per thread ----
         {
-            __bf16* yb = (__bf16*)a.y + (size_t)b * a.ph * a.pw * 64;
+            // stores through a descriptor, unconditional (past the frame: out-of-range
+            // offset, dropped) so every thread issues exactly 2 per tile (see vmcnt above)
+            const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)((__bf16*)a.y + (size_t)b * a.ph * a.pw * 64), 0, (int)((size_t)a.ph * a.pw * 128), 0x00020000);
 #pragma unroll
             for (int pass = 0; pass < 2; ++pass) {
                 const int q = pass * 32 + (tid >> 3), ch = tid & 7;
@@ -176,7 +181,8 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemPoolArgs a) {
                         for (int e = 0; e < 4; ++e) m[e] = max_bf16x2(m[e], v[e]);
                     }
                 const int py = PT * ty + pi, px = PT * tx + pj;
-                if (py < a.ph && px < a.pw) *(u32x4*)(yb + ((size_t)py * a.pw + px) * 64 + 8 * ch) = m;
+                const unsigned off = py < a.ph && px < a.pw ? (unsigned)(((py * a.pw + px) * 64 + 8 * ch) * 2) : 0x80000000u;
+                __builtin_amdgcn_raw_buffer_store_b128(m, ry, off, 0, 0);
             }
         }
         buf ^= 1;
@@ -190,7 +196,7 @@ bool vd_stem_pool_ok(int xh, int xw, int ph, int pw) {
     if (e && atoi(e) == 0) return false;
     const int sh = xh - 1, sw = xw - 1;
     return xh >= 2 && xw >= 2 && ph == (sh - 1) / 2 + 1 && pw == (sw - 1) / 2 + 1 &&
-           (double)xh * xw * 16 * 2 < 2147483647.0;
+           (double)xh * xw * 16 * 2 < 2147483647.0 && (double)ph * pw * 128 < 2147483647.0;
 }
 
 hipError_t vd_launch_stem_pool(const StemPoolArgs& a, hipStream_t s) {
