@@ -9,7 +9,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 STEPS=("$@")
 [ ${#STEPS[@]} -eq 0 ] && STEPS=(tests smoke bench)
-BENCH_ARGS=${BENCH_ARGS:-"--steps 10 --warmup 3"}
+BENCH_ARGS=${BENCH_ARGS:-"--steps 20 --warmup 3"}
 PROF_ARGS=${PROF_ARGS:-"--steps 5 --warmup 2 --no-cpu-baseline"}
 PMC_ARGS=${PMC_ARGS:-"--steps 3 --warmup 1 --no-cpu-baseline --no-timing"}
 PYTEST_ARGS=${PYTEST_ARGS:-"tests -m gpu -x -q"}

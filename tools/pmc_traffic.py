@@ -35,7 +35,7 @@ def main(fetch_dir, write_dir, out=None):
     f_kib, nf = per_launch(fetch_dir, "FETCH_SIZE")
     w_kib, nw = per_launch(write_dir, "WRITE_SIZE")
     res = {
-        "kernel": "RetinaFace conv launches (conv_igemm / conv1x1_stream / conv_big), face stream",
+        "kernel": "RetinaFace conv launches (stem_pool / bottleneck / conv_big / conv_igemm / conv1x1_stream), face stream",
         "launches": {"fetch_pass": nf, "write_pass": nw},
         "fetch_size_kib_per_launch": round(f_kib, 1),
         "write_size_kib_per_launch": round(w_kib, 1),
