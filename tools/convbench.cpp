@@ -128,8 +128,43 @@ static void run_block(int reps, int B, int H, int W, int cin, bool ds) {
     }
 }
 
+// fused stem + maxpool (stem.hip) on random bf16 data: B x 321 x 321 x 16 -> B x 160 x 160 x 64
+static void run_stem(int reps, int B) {
+    const int xh = 321, xw = 321, ph = 160, pw = 160;
+    std::vector<uint16_t> hx((size_t)B * xh * xw * 16), hw(4 * 8 * 64 * 8);
+    uint32_t st = 99u;
+    for (auto& v : hx) { st = st * 1664525u + 1013904223u; v = f2bf(((st >> 8) & 0xffff) / 65536.0f); }
+    for (auto& v : hw) { st = st * 1664525u + 1013904223u; v = f2bf((((st >> 8) & 0xffff) / 32768.0f - 1.0f) * 0.1f); }
+    StemPoolArgs a{};
+    void *dx, *dy, *dw;
+    float *dsc, *dsh;
+    CK(hipMalloc(&dx, hx.size() * 2)); CK(hipMalloc(&dy, (size_t)B * ph * pw * 64 * 2)); CK(hipMalloc(&dw, hw.size() * 2));
+    CK(hipMalloc(&dsc, 64 * 4)); CK(hipMalloc(&dsh, 64 * 4));
+    CK(hipMemcpy(dx, hx.data(), hx.size() * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dw, hw.data(), hw.size() * 2, hipMemcpyHostToDevice));
+    std::vector<float> one(64, 1.0f), zero(64, 0.0f);
+    CK(hipMemcpy(dsc, one.data(), 256, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dsh, zero.data(), 256, hipMemcpyHostToDevice));
+    a.x = dx; a.B = B; a.xh = xh; a.xw = xw; a.y = dy; a.ph = ph; a.pw = pw; a.wf = dw; a.scale = dsc; a.shift = dsh;
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+    for (int i = 0; i < 3; ++i) CK(vd_launch_stem_pool(a, 0));
+    CK(hipEventRecord(e0, 0));
+    for (int i = 0; i < reps; ++i) CK(vd_launch_stem_pool(a, 0));
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    const double us = ms * 1e3 / reps, fl = 2.0 * B * 320.0 * 320 * 64 * 147;
+    printf("stem+pool B=%d  %8.1f us  %7.1f TF/s (147-term)\n", B, us, fl / us * 1e-6);
+}
+
 int main(int argc, char** argv) {
     const int reps = argc > 1 ? atoi(argv[1]) : 20;
+    if (argc == 3 && std::string(argv[2]) == "stem") {
+        run_stem(reps, 64);
+        return 0;
+    }
     if (argc == 3 && std::string(argv[2]) == "block") {
         run_block(reps, 64, 160, 160, 64, true);
         run_block(reps, 64, 160, 160, 256, false);

@@ -10,8 +10,8 @@
 // map of a 640x640 batch (839 MB at B = 64) is never written or read back.
 //
 // Persistent workgroups of 4 waves walk 8x8 tiles of pool outputs:
-//   - the 20x20 X' tile (13 KB) arrives by LDS-DMA, double-buffered: the next tile's
-//     is in flight while this one computes;
+//   - the 20x20 X' tile (13 KB) arrives by LDS-DMA; the next tile's is issued as
+//     soon as stage A is done with the buffer (or, double-buffered, at the top);
 //   - stage A: the 17x17 stem outputs under the pool windows (19 groups of 16
 //     pixels) as D^T = W . X^T with v_mfma_f32_16x16x32_bf16; wave w holds the
 //     weight fragments of channels 32(w&1) .. +32 in VGPRs for good and takes every
@@ -55,10 +55,11 @@ __device__ __forceinline__ unsigned max_bf16x2(unsigned a, unsigned b) {   // no
     return lo | (hi << 16);
 }
 
+template <int NXB>   // X' tile buffers: 2 = next tile's DMA overlaps this tile, 1 = more workgroups per CU
 __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemPoolArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    char* lx = smem;                       // 2 x XBUF
-    char* lst = smem + 2 * XBUF;           // STB
+    char* lx = smem;                       // NXB x XBUF
+    char* lst = smem + NXB * XBUF;         // STB
     char* lscratch = lst + STB;            // 1 KB sink of the padding DMA slots
 
     const int tid = threadIdx.x, lane = tid & 63, li0 = lane & 15, g0 = lane >> 4;
@@ -128,7 +129,7 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemPoolArgs a) {
         // order, and the previous tile's 2 stores per thread are the only younger ops
         __builtin_amdgcn_s_waitcnt(VMCNT2);
         __syncthreads();
-        if (t + tstep < tend) issue_x(t + tstep, buf ^ 1);          // no register loads follow
+        if (NXB == 2 && t + tstep < tend) issue_x(t + tstep, buf ^ 1);   // no register loads follow
         int li = li0, g = g0;
         asm volatile("" : "+v"(li), "+v"(g));
 
@@ -160,6 +161,7 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemPoolArgs a) {
             *(bf16x8_t*)(lst + st_off(p, 4 * np + g)) = o;
         }
         __syncthreads();
+        if (NXB == 1 && t + tstep < tend) issue_x(t + tstep, 0);   // X' buffer free once stage A is done
 
         // ---- stage B: 3x3/2 max pool of the tile, 8 channels per thread ----
         {
@@ -185,8 +187,26 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemPoolArgs a) {
                 __builtin_amdgcn_raw_buffer_store_b128(m, ry, off, 0, 0);
             }
         }
-        buf ^= 1;
+        if (NXB == 2) buf ^= 1;
     }
+}
+
+template <int NXB>
+hipError_t launch_stem(const StemPoolArgs& a, hipStream_t s) {
+    constexpr size_t lds = NXB * XBUF + STB + 1024;
+    static const int cus = [] {
+        (void)hipFuncSetAttribute((const void*)stem_pool_kernel<NXB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+        int dev = 0, n = 256;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        return n > 0 ? n : 256;
+    }();
+    const int per_cu = NXB == 2 ? 2 : 3;                 // LDS: 66 KB / 53 KB per workgroup
+    const int tiles = a.B * ((a.ph + PT - 1) / PT) * ((a.pw + PT - 1) / PT);
+    const int grid = tiles < per_cu * cus ? tiles : per_cu * cus;   // persistent
+    hipLaunchKernelGGL(stem_pool_kernel<NXB>, dim3(grid), dim3(256), lds, s, a);
+    return hipGetLastError();
 }
 
 }  // namespace
@@ -201,17 +221,12 @@ bool vd_stem_pool_ok(int xh, int xw, int ph, int pw) {
 
 hipError_t vd_launch_stem_pool(const StemPoolArgs& a, hipStream_t s) {
     if (a.B <= 0) return hipSuccess;
-    constexpr size_t lds = 2 * XBUF + STB + 1024;
-    static const int cus = [] {
-        (void)hipFuncSetAttribute((const void*)stem_pool_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds);
-        int dev = 0, n = 256;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-        return n > 0 ? n : 256;
+    // one X' buffer and three workgroups per CU measured 9 % faster than two buffers
+    // (DMA overlapping the whole tile) at two workgroups per CU: the kernel is
+    // latency-bound, occupancy wins (VD_STEM_NXB=2 selects the other form)
+    static const int nxb = [] {
+        const char* e = getenv("VD_STEM_NXB");
+        return e && atoi(e) == 2 ? 2 : 1;
     }();
-    const int tiles = a.B * ((a.ph + PT - 1) / PT) * ((a.pw + PT - 1) / PT);
-    const int grid = tiles < 2 * cus ? tiles : 2 * cus;   // persistent, two workgroups per CU
-    hipLaunchKernelGGL(stem_pool_kernel, dim3(grid), dim3(256), lds, s, a);
-    return hipGetLastError();
+    return nxb == 1 ? launch_stem<1>(a, s) : launch_stem<2>(a, s);
 }
