@@ -95,6 +95,103 @@ __global__ __launch_bounds__(256) void letterbox_s2d_kernel(LetterboxArgs a) {
     *(uint4*)(out + 8) = *(const uint4*)(t + 8);
 }
 
+// Space-to-depth form with the source rows staged in LDS: one workgroup per
+// (frame, X' row Y) loads the <= 4 source rows its two canvas rows interpolate from
+// with 16-B loads (only rows some output reads: 2 of every 3 at 1080p -> 360), then
+// every 2x2 block is computed from LDS. Same arithmetic as resized_px3 / canvas_px.
+constexpr int LB_LDS_MAX = 16384;   // max bytes per staged source row (frames up to 5461 px wide)
+
+__device__ __forceinline__ void lb_src_rows(const LetterboxArgs& a, int y, int* r0, int* r1, Tap* ty, bool* inside) {
+    const int ry = y - a.top;
+    *inside = (unsigned)y < (unsigned)a.oh && (unsigned)ry < (unsigned)a.nh;
+    *r0 = *r1 = -1;
+    if (!*inside) return;
+    if (a.mode == LB_COPY) { *r0 = *r1 = ry; return; }
+    if (a.mode == LB_AREA2) { *r0 = 2 * ry; *r1 = 2 * ry + 1; return; }
+    *ty = linear_tap(ry, a.ih, a.scale_y);
+    *r0 = ty->s0;
+    *r1 = ty->s1;
+}
+
+__device__ __forceinline__ void lb_px_lds(const LetterboxArgs& a, const uint8_t* L0, const uint8_t* L1, const Tap& ty,
+                                          int x, bool row_in, float v[3]) {
+    const int rx = x - a.left;
+    const bool inside = row_in && (unsigned)rx < (unsigned)a.nw;
+    int p3[3] = {0, 0, 0};
+    if (inside) {
+        if (a.mode == LB_COPY) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) p3[c] = L0[rx * 3 + c];
+        } else if (a.mode == LB_AREA2) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+                p3[c] = (L0[6 * rx + c] + L0[6 * rx + c + 3] + L1[6 * rx + c] + L1[6 * rx + c + 3] + 2) >> 2;
+        } else {
+            const Tap tx = linear_tap(rx, a.iw, a.scale_x);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const int d0 = L0[tx.s0 * 3 + c] * tx.a0 + L0[tx.s1 * 3 + c] * tx.a1;
+                const int d1 = L1[tx.s0 * 3 + c] * tx.a0 + L1[tx.s1 * 3 + c] * tx.a1;
+                const int q = ((((d0 >> 4) * ty.a0) >> 16) + (((d1 >> 4) * ty.a1) >> 16) + 2) >> 2;
+                p3[c] = q < 0 ? 0 : (q > 255 ? 255 : q);
+            }
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const int pv = a.flip ? p3[2 - c] : p3[c];
+        const float px = inside ? (float)pv : a.pad_value;
+        v[c] = VD_FDIV(VD_FSUB(px, a.mean[c]), a.div);
+    }
+}
+
+__global__ __launch_bounds__(256) void letterbox_s2d_lds_kernel(LetterboxArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lrow[];   // 4 staged rows of RS bytes
+    const int Y = blockIdx.x, f = blockIdx.y;
+    const int OW = a.ow / 2 + 1, OH = a.oh / 2 + 1;
+    const uint8_t* img = a.src + (size_t)f * a.ih * a.pitch;
+    int rows[4];
+    Tap ty[2];
+    bool rin[2];
+    lb_src_rows(a, 2 * Y - 1, &rows[0], &rows[1], &ty[0], &rin[0]);
+    lb_src_rows(a, 2 * Y, &rows[2], &rows[3], &ty[1], &rin[1]);
+    const int rb = a.iw * 3;
+    const int nch = (rb + 15) / 16;
+    const int RS = nch * 16;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (rows[k] < 0) continue;
+        const uint8_t* src = img + (size_t)rows[k] * a.pitch;
+        uint8_t* dst = lrow + k * RS;
+        if (((uintptr_t)src & 15) == 0) {
+            for (int i = threadIdx.x; i < nch; i += 256) {
+                if (16 * i + 16 <= rb) *(uint4*)(dst + 16 * i) = *(const uint4*)(src + 16 * i);
+                else for (int b = 16 * i; b < rb; ++b) dst[b] = src[b];
+            }
+        } else {
+            for (int i = threadIdx.x; i < rb; i += 256) dst[i] = src[i];
+        }
+    }
+    __syncthreads();
+    for (int X = threadIdx.x; X < OW; X += 256) {
+        __bf16 t[16];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int h = s >> 1;
+            const int x = 2 * X + (s & 1) - 1;
+            float v[3] = {0.f, 0.f, 0.f};   // conv zero padding outside the canvas
+            const int y = 2 * Y + h - 1;
+            if ((unsigned)y < (unsigned)a.oh && (unsigned)x < (unsigned)a.ow)
+                lb_px_lds(a, lrow + (2 * h) * RS, lrow + (2 * h + 1) * RS, ty[h], x, rin[h], v);
+            t[4 * s + 0] = (__bf16)v[0]; t[4 * s + 1] = (__bf16)v[1]; t[4 * s + 2] = (__bf16)v[2];
+            t[4 * s + 3] = (__bf16)0.f;
+        }
+        __bf16* out = (__bf16*)a.out + (((size_t)f * OH + Y) * OW + X) * 16;
+        *(uint4*)out = *(const uint4*)t;
+        *(uint4*)(out + 8) = *(const uint4*)(t + 8);
+    }
+}
+
 __global__ __launch_bounds__(256) void letterbox_kernel(LetterboxArgs a) {
     const int x = blockIdx.x * 256 + threadIdx.x;
     const int y = blockIdx.y;
@@ -175,6 +272,18 @@ __global__ __launch_bounds__(256) void upsample2x_kernel(const T* x, int xh, int
 }  // namespace
 
 hipError_t vd_launch_letterbox(const LetterboxArgs& a, hipStream_t s) {
+    if (a.s2d && a.iw * 3 <= LB_LDS_MAX) {
+        static const bool attr = [] {
+            (void)hipFuncSetAttribute((const void*)letterbox_s2d_lds_kernel,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 4 * LB_LDS_MAX);
+            return true;
+        }();
+        (void)attr;
+        const size_t lds = 4 * (size_t)((a.iw * 3 + 15) / 16 * 16);
+        dim3 grid(a.oh / 2 + 1, a.n);
+        hipLaunchKernelGGL(letterbox_s2d_lds_kernel, grid, dim3(256), lds, s, a);
+        return hipGetLastError();
+    }
     if (a.s2d) {
         dim3 grid((a.ow / 2 + 1 + 255) / 256, a.oh / 2 + 1, a.n);
         hipLaunchKernelGGL(letterbox_s2d_kernel, grid, dim3(256), 0, s, a);
