@@ -638,9 +638,10 @@ bool vd_conv_big_ok(const ConvArgs& a) {
     const char* e = getenv("VD_CONV_BIG");   // read per call: tests lower it to reach small shapes
     const int min_tiles = e ? atoi(e) : 100;
     if (min_tiles <= 0 || a.out_f32) return false;
-    // measured (tools/conv_layers.py A/B): ahead of the 128x128 GEMM only with long K loops
+    // measured (tools/convbench): at K = 512 ahead of the 128x128 GEMM by 14 % on the
+    // 409600 x 256 layers (layer3.0 conv1, FPN output1), level on the 25600 x 2048 ones
     const char* ek = getenv("VD_CONV_BIG_KMIN");
-    const int kmin = ek ? atoi(ek) : 1024;
+    const int kmin = ek ? atoi(ek) : 512;
     if ((a.cin_pad % 64) != 0 || (a.cout % 256) != 0 || a.kpad / 64 < 2 || a.kpad < kmin) return false;
     if (((a.ldy | a.ycoff) & 7) || ((a.ldx | a.xcoff) & 7)) return false;
     if (a.res_mode != VD_RES_NONE && ((a.res_ld | a.res_coff) & 7)) return false;
