@@ -58,7 +58,7 @@ def main(path, B=64):
     conv_keys = ("conv_igemm", "conv1x1_stream", "conv_big", "bottleneck_kernel", "stem_pool_kernel")
     if not any("bottleneck_kernel" in r["Kernel_Name"] for r in allk):
         plan = face_plan(B, block=False)
-    li = max(i for i, r in enumerate(allk) if "letterbox_s2d_kernel" in r["Kernel_Name"]
+    li = max(i for i, r in enumerate(allk) if "letterbox_s2d" in r["Kernel_Name"]
              or ("letterbox_kernel" in r["Kernel_Name"] and int(r["Grid_Size_Y"]) == 640))
     stream = allk[li]["Stream_Id"]
     last = [r for r in allk[li:] if r["Stream_Id"] == stream and any(k in r["Kernel_Name"] for k in conv_keys)]

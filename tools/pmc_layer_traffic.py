@@ -22,7 +22,7 @@ def last_step(d, counter):
     for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
         if r["Counter_Name"] == counter:
             vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
-    li = max(i for i, r in enumerate(trace) if "letterbox_s2d_kernel" in r["Kernel_Name"])
+    li = max(i for i, r in enumerate(trace) if "letterbox_s2d" in r["Kernel_Name"])
     stream = trace[li]["Stream_Id"]
     rows = [r for r in trace[li:] if r["Stream_Id"] == stream and any(k in r["Kernel_Name"] for k in KEYS)]
     return [(vals.get(r["Dispatch_Id"], 0.0), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3)

@@ -13,7 +13,7 @@ import sys
 
 FAMILIES = [("conv", ("conv_igemm_kernel", "conv1x1_stream_kernel", "conv_big_kernel", "bottleneck_kernel",
                        "stem_pool_kernel")),
-            ("mosaic", ("mosaic_",)), ("letterbox", ("letterbox_kernel", "letterbox_s2d_kernel")),
+            ("mosaic", ("mosaic_",)), ("letterbox", ("letterbox_kernel", "letterbox_s2d")),
             ("post", ("candidates_kernel", "nms_kernel")), ("other", ("maxpool", "upsample"))]
 CONV = FAMILIES[0][1]
 
@@ -25,7 +25,7 @@ def family(name):
 def face_stream(rows):
     """Stream id(s) of the RetinaFace branch: the stream of the face letterbox
     (space-to-depth form in bf16, the 640-row canvas in fp32)."""
-    face = {r["Stream_Id"] for r in rows if "letterbox_s2d_kernel" in r["Kernel_Name"]}
+    face = {r["Stream_Id"] for r in rows if "letterbox_s2d" in r["Kernel_Name"]}
     if not face:
         face = {r["Stream_Id"] for r in rows if "letterbox_kernel" in r["Kernel_Name"] and r["Grid_Size_Y"] == "640"}
     return face
