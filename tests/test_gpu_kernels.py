@@ -132,12 +132,23 @@ CONV_CASES = [
 ]
 
 
-@pytest.mark.parametrize("prec", ["fp32", "bf16", "bf16-gemm64", "bf16-gemm128", "bf16-gemm256"])
+@pytest.mark.parametrize("prec", ["fp32", "bf16", "bf16-gemm64", "bf16-gemm128", "bf16-gemm256", "bf16-persist64",
+                                  "bf16-persist128"])
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv_matches_torch(gpu, face_ctx_factory, monkeypatch, prec, case):
-    """bf16: the default dispatch (streaming 1x1 / streaming taps / GEMM); bf16-gemm64 and
-    bf16-gemm128: the implicit-GEMM kernel with 64- and 128-row tiles."""
+    """bf16: the default dispatch (streaming 1x1 / streaming taps / persistent GEMM / GEMM);
+    bf16-gemm64 / -gemm128: the one-tile-per-workgroup implicit GEMM with 64- and 128-row
+    tiles; bf16-persist64 / -persist128: the persistent implicit GEMM (conv_persist.hip,
+    any K, dense taps only -- other shapes fall through to the GEMM)."""
+    if prec.startswith("bf16-persist"):
+        monkeypatch.setenv("VD_CONV_TAPS", "0")
+        monkeypatch.setenv("VD_CONV_STREAM", "0")
+        monkeypatch.setenv("VD_CONV_BIG", "0")
+        monkeypatch.setenv("VD_CONV_PERSIST", "1000")
+        monkeypatch.setenv("VD_CONV_PERSIST_SMALL", "100000000" if prec == "bf16-persist64" else "0")
+        prec = "bf16"
     if prec.startswith("bf16-gemm"):
+        monkeypatch.setenv("VD_CONV_PERSIST", "0")
         monkeypatch.setenv("VD_CONV_TAPS", "0")
         monkeypatch.setenv("VD_CONV_STREAM", "0")
         monkeypatch.setenv("VD_CONV_SMALL", "100000000" if prec == "bf16-gemm64" else "0")

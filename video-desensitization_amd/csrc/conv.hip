@@ -441,6 +441,7 @@ hipError_t vd_launch_conv(const ConvArgs& a, bool f32, hipStream_t s) {
     if (!f32 && vd_conv_big_ok(a)) return vd_launch_conv_big(a, s);
     if (!f32 && vd_conv_big128_ok(a)) return vd_launch_conv_big128(a, s);
     if (!f32 && vd_conv_taps_ok(a)) return vd_launch_conv_taps(a, s);
+    if (!f32 && dense && vd_conv_persist_ok(a)) return vd_launch_conv_persist(a, s);
     if (f32) {
         if (a.cout <= 32) return launch_bn<float, 128, 32>(a, dense, s);
         if (a.cout <= 64) return launch_bn<float, 128, 64>(a, dense, s);

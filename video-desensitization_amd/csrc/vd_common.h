@@ -124,6 +124,8 @@ bool vd_conv_taps_ok(const ConvArgs& a);
 bool vd_conv1x1_dual_ok(const ConvArgs& a);
 hipError_t vd_launch_conv_taps(const ConvArgs& a, hipStream_t s);
 hipError_t vd_launch_conv(const ConvArgs& a, bool f32, hipStream_t s);
+bool vd_conv_persist_ok(const ConvArgs& a);
+hipError_t vd_launch_conv_persist(const ConvArgs& a, hipStream_t s);
 bool vd_block_ok(int cin, bool ds, int h, int w);
 bool vd_stem_pool_ok(int xh, int xw, int ph, int pw);
 hipError_t vd_launch_stem_pool(const StemPoolArgs& a, hipStream_t s);
