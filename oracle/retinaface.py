@@ -169,10 +169,50 @@ class RetinaFaceR50(nn.Module):
         return loc, F.softmax(cls, dim=-1), ldm
 
 
+def _dw(inp, oup, stride):                             # mobilenet025.py:10-19 (conv_dw)
+    return nn.Sequential(nn.Conv2d(inp, inp, 3, stride, 1, groups=inp, bias=False), nn.BatchNorm2d(inp),
+                         nn.LeakyReLU(negative_slope=0.1, inplace=True),
+                         nn.Conv2d(inp, oup, 1, 1, 0, bias=False), nn.BatchNorm2d(oup),
+                         nn.LeakyReLU(negative_slope=0.1, inplace=True))
+
+
+class MobileNetV1Body(nn.Module):
+    """mobilenet025.py:21-48 up to stage3, returning stage1/2/3 (cfg_mnet
+    return_layers, config.py:1-16): 64/128/256 channels at strides 8/16/32."""
+
+    def __init__(self):
+        super().__init__()
+        self.stage1 = nn.Sequential(conv_bn(3, 8, 2, leaky=0.1), _dw(8, 16, 1), _dw(16, 32, 2), _dw(32, 32, 1),
+                                    _dw(32, 64, 2), _dw(64, 64, 1))
+        self.stage2 = nn.Sequential(_dw(64, 128, 2), *[_dw(128, 128, 1) for _ in range(5)])
+        self.stage3 = nn.Sequential(_dw(128, 256, 2), _dw(256, 256, 1))
+
+    def forward(self, x):
+        s1 = self.stage1(x)
+        s2 = self.stage2(s1)
+        return [s1, s2, self.stage3(s2)]
+
+
+class RetinaFaceMnet(RetinaFaceR50):
+    """retinaface.py:53-148 with cfg_mnet (in_channel 32, out_channel 64)."""
+
+    def __init__(self):
+        nn.Module.__init__(self)
+        self.body = MobileNetV1Body()
+        self.fpn = FPN([64, 128, 256], 64)
+        self.ssh1 = SSH(64, 64)
+        self.ssh2 = SSH(64, 64)
+        self.ssh3 = SSH(64, 64)
+        self.ClassHead = nn.ModuleList([_Head(64, 4) for _ in range(3)])
+        self.BboxHead = nn.ModuleList([_Head(64, 8) for _ in range(3)])
+        self.LandmarkHead = nn.ModuleList([_Head(64, 20) for _ in range(3)])
+
+
 def build_oracle_model(state_dict):
     """Instantiate the oracle network from a reference-keyed state_dict
-    (numpy arrays or tensors)."""
-    m = RetinaFaceR50().eval()
+    (numpy arrays or tensors); body.stage1.* keys select the MobileNet-0.25
+    model (the reference's backbone="mobilenet", retinaface.py:60)."""
+    m = (RetinaFaceMnet() if "body.stage1.0.0.weight" in state_dict else RetinaFaceR50()).eval()
     sd = {k: torch.as_tensor(v) for k, v in state_dict.items()}
     missing, unexpected = m.load_state_dict(sd, strict=False)
     missing = [k for k in missing if not k.endswith("num_batches_tracked")]

@@ -67,6 +67,8 @@ def face_weights(kind="default"):
             _W[kind] = weights.retinaface_state_dict(0)
         elif kind == "dense":      # thousands of candidates per frame: stresses sort/NMS paths
             _W[kind] = weights.retinaface_state_dict(0, cls_bias={0: -2.0, 1: -1.0, 2: 0.5})
+        elif kind == "mnet":       # backbone="mobilenet" (cfg_mnet)
+            _W[kind] = weights.retinaface_mnet_state_dict(0)
         else:
             raise KeyError(kind)
     return _W[kind]

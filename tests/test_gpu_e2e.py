@@ -49,20 +49,22 @@ def _rel(a, b):
     return np.abs(a - b).max() / (np.abs(b).max() + 1e-12)
 
 
-@pytest.mark.parametrize("h,w", [(1080, 1920), (720, 1280)])
-def test_heads_fp32_match_oracle(gpu, face_ctx_factory, h, w):
-    ctx = face_ctx_factory("fp32", 8)
+@pytest.mark.parametrize("h,w,wkind", [(1080, 1920, "default"), (720, 1280, "default"), (1080, 1920, "mnet"),
+                                        (720, 1280, "mnet")])
+def test_heads_fp32_match_oracle(gpu, face_ctx_factory, h, w, wkind):
+    ctx = face_ctx_factory("fp32", 8, wkind)
     fr = _frames(2, h, w)
     loc, conf, ldm = ctx.forward_heads(fr)
-    eloc, econf, eldm = _oracle_heads(fr)
+    eloc, econf, eldm = _oracle_heads(fr, wkind)
     assert _rel(loc, eloc) < 1e-4 and _rel(conf, econf) < 1e-4 and _rel(ldm, eldm) < 1e-4
 
 
-def test_heads_bf16_close(gpu, face_ctx_factory):
-    ctx = face_ctx_factory("bf16", 8)
+@pytest.mark.parametrize("wkind", ["default", "mnet"])
+def test_heads_bf16_close(gpu, face_ctx_factory, wkind):
+    ctx = face_ctx_factory("bf16", 8, wkind)
     fr = _frames(2, 1080, 1920)
     loc, conf, _ = ctx.forward_heads(fr)
-    eloc, econf, _ = _oracle_heads(fr)
+    eloc, econf, _ = _oracle_heads(fr, wkind)
     assert _rel(loc, eloc) < 6e-2 and _rel(conf, econf) < 6e-2
 
 
@@ -143,11 +145,12 @@ def _near_decision(conf_b, boxes_norm, thr=0.5, iou=0.4, eps=1e-4):
     return near
 
 
-def test_detect_fp32_matches_oracle(gpu, face_ctx_factory):
-    ctx = face_ctx_factory("fp32", 8)
+@pytest.mark.parametrize("wkind", ["default", "mnet"])
+def test_detect_fp32_matches_oracle(gpu, face_ctx_factory, wkind):
+    ctx = face_ctx_factory("fp32", 8, wkind)
     fr = _frames(3, 1080, 1920, seed=2)
     got = ctx.detect(fr)
-    eloc, econf, _ = _oracle_heads(fr)
+    eloc, econf, _ = _oracle_heads(fr, wkind)
     pri = oanchors.get_anchors((640, 640))
     exact = 0
     for b in range(3):
@@ -176,11 +179,12 @@ def test_process_mosaic_exact_given_boxes(gpu, face_ctx_factory):
         assert int(faces.count.sum()) > 0
 
 
-def test_detect_bf16_agrees(gpu, face_ctx_factory):
-    ctx = face_ctx_factory("bf16", 8)
+@pytest.mark.parametrize("wkind", ["default", "mnet"])
+def test_detect_bf16_agrees(gpu, face_ctx_factory, wkind):
+    ctx = face_ctx_factory("bf16", 8, wkind)
     fr = _frames(2, 1080, 1920)
     got = ctx.detect(fr)
-    eloc, econf, _ = _oracle_heads(fr)
+    eloc, econf, _ = _oracle_heads(fr, wkind)
     pri = oanchors.get_anchors((640, 640))
     matched = total = 0
     for b in range(2):
@@ -211,6 +215,19 @@ def test_retinaface_drop_in(gpu):
         assert img is src
         assert isinstance(boxes, list) and all(len(b) == 4 and isinstance(b[0], float) for b in boxes)
     # int() of the returned floats == the library's int boxes
+    raw = det.detect_boxes(imgs)
+    for (_, boxes), (xf, xi, _) in zip(res, raw):
+        assert [[int(v) for v in b] for b in boxes] == xi.tolist()
+
+
+def test_retinaface_drop_in_mobilenet(gpu):
+    """Retinaface(backbone="mobilenet") (face.py:35) on seeded random cfg_mnet weights."""
+    from vdmi import Retinaface
+    det = Retinaface(model_path="/nonexistent.pth", backbone="mobilenet", input_shape=[640, 640, 3],
+                     nms_iou=0.4, precision="fp32", max_batch=4, weights=face_weights("mnet"))
+    imgs = list(_frames(2, 720, 1280, seed=9))
+    res = det.detect_images(imgs)
+    assert len(res) == 2 and sum(len(b) for _, b in res) > 0
     raw = det.detect_boxes(imgs)
     for (_, boxes), (xf, xi, _) in zip(res, raw):
         assert [[int(v) for v in b] for b in boxes] == xi.tolist()

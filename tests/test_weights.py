@@ -2,7 +2,7 @@
 import numpy as np
 import torch
 
-from oracle.retinaface import RetinaFaceR50, build_oracle_model
+from oracle.retinaface import RetinaFaceMnet, RetinaFaceR50, build_oracle_model
 
 
 def test_retinaface_keys_match_reference_module_tree():
@@ -19,6 +19,27 @@ def test_retinaface_keys_match_reference_module_tree():
               "ssh3.conv7x7_3.1.bias", "ClassHead.0.conv1x1.weight", "LandmarkHead.2.conv1x1.bias"):
         assert k in sd
     assert sum(v.size for k, v in sd.items() if k.endswith("weight") and v.ndim == 4) > 27e6
+
+
+def test_retinaface_mnet_keys_match_reference_module_tree():
+    """backbone="mobilenet": MobileNetV1 stage1..3 (mobilenet025.py:21-48) + FPN/SSH/heads at 64."""
+    from vdmi import weights
+    sd = weights.retinaface_mnet_state_dict(0)
+    ref = {k: tuple(v.shape) for k, v in RetinaFaceMnet().state_dict().items()
+           if not k.endswith("num_batches_tracked")}
+    assert set(sd) == set(ref)
+    for k, v in sd.items():
+        assert v.shape == ref[k], k
+    for k, shape in (("body.stage1.0.0.weight", (8, 3, 3, 3)), ("body.stage1.1.0.weight", (8, 1, 3, 3)),
+                     ("body.stage1.5.4.running_var", (64,)), ("body.stage2.0.3.weight", (128, 64, 1, 1)),
+                     ("body.stage3.1.3.weight", (256, 256, 1, 1)), ("fpn.output3.0.weight", (64, 256, 1, 1)),
+                     ("ssh1.conv5X5_1.0.weight", (16, 64, 3, 3)), ("ClassHead.2.conv1x1.weight", (4, 64, 1, 1))):
+        assert sd[k].shape == shape, k
+    m = build_oracle_model(sd)
+    assert isinstance(m, RetinaFaceMnet)
+    with torch.no_grad():
+        loc, conf, _ = m(torch.zeros(1, 3, 64, 64))
+    assert loc.shape == (1, 168, 4) and torch.allclose(conf.sum(-1), torch.ones(1, 168))
 
 
 def test_weights_deterministic_and_vdw_roundtrip():

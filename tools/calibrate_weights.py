@@ -1,4 +1,4 @@
-"""Calibrate the RetinaFace random-weight class head (vdmi.weights.CLS_*).
+"""Calibrate the RetinaFace random-weight class head (vdmi.weights.CLS_*, MNET_CLS_*).
 
 Runs the CPU oracle on a synthetic 1920x1080 frame with uncalibrated heads,
 measures the per-level distribution of the (class1 - class0) logit difference,
@@ -20,9 +20,10 @@ from oracle.retinaface import build_oracle_model  # noqa: E402
 from vdmi import synth, weights                   # noqa: E402
 
 
-def main(targets=(0.003, 0.001, 0.001), seed=0, frames=4):
+def main(targets=(0.003, 0.001, 0.001), seed=0, frames=4, mnet=False):
     torch.set_num_threads(os.cpu_count())
-    sd = weights.retinaface_state_dict(seed, cls_bias=0.0)
+    gen = weights.retinaface_mnet_state_dict if mnet else weights.retinaface_state_dict
+    sd = gen(seed, cls_bias=0.0)
     m = build_oracle_model(sd)
     offs = [0, 12800, 16000, 16800]
     qs = [[] for _ in range(3)]
@@ -39,4 +40,4 @@ def main(targets=(0.003, 0.001, 0.001), seed=0, frames=4):
 
 
 if __name__ == "__main__":
-    main()
+    main(mnet="--mnet" in sys.argv)   # --mnet: the backbone="mobilenet" generator

@@ -66,6 +66,47 @@ int stem_s2d(Ctx& c, const WMap& W, int* idx) {
     *idx = (int)c.convs.size() - 1;
     return VD_OK;
 }
+// MobileNetV1-0.25 body (detect_face/nets/mobilenet025.py:21-48, cfg_mnet
+// return_layers stage1/2/3 -> 64/128/256 channels at strides 8/16/32): conv_bn(3, 8, 2)
+// then conv_dw blocks = depthwise 3x3 (+BN+LeakyReLU 0.1, dwconv.hip) and pointwise
+// 1x1 (+BN+LeakyReLU 0.1, the streaming 1x1 kernel). Keys: body.stageS.I.{0,1}
+// (conv_bn) and body.stageS.I.{0,1,3,4} (conv_dw: dw conv, bn, pw conv, bn).
+int build_mnet_body(Ctx& c, const WMap& W, FaceNet& F, Act feats[3]) {
+    constexpr float SLOPE = 0.1f;
+    int rc, ci;
+    const HT* w0 = find_t(W, "body.stage1.0.0.weight");
+    if (!w0 || w0->shape.size() != 4) return vd_set_error(VD_ERR_WEIGHTS, "missing body.stage1.0.0.weight");
+    if ((rc = c.make_conv_bn(W, "body.stage1.0.0.weight", "body.stage1.0.1", BN_EPS, 2, 1, VD_ACT_LEAKY, SLOPE, &ci)))
+        return rc;
+    Act x;
+    if ((rc = c.act(x, (F.input.h - 1) / 2 + 1, (F.input.w - 1) / 2 + 1, c.convs[ci].cout))) return rc;
+    if ((rc = c.add_conv(F.net, ci, F.input, 0, x, 0))) return rc;
+    F.net.stage_end[0] = (int)F.net.ops.size();
+    // (stage, number of modules, strides of the conv_dw modules)
+    const int nmod[3] = {6, 6, 2};
+    for (int st = 0; st < 3; ++st) {
+        for (int i = (st == 0 ? 1 : 0); i < nmod[st]; ++i) {
+            const std::string p = "body.stage" + std::to_string(st + 1) + "." + std::to_string(i);
+            const HT* pw = find_t(W, p + ".3.weight");
+            if (!pw || pw->shape.size() != 4) return vd_set_error(VD_ERR_WEIGHTS, "missing %s.3.weight", p.c_str());
+            // stride 2 on the first module of stage2/3 and on stage1 modules 2 and 4 (:29-33)
+            const int s = (st == 0 && (i == 2 || i == 4)) || (st > 0 && i == 0) ? 2 : 1;
+            int di, pi;
+            if ((rc = c.make_dwconv_bn(W, p + ".0.weight", p + ".1", BN_EPS, s, VD_ACT_LEAKY, SLOPE, &di))) return rc;
+            if ((rc = c.make_conv_bn(W, p + ".3.weight", p + ".4", BN_EPS, 1, 0, VD_ACT_LEAKY, SLOPE, &pi))) return rc;
+            Act t, y;
+            if ((rc = c.act(t, (x.h - 1) / s + 1, (x.w - 1) / s + 1, x.c))) return rc;
+            if ((rc = c.add_dwconv(F.net, di, x, t))) return rc;
+            if ((rc = c.act(y, t.h, t.w, c.convs[pi].cout))) return rc;
+            if ((rc = c.add_conv(F.net, pi, t, 0, y, 0))) return rc;
+            x = y;
+        }
+        feats[st] = x;
+        F.net.stage_end[st + 1] = (int)F.net.ops.size();
+    }
+    F.net.stage_end[4] = (int)F.net.ops.size();
+    return VD_OK;
+}
 }  // namespace
 
 int vd_build_face(Ctx& c, const WMap& W) {
@@ -75,11 +116,16 @@ int vd_build_face(Ctx& c, const WMap& W) {
     const int H = F.in_h, Wd = F.in_w;
     const int cpad = c.f32 ? 4 : 8;
     int rc;
-    F.s2d = !c.f32 && H % 2 == 0 && Wd % 2 == 0;
+    F.mnet = find_t(W, "body.stage1.0.0.weight") != nullptr;   // cfg_mnet (face.py:35, retinaface.py:60)
+    F.s2d = !c.f32 && !F.mnet && H % 2 == 0 && Wd % 2 == 0;
     if (F.s2d) rc = c.act(F.input, H / 2 + 1, Wd / 2 + 1, 16);
     else rc = c.act(F.input, H, Wd, cpad);
     if (rc) return rc;
 
+    Act feats[3];
+    if (F.mnet) {
+        if ((rc = build_mnet_body(c, W, F, feats))) return rc;
+    } else {
     // ---- stem: conv1 7x7/2 + bn1 + relu, maxpool 3x3/2 pad 1 ----
     int ci;
     if (F.s2d) rc = stem_s2d(c, W, &ci);
@@ -102,7 +148,6 @@ int vd_build_face(Ctx& c, const WMap& W) {
 
     // ---- layer1..4 (Bottleneck x [3,4,6,3]) ----
     Act x = pool;
-    Act feats[3];
     const int planes_l[4] = {64, 128, 256, 512}, blocks_l[4] = {3, 4, 6, 3}, stride_l[4] = {1, 2, 2, 2};
     for (int li = 0; li < 4; ++li) {
         const int planes = planes_l[li];
@@ -154,14 +199,22 @@ int vd_build_face(Ctx& c, const WMap& W) {
         if (li >= 1) feats[li - 1] = x;   // layer2/3/4 -> C3/C4/C5 (config.py:26)
         F.net.stage_end[li + 1] = (int)F.net.ops.size();
     }
+    }   // ResNet-50 body
 
     // ---- FPN ----
+    // leaky = 0.1 if out_channels <= 64 else 0 (layers.py:71): LeakyReLU(0.1) for
+    // cfg_mnet (64), ReLU for cfg_re50 (256)
+    const HT* fo = find_t(W, "fpn.output1.0.weight");
+    if (!fo || fo->shape.size() != 4) return vd_set_error(VD_ERR_WEIGHTS, "missing fpn.output1.0.weight");
+    const bool fleaky = fo->shape[0] <= 64;
+    const int fact = fleaky ? VD_ACT_LEAKY : VD_ACT_RELU;
+    const float fslope = fleaky ? 0.1f : 0.f;
     int o1c, o2c, o3c, m1c, m2c;
-    if ((rc = conv_bn(c, W, "fpn.output1.0.weight", "fpn.output1.1", 1, 0, VD_ACT_RELU, &o1c))) return rc;
-    if ((rc = conv_bn(c, W, "fpn.output2.0.weight", "fpn.output2.1", 1, 0, VD_ACT_RELU, &o2c))) return rc;
-    if ((rc = conv_bn(c, W, "fpn.output3.0.weight", "fpn.output3.1", 1, 0, VD_ACT_RELU, &o3c))) return rc;
-    if ((rc = conv_bn(c, W, "fpn.merge1.0.weight", "fpn.merge1.1", 1, 1, VD_ACT_RELU, &m1c))) return rc;
-    if ((rc = conv_bn(c, W, "fpn.merge2.0.weight", "fpn.merge2.1", 1, 1, VD_ACT_RELU, &m2c))) return rc;
+    if ((rc = c.make_conv_bn(W, "fpn.output1.0.weight", "fpn.output1.1", BN_EPS, 1, 0, fact, fslope, &o1c))) return rc;
+    if ((rc = c.make_conv_bn(W, "fpn.output2.0.weight", "fpn.output2.1", BN_EPS, 1, 0, fact, fslope, &o2c))) return rc;
+    if ((rc = c.make_conv_bn(W, "fpn.output3.0.weight", "fpn.output3.1", BN_EPS, 1, 0, fact, fslope, &o3c))) return rc;
+    if ((rc = c.make_conv_bn(W, "fpn.merge1.0.weight", "fpn.merge1.1", BN_EPS, 1, 1, fact, fslope, &m1c))) return rc;
+    if ((rc = c.make_conv_bn(W, "fpn.merge2.0.weight", "fpn.merge2.1", BN_EPS, 1, 1, fact, fslope, &m2c))) return rc;
     const int oc = c.convs[o1c].cout;
     Act o1, o2, o3, m1, m2;
     if ((rc = c.act(o3, feats[2].h, feats[2].w, oc))) return rc;
@@ -182,9 +235,19 @@ int vd_build_face(Ctx& c, const WMap& W) {
         const std::string pre = "ssh" + std::to_string(l + 1);
         int s3, s51, s52, s72, s73;
         if ((rc = conv_bn(c, W, pre + ".conv3X3.0.weight", pre + ".conv3X3.1", 1, 1, VD_ACT_RELU, &s3))) return rc;
-        if ((rc = conv_bn(c, W, pre + ".conv5X5_1.0.weight", pre + ".conv5X5_1.1", 1, 1, VD_ACT_RELU, &s51))) return rc;
+        // conv5X5_1 / conv7X7_2: LeakyReLU(leaky), leaky = 0.1 if out_channel <= 64 (layers.py:41);
+        // the three concat branches take the post-concat ReLU (layers.py:64-65)
+        const HT* s3w = find_t(W, pre + ".conv3X3.0.weight");
+        const bool sleaky = s3w && s3w->shape.size() == 4 && 2 * s3w->shape[0] <= 64;
+        const int sact = sleaky ? VD_ACT_LEAKY : VD_ACT_RELU;
+        const float sslope = sleaky ? 0.1f : 0.f;
+        if ((rc = c.make_conv_bn(W, pre + ".conv5X5_1.0.weight", pre + ".conv5X5_1.1", BN_EPS, 1, 1, sact, sslope,
+                                 &s51)))
+            return rc;
         if ((rc = conv_bn(c, W, pre + ".conv5X5_2.0.weight", pre + ".conv5X5_2.1", 1, 1, VD_ACT_RELU, &s52))) return rc;
-        if ((rc = conv_bn(c, W, pre + ".conv7X7_2.0.weight", pre + ".conv7X7_2.1", 1, 1, VD_ACT_RELU, &s72))) return rc;
+        if ((rc = c.make_conv_bn(W, pre + ".conv7X7_2.0.weight", pre + ".conv7X7_2.1", BN_EPS, 1, 1, sact, sslope,
+                                 &s72)))
+            return rc;
         if ((rc = conv_bn(c, W, pre + ".conv7x7_3.0.weight", pre + ".conv7x7_3.1", 1, 1, VD_ACT_RELU, &s73))) return rc;
         const Act& f = fpn_out[l];
         const int c3o = c.convs[s3].cout, c5o = c.convs[s52].cout, c7o = c.convs[s73].cout;

@@ -44,7 +44,16 @@ struct Block {
     float* bn = nullptr;
 };
 
-enum { OP_CONV = 0, OP_MAXPOOL = 1, OP_UPSAMPLE = 2, OP_BLOCK = 3, OP_STEMPOOL = 4 };
+// Depthwise 3x3 conv + BN + activation (dwconv.hip): MobileNetV1 conv_dw.
+struct DwConv {
+    int c = 0, stride = 1, act = 0;
+    float slope = 0.f;
+    void* w = nullptr;                 // [9][c] in the compute type
+    float* scale = nullptr;
+    float* shift = nullptr;
+};
+
+enum { OP_CONV = 0, OP_MAXPOOL = 1, OP_UPSAMPLE = 2, OP_BLOCK = 3, OP_STEMPOOL = 4, OP_DWCONV = 5 };
 
 struct Op {
     int kind = OP_CONV;
@@ -80,6 +89,7 @@ struct FaceNet {
     bool loaded = false;
     int in_h = 640, in_w = 640;
     bool s2d = false;               // bf16: stem input in space-to-depth form (pre.hip letterbox_s2d_kernel)
+    bool mnet = false;              // MobileNetV1-0.25 backbone (cfg_mnet) instead of ResNet-50
     Act input;
     Net net;
     Act heads[3];
@@ -131,6 +141,7 @@ struct Ctx {
     std::vector<void*> allocs;
     std::vector<Conv> convs;
     std::vector<Block> blocks;
+    std::vector<DwConv> dwconvs;
     FaceNet face;
     PlateNet plate;
     void* stage_in = nullptr;  size_t stage_in_bytes = 0;
@@ -160,6 +171,10 @@ struct Ctx {
     int add_block(Net& net, int bi, const Act& x, Act& y);
     int run_block_op(const Op& op, int f0, int n, int fam = 0);
     int add_stem_pool(Net& net, int ci, const Act& x, Act& y);
+    int make_dwconv_bn(const WMap& W, const std::string& wkey, const std::string& bn, float eps, int stride, int act,
+                       float slope, int* idx);
+    int add_dwconv(Net& net, int di, const Act& x, Act& y);
+    int run_dwconv_op(const Op& op, int f0, int n);
     int run_stem_pool_op(const Op& op, int f0, int n, int fam = 0);
     void t_begin(int fam, double work);
     void t_end();

@@ -190,6 +190,59 @@ int Ctx::make_conv_bn(const WMap& W, const std::string& wkey, const std::string&
     return VD_OK;
 }
 
+// Depthwise 3x3 conv [c][1][3][3] + BatchNorm at `bn` (mobilenet025.py:10-14), weights
+// stored tap-major [9][c] in the compute type (dwconv.hip reads 16 B of channels per tap).
+int Ctx::make_dwconv_bn(const WMap& W, const std::string& wkey, const std::string& bn, float eps, int stride,
+                        int act, float slope, int* idx) {
+    const HT* w = find_t(W, wkey);
+    if (!w || w->shape.size() != 4 || w->shape[1] != 1 || w->shape[2] != 3 || w->shape[3] != 3)
+        return vd_set_error(VD_ERR_WEIGHTS, "missing/bad depthwise weight %s", wkey.c_str());
+    const HT* g = find_t(W, bn + ".weight");
+    const HT* b = find_t(W, bn + ".bias");
+    const HT* m = find_t(W, bn + ".running_mean");
+    const HT* v = find_t(W, bn + ".running_var");
+    if (!g || !b || !m || !v) return vd_set_error(VD_ERR_WEIGHTS, "missing BatchNorm tensors under %s", bn.c_str());
+    DwConv d;
+    d.c = w->shape[0]; d.stride = stride; d.act = act; d.slope = slope;
+    if (d.c % (f32 ? 4 : 8)) return vd_set_error(VD_ERR_WEIGHTS, "depthwise %s: %d channels", wkey.c_str(), d.c);
+    std::vector<float> wt((size_t)9 * d.c), sc(d.c), sh(d.c);
+    for (int c = 0; c < d.c; ++c) {
+        for (int t = 0; t < 9; ++t) wt[(size_t)t * d.c + c] = w->data[(size_t)c * 9 + t];
+        const float alpha = g->data[c] / std::sqrt(v->data[c] + eps);
+        sc[c] = alpha;
+        sh[c] = b->data[c] - m->data[c] * alpha;
+    }
+    int rc;
+    if (f32) {
+        if ((rc = dalloc(&d.w, wt.size() * 4))) return rc;
+        VD_CHECK_HIP(hipMemcpy(d.w, wt.data(), wt.size() * 4, hipMemcpyHostToDevice));
+    } else {
+        std::vector<uint16_t> h(wt.size());
+        for (size_t i = 0; i < wt.size(); ++i) h[i] = f32_to_bf16_rne(wt[i]);
+        if ((rc = dalloc(&d.w, h.size() * 2))) return rc;
+        VD_CHECK_HIP(hipMemcpy(d.w, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+    }
+    if ((rc = dalloc((void**)&d.scale, d.c * 4)) || (rc = dalloc((void**)&d.shift, d.c * 4))) return rc;
+    VD_CHECK_HIP(hipMemcpy(d.scale, sc.data(), d.c * 4, hipMemcpyHostToDevice));
+    VD_CHECK_HIP(hipMemcpy(d.shift, sh.data(), d.c * 4, hipMemcpyHostToDevice));
+    dwconvs.push_back(d);
+    *idx = (int)dwconvs.size() - 1;
+    return VD_OK;
+}
+
+int Ctx::add_dwconv(Net& net, int di, const Act& x, Act& y) {
+    const DwConv& d = dwconvs[di];
+    if (x.c < d.c || y.c < d.c || y.h != (x.h - 1) / d.stride + 1 || y.w != (x.w - 1) / d.stride + 1)
+        return vd_set_error(VD_ERR_ARG, "depthwise conv plan shape mismatch");
+    Op op{};
+    op.kind = OP_DWCONV;
+    op.conv = di;
+    op.x = x;
+    op.y = y;
+    net.ops.push_back(op);
+    return VD_OK;
+}
+
 // Several 1x1 conv heads with bias fused along Cout (retinaface.py:90-92,140-142).
 int Ctx::make_conv_cat(const WMap& W, const std::vector<std::string>& wkeys, const std::vector<std::string>& bkeys,
                        int act, int* out_idx) {
@@ -309,6 +362,20 @@ int Ctx::run_conv_op(const Op& op, int f0, int n, int fam) {
     return VD_OK;
 }
 
+int Ctx::run_dwconv_op(const Op& op, int f0, int n) {
+    const DwConv& d = dwconvs[op.conv];
+    DwConvArgs a{};
+    a.x = foff(op.x, f0); a.xh = op.x.h; a.xw = op.x.w; a.ldx = op.x.c; a.xcoff = 0;
+    a.w = d.w; a.scale = d.scale; a.shift = d.shift;
+    a.y = (void*)foff(op.y, f0); a.yh = op.y.h; a.yw = op.y.w; a.ldy = op.y.c; a.ycoff = 0;
+    a.B = n; a.c = d.c; a.stride = d.stride; a.act = d.act; a.slope = d.slope;
+    t_begin(4, 0);
+    hipError_t e = vd_launch_dwconv(a, f32, stream);
+    t_end();
+    if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "depthwise conv: %s", hipGetErrorString(e));
+    return VD_OK;
+}
+
 int Ctx::run_ops(const Net& net, int b, int e, int f0, int n) {
     for (int i = b; i < e; ++i) {
         const Op& op = net.ops[i];
@@ -319,6 +386,8 @@ int Ctx::run_ops(const Net& net, int b, int e, int f0, int n) {
             rc = run_block_op(op, f0, n, net.conv_fam);
         } else if (op.kind == OP_STEMPOOL) {
             rc = run_stem_pool_op(op, f0, n, net.conv_fam);
+        } else if (op.kind == OP_DWCONV) {
+            rc = run_dwconv_op(op, f0, n);
         } else if (op.kind == OP_MAXPOOL) {
             t_begin(4, 0);
             hipError_t er = vd_launch_maxpool(f32, foff(op.x, f0), n, op.x.h, op.x.w, op.x.c, op.xcoff,

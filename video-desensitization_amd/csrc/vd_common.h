@@ -48,6 +48,15 @@ struct BlockArgs {
     int mode;                    // experiments (tools/convbench VD_BLOCK_MODE); 0 in production
 };
 
+// Depthwise 3x3 conv (pad 1) + BN + activation, NHWC (dwconv.hip): MobileNetV1 conv_dw.
+struct DwConvArgs {
+    const void* x; int xh, xw, ldx, xcoff;
+    const void* w;                               // [9 taps][c] (dy-major), compute type
+    const float* scale; const float* shift;
+    void* y; int yh, yw, ldy, ycoff;
+    int B, c, stride, act; float slope;
+};
+
 // RetinaFace stem conv (space-to-depth form) + maxpool in one kernel (stem.hip):
 // x = X' [B][xh][xw][16] -> y = pooled [B][ph][pw][64].
 struct StemPoolArgs {
@@ -128,6 +137,7 @@ bool vd_conv_persist_ok(const ConvArgs& a);
 hipError_t vd_launch_conv_persist(const ConvArgs& a, hipStream_t s);
 bool vd_block_ok(int cin, bool ds, int h, int w);
 bool vd_stem_pool_ok(int xh, int xw, int ph, int pw);
+hipError_t vd_launch_dwconv(const DwConvArgs& a, bool f32, hipStream_t s);
 hipError_t vd_launch_stem_pool(const StemPoolArgs& a, hipStream_t s);
 hipError_t vd_launch_block(const BlockArgs& a, hipStream_t s);
 hipError_t vd_launch_letterbox(const LetterboxArgs& a, hipStream_t s);

@@ -5,7 +5,7 @@ attribute (read at combine_detect.py:866), same ``detect_images`` contract
 (face.py:120-150): a list of uint8 HxWx3 RGB arrays in, a list of
 ``(image, [[x1, y1, x2, y2], ...])`` out, boxes as Python floats in source
 pixels, in NMS (descending score) order. Everything between — letterbox,
-ResNet-50/FPN/SSH forward, decode, NMS, correction — runs in HIP kernels.
+ResNet-50 (or MobileNet-0.25)/FPN/SSH forward, decode, NMS, correction — runs in HIP kernels.
 
 Differences, all deliberate:
 * ``cuda=False`` raises: the product path has no CPU fallback (the reference's
@@ -24,7 +24,7 @@ import numpy as np
 
 from . import _lib
 from .context import Context
-from .weights import load_reference_checkpoint, retinaface_state_dict
+from .weights import load_reference_checkpoint, retinaface_mnet_state_dict, retinaface_state_dict
 
 
 class Retinaface(object):
@@ -53,9 +53,8 @@ class Retinaface(object):
         self.__dict__.update(self._defaults)
         for name, value in kwargs.items():
             setattr(self, name, value)
-        if self.backbone != "resnet50":
-            raise ValueError("only backbone='resnet50' (cfg_re50) is on the MI355X path "
-                             "(combine_detect.py:859 fixes it)")
+        if self.backbone not in ("resnet50", "mobilenet"):   # face.py:35: cfg_mnet / cfg_re50
+            raise ValueError(f"backbone must be 'resnet50' or 'mobilenet', got {self.backbone!r}")
         if not self.letterbox_image:
             raise ValueError("Batch inference requires letterbox_image=True for shape alignment.")  # face.py:80
         if not self.cuda:
@@ -78,7 +77,7 @@ class Retinaface(object):
             sd = load_reference_checkpoint(self.model_path)
         else:
             warnings.warn(f"{self.model_path} not found: using seeded random RetinaFace weights (seed={self.seed})")
-            sd = retinaface_state_dict(self.seed)
+            sd = (retinaface_mnet_state_dict if self.backbone == "mobilenet" else retinaface_state_dict)(self.seed)
         self.ctx.load_weights(_lib.VD_NET_RETINAFACE, sd)
 
     def detect_boxes(self, images):

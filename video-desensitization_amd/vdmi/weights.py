@@ -31,6 +31,8 @@ import numpy as np
 # mostly small: a crowded street scene rather than one box per anchor).
 CLS_HEAD_STD = 0.02
 CLS_BIAS_DELTA = {0: -9.3, 1: -6.47, 2: -1.68}
+# Same targets for the backbone="mobilenet" generator (tools/calibrate_weights.py --mnet).
+MNET_CLS_BIAS_DELTA = {0: 0.0, 1: -4.04, 2: -2.93}
 LOC_HEAD_STD = 0.01
 RESIDUAL_GAMMA = 0.25
 
@@ -75,29 +77,59 @@ def retinaface_state_dict(seed=0, cls_std=None, cls_bias=None):
                 sd[p + ".downsample.0.weight"] = _conv(rng, planes * 4, inplanes, 1)
                 _bn(rng, sd, p + ".downsample.1", planes * 4)
             inplanes = planes * 4
-    for i, cin in zip((1, 2, 3), (512, 1024, 2048)):
-        sd[f"fpn.output{i}.0.weight"] = _conv(rng, 256, cin, 1)
-        _bn(rng, sd, f"fpn.output{i}.1", 256)
+    _fpn_ssh_heads(rng, sd, (512, 1024, 2048), 256, cls_std, cls_bias)
+    return sd
+
+
+def _fpn_ssh_heads(rng, sd, in_list, oc, cls_std, cls_bias):
+    """FPN (layers.py:68-88), SSH x3 (:37-51) and the three head lists
+    (retinaface.py:13-51) for out_channel ``oc``."""
+    for i, cin in zip((1, 2, 3), in_list):
+        sd[f"fpn.output{i}.0.weight"] = _conv(rng, oc, cin, 1)
+        _bn(rng, sd, f"fpn.output{i}.1", oc)
     for i in (1, 2):
-        sd[f"fpn.merge{i}.0.weight"] = _conv(rng, 256, 256, 3)
-        _bn(rng, sd, f"fpn.merge{i}.1", 256)
+        sd[f"fpn.merge{i}.0.weight"] = _conv(rng, oc, oc, 3)
+        _bn(rng, sd, f"fpn.merge{i}.1", oc)
     for s in (1, 2, 3):
         p = f"ssh{s}"
-        for name, cout, cin in (("conv3X3", 128, 256), ("conv5X5_1", 64, 256), ("conv5X5_2", 64, 64),
-                                ("conv7X7_2", 64, 64), ("conv7x7_3", 64, 64)):
+        q = oc // 4
+        for name, cout, cin in (("conv3X3", oc // 2, oc), ("conv5X5_1", q, oc), ("conv5X5_2", q, q),
+                                ("conv7X7_2", q, q), ("conv7x7_3", q, q)):
             sd[f"{p}.{name}.0.weight"] = _conv(rng, cout, cin, 3)
             _bn(rng, sd, f"{p}.{name}.1", cout)
     cstd = CLS_HEAD_STD if cls_std is None else cls_std
     cb = CLS_BIAS_DELTA if cls_bias is None else cls_bias
     for lvl in range(3):
-        sd[f"ClassHead.{lvl}.conv1x1.weight"] = _conv(rng, 4, 256, 1, std=cstd)
+        sd[f"ClassHead.{lvl}.conv1x1.weight"] = _conv(rng, 4, oc, 1, std=cstd)
         b = np.zeros(4, np.float32)
         b[1] = b[3] = cb[lvl] if isinstance(cb, dict) else cb   # class-1 logit of both anchors
         sd[f"ClassHead.{lvl}.conv1x1.bias"] = b
-        sd[f"BboxHead.{lvl}.conv1x1.weight"] = _conv(rng, 8, 256, 1, std=LOC_HEAD_STD)
+        sd[f"BboxHead.{lvl}.conv1x1.weight"] = _conv(rng, 8, oc, 1, std=LOC_HEAD_STD)
         sd[f"BboxHead.{lvl}.conv1x1.bias"] = np.zeros(8, np.float32)
-        sd[f"LandmarkHead.{lvl}.conv1x1.weight"] = _conv(rng, 20, 256, 1, std=LOC_HEAD_STD)
+        sd[f"LandmarkHead.{lvl}.conv1x1.weight"] = _conv(rng, 20, oc, 1, std=LOC_HEAD_STD)
         sd[f"LandmarkHead.{lvl}.conv1x1.bias"] = np.zeros(20, np.float32)
+
+
+def retinaface_mnet_state_dict(seed=0, cls_std=None, cls_bias=None):
+    """Keys/shapes of RetinaFace(cfg_mnet): MobileNetV1-0.25 under ``body``
+    (detect_face/nets/mobilenet025.py:21-48, stage1/2/3 returned; the fc head is
+    dropped like IntermediateLayerGetter does), FPN [64, 128, 256] -> 64, SSH(64, 64),
+    heads on 64 channels (retinaface.py:60-92). Same recipe as the ResNet one
+    (stem / 64 for raw-pixel input), class bias calibrated to the same pass rates."""
+    rng = _rng(500 + seed)
+    sd = {"body.stage1.0.0.weight": _conv(rng, 8, 3, 3) / np.float32(64.0)}
+    _bn(rng, sd, "body.stage1.0.1", 8)
+    chans = {1: [(8, 16), (16, 32), (32, 32), (32, 64), (64, 64)],
+             2: [(64, 128)] + [(128, 128)] * 5,
+             3: [(128, 256), (256, 256)]}
+    for st, mods in chans.items():
+        for i, (cin, cout) in enumerate(mods):
+            p = f"body.stage{st}.{i + (1 if st == 1 else 0)}"
+            sd[p + ".0.weight"] = _conv(rng, cin, 1, 3)   # depthwise: fan_in 9
+            _bn(rng, sd, p + ".1", cin)
+            sd[p + ".3.weight"] = _conv(rng, cout, cin, 1)
+            _bn(rng, sd, p + ".4", cout)
+    _fpn_ssh_heads(rng, sd, (64, 128, 256), 64, cls_std, MNET_CLS_BIAS_DELTA if cls_bias is None else cls_bias)
     return sd
 
 
