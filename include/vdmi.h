@@ -130,8 +130,9 @@ int vd_process(vd_ctx* ctx, const uint8_t* in, uint8_t* out, int n, int h, int w
 /* When enabled, every launch of kernel family `fam` is bracketed by HIP events
  * on the context stream; vd_timing_read returns the summed duration (ms), the
  * launch count and the summed algorithmic work (FLOP or bytes) since the last
- * reset. Families: 0 = RetinaFace conv (implicit GEMM / streaming 1x1), 1 = mosaic,
- * 2 = letterbox, 3 = post (decode/NMS), 4 = other, 5 = YOLOv8n plate conv. */
+ * reset. Families: 0 = RetinaFace conv (implicit GEMM / streaming 1x1), 1 = mosaic
+ * output pass, 2 = letterbox, 3 = post (decode/NMS), 4 = other, 5 = YOLOv8n plate
+ * conv, 6 = mosaic cell table (box prep + walked cell colours). */
 int vd_timing_enable(vd_ctx* ctx, int on);
 int vd_timing_reset(vd_ctx* ctx);
 int vd_timing_read(vd_ctx* ctx, int fam, double* ms, int64_t* launches, double* work);

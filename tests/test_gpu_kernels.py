@@ -86,6 +86,57 @@ def test_mosaic_many_boxes_band_overflow(gpu, face_ctx_factory):
     np.testing.assert_array_equal(got[0], omosaic.mosaic_frame(frames[0], boxes[0], 8))
 
 
+@pytest.mark.parametrize("nbox", [255, 256, 257])
+def test_mosaic_box_count_boundary(gpu, face_ctx_factory, nbox):
+    """Frames at the fast-path box limit (256: overlap graph + cell table; 257:
+    per-pixel walk), next to a frame with no boxes and one with a single box."""
+    from vdmi import mosaic_frames, synth
+    ctx = face_ctx_factory("bf16", 8)
+    rng = np.random.default_rng(nbox)
+    h, w = 270, 480
+    frames = synth.frames(3, h, w, seed=nbox)
+    big = [tuple(int(v) for v in (x, y, x + rng.integers(4, 60), y + rng.integers(4, 60)))
+           for x, y in zip(rng.integers(-20, w, nbox), rng.integers(-20, h, nbox))]
+    boxes = [big, [], [(100, 50, 300, 200)]]
+    got = mosaic_frames(frames, boxes, 8, ctx=ctx)
+    for i in range(3):
+        np.testing.assert_array_equal(got[i], omosaic.mosaic_frame(frames[i], boxes[i], 8))
+
+
+def test_mosaic_wide_band_arena_overflow(gpu, face_ctx_factory):
+    """Bands whose boxes' widths sum past the per-band column map (3072 columns)
+    compute the cell column per pixel, bands whose cells exceed the LDS slice
+    (2048) read the global cell table; mixed with bands that fit."""
+    from vdmi import mosaic_frames, synth
+    ctx = face_ctx_factory("bf16", 8)
+    frames = synth.frames(3, 1080, 1920, seed=11)
+    boxes = [[(17 * i, 100 + 9 * i, 1900 - 13 * i, 400 + 7 * i) for i in range(12)] + [(5, 700, 333, 1000)],
+             [(0, 0, 1920, 1080), (100, 100, 1800, 1000), (3, 5, 1917, 1077), (600, 0, 1300, 1080)],
+             [(100, 200, 1100, 600), (900, 500, 1500, 900)]]   # level 2: cells overflow the LDS slice
+    for level in (2, 5, 8):
+        got = mosaic_frames(frames, boxes, level, ctx=ctx)
+        for i in range(3):
+            np.testing.assert_array_equal(got[i], omosaic.mosaic_frame(frames[i], boxes[i], level))
+
+
+def test_mosaic_row_classes_and_wide_cells(gpu, face_ctx_factory):
+    """Bands with more distinct row box-sets than column maps (staggered box tops
+    inside one band), and a level-1 box wider than the map's 11-bit cell column."""
+    from vdmi import mosaic_frames, synth
+    ctx = face_ctx_factory("bf16", 8)
+    frames = synth.frames(2, 1080, 1920, seed=13)
+    stag = [(40 + 150 * i, 33 + 2 * i, 200 + 150 * i, 90 + 3 * i) for i in range(12)]
+    stag += [(0, 36, 1920, 41), (500, 30, 900, 47)]
+    got = mosaic_frames(frames, [stag, stag[::-1]], 8, ctx=ctx)
+    for i, bl in enumerate([stag, stag[::-1]]):
+        np.testing.assert_array_equal(got[i], omosaic.mosaic_frame(frames[i], bl, 8))
+    wide = synth.frames(1, 96, 2208, seed=14)
+    bl = [(3, 5, 2150, 60), (100, 20, 300, 90)]
+    for level in (1, 2):
+        got = mosaic_frames(wide, [bl], level, ctx=ctx)
+        np.testing.assert_array_equal(got[0], omosaic.mosaic_frame(wide[0], bl, level))
+
+
 def test_mosaic_single_drop_in(gpu):
     from vdmi import mosaic_rectangle_region_single, synth
     img = synth.frame(120, 160, 0)

@@ -1,0 +1,77 @@
+"""Mosaic-only timing on 64 synthetic 1080p frames already in HBM.
+
+Box sets: none (pure copy), SURVEY §8d blur-only lists (8/frame, seed 1) and the
+detector's own face boxes from one bench-shaped vd_process step. Prints the mean
+time of one vd_mosaic call (HIP events around it) and the HBM rate over the
+algorithmic 2*W*H*3 bytes per frame.
+
+    python tools/mosaicbench.py [--iters 50]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "video-desensitization_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--batch", type=int, default=64)
+    a = ap.parse_args()
+    import vdmi
+    from vdmi import _lib, synth, weights
+    B, H, W = a.batch, 1080, 1920
+    dev = torch.device("cuda:0")
+    ctx = vdmi.Context(device=0, precision="bf16", max_batch=B)
+    ctx.load_weights(0, weights.retinaface_state_dict(0))
+    frames = torch.from_numpy(synth.frames(B, H, W, seed=0)).to(dev)
+    out = torch.empty_like(frames)
+    stream = torch.cuda.current_stream(dev)
+    ctx.set_stream(stream.cuda_stream)
+    faces = vdmi.DeviceBoxes(B, 256, dev)
+    ctx.process(frames, out, faces=faces, flags=_lib.VD_PROC_FACES)
+    torch.cuda.synchronize()
+    cnt = faces.count.cpu().numpy()
+    xy = faces.xyxy.cpu().numpy()
+    area = sum(int(max(0, min(W, b[2]) - max(0, b[0])) * max(0, min(H, b[3]) - max(0, b[1])))
+               for f in range(B) for b in xy[f, :cnt[f]])
+    sets = {
+        "none": (np.zeros((B, 1, 4), np.int32), np.zeros(B, np.int32)),
+        "survey8": (synth.box_lists(B, H, W, 8, seed=1), np.full(B, 8, np.int32)),
+        "faces": (xy[:, :max(1, int(cnt.max()))].copy(), cnt.astype(np.int32)),
+    }
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    np.save(os.path.join(ROOT, "gpurun_out", "face_boxes.npy"), np.concatenate([cnt[:, None, None].repeat(4, 2), xy], 1))
+    res = {"faces_per_frame": float(cnt.mean()), "face_box_area_per_frame": area / B}
+    for name, (bx, bc) in sets.items():
+        bxd = torch.from_numpy(np.ascontiguousarray(bx)).to(dev)
+        bcd = torch.from_numpy(np.ascontiguousarray(bc)).to(dev)
+        s = _lib.vd_boxes(bxd.shape[1], _lib.VD_DEVICE, bcd.data_ptr(), bxd.data_ptr(), None, None, None)
+
+        def call():
+            _lib.check(ctx._lib.vd_mosaic(ctx._h, frames.data_ptr(), out.data_ptr(), B, H, W, W * 3,
+                                          _lib.VD_DEVICE, __import__("ctypes").byref(s), 8,
+                                          _lib.VD_MOSAIC_OUT_OF_PLACE))
+        for _ in range(3):
+            call()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.iters):
+            call()
+        e1.record()
+        torch.cuda.synchronize()
+        us = e0.elapsed_time(e1) / a.iters * 1e3
+        res[name] = {"us": round(us, 1), "GB/s": round(2.0 * B * H * W * 3 / (us * 1e-6) / 1e9, 1)}
+    print(json.dumps(res), flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -561,9 +561,13 @@ int Ctx::launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w, siz
     const int tcap = (cnt0 ? cap0 : 0) + (cnt1 ? cap1 : 0);
     int rc = ensure_staging(&mosaic_table, &mosaic_table_bytes, vd_mosaic_table_bytes(n, tcap) + 64);
     if (rc) return rc;
-    t_begin(1, 2.0 * n * (double)h * w * 3);
+    t_begin(6, 0);
     hipError_t e = vd_launch_mosaic(in, out, n, h, w, pitch, cnt0, xy0, cap0, cnt1, xy1, cap1, level, mosaic_table,
-                                    stream);
+                                    1, stream);
+    t_end();
+    if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "mosaic: %s", hipGetErrorString(e));
+    t_begin(1, 2.0 * n * (double)h * w * 3);
+    e = vd_launch_mosaic(in, out, n, h, w, pitch, cnt0, xy0, cap0, cnt1, xy1, cap1, level, mosaic_table, 2, stream);
     t_end();
     if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "mosaic: %s", hipGetErrorString(e));
     return VD_OK;

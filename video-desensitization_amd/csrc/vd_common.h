@@ -150,7 +150,7 @@ hipError_t vd_launch_post(const PostArgs& p, hipStream_t s);
 hipError_t vd_launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w, size_t pitch,
                             const int* cnt0, const int* xy0, int cap0,
                             const int* cnt1, const int* xy1, int cap1, int level, void* table,
-                            hipStream_t s);
+                            int stages, hipStream_t s);   // stages: 1 = cell table, 2 = output pass
 size_t vd_mosaic_table_bytes(int n, int tcap);
 
 #define VD_CHECK_HIP(expr)                                                     \

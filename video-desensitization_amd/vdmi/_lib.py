@@ -20,7 +20,7 @@ VD_NET_RETINAFACE, VD_NET_YOLOV8N = 0, 1
 VD_WEIGHTS_VDW1 = 1
 VD_MOSAIC_OUT_OF_PLACE = 0
 VD_PROC_FACES, VD_PROC_PLATES, VD_PROC_MOSAIC, VD_PROC_MOSAIC_PLATES = 1, 2, 4, 8
-FAM_CONV, FAM_MOSAIC, FAM_LETTERBOX, FAM_POST, FAM_OTHER, FAM_PLATE_CONV = 0, 1, 2, 3, 4, 5
+FAM_CONV, FAM_MOSAIC, FAM_LETTERBOX, FAM_POST, FAM_OTHER, FAM_PLATE_CONV, FAM_MOSAIC_CELLS = 0, 1, 2, 3, 4, 5, 6
 
 _ERRNAMES = {VD_ERR_ARG: "VD_ERR_ARG", VD_ERR_HIP: "VD_ERR_HIP", VD_ERR_CAPACITY: "VD_ERR_CAPACITY",
              VD_ERR_WEIGHTS: "VD_ERR_WEIGHTS", VD_ERR_STATE: "VD_ERR_STATE", VD_ERR_NOMEM: "VD_ERR_NOMEM"}
