@@ -170,12 +170,17 @@ CONV_CASES = [
     (1, 16, 16, 48, 24, 1, 1, 0, 3, 2),       # cin 48 generic, res after act
     (1, 12, 10, 256, 32, 1, 1, 0, 0, 0),      # heads (BN=32 tile)
     (1, 9, 11, 512, 200, 3, 1, 1, 2, 1),      # cout not a tile multiple, leaky
-    # 1x1 streaming kernel (bf16, K 64/128/256): bottleneck conv3 / conv1 / downsample shapes
+    # 1x1 streaming kernel (bf16, K 64/128/256/512): bottleneck conv3 / conv1 / downsample shapes
     (2, 21, 23, 64, 256, 1, 1, 0, 1, 1),      # conv3 + residual, M not a multiple of 16
     (1, 18, 18, 256, 512, 1, 2, 0, 0, 0),     # stride-2 downsample
     (1, 10, 14, 128, 512, 1, 1, 0, 1, 1),
     (2, 9, 7, 256, 128, 1, 1, 0, 3, 0),       # SiLU
     (1, 13, 11, 128, 192, 1, 1, 0, 0, 2),     # residual after (no) activation, 64-channel slices
+    # 1x1 streaming kernel at K = 512 (16 k-steps, 128 KB weight slice in LDS)
+    (2, 15, 17, 512, 128, 1, 1, 0, 1, 0),     # bottleneck conv1 of layer2
+    (1, 18, 18, 512, 256, 1, 2, 0, 0, 0),     # stride-2 downsample (layer3.0)
+    (1, 9, 10, 512, 256, 1, 1, 0, 1, 1),      # residual before ReLU (layer4 conv3 form)
+    (1, 11, 13, 512, 192, 1, 1, 0, 0, 2),     # 64-channel slices, residual after activation
     # streaming taps kernel (K <= 320, Cout % 16 == 0): YOLO C2f bottleneck / 1x1 / stride-2 shapes
     (2, 14, 18, 16, 16, 3, 1, 1, 3, 2),       # 16-channel slice, SiLU, shortcut after activation
     (1, 20, 22, 32, 48, 1, 1, 0, 3, 0),       # 1x1 with K 32 (< one k-tile), three 16-channel slices

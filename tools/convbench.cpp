@@ -180,6 +180,12 @@ int main(int argc, char** argv) {
             {"y.c2f48", 64, 48, 80, 192, 64, 1, 1, 0, 0}, {"f.l1c2", 64, 160, 160, 64, 64, 3, 1, 1, 0},
             {"f.ssh52", 64, 80, 80, 64, 64, 3, 1, 1, 0},
         };
+    } else if (argc == 3 && std::string(argv[2]) == "k512") {   // 1x1 layers of the HBM-bound family
+        layers = {
+            {"l2.c1", 64, 80, 80, 512, 128, 1, 1, 0, 0},   {"l3.0.c1", 64, 80, 80, 512, 256, 1, 1, 0, 0},
+            {"l3.0.ds", 64, 80, 80, 512, 1024, 1, 2, 0, 0}, {"l4.c3", 64, 20, 20, 512, 2048, 1, 1, 0, 1},
+            {"l3.c3", 64, 40, 40, 256, 1024, 1, 1, 0, 1},   {"l2.c3", 64, 80, 80, 128, 512, 1, 1, 0, 1},
+        };
     } else if (argc >= 10) {
         layers.push_back({"custom", atoi(argv[2]), atoi(argv[3]), atoi(argv[4]), atoi(argv[5]), atoi(argv[6]),
                           atoi(argv[7]), atoi(argv[8]), atoi(argv[9]), 0});

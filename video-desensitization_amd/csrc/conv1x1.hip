@@ -350,7 +350,9 @@ bool mode_ok(const ConvArgs& a) {
 bool vd_conv1x1_stream_ok(const ConvArgs& a) {
     const char* e = getenv("VD_CONV_STREAM");   // read per call (A/B and tests)
     if ((e && atoi(e) == 0) || a.kh != 1 || a.kw != 1 || a.pad != 0) return false;
-    if (a.cin_pad != 64 && a.cin_pad != 128 && a.cin_pad != 256) return false;
+    const char* e5 = getenv("VD_CONV_STREAM512");
+    const bool k512 = a.cin_pad == 512 && !(e5 && atoi(e5) == 0);
+    if (a.cin_pad != 64 && a.cin_pad != 128 && a.cin_pad != 256 && !k512) return false;
     if (a.kpad < a.cin_pad || (a.cout % 64) != 0) return false;
     if ((a.ldx | a.xcoff) & 7) return false;
     if ((a.ldy | a.ycoff) & 7) return false;
@@ -379,6 +381,7 @@ hipError_t vd_launch_conv1x1_stream(const ConvArgs& a, hipStream_t s) {
     const bool wide = a.cout % 128 == 0;
     if (a.cin_pad == 64) return wide ? launch_mode<2, 8, false>(a, s) : launch_mode<2, 4, false>(a, s);
     if (a.cin_pad == 128) return wide ? launch_mode<4, 8, false>(a, s) : launch_mode<4, 4, false>(a, s);
+    if (a.cin_pad == 512) return wide ? launch_mode<16, 8, false>(a, s) : launch_mode<16, 4, false>(a, s);
     return wide ? launch_mode<8, 8, false>(a, s) : launch_mode<8, 4, false>(a, s);
 }
 
