@@ -181,6 +181,10 @@ CONV_CASES = [
     (1, 18, 18, 512, 256, 1, 2, 0, 0, 0),     # stride-2 downsample (layer3.0)
     (1, 9, 10, 512, 256, 1, 1, 0, 1, 1),      # residual before ReLU (layer4 conv3 form)
     (1, 11, 13, 512, 192, 1, 1, 0, 0, 2),     # 64-channel slices, residual after activation
+    # 256-channel slices (K 128/256, Cout % 256 == 0): layer2/3 conv3 + identity
+    (2, 10, 13, 128, 512, 1, 1, 0, 1, 1),
+    (1, 9, 9, 256, 1024, 1, 1, 0, 1, 1),
+    (1, 12, 11, 256, 256, 1, 2, 0, 0, 0),     # stride 2, one chunk
     # streaming taps kernel (K <= 320, Cout % 16 == 0): YOLO C2f bottleneck / 1x1 / stride-2 shapes
     (2, 14, 18, 16, 16, 3, 1, 1, 3, 2),       # 16-channel slice, SiLU, shortcut after activation
     (1, 20, 22, 32, 48, 1, 1, 0, 3, 0),       # 1x1 with K 32 (< one k-tile), three 16-channel slices

@@ -377,7 +377,12 @@ hipError_t vd_launch_conv1x1_stream(const ConvArgs& a, hipStream_t s) {
         if (a.cin_pad == 64) return launch_stream<2, 8, VD_ACT_RELU, VD_RES_NONE, false, 2>(a, s);
         return launch_stream<4, 8, VD_ACT_RELU, VD_RES_NONE, false, 8>(a, s);
     }
-    // 128-channel slices (64 when Cout is not a multiple of 128); K 64/128/256
+    // 256-channel slices at K 128/256 when Cout allows (bottleneck conv3 of layer2/3:
+    // 1.1-1.2x the 128-channel form, tools/convbench k512; VD_STREAM_NTT=8 keeps 128),
+    // else 128-channel slices (64 when Cout is not a multiple of 128)
+    static const int ntt_env = [] { const char* e = getenv("VD_STREAM_NTT"); return e ? atoi(e) : 16; }();
+    if (ntt_env == 16 && a.cout % 256 == 0 && a.cin_pad == 128) return launch_mode<4, 16, false>(a, s);
+    if (ntt_env == 16 && a.cout % 256 == 0 && a.cin_pad == 256) return launch_mode<8, 16, false>(a, s);
     const bool wide = a.cout % 128 == 0;
     if (a.cin_pad == 64) return wide ? launch_mode<2, 8, false>(a, s) : launch_mode<2, 4, false>(a, s);
     if (a.cin_pad == 128) return wide ? launch_mode<4, 8, false>(a, s) : launch_mode<4, 4, false>(a, s);
