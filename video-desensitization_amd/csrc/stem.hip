@@ -49,10 +49,13 @@ __device__ __forceinline__ f32x4_t mfma(const u32x4& a, const u32x4& b, const f3
                                                    c, 0, 0, 0);
 }
 
-__device__ __forceinline__ unsigned max_bf16x2(unsigned a, unsigned b) {   // non-negative bf16 pairs
-    const unsigned lo = (a & 0xffffu) > (b & 0xffffu) ? (a & 0xffffu) : (b & 0xffffu);
-    const unsigned hi = (a >> 16) > (b >> 16) ? (a >> 16) : (b >> 16);
-    return lo | (hi << 16);
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// max of two pairs of non-negative bf16 (their bit patterns order as unsigned
+// 16-bit integers): one v_pk_max_u16
+__device__ __forceinline__ unsigned max_bf16x2(unsigned a, unsigned b) {
+    return __builtin_bit_cast(unsigned, __builtin_elementwise_max(__builtin_bit_cast(u16x2, a),
+                                                                 __builtin_bit_cast(u16x2, b)));
 }
 
 template <int NXB>   // X' tile buffers: 2 = next tile's DMA overlaps this tile, 1 = more workgroups per CU
