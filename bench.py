@@ -81,9 +81,11 @@ def pmc_traffic():
     files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
                                           "r*_pmc_traffic.json")))
     if not files:
-        return None, None
+        return None, None, None
     d = json.load(open(files[-1]))
-    return d.get("traffic_bytes_per_launch"), os.path.join("profiles", os.path.basename(files[-1]))
+    src = os.path.join("profiles", os.path.basename(files[-1]))
+    blur = (d.get("mosaic_out_kernel") or {}).get("traffic_bytes_per_launch")
+    return d.get("traffic_bytes_per_launch"), src, blur
 
 
 def main():
@@ -179,7 +181,7 @@ def main():
         oms, on_, _ = ctx.timing_read(_lib.FAM_OTHER)
         yms, yn, yflop = ctx.timing_read(_lib.FAM_PLATE_CONV)
         ach = cflop / (cms * 1e-3) / 1e12 if cms > 0 else 0.0
-        traffic, tsrc = pmc_traffic()
+        traffic, tsrc, blur_traffic = pmc_traffic()
         roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_TFLOPS[a.precision], "unit": "TFLOP/s",
                 "frac": round(ach / PEAK_TFLOPS[a.precision], 4), "traffic": traffic,
                 "kernel": "RetinaFace conv family: stem_pool + bottleneck (fused layer1) + conv_big + conv_igemm + "
@@ -196,6 +198,7 @@ def main():
         blur = {"bound": "hbm", "achieved": round(bach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": round(bach / PEAK_HBM_GBS, 4), "avg_launch_ms": round(mms / max(mn, 1), 4),
                 "bytes_per_launch": round(mbytes / max(mn, 1)), "kernel": "mosaic_out_kernel",
+                "traffic": blur_traffic, "traffic_source": tsrc,
                 "family": {"kernels": "mosaic_cell_kernel + mosaic_out_kernel", "achieved": round(fach, 1),
                            "frac": round(fach / PEAK_HBM_GBS, 4),
                            "avg_ms_per_step": round((mms + cms6) / max(mn, 1), 4)}}

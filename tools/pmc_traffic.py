@@ -31,9 +31,20 @@ def per_launch(d, counter):
     return sum(vals) / max(len(vals), 1), len(vals)
 
 
+def per_launch_named(d, counter, name):
+    """Average counter per launch of the kernels whose name contains `name`."""
+    trace = list(csv.DictReader(open(os.path.join(d, "run_kernel_trace.csv"))))
+    ids = {r["Dispatch_Id"] for r in trace if name in r["Kernel_Name"]}
+    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv")))
+            if r["Counter_Name"] == counter and r["Dispatch_Id"] in ids]
+    return sum(vals) / max(len(vals), 1), len(vals)
+
+
 def main(fetch_dir, write_dir, out=None):
     f_kib, nf = per_launch(fetch_dir, "FETCH_SIZE")
     w_kib, nw = per_launch(write_dir, "WRITE_SIZE")
+    mf, mnf = per_launch_named(fetch_dir, "FETCH_SIZE", "mosaic_out_kernel")
+    mw, mnw = per_launch_named(write_dir, "WRITE_SIZE", "mosaic_out_kernel")
     res = {
         "kernel": "RetinaFace conv launches (stem_pool / bottleneck / conv_big / conv_igemm / conv1x1_stream), face stream",
         "launches": {"fetch_pass": nf, "write_pass": nw},
@@ -42,6 +53,9 @@ def main(fetch_dir, write_dir, out=None):
         "traffic_bytes_per_launch": round((2.0 * f_kib + w_kib) * 1024.0),
         "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (KiB counters; gfx950 FETCH_SIZE = half of "
                       "wide coalesced reads); Infinity-Cache hits included",
+        "mosaic_out_kernel": {"launches": {"fetch_pass": mnf, "write_pass": mnw},
+                              "fetch_size_kib_per_launch": round(mf, 1), "write_size_kib_per_launch": round(mw, 1),
+                              "traffic_bytes_per_launch": round((2.0 * mf + mw) * 1024.0)},
     }
     txt = json.dumps(res, indent=1)
     if out:
