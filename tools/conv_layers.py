@@ -69,7 +69,10 @@ def main(path, B=64):
         fl = 2.0 * M * N * K
         tot_t += dt
         tot_f += fl
-        kn = ("STEM+POOL" if "stem_pool" in r["Kernel_Name"] else "BLOCK" if "bottleneck" in r["Kernel_Name"] else "BIG" if "conv_big" in r["Kernel_Name"] else "S:" + r["Kernel_Name"].split("<")[1][:12] if "conv1x1_stream" in r["Kernel_Name"] else "G:" + r["Kernel_Name"].split("conv_igemm_kernel")[1][:22])
+        n_ = r["Kernel_Name"]
+        kn = ("STEM+POOL" if "stem_pool" in n_ else "BLOCK" if "bottleneck" in n_ else "BIG" if "conv_big" in n_
+              else "S:" + n_.split("<")[1][:12] if "conv1x1_stream" in n_
+              else "G:" + n_.split("conv_igemm_kernel")[1][:22] if "conv_igemm_kernel" in n_ else n_[:24])
         print(f"{name:12s} M={M:8d} N={N:5d} K={K:5d} {dt*1e6:8.1f} us {fl/dt/1e12:7.1f} TF/s  {kn}")
     print(f"total {tot_t*1e3:.2f} ms  {tot_f/tot_t/1e12:.1f} TF/s")
 
