@@ -57,6 +57,8 @@ extern "C" {
 
 #define VD_PREC_BF16 0       /* bf16 operands, f32 accumulate (performance mode) */
 #define VD_PREC_FP32 1       /* f32 operands, exact-f32 MFMA (parity mode)       */
+#define VD_PREC_FP16 2       /* fp16 operands, f32 accumulate (implicit GEMM on   *
+                              * v_mfma_f32_16x16x32_f16; no bf16-only fusions)    */
 
 #define VD_NET_RETINAFACE 0  /* detect_face/retinaface.py, cfg_re50 */
 #define VD_NET_YOLOV8N    1  /* ultralytics YOLOv8n plate detector [ext] */

@@ -68,6 +68,46 @@ def test_heads_bf16_close(gpu, face_ctx_factory, wkind):
     assert _rel(loc, eloc) < 6e-2 and _rel(conf, econf) < 6e-2
 
 
+@pytest.mark.parametrize("h,w,wkind", [(1080, 1920, "default"), (2160, 3840, "default"), (1080, 1920, "mnet")])
+def test_heads_fp16_close(gpu, face_ctx_factory, h, w, wkind):
+    """fp16 mode (VD_PREC_FP16: fp16 operands and activations on
+    v_mfma_f32_16x16x32_f16, f32 accumulation; BASELINE config 5 names the fp16
+    conv path, here with 4K frames): 10 mantissa bits against bf16's 7, so the
+    heads sit an order of magnitude closer to the f32 oracle than bf16's."""
+    ctx = face_ctx_factory("fp16", 2, wkind)
+    fr = _frames(2, h, w, seed=17)
+    loc, conf, ldm = ctx.forward_heads(fr)
+    eloc, econf, eldm = _oracle_heads(fr, wkind)
+    assert _rel(loc, eloc) < 1e-2 and _rel(conf, econf) < 1e-2 and _rel(ldm, eldm) < 1e-2
+
+
+def test_detect_fp16_agrees_4k(gpu, face_ctx_factory):
+    """fp16 detect + box correction on 4K frames against the f32 oracle's boxes. The
+    4K frames are 2x nearest upsamples of 1080p synthetic frames, so the ratio-6
+    letterbox (0.5/0.5 bilinear of rows/cols 6x+2, 6x+3) sees real structure and the
+    calibrated random weights fire (raw 4K noise averages out to no faces)."""
+    ctx = face_ctx_factory("fp16", 2)
+    fr = np.repeat(np.repeat(_frames(2, 1080, 1920, seed=17), 2, axis=1), 2, axis=2)
+    got = ctx.detect(fr)
+    eloc, econf, _ = _oracle_heads(fr)
+    pri = oanchors.get_anchors((640, 640))
+    matched = total = 0
+    for b in range(2):
+        _, boxes, _ = obbox.postprocess_frame(eloc[b], econf[b], pri, 0.5, 0.4)
+        e = obbox.correct_and_scale(boxes, 2160, 3840)
+        g = got.frame(b)[1]
+        total += len(e)
+        for r in e:
+            if len(g) == 0:
+                break
+            x1 = np.maximum(r[0], g[:, 0]); y1 = np.maximum(r[1], g[:, 1])
+            x2 = np.minimum(r[2], g[:, 2]); y2 = np.minimum(r[3], g[:, 3])
+            inter = np.clip(x2 - x1, 0, None) * np.clip(y2 - y1, 0, None)
+            iou = inter / ((r[2] - r[0]) * (r[3] - r[1]) + (g[:, 2] - g[:, 0]) * (g[:, 3] - g[:, 1]) - inter)
+            matched += iou.max() >= 0.9
+    assert total > 0 and matched / total >= 0.95, (matched, total)
+
+
 def test_heads_bf16_fused_downsample_matches_unfused(gpu, monkeypatch):
     """bf16 plans fuse each bottleneck's conv3 + downsample into one streaming pass
     (layer1.0, layer2.0); VD_CONV_DUAL=0 at weight load keeps them separate. The

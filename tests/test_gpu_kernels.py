@@ -192,8 +192,8 @@ CONV_CASES = [
 ]
 
 
-@pytest.mark.parametrize("prec", ["fp32", "bf16", "bf16-gemm64", "bf16-gemm128", "bf16-gemm256", "bf16-persist64",
-                                  "bf16-persist128"])
+@pytest.mark.parametrize("prec", ["fp32", "bf16", "fp16", "bf16-gemm64", "bf16-gemm128", "bf16-gemm256",
+                                  "bf16-persist64", "bf16-persist128"])
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv_matches_torch(gpu, face_ctx_factory, monkeypatch, prec, case):
     """bf16: the default dispatch (streaming 1x1 / streaming taps / persistent GEMM / GEMM);
@@ -223,8 +223,9 @@ def test_conv_matches_torch(gpu, face_ctx_factory, monkeypatch, prec, case):
     shift = rng.standard_normal(cout).astype(F32) * F32(0.1)
     oh, ow = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
     res = rng.standard_normal((n, oh, ow, cout)).astype(F32) if res_mode else None
-    if prec == "bf16":   # the kernel sees bf16 operands: compare against the same rounded inputs
-        bf = lambda a: torch.from_numpy(a).bfloat16().float().numpy()
+    if prec in ("bf16", "fp16"):   # the kernel sees 16-bit operands: compare against the same rounded inputs
+        dt = torch.bfloat16 if prec == "bf16" else torch.float16
+        bf = lambda a: torch.from_numpy(a).to(dt).float().numpy()
         x, wt = bf(x), bf(wt)
         res = bf(res) if res is not None else None
     got = ctx.conv2d(x, wt, s, p, scale, shift, act, 0.1, res, res_mode)
@@ -237,7 +238,7 @@ def test_conv_matches_torch(gpu, face_ctx_factory, monkeypatch, prec, case):
          3: lambda v: v / (1 + np.exp(-v))}[act](y)
     if res_mode == 2:
         y = y + res
-    tol = 2e-5 if prec == "fp32" else 2e-2
+    tol = {"fp32": 2e-5, "fp16": 1e-3}.get(prec, 2e-2)
     err = np.abs(got - y).max() / (np.abs(y).max() + 1e-6)
     assert got.shape == y.shape
     assert err < tol, f"rel err {err}"

@@ -52,6 +52,14 @@ def test_plate_raw_fp32(gpu, h, w):
     assert _rel(got, exp) < 1e-4
 
 
+def test_plate_raw_fp16_close(gpu):
+    from vdmi import synth
+    fr = synth.frames(2, 1080, 1920, seed=5)
+    got = _ctx("fp16").plate_raw(fr)
+    exp, _, _ = _oracle_raw(fr)
+    assert _rel(got[:, 64:], exp[:, 64:]) < 1e-2
+
+
 def test_plate_raw_bf16_close(gpu):
     from vdmi import synth
     fr = synth.frames(2, 1080, 1920, seed=5)

@@ -53,7 +53,7 @@ bool is_conv(const Conv& c, int cin, int cout, int k, int stride, int pad, int a
 }  // namespace
 
 bool Ctx::block_ok(int c1, int c2, int c3, int cd, const Act& x) const {
-    if (f32 || x.f32) return false;
+    if (f32 || f16 || x.f32) return false;
     const bool ds = cd >= 0;
     const int cin = x.c;
     if (!vd_block_ok(cin, ds, x.h, x.w)) return false;
@@ -128,7 +128,7 @@ int Ctx::add_block(Net& net, int bi, const Act& x, Act& y) {
 // stem conv (space-to-depth 4x4, 16 -> 64) + maxpool 3x3/2 (stem.hip)
 int Ctx::add_stem_pool(Net& net, int ci, const Act& x, Act& y) {
     const Conv& cv = convs[ci];
-    if (f32 || x.f32 || y.f32 || cv.cin != 16 || cv.cin_pad != 16 || cv.cout != 64 || cv.kh != 4 || cv.kw != 4 ||
+    if (f32 || f16 || x.f32 || y.f32 || cv.cin != 16 || cv.cin_pad != 16 || cv.cout != 64 || cv.kh != 4 || cv.kw != 4 ||
         cv.stride != 1 || cv.pad != 1 || cv.act != VD_ACT_RELU || cv.kpad != 256 || x.c != 16 || y.c != 64 ||
         !vd_stem_pool_ok(x.h, x.w, y.h, y.w))
         return vd_set_error(VD_ERR_ARG, "fused stem plan shape mismatch");
@@ -198,7 +198,7 @@ extern "C" int vdt_bottleneck(vd_ctx* h, const float* x, int n, int hh, int ww, 
     if (!ctx) return vd_set_error(VD_ERR_ARG, "null context");
     std::lock_guard<std::mutex> lk(ctx->mu);
     if (hipSetDevice(ctx->device) != hipSuccess) return vd_set_error(VD_ERR_HIP, "hipSetDevice failed");
-    if (ctx->f32) return vd_set_error(VD_ERR_ARG, "vdt_bottleneck: bf16 contexts only");
+    if (ctx->f32 || ctx->f16) return vd_set_error(VD_ERR_ARG, "vdt_bottleneck: bf16 contexts only");
     if (n <= 0 || hh <= 0 || ww <= 0 || !x || !w1 || !w2 || !w3 || !bn1 || !bn2 || !bn3 || !y ||
         (cin != 64 && cin != 256) || (wd && !bnd) || (!wd && cin != 256))
         return vd_set_error(VD_ERR_ARG, "vdt_bottleneck: bad arguments");

@@ -35,6 +35,7 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));   // native vector (
 
 template <typename T> struct Elem;
 template <> struct Elem<__bf16> { static constexpr int VEC = 8; };
+template <> struct Elem<_Float16> { static constexpr int VEC = 8; };
 template <> struct Elem<float>  { static constexpr int VEC = 4; };
 
 __device__ __forceinline__ int lds_off(int row, int chunk) {
@@ -51,7 +52,7 @@ __device__ __forceinline__ float act_apply(float v, int act, float slope) {
 template <typename T>
 __device__ __forceinline__ float load_elem(const void* p, size_t off) {
     if constexpr (std::is_same<T, float>::value) return ((const float*)p)[off];
-    else return (float)((const __bf16*)p)[off];
+    else return (float)((const T*)p)[off];
 }
 
 // 16 zero bytes: the LDS-DMA source of padding taps (conv zero padding, K padding).
@@ -237,6 +238,10 @@ __global__ __launch_bounds__(NT) void conv_igemm_kernel(ConvArgs a) {
                     const float* fb = (const float*)&bfr[j];                              \
                     _Pragma("unroll") for (int e = 0; e < 4; ++e)                         \
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[e], fb[e], acc[i][j], 0, 0, 0); \
+                } else if constexpr (std::is_same<T, _Float16>::value) {                  \
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(                   \
+                        __builtin_bit_cast(f16x8_t, af[i]), __builtin_bit_cast(f16x8_t, bfr[j]), \
+                        acc[i][j], 0, 0, 0);                                              \
                 } else {                                                                  \
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(                  \
                         __builtin_bit_cast(bf16x8_t, af[i]), __builtin_bit_cast(bf16x8_t, bfr[j]), \
@@ -339,7 +344,9 @@ __global__ __launch_bounds__(NT) void conv_igemm_kernel(ConvArgs a) {
                 const float4 e0 = *(const float4*)er, e1 = *(const float4*)(er + 4);
                 const float ev[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
                 if (pf) {
-                    const bf16x8_t rb8 = __builtin_bit_cast(bf16x8_t, rpf[q]);
+                    using H = typename std::conditional<std::is_same<T, float>::value, __bf16, T>::type;
+                    typedef H t8_t __attribute__((ext_vector_type(8)));
+                    const t8_t rb8 = __builtin_bit_cast(t8_t, rpf[q]);
 #pragma unroll
                     for (int e = 0; e < 8; ++e) rv[e] = (float)rb8[e];
                 } else if (a.res_mode != VD_RES_NONE) {   // f32 residual, read here
@@ -366,10 +373,12 @@ __global__ __launch_bounds__(NT) void conv_igemm_kernel(ConvArgs a) {
                     *(float4*)((float*)a.y + yo) = make_float4(v[0], v[1], v[2], v[3]);
                     *(float4*)((float*)a.y + yo + 4) = make_float4(v[4], v[5], v[6], v[7]);
                 } else {
-                    bf16x8_t o;
+                    using H = typename std::conditional<std::is_same<T, float>::value, __bf16, T>::type;
+                    typedef H t8_t __attribute__((ext_vector_type(8)));
+                    t8_t o;
 #pragma unroll
-                    for (int e = 0; e < 8; ++e) o[e] = (__bf16)v[e];
-                    *(bf16x8_t*)((__bf16*)a.y + yo) = o;
+                    for (int e = 0; e < 8; ++e) o[e] = (H)v[e];
+                    *(t8_t*)((H*)a.y + yo) = o;
                 }
             } else {
                 size_t roff = 0;
@@ -390,7 +399,7 @@ __global__ __launch_bounds__(NT) void conv_igemm_kernel(ConvArgs a) {
                     t = act_apply(t, a.act, a.slope);
                     if (a.res_mode == VD_RES_POST_ACT) t += rv;
                     if (a.out_f32 || std::is_same<T, float>::value) ((float*)a.y)[yo + e] = t;
-                    else ((__bf16*)a.y)[yo + e] = (__bf16)t;
+                    else ((T*)a.y)[yo + e] = (T)t;
                 }
             }
         }
@@ -434,8 +443,20 @@ hipError_t vd_launch_conv(const ConvArgs& a, bool f32, hipStream_t s) {
     const int bke = 8 * vec;
     const bool dense = (a.cin_pad % bke) == 0;
     if (a.x2) {   // fused conv3 + downsample: planned only where the dual streaming kernel applies
-        if (f32 || !vd_conv1x1_dual_ok(a)) return hipErrorInvalidValue;
+        if (f32 || a.f16 || !vd_conv1x1_dual_ok(a)) return hipErrorInvalidValue;
         return vd_launch_conv1x1_stream(a, s);
+    }
+    if (a.f16) {   // fp16 mode (VD_PREC_FP16): the implicit GEMM on v_mfma_f32_16x16x32_f16
+        const int bn = a.cout <= 32 ? 32 : (a.cout <= 64 ? 64 : 128);
+        const long tiles128 = (long)((a.M + 127) / 128) * ((a.cout + bn - 1) / bn);
+        if (tiles128 < 512) {
+            if (bn == 32) return launch_bn<_Float16, 64, 32>(a, dense, s);
+            if (bn == 64) return launch_bn<_Float16, 64, 64>(a, dense, s);
+            return launch_bn<_Float16, 64, 128>(a, dense, s);
+        }
+        if (bn == 32) return launch_bn<_Float16, 128, 32>(a, dense, s);
+        if (bn == 64) return launch_bn<_Float16, 128, 64>(a, dense, s);
+        return launch_bn<_Float16, 128, 128>(a, dense, s);
     }
     if (!f32 && vd_conv1x1_stream_ok(a)) return vd_launch_conv1x1_stream(a, s);
     if (!f32 && vd_conv_big_ok(a)) return vd_launch_conv_big(a, s);

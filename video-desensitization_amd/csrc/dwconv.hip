@@ -16,6 +16,7 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 template <typename T> struct DwVec;
 template <> struct DwVec<__bf16> { static constexpr int N = 8; };
+template <> struct DwVec<_Float16> { static constexpr int N = 8; };
 template <> struct DwVec<float>  { static constexpr int N = 4; };
 
 __device__ __forceinline__ float act_apply(float v, int act, float slope) {
@@ -68,13 +69,14 @@ __global__ __launch_bounds__(256) void dwconv3x3_kernel(DwConvArgs a) {
 
 }  // namespace
 
-hipError_t vd_launch_dwconv(const DwConvArgs& a, bool f32, hipStream_t s) {
+hipError_t vd_launch_dwconv(const DwConvArgs& a, bool f32, bool f16, hipStream_t s) {
     const int n = f32 ? 4 : 8;
     if (a.c % n || a.ldx % n || a.xcoff % n || a.ldy % n || a.ycoff % n) return hipErrorInvalidValue;
     const long total = (long)a.B * a.yh * a.yw * (a.c / n);
     if (total <= 0) return hipSuccess;
     const dim3 grid((unsigned)((total + 255) / 256));
     if (f32) hipLaunchKernelGGL(dwconv3x3_kernel<float>, grid, dim3(256), 0, s, a);
+    else if (f16) hipLaunchKernelGGL(dwconv3x3_kernel<_Float16>, grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL(dwconv3x3_kernel<__bf16>, grid, dim3(256), 0, s, a);
     return hipGetLastError();
 }

@@ -117,7 +117,7 @@ int vd_build_face(Ctx& c, const WMap& W) {
     const int cpad = c.f32 ? 4 : 8;
     int rc;
     F.mnet = find_t(W, "body.stage1.0.0.weight") != nullptr;   // cfg_mnet (face.py:35, retinaface.py:60)
-    F.s2d = !c.f32 && !F.mnet && H % 2 == 0 && Wd % 2 == 0;
+    F.s2d = !c.f32 && !c.f16 && !F.mnet && H % 2 == 0 && Wd % 2 == 0;
     if (F.s2d) rc = c.act(F.input, H / 2 + 1, Wd / 2 + 1, 16);
     else rc = c.act(F.input, H, Wd, cpad);
     if (rc) return rc;

@@ -134,6 +134,7 @@ struct Ctx {
     vd_cfg cfg{};
     int device = 0;
     bool f32 = false;
+    bool f16 = false;                             // VD_PREC_FP16: fp16 operands/activations (GEMM path only)
     hipStream_t stream = nullptr, own_stream = nullptr;
     hipStream_t stream2 = nullptr;               // plate branch runs beside the face branch
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;

@@ -285,7 +285,7 @@ int vd_plate_forward(Ctx& c, const uint8_t* d, int n, int h, int w, size_t pitch
     a.mean[0] = a.mean[1] = a.mean[2] = 0.f;
     a.div = 255.f;
     a.flip = 1;   // im[..., ::-1]: the RGB frames are treated as BGR
-    a.out = P.input.p; a.cpad = P.input.c; a.out_f32 = c.f32 ? 1 : 0;
+    a.out = P.input.p; a.cpad = P.input.c; a.out_f32 = c.f32 ? 1 : 0; a.out_f16 = c.f16 ? 1 : 0;
     c.t_begin(2, (double)n * (nh * (double)w * 3 + (double)oh * ow * a.cpad * (c.f32 ? 4 : 2)));
     hipError_t e = vd_launch_letterbox(a, c.stream);
     c.t_end();

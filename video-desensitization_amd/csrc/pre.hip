@@ -206,6 +206,13 @@ __global__ __launch_bounds__(256) void letterbox_kernel(LetterboxArgs a) {
         float4 w0 = make_float4(v[0], v[1], v[2], 0.f);
         *(float4*)out = w0;
         for (int c = 4; c < a.cpad; c += 4) *(float4*)(out + c) = make_float4(0.f, 0.f, 0.f, 0.f);
+    } else if (a.out_f16) {   // integers in [-123, 151]: exact in fp16 as in bf16
+        _Float16* out = (_Float16*)a.out + o;
+        _Float16 tmp[8];
+        tmp[0] = (_Float16)v[0]; tmp[1] = (_Float16)v[1]; tmp[2] = (_Float16)v[2];
+        for (int c = 3; c < 8; ++c) tmp[c] = (_Float16)0.f;
+        *(uint4*)out = *(const uint4*)tmp;
+        for (int c = 8; c < a.cpad; c += 8) *(uint4*)(out + c) = make_uint4(0, 0, 0, 0);
     } else {
         __bf16* out = (__bf16*)a.out + o;
         __bf16 tmp[8];
@@ -294,7 +301,7 @@ hipError_t vd_launch_letterbox(const LetterboxArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t vd_launch_maxpool(bool f32, const void* x, int n, int xh, int xw, int ldx, int xcoff,
+hipError_t vd_launch_maxpool(bool f32, bool f16, const void* x, int n, int xh, int xw, int ldx, int xcoff,
                              void* y, int yh, int yw, int ldy, int ycoff, int c, int k, int st, int p,
                              hipStream_t s) {
     const int vec = f32 ? 4 : 8;
@@ -303,12 +310,16 @@ hipError_t vd_launch_maxpool(bool f32, const void* x, int n, int xh, int xw, int
     if (f32)
         hipLaunchKernelGGL(maxpool_kernel<float>, grid, dim3(256), 0, s, (const float*)x, xh, xw, ldx, xcoff,
                            (float*)y, yh, yw, ldy, ycoff, c, k, st, p, total);
+    else if (f16)
+        hipLaunchKernelGGL(maxpool_kernel<_Float16>, grid, dim3(256), 0, s, (const _Float16*)x, xh, xw, ldx, xcoff,
+                           (_Float16*)y, yh, yw, ldy, ycoff, c, k, st, p, total);
     else
         hipLaunchKernelGGL(maxpool_kernel<__bf16>, grid, dim3(256), 0, s, (const __bf16*)x, xh, xw, ldx, xcoff,
                            (__bf16*)y, yh, yw, ldy, ycoff, c, k, st, p, total);
     return hipGetLastError();
 }
 
+// (a pure copy: the bf16 instantiation moves fp16 bits unchanged)
 hipError_t vd_launch_upsample2x(bool f32, const void* x, int n, int xh, int xw, int ldx, int xcoff,
                                 void* y, int ldy, int ycoff, int c, hipStream_t s) {
     const int vec = f32 ? 4 : 8;

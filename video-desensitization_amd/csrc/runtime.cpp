@@ -117,6 +117,29 @@ static uint16_t f32_to_bf16_rne(float f) {
     return (uint16_t)(u >> 16);
 }
 
+static uint16_t f32_to_f16_rne(float f) {   // IEEE binary16, round to nearest even (clang _Float16)
+    const _Float16 h = (_Float16)f;
+    uint16_t u;
+    memcpy(&u, &h, 2);
+    return u;
+}
+
+static float f16_bits_to_f32(uint16_t u) {
+    _Float16 h;
+    memcpy(&h, &u, 2);
+    return (float)h;
+}
+
+// host-side 16-bit encoding of the context's half type
+static inline uint16_t to_half(bool f16, float v) { return f16 ? f32_to_f16_rne(v) : f32_to_bf16_rne(v); }
+static inline float from_half(bool f16, uint16_t u) {
+    if (f16) return f16_bits_to_f32(u);
+    uint32_t w = (uint32_t)u << 16;
+    float v;
+    memcpy(&v, &w, 4);
+    return v;
+}
+
 int Ctx::upload_conv(Conv& cv, const std::vector<float>& w_oihw, const std::vector<float>& scale,
                      const std::vector<float>& shift) {
     const int vec = f32 ? 4 : 8;
@@ -139,7 +162,7 @@ int Ctx::upload_conv(Conv& cv, const std::vector<float>& w_oihw, const std::vect
         VD_CHECK_HIP(hipMemcpy(cv.w, packed.data(), packed.size() * 4, hipMemcpyHostToDevice));
     } else {
         std::vector<uint16_t> h(packed.size());
-        for (size_t i = 0; i < packed.size(); ++i) h[i] = f32_to_bf16_rne(packed[i]);
+        for (size_t i = 0; i < packed.size(); ++i) h[i] = to_half(f16, packed[i]);
         rc = dalloc(&cv.w, h.size() * 2);
         if (rc) return rc;
         VD_CHECK_HIP(hipMemcpy(cv.w, h.data(), h.size() * 2, hipMemcpyHostToDevice));
@@ -218,7 +241,7 @@ int Ctx::make_dwconv_bn(const WMap& W, const std::string& wkey, const std::strin
         VD_CHECK_HIP(hipMemcpy(d.w, wt.data(), wt.size() * 4, hipMemcpyHostToDevice));
     } else {
         std::vector<uint16_t> h(wt.size());
-        for (size_t i = 0; i < wt.size(); ++i) h[i] = f32_to_bf16_rne(wt[i]);
+        for (size_t i = 0; i < wt.size(); ++i) h[i] = to_half(f16, wt[i]);
         if ((rc = dalloc(&d.w, h.size() * 2))) return rc;
         VD_CHECK_HIP(hipMemcpy(d.w, h.data(), h.size() * 2, hipMemcpyHostToDevice));
     }
@@ -270,7 +293,7 @@ int Ctx::make_conv_cat(const WMap& W, const std::vector<std::string>& wkeys, con
 
 // Bottleneck conv3 (ci on x) + downsample (c2 on x2, strided 1x1) in one op.
 bool Ctx::dual_ok(int ci, int c2, const Act& y) const {
-    if (f32) return false;
+    if (f32 || f16) return false;
     const Conv& a = convs[ci];
     const Conv& b = convs[c2];
     ConvArgs t{};
@@ -347,6 +370,7 @@ int Ctx::run_conv_op(const Op& op, int f0, int n, int fam) {
     a.kh = cv.kh; a.kw = cv.kw; a.stride = cv.stride; a.pad = cv.pad;
     a.M = n * op.y.h * op.y.w;
     a.act = cv.act; a.slope = cv.slope; a.out_f32 = op.y.f32 ? 1 : 0;
+    a.f16 = f16 ? 1 : 0;
     double flops = cv.flops_per_px * a.M;
     if (op.conv2 >= 0) {
         const Conv& c2 = convs[op.conv2];
@@ -370,7 +394,7 @@ int Ctx::run_dwconv_op(const Op& op, int f0, int n) {
     a.y = (void*)foff(op.y, f0); a.yh = op.y.h; a.yw = op.y.w; a.ldy = op.y.c; a.ycoff = 0;
     a.B = n; a.c = d.c; a.stride = d.stride; a.act = d.act; a.slope = d.slope;
     t_begin(4, 0);
-    hipError_t e = vd_launch_dwconv(a, f32, stream);
+    hipError_t e = vd_launch_dwconv(a, f32, f16, stream);
     t_end();
     if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "depthwise conv: %s", hipGetErrorString(e));
     return VD_OK;
@@ -390,7 +414,7 @@ int Ctx::run_ops(const Net& net, int b, int e, int f0, int n) {
             rc = run_dwconv_op(op, f0, n);
         } else if (op.kind == OP_MAXPOOL) {
             t_begin(4, 0);
-            hipError_t er = vd_launch_maxpool(f32, foff(op.x, f0), n, op.x.h, op.x.w, op.x.c, op.xcoff,
+            hipError_t er = vd_launch_maxpool(f32, f16, foff(op.x, f0), n, op.x.h, op.x.w, op.x.c, op.xcoff,
                                               (void*)foff(op.y, f0), op.y.h, op.y.w, op.y.c, op.ycoff, op.ch, op.k,
                                               op.s, op.p, stream);
             t_end();
@@ -505,7 +529,7 @@ int Ctx::face_letterbox(const uint8_t* dframes, int n, int h, int w, size_t pitc
     a.mean[0] = 104.f; a.mean[1] = 117.f; a.mean[2] = 123.f;
     a.div = 1.f;
     a.flip = 0;
-    a.out = face.input.p; a.cpad = face.input.c; a.out_f32 = f32 ? 1 : 0;
+    a.out = face.input.p; a.cpad = face.input.c; a.out_f32 = f32 ? 1 : 0; a.out_f16 = f16 ? 1 : 0;
     a.s2d = face.s2d ? 1 : 0;
     t_begin(2, (double)n * (a.nh * (double)w * 3 + (double)a.oh * a.ow * a.cpad * (f32 ? 4 : 2)));
     hipError_t e = vd_launch_letterbox(a, stream);
@@ -613,7 +637,8 @@ int vd_create(const vd_cfg* cfg, int device, vd_ctx** out) {
     if (cfg) c = *cfg; else vd_default_cfg(&c);
     if (c.max_batch <= 0 || c.input_h % 32 || c.input_w % 32 || c.input_h <= 0 || c.input_w <= 0)
         return vd_set_error(VD_ERR_ARG, "cfg: max_batch>0 and input dims multiple of 32 required");
-    if (c.precision != VD_PREC_BF16 && c.precision != VD_PREC_FP32) return vd_set_error(VD_ERR_ARG, "cfg: bad precision");
+    if (c.precision != VD_PREC_BF16 && c.precision != VD_PREC_FP32 && c.precision != VD_PREC_FP16)
+        return vd_set_error(VD_ERR_ARG, "cfg: bad precision");
     if (c.mosaic_level <= 0) c.mosaic_level = 8;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
@@ -623,6 +648,7 @@ int vd_create(const vd_cfg* cfg, int device, vd_ctx** out) {
     ctx->cfg = c;
     ctx->device = device;
     ctx->f32 = c.precision == VD_PREC_FP32;
+    ctx->f16 = c.precision == VD_PREC_FP16;
     if (hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return vd_set_error(VD_ERR_HIP, "hipStreamCreate failed");
@@ -942,7 +968,7 @@ int vdt_letterbox(vd_ctx* h, const uint8_t* frames, int n, int fh, int fw, size_
             float v = 0.f;
             if (c < in.c) {
                 if (ctx->f32) v = hf[i * in.c + c];
-                else { uint32_t u = (uint32_t)hb[i * in.c + c] << 16; memcpy(&v, &u, 4); }
+                else v = from_half(ctx->f16, hb[i * in.c + c]);
             }
             out[i * cpad + c] = v;
         }
@@ -1034,7 +1060,7 @@ int vdt_conv2d(vd_ctx* h, const float* x, int n, int xh, int xw, int cin, const 
         for (int c = 0; c < cin; ++c) {
             float v = x[p * cin + c];
             if (ctx->f32) memcpy(&xb[(p * ldx + c) * 4], &v, 4);
-            else { uint16_t b = f32_to_bf16_rne(v); memcpy(&xb[(p * ldx + c) * 2], &b, 2); }
+            else { uint16_t b = to_half(ctx->f16, v); memcpy(&xb[(p * ldx + c) * 2], &b, 2); }
         }
     void *dx = nullptr, *dy = nullptr, *dr = nullptr;
     if ((rc = ctx->dalloc(&dx, xb.size()))) return rc;
@@ -1046,7 +1072,7 @@ int vdt_conv2d(vd_ctx* h, const float* x, int n, int xh, int xw, int cin, const 
             for (int c = 0; c < cout; ++c) {
                 float v = res[p * cout + c];
                 if (ctx->f32) memcpy(&rb[(p * ldy + c) * 4], &v, 4);
-                else { uint16_t b = f32_to_bf16_rne(v); memcpy(&rb[(p * ldy + c) * 2], &b, 2); }
+                else { uint16_t b = to_half(ctx->f16, v); memcpy(&rb[(p * ldy + c) * 2], &b, 2); }
             }
         if ((rc = ctx->dalloc(&dr, rb.size()))) return rc;
         VD_CHECK_HIP(hipMemcpy(dr, rb.data(), rb.size(), hipMemcpyHostToDevice));
@@ -1059,7 +1085,7 @@ int vdt_conv2d(vd_ctx* h, const float* x, int n, int xh, int xw, int cin, const 
     a.y = dy; a.yh = oh; a.yw = ow; a.ldy = ldy; a.ycoff = 0;
     a.B = n; a.cin_pad = cv.cin_pad; a.cout = cout; a.kpad = cv.kpad;
     a.kh = kh; a.kw = kw; a.stride = stride; a.pad = pad; a.M = n * oh * ow;
-    a.act = act; a.slope = slope; a.out_f32 = 1;
+    a.act = act; a.slope = slope; a.out_f32 = 1; a.f16 = ctx->f16 ? 1 : 0;
     hipError_t e = vd_launch_conv(a, ctx->f32, ctx->stream);
     if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "conv launch: %s", hipGetErrorString(e));
     VD_CHECK_HIP(hipStreamSynchronize(ctx->stream));

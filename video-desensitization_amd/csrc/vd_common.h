@@ -6,6 +6,7 @@
 #include <stddef.h>
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 enum VdAct { VD_ACT_NONE = 0, VD_ACT_RELU = 1, VD_ACT_LEAKY = 2, VD_ACT_SILU = 3 };
@@ -26,6 +27,7 @@ struct ConvArgs {
     int kh, kw, stride, pad;
     int M;                                       // B*yh*yw
     int act; float slope; int res_mode; int out_f32;
+    int f16;                                     // 16-bit type is fp16 (VD_PREC_FP16), else bf16
     int ntiles_n;                                // ceil(cout / BN)
     // optional second 1x1 conv summed before the activation (bottleneck conv3 +
     // downsample in one pass): y = act(acc*scale + shift + acc2*scale2 + shift2)
@@ -117,6 +119,7 @@ struct LetterboxArgs {
     float div;             // divisor after mean (1, or 255 for ultralytics' im /= 255)
     int flip;              // 1: output channel c takes source channel 2-c
     void* out; int cpad; int out_f32;
+    int out_f16;           // 16-bit canvas in fp16 (VD_PREC_FP16) instead of bf16
     int s2d;               // 1: space-to-depth canvas for the stride-2 stem (bf16, 16 channels):
                            //    out[Y][X][(py*2+px)*4 + c] = canvas[2Y+py-1][2X+px-1][c], 0 off-canvas,
                            //    Y in [0, oh/2], X in [0, ow/2]
@@ -137,11 +140,11 @@ bool vd_conv_persist_ok(const ConvArgs& a);
 hipError_t vd_launch_conv_persist(const ConvArgs& a, hipStream_t s);
 bool vd_block_ok(int cin, bool ds, int h, int w);
 bool vd_stem_pool_ok(int xh, int xw, int ph, int pw);
-hipError_t vd_launch_dwconv(const DwConvArgs& a, bool f32, hipStream_t s);
+hipError_t vd_launch_dwconv(const DwConvArgs& a, bool f32, bool f16, hipStream_t s);
 hipError_t vd_launch_stem_pool(const StemPoolArgs& a, hipStream_t s);
 hipError_t vd_launch_block(const BlockArgs& a, hipStream_t s);
 hipError_t vd_launch_letterbox(const LetterboxArgs& a, hipStream_t s);
-hipError_t vd_launch_maxpool(bool f32, const void* x, int n, int xh, int xw, int ldx, int xcoff,
+hipError_t vd_launch_maxpool(bool f32, bool f16, const void* x, int n, int xh, int xw, int ldx, int xcoff,
                              void* y, int yh, int yw, int ldy, int ycoff, int c, int k, int st, int p,
                              hipStream_t s);
 hipError_t vd_launch_upsample2x(bool f32, const void* x, int n, int xh, int xw, int ldx, int xcoff,

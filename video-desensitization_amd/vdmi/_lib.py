@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("VDMI_LIB", os.path.join(HERE, "libvdmi.so"))
 VD_OK = 0
 VD_ERR_ARG, VD_ERR_HIP, VD_ERR_CAPACITY, VD_ERR_WEIGHTS, VD_ERR_STATE, VD_ERR_NOMEM = -1, -2, -3, -4, -5, -6
 VD_HOST, VD_DEVICE = 0, 1
-VD_PREC_BF16, VD_PREC_FP32 = 0, 1
+VD_PREC_BF16, VD_PREC_FP32, VD_PREC_FP16 = 0, 1, 2
 VD_NET_RETINAFACE, VD_NET_YOLOV8N = 0, 1
 VD_WEIGHTS_VDW1 = 1
 VD_MOSAIC_OUT_OF_PLACE = 0

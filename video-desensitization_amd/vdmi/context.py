@@ -62,7 +62,14 @@ class Context:
         cfg = _lib.default_cfg()
         cfg.input_h, cfg.input_w = int(input_shape[0]), int(input_shape[1])
         cfg.max_batch = int(max_batch)
-        cfg.precision = _lib.VD_PREC_FP32 if precision in ("fp32", "f32", "float32") else _lib.VD_PREC_BF16
+        if precision in ("fp32", "f32", "float32"):
+            cfg.precision = _lib.VD_PREC_FP32
+        elif precision in ("fp16", "f16", "float16", "half"):
+            cfg.precision = _lib.VD_PREC_FP16
+        elif precision in ("bf16", "bfloat16"):
+            cfg.precision = _lib.VD_PREC_BF16
+        else:
+            raise ValueError(f"precision {precision!r}: expected 'bf16', 'fp16' or 'fp32'")
         cfg.confidence = float(confidence)
         cfg.nms_iou = float(nms_iou)
         cfg.max_boxes = int(max_boxes)
@@ -73,7 +80,7 @@ class Context:
         cfg.reserved[0], cfg.reserved[1] = int(microbatch), int(microbatch_stage)
         self.cfg = cfg
         self.device = int(device)
-        self.precision = "fp32" if cfg.precision == _lib.VD_PREC_FP32 else "bf16"
+        self.precision = {_lib.VD_PREC_FP32: "fp32", _lib.VD_PREC_FP16: "fp16"}.get(cfg.precision, "bf16")
         h = ctypes.c_void_p()
         check(lib.vd_create(ctypes.byref(cfg), self.device, ctypes.byref(h)))
         self._h = h
