@@ -271,3 +271,23 @@ def test_retinaface_drop_in_mobilenet(gpu):
     raw = det.detect_boxes(imgs)
     for (_, boxes), (xf, xi, _) in zip(res, raw):
         assert [[int(v) for v in b] for b in boxes] == xi.tolist()
+
+
+def test_heads_bf16_chain_matches_unfused(gpu, monkeypatch):
+    """bf16 plans run layer2's conv3(+bn3+identity+relu) and the next block's conv1
+    (+bn1+relu) as one kernel (chain.hip: the block output is handed over in LDS as
+    MFMA B fragments); VD_CHAIN=0 keeps the two streaming launches. Same bf16 weights,
+    same K order and the same bf16 rounding points."""
+    import vdmi
+    fr = _frames(2, 1080, 1920, seed=11)
+    out = {}
+    for chain in ("1", "0"):
+        monkeypatch.setenv("VD_CHAIN", chain)
+        ctx = vdmi.Context(precision="bf16", max_batch=2)
+        try:
+            ctx.load_weights(0, face_weights("default"))
+            out[chain] = ctx.forward_heads(fr)
+        finally:
+            ctx.close()
+    for a, b in zip(out["1"], out["0"]):
+        assert _rel(a, b) < 2e-3, _rel(a, b)

@@ -8,10 +8,12 @@ import csv
 import sys
 
 
-def face_plan(B=64, H=640, W=640, fused=True, block=True):
+def face_plan(B=64, H=640, W=640, fused=True, block=True, chain=True):
     """(name, M, N, K) of every conv launch in face_net.cpp order; with `block` the
     three layer1 bottlenecks are one launch each (block.hip), K = their summed
-    reduction depth per output channel of 256 (same FLOPs)."""
+    reduction depth per output channel of 256 (same FLOPs); with `chain`
+    layer2.1/2.2's conv3 runs with the next block's conv1 (chain.hip, N=512 K=256
+    carries both layers' FLOPs)."""
     L = []
     h, w = H // 2, W // 2
     L.append(("stem7x7", B * h * w, 64, 3 * 49))
@@ -25,7 +27,10 @@ def face_plan(B=64, H=640, W=640, fused=True, block=True):
                 L.append((f"l1.{bi}.block", B * h * w, 256, k))
                 cin = planes * 4
                 continue
-            L.append((f"l{li+1}.{bi}.c1", B * h * w, planes, cin))
+            if chain and li == 1 and bi in (2, 3):
+                pass                            # ran inside the previous block's chain launch
+            else:
+                L.append((f"l{li+1}.{bi}.c1", B * h * w, planes, cin))
             oh, ow = h // s, w // s
             L.append((f"l{li+1}.{bi}.c2", B * oh * ow, planes, planes * 9))
             if bi == 0 and fused and li < 2:     # bf16 plan: conv3 + downsample in one pass
@@ -33,7 +38,10 @@ def face_plan(B=64, H=640, W=640, fused=True, block=True):
             else:
                 if bi == 0:
                     L.append((f"l{li+1}.{bi}.ds", B * oh * ow, planes * 4, cin))
-                L.append((f"l{li+1}.{bi}.c3", B * oh * ow, planes * 4, planes))
+                if chain and li == 1 and bi in (1, 2):
+                    L.append((f"l2.{bi}.c3+l2.{bi+1}.c1", B * oh * ow, planes * 4, 2 * planes))
+                else:
+                    L.append((f"l{li+1}.{bi}.c3", B * oh * ow, planes * 4, planes))
             cin = planes * 4
             h, w = oh, ow
     s = [(H // 8, 512), (H // 16, 1024), (H // 32, 2048)]
@@ -55,9 +63,9 @@ def main(path, B=64):
     # The face forward may share the GPU with the plate network on a second
     # stream: anchor on the last face letterbox (space-to-depth form in bf16)
     # and take the conv launches that follow it on the same stream.
-    conv_keys = ("conv_igemm", "conv1x1_stream", "conv_big", "bottleneck_kernel", "stem_pool_kernel")
-    if not any("bottleneck_kernel" in r["Kernel_Name"] for r in allk):
-        plan = face_plan(B, block=False)
+    conv_keys = ("conv_igemm", "conv1x1_stream", "conv_big", "bottleneck_kernel", "stem_pool_kernel", "chain_kernel")
+    plan = face_plan(B, block=any("bottleneck_kernel" in r["Kernel_Name"] for r in allk),
+                     chain=any("chain_kernel" in r["Kernel_Name"] for r in allk))
     li = max(i for i, r in enumerate(allk) if "letterbox_s2d" in r["Kernel_Name"]
              or ("letterbox_kernel" in r["Kernel_Name"] and int(r["Grid_Size_Y"]) == 640))
     stream = allk[li]["Stream_Id"]
@@ -71,7 +79,7 @@ def main(path, B=64):
         tot_f += fl
         n_ = r["Kernel_Name"]
         kn = ("STEM+POOL" if "stem_pool" in n_ else "BLOCK" if "bottleneck" in n_ else "BIG" if "conv_big" in n_
-              else "S:" + n_.split("<")[1][:12] if "conv1x1_stream" in n_
+              else "CHAIN" if "chain_kernel" in n_ else "S:" + n_.split("<")[1][:12] if "conv1x1_stream" in n_
               else "G:" + n_.split("conv_igemm_kernel")[1][:22] if "conv_igemm_kernel" in n_ else n_[:24])
         print(f"{name:12s} M={M:8d} N={N:5d} K={K:5d} {dt*1e6:8.1f} us {fl/dt/1e12:7.1f} TF/s  {kn}")
     print(f"total {tot_t*1e3:.2f} ms  {tot_f/tot_t/1e12:.1f} TF/s")

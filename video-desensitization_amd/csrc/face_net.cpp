@@ -151,6 +151,7 @@ int vd_build_face(Ctx& c, const WMap& W) {
     const int planes_l[4] = {64, 128, 256, 512}, blocks_l[4] = {3, 4, 6, 3}, stride_l[4] = {1, 2, 2, 2};
     for (int li = 0; li < 4; ++li) {
         const int planes = planes_l[li];
+        const size_t layer_begin = F.net.ops.size();
         for (int bi = 0; bi < blocks_l[li]; ++bi) {
             const std::string pre = "body.layer" + std::to_string(li + 1) + "." + std::to_string(bi);
             const int s = bi == 0 ? stride_l[li] : 1;
@@ -197,6 +198,7 @@ int vd_build_face(Ctx& c, const WMap& W) {
             x = out;
         }
         if (li >= 1) feats[li - 1] = x;   // layer2/3/4 -> C3/C4/C5 (config.py:26)
+        c.fuse_chains(F.net, layer_begin);   // conv3 -> next conv1 pairs (layer2, chain.hip)
         F.net.stage_end[li + 1] = (int)F.net.ops.size();
     }
     }   // ResNet-50 body

@@ -53,7 +53,7 @@ struct DwConv {
     float* shift = nullptr;
 };
 
-enum { OP_CONV = 0, OP_MAXPOOL = 1, OP_UPSAMPLE = 2, OP_BLOCK = 3, OP_STEMPOOL = 4, OP_DWCONV = 5 };
+enum { OP_CONV = 0, OP_MAXPOOL = 1, OP_UPSAMPLE = 2, OP_BLOCK = 3, OP_STEMPOOL = 4, OP_DWCONV = 5, OP_CHAIN = 6 };
 
 struct Op {
     int kind = OP_CONV;
@@ -65,6 +65,7 @@ struct Op {
     int ch = 0, k = 0, s = 0, p = 0;   // maxpool / upsample
     int blk = -1;                      // OP_BLOCK: index into Ctx::blocks (x -> y)
     void* wf = nullptr;                // OP_STEMPOOL: conv's weight fragments (conv = the stem conv)
+    Act y2;                            // OP_CHAIN: conv = conv3 (x -> y, identity r), conv2 = next conv1 (y -> y2)
 };
 
 struct Net {
@@ -176,6 +177,8 @@ struct Ctx {
                        float slope, int* idx);
     int add_dwconv(Net& net, int di, const Act& x, Act& y);
     int run_dwconv_op(const Op& op, int f0, int n);
+    int run_chain_op(const Op& op, int f0, int n, int fam = 0);
+    void fuse_chains(Net& net, size_t begin);
     int run_stem_pool_op(const Op& op, int f0, int n, int fam = 0);
     void t_begin(int fam, double work);
     void t_end();

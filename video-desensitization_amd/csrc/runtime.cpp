@@ -386,6 +386,59 @@ int Ctx::run_conv_op(const Op& op, int f0, int n, int fam) {
     return VD_OK;
 }
 
+// conv3 (+ identity) of one bottleneck and conv1 of the next in one pass (chain.hip)
+int Ctx::run_chain_op(const Op& op, int f0, int n, int fam) {
+    const Conv& c3 = convs[op.conv];
+    const Conv& c1 = convs[op.conv2];
+    ChainArgs a{};
+    a.t2 = foff(op.x, f0); a.ld_t2 = op.x.c;
+    a.res = foff(op.r, f0); a.ld_res = op.r.c;
+    a.w3 = c3.w; a.kpad3 = c3.kpad; a.sc3 = c3.scale; a.sh3 = c3.shift;
+    a.w1 = c1.w; a.kpad1 = c1.kpad; a.sc1 = c1.scale; a.sh1 = c1.shift;
+    a.y = (void*)foff(op.y, f0); a.ld_y = op.y.c;
+    a.y2 = (void*)foff(op.y2, f0); a.ld_y2 = op.y2.c;
+    a.M = n * op.y.h * op.y.w;
+    t_begin(fam, (c3.flops_per_px + c1.flops_per_px) * a.M);
+    hipError_t e = vd_launch_chain(a, stream);
+    t_end();
+    if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "chain launch: %s", hipGetErrorString(e));
+    return VD_OK;
+}
+
+// Peephole over ops [begin, end) of a bf16 plan: a bottleneck conv3 (1x1, + identity
+// before the ReLU) immediately followed by a 1x1 conv that reads exactly its output
+// (the next bottleneck's conv1) becomes one OP_CHAIN where chain.hip covers the shape.
+void Ctx::fuse_chains(Net& net, size_t begin) {
+    if (f32 || f16) return;
+    std::vector<Op> out(net.ops.begin(), net.ops.begin() + begin);
+    for (size_t i = begin; i < net.ops.size(); ++i) {
+        const Op& a = net.ops[i];
+        if (i + 1 < net.ops.size() && a.kind == OP_CONV && net.ops[i + 1].kind == OP_CONV && a.conv2 < 0) {
+            const Op& b = net.ops[i + 1];
+            const Conv& c3 = convs[a.conv];
+            const Conv& c1 = convs[b.conv];
+            const bool shape = c3.kh == 1 && c3.kw == 1 && c3.stride == 1 && c3.pad == 0 && c3.act == VD_ACT_RELU &&
+                               c1.kh == 1 && c1.kw == 1 && c1.stride == 1 && c1.pad == 0 && c1.act == VD_ACT_RELU &&
+                               a.r.p && a.rmode == VD_RES_PRE_ACT && !a.rup && a.rcoff == 0 && a.xcoff == 0 &&
+                               a.ycoff == 0 && b.conv2 < 0 && !b.r.p && b.x.p == a.y.p && b.xcoff == 0 &&
+                               b.ycoff == 0 && !a.y.f32 && !b.y.f32 && c3.cin_pad == a.x.c &&
+                               c1.cin_pad == c3.cout && a.r.h == a.y.h && a.r.w == a.y.w;
+            const long M = (long)cfg.max_batch * a.y.h * a.y.w;
+            if (shape && vd_chain_ok(c3.cin_pad, c3.cout, c3.kpad, c1.kpad, a.x.c, a.r.c, a.y.c, b.y.c, M)) {
+                Op op = a;
+                op.kind = OP_CHAIN;
+                op.conv2 = b.conv;
+                op.y2 = b.y;
+                out.push_back(op);
+                ++i;
+                continue;
+            }
+        }
+        out.push_back(a);
+    }
+    net.ops.swap(out);
+}
+
 int Ctx::run_dwconv_op(const Op& op, int f0, int n) {
     const DwConv& d = dwconvs[op.conv];
     DwConvArgs a{};
@@ -408,6 +461,8 @@ int Ctx::run_ops(const Net& net, int b, int e, int f0, int n) {
             rc = run_conv_op(op, f0, n, net.conv_fam);
         } else if (op.kind == OP_BLOCK) {
             rc = run_block_op(op, f0, n, net.conv_fam);
+        } else if (op.kind == OP_CHAIN) {
+            rc = run_chain_op(op, f0, n, net.conv_fam);
         } else if (op.kind == OP_STEMPOOL) {
             rc = run_stem_pool_op(op, f0, n, net.conv_fam);
         } else if (op.kind == OP_DWCONV) {

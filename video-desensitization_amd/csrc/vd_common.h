@@ -50,6 +50,20 @@ struct BlockArgs {
     int mode;                    // experiments (tools/convbench VD_BLOCK_MODE); 0 in production
 };
 
+// A bottleneck's conv3 (+ identity, ReLU) and the next bottleneck's conv1 in one
+// pass (chain.hip): y = relu(bn3(w3 . t2) + res) [M][512], y2 = relu(bn1'(w1 . y)) [M][128].
+struct ChainArgs {
+    const void* t2; int ld_t2;            // [M][128] bf16
+    const void* res; int ld_res;          // identity [M][512]
+    const void* w3; int kpad3;            // conv3 weights [>= 512][kpad3] bf16
+    const float* sc3; const float* sh3;   // bn3 folded
+    const void* w1; int kpad1;            // next conv1 weights [>= 128][kpad1] bf16
+    const float* sc1; const float* sh1;   // next bn1 folded
+    void* y; int ld_y;                    // block output [M][512]
+    void* y2; int ld_y2;                  // next block's t1 [M][128]
+    int M;
+};
+
 // Depthwise 3x3 conv (pad 1) + BN + activation, NHWC (dwconv.hip): MobileNetV1 conv_dw.
 struct DwConvArgs {
     const void* x; int xh, xw, ldx, xcoff;
@@ -143,6 +157,8 @@ bool vd_stem_pool_ok(int xh, int xw, int ph, int pw);
 hipError_t vd_launch_dwconv(const DwConvArgs& a, bool f32, bool f16, hipStream_t s);
 hipError_t vd_launch_stem_pool(const StemPoolArgs& a, hipStream_t s);
 hipError_t vd_launch_block(const BlockArgs& a, hipStream_t s);
+bool vd_chain_ok(int cmid, int cout, int kpad3, int kpad1, int ld_t2, int ld_res, int ld_y, int ld_y2, long M);
+hipError_t vd_launch_chain(const ChainArgs& a, hipStream_t s);
 hipError_t vd_launch_letterbox(const LetterboxArgs& a, hipStream_t s);
 hipError_t vd_launch_maxpool(bool f32, bool f16, const void* x, int n, int xh, int xw, int ldx, int xcoff,
                              void* y, int yh, int yw, int ldy, int ycoff, int c, int k, int st, int p,
