@@ -184,7 +184,7 @@ def main():
         traffic, tsrc, blur_traffic = pmc_traffic()
         roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_TFLOPS[a.precision], "unit": "TFLOP/s",
                 "frac": round(ach / PEAK_TFLOPS[a.precision], 4), "traffic": traffic,
-                "kernel": "RetinaFace conv family: stem_pool + bottleneck (fused layer1) + conv_big + conv_igemm + "
+                "kernel": "RetinaFace conv family: stem_pool + bottleneck (fused layer1) + chain (layer2) + conv_big + conv_igemm + "
                           "conv1x1_stream launches of a step (the plate net runs concurrently on a second stream)",
                 "avg_launch_ms": round(cms / max(cn, 1), 4), "launches": cn,
                 "flop_per_launch": round(cflop / max(cn, 1)), "traffic_unit": "bytes per launch (HBM, PMC)",

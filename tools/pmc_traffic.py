@@ -46,7 +46,7 @@ def main(fetch_dir, write_dir, out=None):
     mf, mnf = per_launch_named(fetch_dir, "FETCH_SIZE", "mosaic_out_kernel")
     mw, mnw = per_launch_named(write_dir, "WRITE_SIZE", "mosaic_out_kernel")
     res = {
-        "kernel": "RetinaFace conv launches (stem_pool / bottleneck / conv_big / conv_igemm / conv1x1_stream), face stream",
+        "kernel": "RetinaFace conv launches (stem_pool / bottleneck / chain / conv_big / conv_igemm / conv1x1_stream), face stream",
         "launches": {"fetch_pass": nf, "write_pass": nw},
         "fetch_size_kib_per_launch": round(f_kib, 1),
         "write_size_kib_per_launch": round(w_kib, 1),
