@@ -291,3 +291,23 @@ def test_heads_bf16_chain_matches_unfused(gpu, monkeypatch):
             ctx.close()
     for a, b in zip(out["1"], out["0"]):
         assert _rel(a, b) < 2e-3, _rel(a, b)
+
+
+def test_heads_bf16_ssh_fused_matches_unfused(gpu, monkeypatch):
+    """ReLU-SSH plans (cfg_re50) run conv5X5_1 and conv3X3 as one conv with Cout
+    64 + 128 on a 192-wide tile, writing [t5 | c3] of one concat buffer;
+    VD_SSH_FUSE=0 keeps the two convs. Every output channel sees the same K order
+    and the same rounding: the heads are identical."""
+    import vdmi
+    fr = _frames(2, 1080, 1920, seed=13)
+    out = {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("VD_SSH_FUSE", fuse)
+        ctx = vdmi.Context(precision="bf16", max_batch=2)
+        try:
+            ctx.load_weights(0, face_weights("default"))
+            out[fuse] = ctx.forward_heads(fr)
+        finally:
+            ctx.close()
+    for a, b in zip(out["1"], out["0"]):
+        np.testing.assert_array_equal(a, b)

@@ -170,6 +170,8 @@ CONV_CASES = [
     (1, 16, 16, 48, 24, 1, 1, 0, 3, 2),       # cin 48 generic, res after act
     (1, 12, 10, 256, 32, 1, 1, 0, 0, 0),      # heads (BN=32 tile)
     (1, 9, 11, 512, 200, 3, 1, 1, 2, 1),      # cout not a tile multiple, leaky
+    (2, 23, 21, 256, 192, 3, 1, 1, 1, 0),     # 192-wide N tile: fused SSH conv5X5_1 + conv3X3
+    (1, 15, 17, 64, 160, 3, 1, 1, 2, 1),      # 192-wide N tile, cout 160, leaky + residual
     # 1x1 streaming kernel (bf16, K 64/128/256/512): bottleneck conv3 / conv1 / downsample shapes
     (2, 21, 23, 64, 256, 1, 1, 0, 1, 1),      # conv3 + residual, M not a multiple of 16
     (1, 18, 18, 256, 512, 1, 2, 0, 0, 0),     # stride-2 downsample

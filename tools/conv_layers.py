@@ -8,12 +8,13 @@ import csv
 import sys
 
 
-def face_plan(B=64, H=640, W=640, fused=True, block=True, chain=True):
+def face_plan(B=64, H=640, W=640, fused=True, block=True, chain=True, ssh_fused=True):
     """(name, M, N, K) of every conv launch in face_net.cpp order; with `block` the
     three layer1 bottlenecks are one launch each (block.hip), K = their summed
     reduction depth per output channel of 256 (same FLOPs); with `chain`
     layer2.1/2.2's conv3 runs with the next block's conv1 (chain.hip, N=512 K=256
-    carries both layers' FLOPs)."""
+    carries both layers' FLOPs); with `ssh_fused` each SSH's conv5X5_1 and conv3X3
+    are one 192-channel conv."""
     L = []
     h, w = H // 2, W // 2
     L.append(("stem7x7", B * h * w, 64, 3 * 49))
@@ -52,7 +53,9 @@ def face_plan(B=64, H=640, W=640, fused=True, block=True, chain=True):
     L.append(("fpn.m1", B * s[0][0] ** 2, 256, 256 * 9))
     for l, hh in enumerate((H // 8, H // 16, H // 32)):
         m = B * hh * hh
-        L += [(f"ssh{l}.c3", m, 128, 2304), (f"ssh{l}.c51", m, 64, 2304), (f"ssh{l}.c52", m, 64, 576),
+        L += ([(f"ssh{l}.c51+c3", m, 192, 2304)] if ssh_fused else
+              [(f"ssh{l}.c3", m, 128, 2304), (f"ssh{l}.c51", m, 64, 2304)])
+        L += [(f"ssh{l}.c52", m, 64, 576),
               (f"ssh{l}.c72", m, 64, 576), (f"ssh{l}.c73", m, 64, 576), (f"head{l}", m, 32, 256)]
     return L
 

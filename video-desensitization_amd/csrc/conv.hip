@@ -474,7 +474,12 @@ hipError_t vd_launch_conv(const ConvArgs& a, bool f32, hipStream_t s) {
     const long tiles128 = (long)((a.M + 127) / 128) * ((a.cout + bn - 1) / bn);
     const char* e = getenv("VD_CONV_SMALL");
     const long small_lim = e ? atol(e) : 512;
+    // Cout 129-192 (the fused SSH conv5X5_1 + conv3X3): one 192-wide N tile instead
+    // of two 128-wide ones, so each A tile is staged once (VD_CONV_N192=0: off)
+    const char* e192 = getenv("VD_CONV_N192");
+    const bool n192 = a.cout > 128 && a.cout <= 192 && !(e192 && atoi(e192) == 0);
     if (tiles128 < small_lim) {
+        if (n192) return launch_bn<__bf16, 64, 192>(a, dense, s);
         if (bn == 32) return launch_bn<__bf16, 64, 32>(a, dense, s);
         if (bn == 64) return launch_bn<__bf16, 64, 64>(a, dense, s);
         return launch_bn<__bf16, 64, 128>(a, dense, s);
@@ -486,5 +491,6 @@ hipError_t vd_launch_conv(const ConvArgs& a, bool f32, hipStream_t s) {
         if (dense && tall_min > 0 && tiles128 >= tall_min) return launch_bn<__bf16, 256, 64>(a, dense, s);
         return launch_bn<__bf16, 128, 64>(a, dense, s);
     }
+    if (n192) return launch_bn<__bf16, 128, 192>(a, dense, s);
     return launch_bn<__bf16, 128, 128>(a, dense, s);
 }

@@ -8,13 +8,15 @@
 //   {Bbox,Class,Landmark}Head.{l}.conv1x1   1x1 heads (retinaface.py:13-51)
 // Fusions: BN (eval) + activation + residual in every conv epilogue; the FPN
 // upsample-add is the lateral conv's epilogue (nearest-2x residual); the SSH
-// concat is three convs writing channel slices [0,128), [128,192), [192,256)
-// of one buffer with the post-concat ReLU applied per slice; the three heads
-// of a level are one 256->32 conv (channels 0-7 bbox, 8-11 class, 12-31 landm).
+// concat is convs writing channel slices of one buffer with the post-concat ReLU
+// applied per slice (ReLU SSH: [t5 | c3 | c5 | c7], conv5X5_1 and conv3X3 as one
+// 192-channel conv, the heads reading [c3 | c5 | c7]); the three heads of a level
+// are one 256->32 conv (channels 0-7 bbox, 8-11 class, 12-31 landm).
 #include "nets.h"
 #include "vd_math.h"
 
 #include <cmath>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -233,6 +235,8 @@ int vd_build_face(Ctx& c, const WMap& W) {
     const Act fpn_out[3] = {m1, m2, o3};
 
     // ---- SSH x3 + fused heads ----
+    const char* sfe = getenv("VD_SSH_FUSE");   // 0: conv3X3 and conv5X5_1 as two convs
+    const bool ssh_fuse = !(sfe && atoi(sfe) == 0);
     for (int l = 0; l < 3; ++l) {
         const std::string pre = "ssh" + std::to_string(l + 1);
         int s3, s51, s52, s72, s73;
@@ -253,15 +257,32 @@ int vd_build_face(Ctx& c, const WMap& W) {
         if ((rc = conv_bn(c, W, pre + ".conv7x7_3.0.weight", pre + ".conv7x7_3.1", 1, 1, VD_ACT_RELU, &s73))) return rc;
         const Act& f = fpn_out[l];
         const int c3o = c.convs[s3].cout, c5o = c.convs[s52].cout, c7o = c.convs[s73].cout;
+        const int t5c = c.convs[s51].cout;
         Act cat, t5, t7;
-        if ((rc = c.act(cat, f.h, f.w, c3o + c5o + c7o))) return rc;
-        if ((rc = c.act(t5, f.h, f.w, c.convs[s51].cout))) return rc;
+        int hoff = 0;   // channel offset of the concat [c3 | c5 | c7] in `cat`
         if ((rc = c.act(t7, f.h, f.w, c.convs[s72].cout))) return rc;
-        if ((rc = c.add_conv(F.net, s3, f, 0, cat, 0))) return rc;
-        if ((rc = c.add_conv(F.net, s51, f, 0, t5, 0))) return rc;
-        if ((rc = c.add_conv(F.net, s52, t5, 0, cat, c3o))) return rc;
+        if (!sleaky && ssh_fuse) {
+            // conv5X5_1 and conv3X3 read the same input with the same activation
+            // (ReLU: conv3X3's own, after the concat): one conv with Cout t5c + c3o
+            // writing [t5 | c3] into cat = [t5 | c3 | c5 | c7], so the input is read once
+            int s351;
+            if ((rc = c.make_conv_bn_cat(W, {{pre + ".conv5X5_1.0.weight", pre + ".conv5X5_1.1"},
+                                             {pre + ".conv3X3.0.weight", pre + ".conv3X3.1"}},
+                                         BN_EPS, 1, 1, VD_ACT_RELU, 0.f, &s351)))
+                return rc;
+            if ((rc = c.act(cat, f.h, f.w, t5c + c3o + c5o + c7o))) return rc;
+            t5 = cat;
+            hoff = t5c;
+            if ((rc = c.add_conv(F.net, s351, f, 0, cat, 0))) return rc;
+        } else {
+            if ((rc = c.act(cat, f.h, f.w, c3o + c5o + c7o))) return rc;
+            if ((rc = c.act(t5, f.h, f.w, t5c))) return rc;
+            if ((rc = c.add_conv(F.net, s3, f, 0, cat, 0))) return rc;
+            if ((rc = c.add_conv(F.net, s51, f, 0, t5, 0))) return rc;
+        }
+        if ((rc = c.add_conv(F.net, s52, t5, 0, cat, hoff + c3o))) return rc;
         if ((rc = c.add_conv(F.net, s72, t5, 0, t7, 0))) return rc;
-        if ((rc = c.add_conv(F.net, s73, t7, 0, cat, c3o + c5o))) return rc;
+        if ((rc = c.add_conv(F.net, s73, t7, 0, cat, hoff + c3o + c5o))) return rc;
         int hc;
         const std::string L = std::to_string(l);
         if ((rc = c.make_conv_cat(W,
@@ -273,7 +294,7 @@ int vd_build_face(Ctx& c, const WMap& W) {
             return rc;
         if (c.convs[hc].cout != 32) return vd_set_error(VD_ERR_WEIGHTS, "heads of level %d: %d channels != 32", l, c.convs[hc].cout);
         if ((rc = c.act(F.heads[l], f.h, f.w, 32, true))) return rc;
-        if ((rc = c.add_conv(F.net, hc, cat, 0, F.heads[l], 0))) return rc;
+        if ((rc = c.add_conv(F.net, hc, cat, hoff, F.heads[l], 0))) return rc;
     }
 
     // ---- anchors (anchors.py:22-41, Python doubles -> float32) ----

@@ -6,6 +6,7 @@
 #include <mutex>
 #include <string>
 #include <unordered_map>
+#include <utility>
 #include <vector>
 
 struct HT {   // host tensor from the VDW1 container
@@ -162,6 +163,9 @@ struct Ctx {
                     const std::vector<float>& shift);
     int make_conv_bn(const WMap& W, const std::string& wkey, const std::string& bn, float eps, int stride, int pad,
                      int act, float slope, int* out_idx);
+    // convs + BatchNorms {(wkey, bn)} concatenated along Cout (same input, kernel, stride, pad)
+    int make_conv_bn_cat(const WMap& W, const std::vector<std::pair<std::string, std::string>>& parts, float eps,
+                         int stride, int pad, int act, float slope, int* out_idx);
     int make_conv_cat(const WMap& W, const std::vector<std::string>& wkeys, const std::vector<std::string>& bkeys,
                       int act, int* out_idx);
     int add_conv_dual(Net& net, int ci, const Act& x, int c2, const Act& x2, Act& y);

@@ -188,25 +188,45 @@ const HT* find_t(const WMap& W, const std::string& k) {
 // gamma/sqrt(var+eps), beta = bias - mean*alpha, as torch's CPU inference kernel).
 int Ctx::make_conv_bn(const WMap& W, const std::string& wkey, const std::string& bn, float eps, int stride,
                       int pad, int act, float slope, int* out_idx) {
-    const HT* w = find_t(W, wkey);
-    if (!w || w->shape.size() != 4) return vd_set_error(VD_ERR_WEIGHTS, "missing/bad conv weight %s", wkey.c_str());
+    return make_conv_bn_cat(W, {{wkey, bn}}, eps, stride, pad, act, slope, out_idx);
+}
+
+// Several conv+BN pairs reading the same input, stacked along Cout in the given
+// order (the SSH conv5X5_1 + conv3X3 pair of face_net.cpp): one GEMM, per-channel
+// scale/shift, so every output channel is computed exactly as by its own conv.
+int Ctx::make_conv_bn_cat(const WMap& W, const std::vector<std::pair<std::string, std::string>>& parts, float eps,
+                          int stride, int pad, int act, float slope, int* out_idx) {
     Conv cv{};
-    cv.cout = w->shape[0]; cv.cin = w->shape[1]; cv.kh = w->shape[2]; cv.kw = w->shape[3];
-    cv.stride = stride; cv.pad = pad; cv.act = act; cv.slope = slope;
-    std::vector<float> sc(cv.cout, 1.f), sh(cv.cout, 0.f);
-    if (!bn.empty()) {
-        const HT* g = find_t(W, bn + ".weight");
-        const HT* b = find_t(W, bn + ".bias");
-        const HT* m = find_t(W, bn + ".running_mean");
-        const HT* v = find_t(W, bn + ".running_var");
-        if (!g || !b || !m || !v) return vd_set_error(VD_ERR_WEIGHTS, "missing BatchNorm tensors under %s", bn.c_str());
-        for (int n = 0; n < cv.cout; ++n) {
-            float alpha = g->data[n] / std::sqrt(v->data[n] + eps);
-            sc[n] = alpha;
-            sh[n] = b->data[n] - m->data[n] * alpha;
+    std::vector<float> wall, sc, sh;
+    for (size_t i = 0; i < parts.size(); ++i) {
+        const std::string& wkey = parts[i].first;
+        const std::string& bn = parts[i].second;
+        const HT* w = find_t(W, wkey);
+        if (!w || w->shape.size() != 4) return vd_set_error(VD_ERR_WEIGHTS, "missing/bad conv weight %s", wkey.c_str());
+        if (i == 0) { cv.cin = w->shape[1]; cv.kh = w->shape[2]; cv.kw = w->shape[3]; }
+        if (w->shape[1] != cv.cin || w->shape[2] != cv.kh || w->shape[3] != cv.kw)
+            return vd_set_error(VD_ERR_WEIGHTS, "conv shape mismatch at %s", wkey.c_str());
+        const int co = w->shape[0];
+        wall.insert(wall.end(), w->data.begin(), w->data.end());
+        if (bn.empty()) {
+            sc.insert(sc.end(), co, 1.f);
+            sh.insert(sh.end(), co, 0.f);
+        } else {
+            const HT* g = find_t(W, bn + ".weight");
+            const HT* b = find_t(W, bn + ".bias");
+            const HT* m = find_t(W, bn + ".running_mean");
+            const HT* v = find_t(W, bn + ".running_var");
+            if (!g || !b || !m || !v) return vd_set_error(VD_ERR_WEIGHTS, "missing BatchNorm tensors under %s", bn.c_str());
+            for (int n = 0; n < co; ++n) {
+                const float alpha = g->data[n] / std::sqrt(v->data[n] + eps);
+                sc.push_back(alpha);
+                sh.push_back(b->data[n] - m->data[n] * alpha);
+            }
         }
+        cv.cout += co;
     }
-    int rc = upload_conv(cv, w->data, sc, sh);
+    cv.stride = stride; cv.pad = pad; cv.act = act; cv.slope = slope;
+    int rc = upload_conv(cv, wall, sc, sh);
     if (rc) return rc;
     convs.push_back(cv);
     *out_idx = (int)convs.size() - 1;
