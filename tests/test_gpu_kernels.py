@@ -195,7 +195,7 @@ CONV_CASES = [
 
 
 @pytest.mark.parametrize("prec", ["fp32", "bf16", "fp16", "bf16-gemm64", "bf16-gemm128", "bf16-gemm256",
-                                  "bf16-persist64", "bf16-persist128"])
+                                  "bf16-gemm192", "bf16-persist64", "bf16-persist128"])
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv_matches_torch(gpu, face_ctx_factory, monkeypatch, prec, case):
     """bf16: the default dispatch (streaming 1x1 / streaming taps / persistent GEMM / GEMM);
@@ -215,6 +215,7 @@ def test_conv_matches_torch(gpu, face_ctx_factory, monkeypatch, prec, case):
         monkeypatch.setenv("VD_CONV_STREAM", "0")
         monkeypatch.setenv("VD_CONV_SMALL", "100000000" if prec == "bf16-gemm64" else "0")
         monkeypatch.setenv("VD_CONV_TALL", "1" if prec == "bf16-gemm256" else "0")   # 256x64 tiles (N = 64)
+        monkeypatch.setenv("VD_CONV_M192", "1" if prec == "bf16-gemm192" else "0")   # 192x128 tiles (N <= 128)
         prec = "bf16"
     n, h, w, cin, cout, k, s, p, act, res_mode = case
     ctx = face_ctx_factory(prec, 8)

@@ -492,5 +492,11 @@ hipError_t vd_launch_conv(const ConvArgs& a, bool f32, hipStream_t s) {
         return launch_bn<__bf16, 128, 64>(a, dense, s);
     }
     if (n192) return launch_bn<__bf16, 128, 192>(a, dense, s);
+    // Cout 65-128 on large grids: 192-row tiles (same operand footprint as 128x192).
+    // Off by default: 2-6 % slower than 128x128 on layer2's 3x3 (K 1152; fewer tiles,
+    // a worse last wave of the grid)
+    const char* em = getenv("VD_CONV_M192");   // min 128x128 tiles for 192x128 (0: off)
+    const long m192_min = em ? atol(em) : 0;
+    if (m192_min > 0 && tiles128 >= m192_min) return launch_bn<__bf16, 192, 128>(a, dense, s);
     return launch_bn<__bf16, 128, 128>(a, dense, s);
 }
