@@ -117,3 +117,28 @@ def test_process_faces_and_plates_mosaic(gpu):
         # reference mode: plate boxes discarded (combine_detect.py:239)
         np.testing.assert_array_equal(out_ref[b], omosaic.mosaic_frame(fr[b], fb, 8))
     assert int(plates.count.sum()) > 0
+
+
+@pytest.mark.parametrize("h,w", [(1080, 1920), (720, 1280), (640, 640), (480, 640)])
+def test_plate_raw_bf16_s2d_matches_plain(gpu, monkeypatch, h, w):
+    """bf16 plans letterbox the plate canvas in space-to-depth form and run model.0
+    (3x3 stride 2) as a 2x2 conv over it (plate_net.cpp yconv_s2d); VD_PLATE_S2D=0
+    keeps the 8-channel canvas and the 3x3 conv. Same 27 products per output in
+    another f32 order: the raw outputs agree to bf16 rounding, and both stay within
+    the bf16 oracle bound."""
+    import vdmi
+    from vdmi import synth, weights
+    fr = synth.frames(2, h, w, seed=7)
+    out = {}
+    for s2d in ("1", "0"):
+        monkeypatch.setenv("VD_PLATE_S2D", s2d)
+        c = vdmi.Context(precision="bf16", max_batch=2)
+        try:
+            c.load_weights(1, weights.yolov8n_state_dict(0))
+            out[s2d] = c.plate_raw(fr)
+        finally:
+            c.close()
+    exp, _, _ = _oracle_raw(fr)
+    assert out["1"].shape == out["0"].shape == exp.shape
+    assert _rel(out["1"][:, 64:], out["0"][:, 64:]) < 2e-2
+    assert _rel(out["1"][:, 64:], exp[:, 64:]) < 8e-2

@@ -107,6 +107,7 @@ struct PlateNet {
     int imgsz = 640;
     int hstride = 0;                // head channel stride (64 DFL + nc, padded to 4)
     Act input;                      // letterboxed canvas, allocated for imgsz x imgsz
+    bool s2d = false;               // bf16: canvas in space-to-depth form, model.0 as a 2x2 conv
     std::vector<std::pair<std::string, Act>> bufs;   // named activation buffers (max canvas)
     std::vector<std::pair<std::string, int>> conv_idx;
     std::vector<std::pair<long long, Net>> plans;    // per canvas (h<<32|w)

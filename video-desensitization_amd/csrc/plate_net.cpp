@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -58,6 +59,48 @@ int yconv(Ctx& c, const WMap& W, const std::string& pre, int stride) {
                             0.f, &idx);
     if (rc) return rc;
     c.plate.conv_idx.push_back({pre, idx});
+    return VD_OK;
+}
+
+// model.0 (3x3, stride 2, pad 1, 3 -> 16, BN + SiLU) over the space-to-depth canvas
+// X'[Y][X][(py*2+px)*4 + c] = x[2Y+py-1][2X+px-1][c] (the face stem's form, pre.hip):
+// a 2x2, stride-1, pad-0 conv with 16 input channels, W'[n][(py*2+px)*4+c][ta][tb] =
+// W[n][c][2ta+py][2tb+px] (zero where 2ta+py or 2tb+px is 3, and for the 4th channel
+// of each sub-pixel). Same 27 products per output; the canvas is 8 B per pixel
+// instead of 16 (cpad 8).
+int yconv_s2d(Ctx& c, const WMap& W, const std::string& pre) {
+    const HT* w = find_t(W, pre + ".conv.weight");
+    const HT* g = find_t(W, pre + ".bn.weight");
+    const HT* b = find_t(W, pre + ".bn.bias");
+    const HT* m = find_t(W, pre + ".bn.running_mean");
+    const HT* v = find_t(W, pre + ".bn.running_var");
+    if (!w || w->shape.size() != 4 || w->shape[1] != 3 || w->shape[2] != 3 || w->shape[3] != 3)
+        return vd_set_error(VD_ERR_WEIGHTS, "missing/bad %s.conv.weight", pre.c_str());
+    if (!g || !b || !m || !v) return vd_set_error(VD_ERR_WEIGHTS, "missing BatchNorm tensors under %s.bn", pre.c_str());
+    Conv cv{};
+    cv.cout = w->shape[0]; cv.cin = 16; cv.kh = 2; cv.kw = 2;
+    cv.stride = 1; cv.pad = 0; cv.act = VD_ACT_SILU; cv.slope = 0.f;
+    std::vector<float> wt((size_t)cv.cout * 16 * 4, 0.f), sc(cv.cout), sh(cv.cout);
+    for (int n = 0; n < cv.cout; ++n) {
+        for (int ta = 0; ta < 2; ++ta)
+            for (int tb = 0; tb < 2; ++tb)
+                for (int py = 0; py < 2; ++py)
+                    for (int px = 0; px < 2; ++px)
+                        for (int ch = 0; ch < 3; ++ch) {
+                            const int dy = 2 * ta + py, dx = 2 * tb + px;
+                            if (dy > 2 || dx > 2) continue;
+                            wt[(((size_t)n * 16 + (py * 2 + px) * 4 + ch) * 2 + ta) * 2 + tb] =
+                                w->data[(((size_t)n * 3 + ch) * 3 + dy) * 3 + dx];
+                        }
+        const float alpha = g->data[n] / std::sqrt(v->data[n] + YOLO_BN_EPS);
+        sc[n] = alpha;
+        sh[n] = b->data[n] - m->data[n] * alpha;
+    }
+    int rc = c.upload_conv(cv, wt, sc, sh);
+    if (rc) return rc;
+    cv.flops_per_px = 2.0 * cv.cout * 3 * 9;   // algorithmic work of the original 3x3 conv
+    c.convs.push_back(cv);
+    c.plate.conv_idx.push_back({pre, (int)c.convs.size() - 1});
     return VD_OK;
 }
 
@@ -164,7 +207,8 @@ int build_plan(Ctx& c, int ch, int cw, Net& net) {
     PlateNet& P = c.plate;
     Planner p{c, net, ch, cw};
     Act in = P.input;
-    in.h = ch; in.w = cw;
+    in.h = P.s2d ? ch / 2 + 1 : ch;
+    in.w = P.s2d ? cw / 2 + 1 : cw;
     p.conv("model.0", in, 0, p.buf("A0"), 0);
     p.conv("model.1", p.buf("A0"), 0, p.buf("A1"), 0);
     p.c2f("model.2", 1, true, p.buf("A1"), 0, "C2", "T2", p.buf("A2"), 0);
@@ -216,7 +260,14 @@ int vd_build_plate(Ctx& c, const WMap& W) {
         return vd_set_error(VD_ERR_WEIGHTS, "plate weights have %d classes, cfg.plate_nc = %d", cls0->shape[0], P.nc);
     int rc;
     static const int strides[] = {2, 2, 1, 2, 1, 2, 1, 2, 1};
-    for (int i : {0, 1, 3, 5, 7}) if ((rc = yconv(c, W, "model." + std::to_string(i), strides[i]))) return rc;
+    // bf16: the letterbox writes the stem input in space-to-depth form (VD_PLATE_S2D=0: off)
+    const char* se = getenv("VD_PLATE_S2D");
+    P.s2d = !c.f32 && !c.f16 && !(se && atoi(se) == 0);
+    if (P.s2d && (rc = yconv_s2d(c, W, "model.0"))) return rc;
+    for (int i : {0, 1, 3, 5, 7}) {
+        if (i == 0 && P.s2d) continue;
+        if ((rc = yconv(c, W, "model." + std::to_string(i), strides[i]))) return rc;
+    }
     for (int i : {16, 19}) if ((rc = yconv(c, W, "model." + std::to_string(i), 2))) return rc;
     if ((rc = c2f_convs(c, W, "model.2", 1))) return rc;
     if ((rc = c2f_convs(c, W, "model.4", 2))) return rc;
@@ -237,7 +288,9 @@ int vd_build_plate(Ctx& c, const WMap& W) {
     }
     // buffers for the imgsz x imgsz canvas
     const int cpad = c.f32 ? 4 : 8;
-    if ((rc = c.act(P.input, P.imgsz, P.imgsz, cpad))) return rc;
+    if (P.s2d) rc = c.act(P.input, P.imgsz / 2 + 1, P.imgsz / 2 + 1, 16);
+    else rc = c.act(P.input, P.imgsz, P.imgsz, cpad);
+    if (rc) return rc;
     for (const Buf& b : kBufs) {
         Act a;
         if ((rc = c.act(a, P.imgsz / b.div, P.imgsz / b.div, b.c))) return rc;
@@ -286,7 +339,9 @@ int vd_plate_forward(Ctx& c, const uint8_t* d, int n, int h, int w, size_t pitch
     a.div = 255.f;
     a.flip = 1;   // im[..., ::-1]: the RGB frames are treated as BGR
     a.out = P.input.p; a.cpad = P.input.c; a.out_f32 = c.f32 ? 1 : 0; a.out_f16 = c.f16 ? 1 : 0;
-    c.t_begin(2, (double)n * (nh * (double)w * 3 + (double)oh * ow * a.cpad * (c.f32 ? 4 : 2)));
+    a.s2d = P.s2d ? 1 : 0;
+    const double obytes = P.s2d ? (double)(oh / 2 + 1) * (ow / 2 + 1) * 32 : (double)oh * ow * a.cpad * (c.f32 ? 4 : 2);
+    c.t_begin(2, (double)n * (nh * (double)w * 3 + obytes));
     hipError_t e = vd_launch_letterbox(a, c.stream);
     c.t_end();
     if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "plate letterbox: %s", hipGetErrorString(e));
