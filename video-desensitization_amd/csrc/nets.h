@@ -105,7 +105,7 @@ struct PlateNet {
     bool loaded = false;
     int nc = 1;
     int imgsz = 640;
-    int hstride = 0;                // head channel stride (64 DFL + nc, padded to 4)
+    int hstride = 0;                // head channel stride (64 DFL + nc, padded to 8)
     Act input;                      // letterboxed canvas, allocated for imgsz x imgsz
     bool s2d = false;               // bf16: canvas in space-to-depth form, model.0 as a 2x2 conv
     std::vector<std::pair<std::string, Act>> bufs;   // named activation buffers (max canvas)

@@ -296,7 +296,7 @@ int vd_build_plate(Ctx& c, const WMap& W) {
         if ((rc = c.act(a, P.imgsz / b.div, P.imgsz / b.div, b.c))) return rc;
         P.bufs.push_back({b.name, a});
     }
-    P.hstride = (64 + P.nc + 3) / 4 * 4;
+    P.hstride = (64 + P.nc + 7) / 8 * 8;   // 8-channel multiple: 16-B vector epilogues for the box head
     P.A_max = 0;
     for (int i = 0; i < 3; ++i) {
         const int s = P.imgsz / (8 << i);
