@@ -5,7 +5,11 @@ prints duration and achieved TFLOP/s per layer.
     python tools/conv_layers.py gpurun_out/prof/run_kernel_trace.csv [batch]
 """
 import csv
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from prof_summary import face_stream  # noqa: E402
 
 
 def face_plan(B=64, H=640, W=640, fused=True, block=True, chain=True, ssh_fused=True):
@@ -69,8 +73,8 @@ def main(path, B=64):
     conv_keys = ("conv_igemm", "conv1x1_stream", "conv_big", "bottleneck_kernel", "stem_pool_kernel", "chain_kernel")
     plan = face_plan(B, block=any("bottleneck_kernel" in r["Kernel_Name"] for r in allk),
                      chain=any("chain_kernel" in r["Kernel_Name"] for r in allk))
-    li = max(i for i, r in enumerate(allk) if "letterbox_s2d" in r["Kernel_Name"]
-             or ("letterbox_kernel" in r["Kernel_Name"] and int(r["Grid_Size_Y"]) == 640))
+    face = face_stream(allk)
+    li = max(i for i, r in enumerate(allk) if r["Stream_Id"] in face and "letterbox" in r["Kernel_Name"])
     stream = allk[li]["Stream_Id"]
     last = [r for r in allk[li:] if r["Stream_Id"] == stream and any(k in r["Kernel_Name"] for k in conv_keys)]
     last = last[:len(plan)]

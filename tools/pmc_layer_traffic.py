@@ -12,6 +12,7 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from conv_layers import face_plan  # noqa: E402
+from prof_summary import face_stream  # noqa: E402
 
 KEYS = ("conv_igemm", "conv1x1_stream", "conv_big", "bottleneck_kernel", "stem_pool_kernel", "chain_kernel")
 
@@ -22,7 +23,8 @@ def last_step(d, counter):
     for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
         if r["Counter_Name"] == counter:
             vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
-    li = max(i for i, r in enumerate(trace) if "letterbox_s2d" in r["Kernel_Name"])
+    face = face_stream(trace)
+    li = max(i for i, r in enumerate(trace) if r["Stream_Id"] in face and "letterbox" in r["Kernel_Name"])
     stream = trace[li]["Stream_Id"]
     rows = [r for r in trace[li:] if r["Stream_Id"] == stream and any(k in r["Kernel_Name"] for k in KEYS)]
     return [(vals.get(r["Dispatch_Id"], 0.0), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3)

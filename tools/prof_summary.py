@@ -22,10 +22,17 @@ def family(name):
     return next((f for f, keys in FAMILIES if any(k in name for k in keys)), None)
 
 
+FACE_ONLY = ("stem_pool_kernel", "bottleneck_kernel", "chain_kernel", "face_candidates_kernel")
+
+
 def face_stream(rows):
-    """Stream id(s) of the RetinaFace branch: the stream of the face letterbox
-    (space-to-depth form in bf16, the 640-row canvas in fp32)."""
-    face = {r["Stream_Id"] for r in rows if "letterbox_s2d" in r["Kernel_Name"]}
+    """Stream id(s) of the RetinaFace branch: the stream of the face-only kernels
+    (fused stem / layer1 blocks / layer2 chain / face decode); failing those, the
+    stream of the 640-row face letterbox (the plate canvas is letterboxed in
+    space-to-depth form too in bf16, so that name alone no longer tells)."""
+    face = {r["Stream_Id"] for r in rows if any(k in r["Kernel_Name"] for k in FACE_ONLY)}
+    if not face:
+        face = {r["Stream_Id"] for r in rows if "letterbox_s2d" in r["Kernel_Name"]}
     if not face:
         face = {r["Stream_Id"] for r in rows if "letterbox_kernel" in r["Kernel_Name"] and r["Grid_Size_Y"] == "640"}
     return face
