@@ -142,3 +142,31 @@ def test_plate_raw_bf16_s2d_matches_plain(gpu, monkeypatch, h, w):
     assert out["1"].shape == out["0"].shape == exp.shape
     assert _rel(out["1"][:, 64:], out["0"][:, 64:]) < 2e-2
     assert _rel(out["1"][:, 64:], exp[:, 64:]) < 8e-2
+
+
+@pytest.mark.parametrize("h,w", [(1080, 1920), (720, 1280), (480, 640), (1080, 1440)])
+def test_process_paired_letterbox_matches_separate(gpu, monkeypatch, h, w):
+    """With faces and plates in one vd_process call, both s2d canvases come from one
+    read of the frames (pre.hip letterbox_s2d_pair_kernel) where the resize geometry
+    matches; VD_LB_PAIR=0 runs the two letterboxes apart. Same per-pixel arithmetic:
+    box lists and mosaicked frames are identical."""
+    import vdmi
+    from vdmi import _lib, synth, weights
+    fr = synth.frames(2, h, w, seed=21)
+    flags = _lib.VD_PROC_FACES | _lib.VD_PROC_PLATES | _lib.VD_PROC_MOSAIC | _lib.VD_PROC_MOSAIC_PLATES
+    res = {}
+    for pair in ("1", "0"):
+        monkeypatch.setenv("VD_LB_PAIR", pair)
+        c = vdmi.Context(precision="bf16", max_batch=2)
+        try:
+            c.load_weights(0, weights.retinaface_state_dict(0))
+            c.load_weights(1, weights.yolov8n_state_dict(0))
+            out, faces, plates = c.process(fr, flags=flags)
+            res[pair] = (out.copy(), [faces.frame(b)[0].copy() for b in range(2)],
+                         [plates.frame(b)[0].copy() for b in range(2)])
+        finally:
+            c.close()
+    np.testing.assert_array_equal(res["1"][0], res["0"][0])
+    for b in range(2):
+        np.testing.assert_array_equal(res["1"][1][b], res["0"][1][b])
+        np.testing.assert_array_equal(res["1"][2][b], res["0"][2][b])

@@ -195,6 +195,7 @@ struct Ctx {
     int box_targets(vd_boxes* out, int n, BoxTargets& t);
     int box_finish(vd_boxes* out, int n, const BoxTargets& t);
     int face_letterbox(const uint8_t* dframes, int n, int h, int w, size_t pitch);
+    void face_letterbox_args(const uint8_t* dframes, int n, int h, int w, size_t pitch, LetterboxArgs* a);
     int face_forward(int n);
     int face_post(int n, int img_h, int img_w, const BoxTargets& t);
     int launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w, size_t pitch, const int* cnt0,
@@ -204,5 +205,7 @@ struct Ctx {
 int vd_alloc_post(Ctx& ctx, PostScratch& ps, int A);
 int vd_build_face(Ctx& ctx, const WMap& W);
 int vd_build_plate(Ctx& ctx, const WMap& W);
-int vd_plate_forward(Ctx& ctx, const uint8_t* dframes, int n, int h, int w, size_t pitch);
+// letterboxed: the canvas was already written (vd_launch_letterbox_pair in vd_process)
+int vd_plate_forward(Ctx& ctx, const uint8_t* dframes, int n, int h, int w, size_t pitch, bool letterboxed = false);
+int vd_plate_letterbox_args(Ctx& ctx, const uint8_t* dframes, int n, int h, int w, size_t pitch, LetterboxArgs* a);
 int vd_plate_post(Ctx& ctx, int n, int img_h, int img_w, const BoxTargets& t);

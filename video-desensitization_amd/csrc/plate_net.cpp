@@ -324,7 +324,7 @@ static void yolo_geometry(int ih, int iw, int imgsz, int* nw, int* nh, int* top,
     *ow = *nw + *left + right;
 }
 
-int vd_plate_forward(Ctx& c, const uint8_t* d, int n, int h, int w, size_t pitch) {
+int vd_plate_letterbox_args(Ctx& c, const uint8_t* d, int n, int h, int w, size_t pitch, LetterboxArgs* out) {
     PlateNet& P = c.plate;
     int nw, nh, top, left, oh, ow;
     yolo_geometry(h, w, P.imgsz, &nw, &nh, &top, &left, &oh, &ow);
@@ -340,11 +340,24 @@ int vd_plate_forward(Ctx& c, const uint8_t* d, int n, int h, int w, size_t pitch
     a.flip = 1;   // im[..., ::-1]: the RGB frames are treated as BGR
     a.out = P.input.p; a.cpad = P.input.c; a.out_f32 = c.f32 ? 1 : 0; a.out_f16 = c.f16 ? 1 : 0;
     a.s2d = P.s2d ? 1 : 0;
-    const double obytes = P.s2d ? (double)(oh / 2 + 1) * (ow / 2 + 1) * 32 : (double)oh * ow * a.cpad * (c.f32 ? 4 : 2);
-    c.t_begin(2, (double)n * (nh * (double)w * 3 + obytes));
-    hipError_t e = vd_launch_letterbox(a, c.stream);
-    c.t_end();
-    if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "plate letterbox: %s", hipGetErrorString(e));
+    *out = a;
+    return VD_OK;
+}
+
+int vd_plate_forward(Ctx& c, const uint8_t* d, int n, int h, int w, size_t pitch, bool letterboxed) {
+    PlateNet& P = c.plate;
+    LetterboxArgs a;
+    int rc0 = vd_plate_letterbox_args(c, d, n, h, w, pitch, &a);
+    if (rc0) return rc0;
+    const int oh = a.oh, ow = a.ow;
+    if (!letterboxed) {
+        const double obytes =
+            P.s2d ? (double)(oh / 2 + 1) * (ow / 2 + 1) * 32 : (double)oh * ow * a.cpad * (c.f32 ? 4 : 2);
+        c.t_begin(2, (double)n * (a.nh * (double)w * 3 + obytes));
+        hipError_t e = vd_launch_letterbox(a, c.stream);
+        c.t_end();
+        if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "plate letterbox: %s", hipGetErrorString(e));
+    }
     const long long key = ((long long)oh << 32) | ow;
     Net* net = nullptr;
     for (auto& pl : P.plans)

@@ -14,6 +14,9 @@
 #include "vd_common.h"
 #include "vd_math.h"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace {
 
 struct Tap { int s0, s1, a0, a1; };
@@ -192,6 +195,77 @@ __global__ __launch_bounds__(256) void letterbox_s2d_lds_kernel(LetterboxArgs a)
     }
 }
 
+// Two space-to-depth canvases of the same frames in one pass (the face and the
+// plate letterbox of vd_process): both resize to the same nw x nh with the same
+// filter, so a source row feeds block row Y of canvas a and block row Y - dY of
+// canvas b; each source row is staged once and both canvases are written from it.
+// Per pixel the arithmetic is exactly letterbox_s2d_lds_kernel's for each canvas.
+// Block rows Y run over the union [y0, y0 + gridDim.x), X over [x0, x0 + nx).
+__global__ __launch_bounds__(256) void letterbox_s2d_pair_kernel(LetterboxArgs a, LetterboxArgs b, int dY, int dX,
+                                                                 int y0, int x0, int nx) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lrow[];
+    const int Y = y0 + (int)blockIdx.x, f = blockIdx.y;
+    const int Yb = Y - dY;
+    const int OWa = a.ow / 2 + 1, OHa = a.oh / 2 + 1, OWb = b.ow / 2 + 1, OHb = b.oh / 2 + 1;
+    const bool ya = (unsigned)Y < (unsigned)OHa, yb = (unsigned)Yb < (unsigned)OHb;
+    const uint8_t* img = a.src + (size_t)f * a.ih * a.pitch;
+    int ra[4] = {-1, -1, -1, -1}, rb[4] = {-1, -1, -1, -1};
+    Tap tya[2], tyb[2];
+    bool rina[2] = {false, false}, rinb[2] = {false, false};
+    if (ya) {
+        lb_src_rows(a, 2 * Y - 1, &ra[0], &ra[1], &tya[0], &rina[0]);
+        lb_src_rows(a, 2 * Y, &ra[2], &ra[3], &tya[1], &rina[1]);
+    }
+    if (yb) {
+        lb_src_rows(b, 2 * Yb - 1, &rb[0], &rb[1], &tyb[0], &rinb[0]);
+        lb_src_rows(b, 2 * Yb, &rb[2], &rb[3], &tyb[1], &rinb[1]);
+    }
+    const int rbytes = a.iw * 3;
+    const int nch = (rbytes + 15) / 16;
+    const int RS = nch * 16;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int row = ra[k] >= 0 ? ra[k] : rb[k];   // the same source row when both canvases need one
+        if (row < 0) continue;
+        const uint8_t* src = img + (size_t)row * a.pitch;
+        uint8_t* dst = lrow + k * RS;
+        if (((uintptr_t)src & 15) == 0) {
+            for (int i = threadIdx.x; i < nch; i += 256) {
+                if (16 * i + 16 <= rbytes) *(uint4*)(dst + 16 * i) = *(const uint4*)(src + 16 * i);
+                else for (int q = 16 * i; q < rbytes; ++q) dst[q] = src[q];
+            }
+        } else {
+            for (int i = threadIdx.x; i < rbytes; i += 256) dst[i] = src[i];
+        }
+    }
+    __syncthreads();
+    for (int X = x0 + (int)threadIdx.x; X < x0 + nx; X += 256) {
+#pragma unroll
+        for (int cv = 0; cv < 2; ++cv) {
+            const LetterboxArgs& c = cv ? b : a;
+            const int XX = cv ? X - dX : X, YY = cv ? Yb : Y;
+            if (!(cv ? yb : ya) || (unsigned)XX >= (unsigned)(cv ? OWb : OWa)) continue;
+            const Tap* ty = cv ? tyb : tya;
+            const bool* rin = cv ? rinb : rina;
+            __bf16 t[16];
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int h = s >> 1;
+                const int x = 2 * XX + (s & 1) - 1;
+                float v[3] = {0.f, 0.f, 0.f};
+                const int y = 2 * YY + h - 1;
+                if ((unsigned)y < (unsigned)c.oh && (unsigned)x < (unsigned)c.ow)
+                    lb_px_lds(c, lrow + (2 * h) * RS, lrow + (2 * h + 1) * RS, ty[h], x, rin[h], v);
+                t[4 * s + 0] = (__bf16)v[0]; t[4 * s + 1] = (__bf16)v[1]; t[4 * s + 2] = (__bf16)v[2];
+                t[4 * s + 3] = (__bf16)0.f;
+            }
+            __bf16* out = (__bf16*)c.out + (((size_t)f * (cv ? OHb : OHa) + YY) * (cv ? OWb : OWa) + XX) * 16;
+            *(uint4*)out = *(const uint4*)t;
+            *(uint4*)(out + 8) = *(const uint4*)(t + 8);
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void letterbox_kernel(LetterboxArgs a) {
     const int x = blockIdx.x * 256 + threadIdx.x;
     const int y = blockIdx.y;
@@ -277,6 +351,33 @@ __global__ __launch_bounds__(256) void upsample2x_kernel(const T* x, int xh, int
 }
 
 }  // namespace
+
+// Same frames, both bf16 space-to-depth canvases, the same resize (nw, nh, filter)
+// and even relative offsets of the pasted images.
+bool vd_letterbox_pair_ok(const LetterboxArgs& a, const LetterboxArgs& b) {
+    const char* e = getenv("VD_LB_PAIR");
+    if (e && atoi(e) == 0) return false;
+    return a.s2d && b.s2d && !a.out_f32 && !b.out_f32 && !a.out_f16 && !b.out_f16 && a.src == b.src && a.n == b.n &&
+           a.ih == b.ih && a.iw == b.iw && a.pitch == b.pitch && a.iw * 3 <= LB_LDS_MAX && a.nw == b.nw &&
+           a.nh == b.nh && a.mode == b.mode && a.scale_x == b.scale_x && a.scale_y == b.scale_y &&
+           ((a.top - b.top) & 1) == 0 && ((a.left - b.left) & 1) == 0;
+}
+
+hipError_t vd_launch_letterbox_pair(const LetterboxArgs& a, const LetterboxArgs& b, hipStream_t s) {
+    if (!vd_letterbox_pair_ok(a, b)) return hipErrorInvalidValue;
+    static const bool attr = [] {
+        (void)hipFuncSetAttribute((const void*)letterbox_s2d_pair_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  4 * LB_LDS_MAX);
+        return true;
+    }();
+    (void)attr;
+    const int dY = (a.top - b.top) / 2, dX = (a.left - b.left) / 2;
+    const int y0 = std::min(0, dY), y1 = std::max(a.oh / 2 + 1, b.oh / 2 + 1 + dY);
+    const int x0 = std::min(0, dX), x1 = std::max(a.ow / 2 + 1, b.ow / 2 + 1 + dX);
+    const size_t lds = 4 * (size_t)((a.iw * 3 + 15) / 16 * 16);
+    hipLaunchKernelGGL(letterbox_s2d_pair_kernel, dim3(y1 - y0, a.n), dim3(256), lds, s, a, b, dY, dX, y0, x0, x1 - x0);
+    return hipGetLastError();
+}
 
 hipError_t vd_launch_letterbox(const LetterboxArgs& a, hipStream_t s) {
     if (a.s2d && a.iw * 3 <= LB_LDS_MAX) {

@@ -590,6 +590,16 @@ int Ctx::box_finish(vd_boxes* out, int n, const BoxTargets& t) {
 }
 
 int Ctx::face_letterbox(const uint8_t* dframes, int n, int h, int w, size_t pitch) {
+    LetterboxArgs a;
+    face_letterbox_args(dframes, n, h, w, pitch, &a);
+    t_begin(2, (double)n * (a.nh * (double)w * 3 + (double)a.oh * a.ow * a.cpad * (f32 ? 4 : 2)));
+    hipError_t e = vd_launch_letterbox(a, stream);
+    t_end();
+    if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "letterbox: %s", hipGetErrorString(e));
+    return VD_OK;
+}
+
+void Ctx::face_letterbox_args(const uint8_t* dframes, int n, int h, int w, size_t pitch, LetterboxArgs* out) {
     LetterboxArgs a{};
     a.src = dframes; a.n = n; a.ih = h; a.iw = w; a.pitch = pitch;
     a.oh = face.in_h; a.ow = face.in_w;
@@ -606,11 +616,7 @@ int Ctx::face_letterbox(const uint8_t* dframes, int n, int h, int w, size_t pitc
     a.flip = 0;
     a.out = face.input.p; a.cpad = face.input.c; a.out_f32 = f32 ? 1 : 0; a.out_f16 = f16 ? 1 : 0;
     a.s2d = face.s2d ? 1 : 0;
-    t_begin(2, (double)n * (a.nh * (double)w * 3 + (double)a.oh * a.ow * a.cpad * (f32 ? 4 : 2)));
-    hipError_t e = vd_launch_letterbox(a, stream);
-    t_end();
-    if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "letterbox: %s", hipGetErrorString(e));
-    return VD_OK;
+    *out = a;
 }
 
 int Ctx::face_forward(int n) {
@@ -917,19 +923,32 @@ int vd_process(vd_ctx* h, const uint8_t* in, uint8_t* out, int n, int fh, int fw
     // Face and plate branches run concurrently (the reference submits them to two
     // threads, combine_detect.py:214-217): plates on stream2, forked/joined by events.
     const bool fork = do_faces && do_plates;
+    // Both canvases from one read of the frames where the geometry allows (pre.hip
+    // letterbox_s2d_pair_kernel); the plate branch then forks after it.
+    bool paired = false;
     if (fork) {
+        LetterboxArgs fa, pa;
+        ctx->face_letterbox_args(d, n, fh, fw, pitch, &fa);
+        if (vd_plate_letterbox_args(*ctx, d, n, fh, fw, pitch, &pa) == VD_OK && vd_letterbox_pair_ok(fa, pa)) {
+            ctx->t_begin(2, (double)n * (fa.nh * (double)fw * 3 + ((double)(fa.oh / 2 + 1) * (fa.ow / 2 + 1) +
+                                                                    (double)(pa.oh / 2 + 1) * (pa.ow / 2 + 1)) * 32));
+            hipError_t e = vd_launch_letterbox_pair(fa, pa, ctx->stream);
+            ctx->t_end();
+            if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "letterbox pair: %s", hipGetErrorString(e));
+            paired = true;
+        }
         VD_CHECK_HIP(hipEventRecord(ctx->ev_fork, ctx->stream));
         VD_CHECK_HIP(hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
     }
     if (do_faces) {
-        if ((rc = ctx->face_letterbox(d, n, fh, fw, pitch))) return rc;
+        if (!paired && (rc = ctx->face_letterbox(d, n, fh, fw, pitch))) return rc;
         if ((rc = ctx->face_forward(n))) return rc;
         if ((rc = ctx->face_post(n, fh, fw, tf))) return rc;
     }
     if (do_plates) {
         hipStream_t main = ctx->stream;
         if (fork) ctx->stream = ctx->stream2;
-        rc = vd_plate_forward(*ctx, d, n, fh, fw, pitch);
+        rc = vd_plate_forward(*ctx, d, n, fh, fw, pitch, paired);
         if (!rc) rc = vd_plate_post(*ctx, n, fh, fw, tp);
         ctx->stream = main;
         if (rc) return rc;

@@ -160,6 +160,8 @@ hipError_t vd_launch_block(const BlockArgs& a, hipStream_t s);
 bool vd_chain_ok(int cmid, int cout, int kpad3, int kpad1, int ld_t2, int ld_res, int ld_y, int ld_y2, long M);
 hipError_t vd_launch_chain(const ChainArgs& a, hipStream_t s);
 hipError_t vd_launch_letterbox(const LetterboxArgs& a, hipStream_t s);
+bool vd_letterbox_pair_ok(const LetterboxArgs& a, const LetterboxArgs& b);
+hipError_t vd_launch_letterbox_pair(const LetterboxArgs& a, const LetterboxArgs& b, hipStream_t s);
 hipError_t vd_launch_maxpool(bool f32, bool f16, const void* x, int n, int xh, int xw, int ldx, int xcoff,
                              void* y, int yh, int yw, int ldy, int ycoff, int c, int k, int st, int p,
                              hipStream_t s);
