@@ -937,14 +937,29 @@ int vd_process(vd_ctx* h, const uint8_t* in, uint8_t* out, int n, int fh, int fw
             if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "letterbox pair: %s", hipGetErrorString(e));
             paired = true;
         }
+    }
+    // VD_PLATE_FORK=s (1-4, experiment): the plate branch starts after face backbone
+    // stage s instead of beside the whole face forward (needs micro-batching off)
+    static const int fork_stage = [] { const char* e = getenv("VD_PLATE_FORK"); return e ? atoi(e) : 0; }();
+    const bool late_fork = fork && fork_stage >= 1 && fork_stage <= 4 && ctx->cfg.reserved[0] <= 0;
+    if (fork && !late_fork) {
         VD_CHECK_HIP(hipEventRecord(ctx->ev_fork, ctx->stream));
         VD_CHECK_HIP(hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
     }
     if (do_faces) {
         if (!paired && (rc = ctx->face_letterbox(d, n, fh, fw, pitch))) return rc;
-        if ((rc = ctx->face_forward(n))) return rc;
+        if (late_fork) {
+            const Net& fn = ctx->face.net;
+            const int split = fn.stage_end[fork_stage];
+            if ((rc = ctx->run_ops(fn, 0, split, 0, n))) return rc;
+            VD_CHECK_HIP(hipEventRecord(ctx->ev_fork, ctx->stream));
+            if ((rc = ctx->run_ops(fn, split, (int)fn.ops.size(), 0, n))) return rc;
+        } else if ((rc = ctx->face_forward(n))) {
+            return rc;
+        }
         if ((rc = ctx->face_post(n, fh, fw, tf))) return rc;
     }
+    if (late_fork) VD_CHECK_HIP(hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
     if (do_plates) {
         hipStream_t main = ctx->stream;
         if (fork) ctx->stream = ctx->stream2;
