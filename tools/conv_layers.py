@@ -70,7 +70,8 @@ def main(path, B=64):
     # The face forward may share the GPU with the plate network on a second
     # stream: anchor on the last face letterbox (space-to-depth form in bf16)
     # and take the conv launches that follow it on the same stream.
-    conv_keys = ("conv_igemm", "conv1x1_stream", "conv_big", "bottleneck_kernel", "stem_pool_kernel", "chain_kernel")
+    conv_keys = ("conv_igemm", "conv1x1_stream", "conv_big", "bottleneck_kernel", "stem_pool_kernel", "chain_kernel",
+                 "conv_persist")
     plan = face_plan(B, block=any("bottleneck_kernel" in r["Kernel_Name"] for r in allk),
                      chain=any("chain_kernel" in r["Kernel_Name"] for r in allk))
     face = face_stream(allk)

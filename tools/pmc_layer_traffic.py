@@ -14,7 +14,8 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from conv_layers import face_plan  # noqa: E402
 from prof_summary import face_stream  # noqa: E402
 
-KEYS = ("conv_igemm", "conv1x1_stream", "conv_big", "bottleneck_kernel", "stem_pool_kernel", "chain_kernel")
+KEYS = ("conv_igemm", "conv1x1_stream", "conv_big", "bottleneck_kernel", "stem_pool_kernel", "chain_kernel",
+        "conv_persist")
 
 
 def last_step(d, counter):
