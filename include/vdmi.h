@@ -16,6 +16,8 @@
  *                                   applied per box in order at     combine_detect.py:246-249
  *   vd_process                   <- the per-batch body of batch_process_images
  *                                                                    combine_detect.py:214-251
+ *   vd_read_boxes                <- the complete per-frame box lists the reference's
+ *                                   loop iterates (combine_detect.py:241-249), past any cap
  *   vd_sync / vd_last_error / vd_destroy: runtime plumbing (no reference equivalent;
  *                                   errors map to the reference's drop-the-batch
  *                                   behaviour at combine_detect.py:226-228 in the
@@ -42,12 +44,12 @@
 extern "C" {
 #endif
 
-#define VDMI_ABI_VERSION 1
+#define VDMI_ABI_VERSION 2   /* 2: complete keep lists (count may exceed cap, vd_read_boxes) */
 
 #define VD_OK            0
 #define VD_ERR_ARG      -1   /* bad argument / shape */
 #define VD_ERR_HIP      -2   /* HIP runtime error */
-#define VD_ERR_CAPACITY -3   /* a per-frame box/candidate capacity was exceeded */
+#define VD_ERR_CAPACITY -3   /* vd_mosaic: a host box list's count exceeds its cap */
 #define VD_ERR_WEIGHTS  -4   /* weight blob missing a tensor / wrong shape */
 #define VD_ERR_STATE    -5   /* call out of order (e.g. detect before weights) */
 #define VD_ERR_NOMEM    -6   /* device allocation failed */
@@ -96,8 +98,11 @@ typedef struct vd_cfg {
 } vd_cfg;
 
 /* Per-frame box lists, caller-allocated. Frame f's boxes live at
- * [f*cap, f*cap + min(count[f], cap)). count[f] may exceed cap; the call then
- * returns VD_ERR_CAPACITY after filling the first cap boxes. */
+ * [f*cap, f*cap + min(count[f], cap)). count[f] is always the COMPLETE keep count
+ * and may exceed cap: the arrays then hold the first cap boxes (NMS order), the
+ * call still succeeds, vd_read_boxes hands out the complete lists, and the
+ * mosaic of vd_process always covers every kept box (the reference blurs every
+ * box, combine_detect.py:241-249). A NULL vd_boxes* skips the caller copy. */
 typedef struct vd_boxes {
     int32_t  cap;
     int32_t  where;     /* VD_HOST or VD_DEVICE for every array below */
@@ -116,6 +121,13 @@ int   vd_create(const vd_cfg* cfg, int device, vd_ctx** out);
 int   vd_destroy(vd_ctx* ctx);
 int   vd_load_weights(vd_ctx* ctx, int net, const void* blob, size_t bytes, int fmt);
 int   vd_set_stream(vd_ctx* ctx, void* hip_stream);   /* NULL -> library-owned stream */
+/* Kernel-selection switches (A/B measurement, tests that force a kernel form onto
+ * small shapes); the defaults are the production plan. Plan switches (block_fuse,
+ * chain, stem_pool, ssh_fuse, plate_s2d) apply to weights loaded afterwards, the
+ * rest to the next launch. Names: conv_stream conv_stream512 conv_dual conv_taps
+ * conv_n192 conv_small conv_big conv_big_kmin stream_ntt lb_pair mosaic_map
+ * block_fuse chain stem_pool ssh_fuse plate_s2d. VD_ERR_ARG for unknown names. */
+int   vd_set_option(vd_ctx* ctx, const char* name, int value);
 void* vd_get_stream(vd_ctx* ctx);
 int   vd_sync(vd_ctx* ctx);
 
@@ -123,10 +135,17 @@ int vd_detect(vd_ctx* ctx, const uint8_t* frames, int n, int h, int w, size_t pi
               int where, vd_boxes* faces);
 int vd_detect_plates(vd_ctx* ctx, const uint8_t* frames, int n, int h, int w, size_t pitch,
                      int where, vd_boxes* plates);
+/* Mosaic of caller box lists; host lists with count[f] > cap are refused
+ * (VD_ERR_CAPACITY: boxes the caller does not hold would go unblurred). */
 int vd_mosaic(vd_ctx* ctx, const uint8_t* in, uint8_t* out, int n, int h, int w, size_t pitch,
               int where, const vd_boxes* boxes, int level, int mode);
 int vd_process(vd_ctx* ctx, const uint8_t* in, uint8_t* out, int n, int h, int w, size_t pitch,
                int where, int flags, vd_boxes* faces, vd_boxes* plates);
+/* The complete keep lists of the last vd_detect / vd_detect_plates / vd_process
+ * call on this context for frames [0, n) of `net` (VD_NET_*), into `out`
+ * (min(count, out->cap) boxes per frame; count = complete count). Ordered on the
+ * context stream after that call; host targets return when the copy is done. */
+int vd_read_boxes(vd_ctx* ctx, int net, int n, vd_boxes* out);
 
 /* ---- instrumentation (bench / profiling) ---------------------------------- */
 /* When enabled, every launch of kernel family `fam` is bracketed by HIP events

@@ -42,8 +42,18 @@ def mosaic_rectangle_region_single(img, x1, y1, x2, y2, mosaic_level=8):
 
 def mosaic_frame(img, boxes, mosaic_level=8):
     """combine_detect.py:246-249: boxes applied in list order, each reading the
-    previous box's output. ``boxes`` are Python-int (x1,y1,x2,y2) tuples."""
+    previous box's output. ``boxes`` are Python-int (x1,y1,x2,y2) tuples.
+    One copy of the frame, then each box rewrites its region from the current
+    state -- the same values as the reference's fresh array per box
+    (mosaic_rectangle_region_single), without a full-frame copy per box
+    (checked against that composition in tests/test_oracle_kat.py)."""
     out = img.copy()
+    h, w = out.shape[:2]
     for (x1, y1, x2, y2) in boxes:
-        out = mosaic_rectangle_region_single(out, int(x1), int(y1), int(x2), int(y2), mosaic_level)
+        x1, y1, x2, y2 = max(0, int(x1)), max(0, int(y1)), min(w, int(x2)), min(h, int(y2))
+        if x2 <= x1 or y2 <= y1:
+            continue
+        mx = mosaic_axis_map(x2 - x1, mosaic_level)
+        my = mosaic_axis_map(y2 - y1, mosaic_level)
+        out[y1:y2, x1:x2] = out[y1:y2, x1:x2][my][:, mx]   # fancy indexing reads a copy first
     return out

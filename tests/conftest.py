@@ -43,10 +43,10 @@ def face_ctx_factory(gpu):
     import vdmi
     from vdmi import weights
 
-    def make(precision="fp32", max_batch=8, wkind="default", **kw):
-        key = (precision, max_batch, wkind, tuple(sorted(kw.items())))
+    def make(precision="fp32", max_batch=8, wkind="default", options=(), **kw):
+        key = (precision, max_batch, wkind, tuple(options), tuple(sorted(kw.items())))
         if key not in _CTX:
-            ctx = vdmi.Context(precision=precision, max_batch=max_batch, **kw)
+            ctx = vdmi.Context(precision=precision, max_batch=max_batch, options=dict(options), **kw)
             ctx.load_weights(0, face_weights(wkind))
             _CTX[key] = ctx
         return _CTX[key]

@@ -22,13 +22,17 @@ def test_shard_range_partitions():
 
 
 def test_pack_unpack_records():
-    from vdmi.dist import pack_records, unpack_records
+    from vdmi.dist import pack_records, rec_width, unpack_records
     count = torch.tensor([2, 0, 5], dtype=torch.int32)
     xyxy = torch.arange(3 * 4 * 4, dtype=torch.int32).reshape(3, 4, 4)
-    rec = pack_records(count, xyxy, 4)
-    assert rec.shape == (3, 17)
+    score = torch.linspace(0.5, 0.99, 12).reshape(3, 4)
+    anchor = torch.arange(100, 112, dtype=torch.int32).reshape(3, 4)
+    rec = pack_records(count, xyxy, 4, score, anchor, torch.tensor([7, 8, 9], dtype=torch.int32))
+    assert rec.shape == (3, rec_width(4)) == (3, 26)
     out = unpack_records(rec)
-    assert out[0] == [(0, 1, 2, 3), (4, 5, 6, 7)] and out[1] == [] and len(out[2]) == 4   # capped
+    assert list(out) == [7, 8, 9]
+    assert out[7][0] == [(0, 1, 2, 3), (4, 5, 6, 7)] and out[8][0] == [] and len(out[9][0]) == 4   # capped
+    assert out[7][1] == score[0, :2].tolist() and out[9][2] == [108, 109, 110, 111] and out[9][3] == 5
 
 
 def _free_port():
@@ -44,14 +48,20 @@ def _worker(rank, world, port, results):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from vdmi.dist import all_gather_records, pack_records, shard_range, unpack_records
-        n_frames, B, cap = 10, 5, 3
+        n_frames, cap = 11, 3                    # uneven shards: 6 + 5 frames, padded to 6
         b, e = shard_range(n_frames, world, rank)
-        assert e - b == B
+        per_rank = -(-n_frames // world)
         # each rank "detects" frame-index-dependent boxes on its own shard
-        count = torch.tensor([(f % 4) for f in range(b, e)], dtype=torch.int32)
+        count = torch.tensor([(f % 5) for f in range(b, e)], dtype=torch.int32)
         xyxy = torch.tensor([[[f, k, f + 10, k + 10] for k in range(cap)] for f in range(b, e)], dtype=torch.int32)
-        allrec = all_gather_records(pack_records(count, xyxy, cap))
-        results[rank] = unpack_records(allrec)
+        score = torch.tensor([[0.5 + f / 100 + k / 1000 for k in range(cap)] for f in range(b, e)])
+        anchor = torch.tensor([[f * 10 + k for k in range(cap)] for f in range(b, e)], dtype=torch.int32)
+        rec = pack_records(count, xyxy, cap, score, anchor, torch.arange(b, e, dtype=torch.int32))
+        if rec.shape[0] < per_rank:
+            pad = torch.zeros((per_rank - rec.shape[0], rec.shape[1]), dtype=torch.int32)
+            pad[:, 0] = -1
+            rec = torch.cat([rec, pad])
+        results[rank] = unpack_records(all_gather_records(rec))
     finally:
         dist.destroy_process_group()
 
@@ -62,5 +72,12 @@ def test_all_gather_two_ranks_gloo():
     mgr = mp.Manager()
     results = mgr.dict()
     mp.spawn(_worker, args=(world, port, results), nprocs=world, join=True)
-    exp = [[(f, k, f + 10, k + 10) for k in range(min(f % 4, 3))] for f in range(10)]
-    assert results[0] == exp and results[1] == exp
+    for r in (0, 1):
+        got = results[r]
+        assert list(got) == list(range(11))
+        for f in range(11):
+            k = min(f % 5, 3)
+            boxes, scores, anchors, count = got[f]
+            assert boxes == [(f, j, f + 10, j + 10) for j in range(k)] and count == f % 5
+            assert anchors == [f * 10 + j for j in range(k)]
+            np.testing.assert_allclose(scores, [0.5 + f / 100 + j / 1000 for j in range(k)], rtol=1e-6)

@@ -108,17 +108,16 @@ def test_detect_fp16_agrees_4k(gpu, face_ctx_factory):
     assert total > 0 and matched / total >= 0.95, (matched, total)
 
 
-def test_heads_bf16_fused_downsample_matches_unfused(gpu, monkeypatch):
+def test_heads_bf16_fused_downsample_matches_unfused(gpu):
     """bf16 plans fuse each bottleneck's conv3 + downsample into one streaming pass
-    (layer1.0, layer2.0); VD_CONV_DUAL=0 at weight load keeps them separate. The
+    (layer1.0, layer2.0); option conv_dual=0 at weight load keeps them separate. The
     only numeric difference is the bf16 rounding of the downsample output that the
     unfused plan stores, so the heads agree far tighter than the oracle bound."""
     import vdmi
     fr = _frames(2, 1080, 1920, seed=3)
     out = {}
     for dual in ("1", "0"):
-        monkeypatch.setenv("VD_CONV_DUAL", dual)
-        ctx = vdmi.Context(precision="bf16", max_batch=2)
+        ctx = vdmi.Context(precision="bf16", max_batch=2, options={"conv_dual": int(dual)})
         try:
             ctx.load_weights(0, face_weights("default"))
             out[dual] = ctx.forward_heads(fr)
@@ -128,16 +127,15 @@ def test_heads_bf16_fused_downsample_matches_unfused(gpu, monkeypatch):
         assert _rel(a, b) < 2e-2
 
 
-def test_heads_bf16_fused_block_matches_unfused(gpu, monkeypatch):
+def test_heads_bf16_fused_block_matches_unfused(gpu):
     """bf16 plans run each layer1 bottleneck as one kernel (block.hip: t1/t2 in LDS);
-    VD_BLOCK_FUSE=0 at weight load keeps the conv-by-conv chain. Same bf16 weights
+    option block_fuse=0 at weight load keeps the conv-by-conv chain. Same bf16 weights
     and the same bf16 rounding points, only the f32 summation order differs."""
     import vdmi
     fr = _frames(2, 1080, 1920, seed=5)
     out = {}
     for fuse in ("1", "0"):
-        monkeypatch.setenv("VD_BLOCK_FUSE", fuse)
-        ctx = vdmi.Context(precision="bf16", max_batch=2)
+        ctx = vdmi.Context(precision="bf16", max_batch=2, options={"block_fuse": int(fuse)})
         try:
             ctx.load_weights(0, face_weights("default"))
             out[fuse] = ctx.forward_heads(fr)
@@ -147,17 +145,16 @@ def test_heads_bf16_fused_block_matches_unfused(gpu, monkeypatch):
         assert _rel(a, b) < 2e-2
 
 
-def test_heads_bf16_fused_stem_pool_matches_unfused(gpu, monkeypatch):
+def test_heads_bf16_fused_stem_pool_matches_unfused(gpu):
     """bf16 plans run conv1 + bn1 + relu + maxpool as one kernel (stem.hip: the stem map
-    stays in LDS); VD_STEM_POOL=0 at weight load keeps the taps conv + maxpool kernels.
+    stays in LDS); option stem_pool=0 at weight load keeps the taps conv + maxpool kernels.
     Same products in the same K order and the same bf16 rounding, max pooling is
     exact: the heads are identical."""
     import vdmi
     fr = _frames(2, 720, 1280, seed=9)
     out = {}
     for fuse in ("1", "0"):
-        monkeypatch.setenv("VD_STEM_POOL", fuse)
-        ctx = vdmi.Context(precision="bf16", max_batch=2)
+        ctx = vdmi.Context(precision="bf16", max_batch=2, options={"stem_pool": int(fuse)})
         try:
             ctx.load_weights(0, face_weights("default"))
             out[fuse] = ctx.forward_heads(fr)
@@ -273,17 +270,16 @@ def test_retinaface_drop_in_mobilenet(gpu):
         assert [[int(v) for v in b] for b in boxes] == xi.tolist()
 
 
-def test_heads_bf16_chain_matches_unfused(gpu, monkeypatch):
+def test_heads_bf16_chain_matches_unfused(gpu):
     """bf16 plans run layer2's conv3(+bn3+identity+relu) and the next block's conv1
     (+bn1+relu) as one kernel (chain.hip: the block output is handed over in LDS as
-    MFMA B fragments); VD_CHAIN=0 keeps the two streaming launches. Same bf16 weights,
+    MFMA B fragments); option chain=0 keeps the two streaming launches. Same bf16 weights,
     same K order and the same bf16 rounding points."""
     import vdmi
     fr = _frames(2, 1080, 1920, seed=11)
     out = {}
     for chain in ("1", "0"):
-        monkeypatch.setenv("VD_CHAIN", chain)
-        ctx = vdmi.Context(precision="bf16", max_batch=2)
+        ctx = vdmi.Context(precision="bf16", max_batch=2, options={"chain": int(chain)})
         try:
             ctx.load_weights(0, face_weights("default"))
             out[chain] = ctx.forward_heads(fr)
@@ -293,17 +289,16 @@ def test_heads_bf16_chain_matches_unfused(gpu, monkeypatch):
         assert _rel(a, b) < 2e-3, _rel(a, b)
 
 
-def test_heads_bf16_ssh_fused_matches_unfused(gpu, monkeypatch):
+def test_heads_bf16_ssh_fused_matches_unfused(gpu):
     """ReLU-SSH plans (cfg_re50) run conv5X5_1 and conv3X3 as one conv with Cout
     64 + 128 on a 192-wide tile, writing [t5 | c3] of one concat buffer;
-    VD_SSH_FUSE=0 keeps the two convs. Every output channel sees the same K order
+    option ssh_fuse=0 keeps the two convs. Every output channel sees the same K order
     and the same rounding: the heads are identical."""
     import vdmi
     fr = _frames(2, 1080, 1920, seed=13)
     out = {}
     for fuse in ("1", "0"):
-        monkeypatch.setenv("VD_SSH_FUSE", fuse)
-        ctx = vdmi.Context(precision="bf16", max_batch=2)
+        ctx = vdmi.Context(precision="bf16", max_batch=2, options={"ssh_fuse": int(fuse)})
         try:
             ctx.load_weights(0, face_weights("default"))
             out[fuse] = ctx.forward_heads(fr)

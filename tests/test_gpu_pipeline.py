@@ -20,7 +20,7 @@ def test_batch_process_images(gpu, tmp_path):
         (tmp_path / name).write_bytes(b"")          # the listing drives the batch order
     saved = {}
     face = vdmi.Retinaface(input_shape=[640, 640, 3], nms_iou=0.4, max_batch=4, weights=weights.retinaface_state_dict(0))
-    plate = vdmi.YOLO("nonexistent.pt", max_batch=4)
+    plate = vdmi.YOLO(weights="random", max_batch=4)
     n, nf, npl = batch_process_images(str(tmp_path), str(tmp_path / "out"), face, plate, batch_size=3,
                                       loader=lambda p: frames[os.path.basename(p)],
                                       saver=lambda img, p: saved.__setitem__(os.path.basename(p), img))

@@ -92,7 +92,7 @@ def test_plate_post_exact_given_raw(gpu, prec):
 
 def test_yolo_drop_in_results(gpu):
     from vdmi import YOLO, synth
-    det = YOLO("nonexistent.pt", precision="fp32", max_batch=4).cuda()
+    det = YOLO(weights="random", precision="fp32", max_batch=4).cuda()
     imgs = list(synth.frames(2, 1080, 1920, seed=6))
     res = det(imgs, verbose=False, conf=0.5)
     assert len(res) == 2 and all(r.orig_shape == (1080, 1920) for r in res)
@@ -120,9 +120,9 @@ def test_process_faces_and_plates_mosaic(gpu):
 
 
 @pytest.mark.parametrize("h,w", [(1080, 1920), (720, 1280), (640, 640), (480, 640)])
-def test_plate_raw_bf16_s2d_matches_plain(gpu, monkeypatch, h, w):
+def test_plate_raw_bf16_s2d_matches_plain(gpu, h, w):
     """bf16 plans letterbox the plate canvas in space-to-depth form and run model.0
-    (3x3 stride 2) as a 2x2 conv over it (plate_net.cpp yconv_s2d); VD_PLATE_S2D=0
+    (3x3 stride 2) as a 2x2 conv over it (plate_net.cpp yconv_s2d); option plate_s2d=0
     keeps the 8-channel canvas and the 3x3 conv. Same 27 products per output in
     another f32 order: the raw outputs agree to bf16 rounding, and both stay within
     the bf16 oracle bound."""
@@ -131,8 +131,7 @@ def test_plate_raw_bf16_s2d_matches_plain(gpu, monkeypatch, h, w):
     fr = synth.frames(2, h, w, seed=7)
     out = {}
     for s2d in ("1", "0"):
-        monkeypatch.setenv("VD_PLATE_S2D", s2d)
-        c = vdmi.Context(precision="bf16", max_batch=2)
+        c = vdmi.Context(precision="bf16", max_batch=2, options={"plate_s2d": int(s2d)})
         try:
             c.load_weights(1, weights.yolov8n_state_dict(0))
             out[s2d] = c.plate_raw(fr)
@@ -145,10 +144,10 @@ def test_plate_raw_bf16_s2d_matches_plain(gpu, monkeypatch, h, w):
 
 
 @pytest.mark.parametrize("h,w", [(1080, 1920), (720, 1280), (480, 640), (1080, 1440)])
-def test_process_paired_letterbox_matches_separate(gpu, monkeypatch, h, w):
+def test_process_paired_letterbox_matches_separate(gpu, h, w):
     """With faces and plates in one vd_process call, both s2d canvases come from one
     read of the frames (pre.hip letterbox_s2d_pair_kernel) where the resize geometry
-    matches; VD_LB_PAIR=0 runs the two letterboxes apart. Same per-pixel arithmetic:
+    matches; option lb_pair=0 runs the two letterboxes apart. Same per-pixel arithmetic:
     box lists and mosaicked frames are identical."""
     import vdmi
     from vdmi import _lib, synth, weights
@@ -156,17 +155,21 @@ def test_process_paired_letterbox_matches_separate(gpu, monkeypatch, h, w):
     flags = _lib.VD_PROC_FACES | _lib.VD_PROC_PLATES | _lib.VD_PROC_MOSAIC | _lib.VD_PROC_MOSAIC_PLATES
     res = {}
     for pair in ("1", "0"):
-        monkeypatch.setenv("VD_LB_PAIR", pair)
-        c = vdmi.Context(precision="bf16", max_batch=2)
+        c = vdmi.Context(precision="bf16", max_batch=2, options={"lb_pair": int(pair)})
         try:
             c.load_weights(0, weights.retinaface_state_dict(0))
             c.load_weights(1, weights.yolov8n_state_dict(0))
+            c.timing(True)
+            c.timing_reset()
             out, faces, plates = c.process(fr, flags=flags)
+            _, n_lb, _ = c.timing_read(_lib.FAM_LETTERBOX)
+            assert n_lb == (1 if pair == "1" else 2), (pair, n_lb)   # the paired kernel really ran
             res[pair] = (out.copy(), [faces.frame(b)[0].copy() for b in range(2)],
                          [plates.frame(b)[0].copy() for b in range(2)])
         finally:
             c.close()
     np.testing.assert_array_equal(res["1"][0], res["0"][0])
+    assert sum(len(x) for x in res["1"][1] + res["1"][2]) > 0      # boxes were found to compare
     for b in range(2):
         np.testing.assert_array_equal(res["1"][1][b], res["0"][1][b])
         np.testing.assert_array_equal(res["1"][2][b], res["0"][2][b])

@@ -57,7 +57,7 @@ def test_struct_layout_matches_header(tmp_path):
 def test_default_cfg_and_version():
     from vdmi import _lib
     lib = _lib.load()
-    assert lib.vd_abi_version() == 1
+    assert lib.vd_abi_version() == 2
     c = _lib.default_cfg()
     assert (c.input_h, c.input_w, c.max_batch) == (640, 640, 64)          # combine_detect.py:860, config.ini:35
     assert abs(c.confidence - 0.5) < 1e-9 and c.nms_iou == 0.4 and c.mosaic_level == 8

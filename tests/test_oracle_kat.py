@@ -196,3 +196,26 @@ def test_mosaic_sequential_overlap_order_matters():
     assert ab[0, 4:12, 0].tolist() == [0] * 8   # b reads a's output at column 4 (= 0)
     assert ba[0, 4:12, 0].tolist() == [0, 0, 0, 0, 4, 4, 4, 4]
     assert ba[0, 0:4, 0].tolist() == [0] * 4
+
+
+def test_mosaic_frame_equals_per_box_copy_composition():
+    """oracle.mosaic.mosaic_frame (one copy, in-place per box) == the reference's
+    composition of mosaic_rectangle_region_single calls (a fresh array per box,
+    combine_detect.py:246-249), incl. overlaps, clipping and empty boxes."""
+    from oracle import mosaic as om
+    from vdmi import synth
+    img = synth.frames(1, 97, 131, seed=5)[0]
+    boxes = [tuple(int(v) for v in b) for b in synth.box_lists(1, 97, 131, per_frame=24, seed=9)[0]]
+    boxes += [(-5, -5, 7, 40), (120, 90, 200, 200), (30, 30, 30, 60), (10, 10, 14, 13)]
+    exp = img.copy()
+    for b in boxes:
+        exp = om.mosaic_rectangle_region_single(exp, *b, 8)
+    np.testing.assert_array_equal(om.mosaic_frame(img, boxes, 8), exp)
+    np.testing.assert_array_equal(om.mosaic_frame(img, boxes, 3), _compose(om, img, boxes, 3))
+
+
+def _compose(om, img, boxes, level):
+    out = img.copy()
+    for b in boxes:
+        out = om.mosaic_rectangle_region_single(out, *b, level)
+    return out

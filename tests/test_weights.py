@@ -97,3 +97,32 @@ def test_oracle_yolo_runs_small():
     raw = raw_heads(lv)
     res = postprocess(raw, [(8, 12), (4, 6), (2, 3)], (64, 96), (64, 96))
     assert len(res) == 1
+
+
+def test_dropins_refuse_missing_weights():
+    """A missing checkpoint is an error, never a silent switch to random weights
+    (a desensitisation run on random weights leaves faces visible)."""
+    import pytest as _pt
+    from vdmi import plate
+    with _pt.raises(FileNotFoundError):
+        plate.load_plate_weights("/nonexistent/best.pt")
+
+
+def test_plate_weights_refuse_pickled_objects(tmp_path):
+    """A pickled ultralytics-style object is refused by the weights-only loader; a
+    converted state_dict file loads."""
+    import fractions
+
+    import pytest as _pt
+    import torch
+    from vdmi import plate, weights
+
+    bad = tmp_path / "best.pt"     # an arbitrary pickled object stands in for an ultralytics model
+    torch.save({"model": fractions.Fraction(1, 3)}, bad)
+    with _pt.raises(ValueError):
+        plate.load_plate_weights(str(bad))
+    sd = {k: torch.from_numpy(v) for k, v in weights.yolov8n_state_dict(0).items()}
+    good = tmp_path / "best_sd.pt"
+    torch.save(sd, good)
+    got = plate.load_plate_weights(str(good))
+    assert set(got) == set(sd) and all(np.array_equal(got[k], sd[k].numpy()) for k in sd)

@@ -1,6 +1,6 @@
 // convbench.cpp — time the conv launchers of libvdmi.so on synthetic bf16 layers
-// (no Python, no host copies in the timed loop). Kernel choice follows the same
-// env knobs as the library (VD_CONV_BIG, VD_CONV_BIG_PH, VD_CONV_STREAM, ...).
+// (no Python, no host copies in the timed loop). Kernel choice is the library's
+// default plan (VdTune defaults; ConvArgs.tune may point at a modified copy).
 //
 //   hipcc -O2 -std=c++17 --offload-arch=gfx950 tools/convbench.cpp \
 //         -Ivideo-desensitization_amd/csrc -Iinclude -Lvideo-desensitization_amd/vdmi -lvdmi \

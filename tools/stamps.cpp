@@ -30,7 +30,6 @@ int main(int argc, char** argv) {
     a.x = x; a.xh = 1; a.xw = M; a.ldx = K; a.w = w; a.scale = sc; a.shift = sh;
     a.y = y; a.yh = 1; a.yw = M; a.ldy = N; a.B = 1; a.cin_pad = K; a.cout = N; a.kpad = K;
     a.kh = a.kw = a.stride = 1; a.M = M; a.act = VD_ACT_NONE;
-    setenv("VD_CONV_BIG_PH", "8", 1);
     for (int i = 0; i < 5; ++i) (void)vd_launch_conv_big(a, 0);
     (void)hipDeviceSynchronize();
     std::vector<unsigned long long> s(8 * 2048);

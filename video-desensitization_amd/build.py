@@ -1,4 +1,4 @@
-"""Build libvdmi.so (HIP, gfx950) and the oracle's C helper, in-tree.
+"""Build libvdmi.so (HIP, gfx950), in-tree.
 
     python video-desensitization_amd/build.py            # incremental
     python video-desensitization_amd/build.py --force    # rebuild everything
@@ -22,8 +22,8 @@ LIB = os.path.join(HERE, "vdmi", "libvdmi.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("VD_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["conv.hip", "conv_persist.hip", "conv1x1.hip", "conv_big.hip", "pre.hip", "post.hip", "mosaic.hip", "yolo_post.hip",
-           "block.hip", "block.cpp", "chain.hip", "stem.hip", "dwconv.hip", "runtime.cpp", "face_net.cpp", "plate_net.cpp"]
+SOURCES = ["conv.hip", "conv1x1.hip", "conv_big.hip", "pre.hip", "post.hip", "mosaic.hip", "block.hip", "block.cpp",
+           "chain.hip", "stem.hip", "dwconv.hip", "runtime.cpp", "face_net.cpp", "plate_net.cpp"]
 HEADERS = ["vd_common.h", "vd_math.h", "nets.h"]
 FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off",
          "-Wall", "-Wno-unused-function", f"-I{os.path.join(ROOT, 'include')}"]
@@ -52,7 +52,10 @@ def _compile(src, force):
 
 def build(force=False, jobs=8):
     os.makedirs(OBJ, exist_ok=True)
-    srcs = [s for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
+    missing = [s for s in SOURCES if not os.path.exists(os.path.join(CSRC, s))]
+    if missing:
+        raise FileNotFoundError(f"missing sources: {missing}")
+    srcs = SOURCES
     with ThreadPoolExecutor(max_workers=jobs) as ex:
         results = list(ex.map(lambda s: _compile(s, force), srcs))
     errs = [e for _, e in results if e]

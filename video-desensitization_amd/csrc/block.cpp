@@ -56,7 +56,7 @@ bool Ctx::block_ok(int c1, int c2, int c3, int cd, const Act& x) const {
     if (f32 || f16 || x.f32) return false;
     const bool ds = cd >= 0;
     const int cin = x.c;
-    if (!vd_block_ok(cin, ds, x.h, x.w)) return false;
+    if (!tune.block_fuse || !vd_block_ok(cin, ds, x.h, x.w)) return false;
     if (!is_conv(convs[c1], cin, 64, 1, 1, 0, VD_ACT_RELU)) return false;
     if (!is_conv(convs[c2], 64, 64, 3, 1, 1, VD_ACT_RELU)) return false;
     if (!is_conv(convs[c3], 64, 256, 1, 1, 0, VD_ACT_RELU)) return false;

@@ -417,8 +417,6 @@ hipError_t launch(const BlockArgs& a, hipStream_t s) {
 }  // namespace
 
 bool vd_block_ok(int cin, bool ds, int h, int w) {
-    const char* e = getenv("VD_BLOCK_FUSE");
-    if (e && atoi(e) == 0) return false;
     if (!((cin == 256 && !ds) || (cin == 64 && ds))) return false;
     return h > 0 && w > 0 && (double)h * w * cin * 2 < 2147483647.0 && (double)h * w * CO * 2 < 2147483647.0;
 }

@@ -213,10 +213,8 @@ __global__ __launch_bounds__(512, 1) void chain_kernel(ChainArgs a) {
 
 // Eligible: the layer2 shape (128 -> 512 -> 128), bf16, dense rows (t2 / identity / out /
 // t1' with channel strides 128 / 512 / 512 / 128, so a group's rows are contiguous for
-// the 1-KB DMA), byte offsets within 2^31 (VD_CHAIN=0 keeps the two-kernel plan).
+// the 1-KB DMA), byte offsets within 2^31 (option chain=0 keeps the two-kernel plan).
 bool vd_chain_ok(int cmid, int cout, int kpad3, int kpad1, int ld_t2, int ld_res, int ld_y, int ld_y2, long M) {
-    const char* e = getenv("VD_CHAIN");
-    if (e && atoi(e) == 0) return false;
     if (cmid != C_MID || cout != C_OUT || kpad3 < C_MID || kpad1 < C_OUT || (kpad3 | kpad1) & 7) return false;
     if (ld_t2 != C_MID || ld_res != C_OUT || ld_y != C_OUT || ld_y2 != C_MID) return false;
     return M > 0 && M * C_OUT * 2 < 0x7fffffffL;

@@ -12,10 +12,10 @@
 //   conv padding); B is the weight packed [Npad][Kpad] at load time.
 //
 //   Block tile BM x BN x (128 bytes of K), 256 threads = 4 wave64s, each wave
-//   a (BM/WAVES_M) x (BN/WAVES_N) sub-tile of 16x16 MFMA tiles. K tiles are
-//   register-staged into a double-buffered LDS image with 128-byte rows and a
-//   (row>>1)&7 XOR swizzle on 16-byte chunks, which makes the ds_read_b128
-//   fragment reads of a 16x16x32 operand conflict-free.
+//   a (BM/WAVES_M) x (BN/WAVES_N) sub-tile of 16x16 MFMA tiles. K tiles arrive
+//   by LDS-DMA (buffer_load ... lds) in a double-buffered LDS image with 128-byte
+//   rows and a (row>>1)&7 XOR swizzle on 16-byte chunks, which makes the
+//   ds_read_b128 fragment reads of a 16x16x32 operand conflict-free.
 //   bf16 mode : v_mfma_f32_16x16x32_bf16, one 16-B fragment per lane per step.
 //   f32  mode : v_mfma_f32_16x16x4_f32 (exact f32), four MFMAs per 16-B fragment.
 //   Epilogue (fused): y = acc*scale + shift (BN eval, same form as torch's
@@ -26,7 +26,6 @@
 //   are placed on one XCD so the panel is fetched into that XCD's L2 once.
 #include "vd_common.h"
 #include <algorithm>
-#include <cstdlib>
 #include <type_traits>
 
 namespace {
@@ -61,7 +60,7 @@ __device__ __attribute__((aligned(16))) unsigned vd_zero16[4] = {0u, 0u, 0u, 0u}
 typedef __attribute__((address_space(3))) void lds_void_t;
 
 // NT threads (4 waves); two LDS stages: one K tile in flight, two barriers per K tile.
-template <typename T, int BM, int BN, int NT, int STAGES, bool DENSE, bool GLDS>
+template <typename T, int BM, int BN, int NT, int STAGES, bool DENSE>
 __global__ __launch_bounds__(NT) void conv_igemm_kernel(ConvArgs a) {
     constexpr int VEC = Elem<T>::VEC;
     constexpr int BKE = 8 * VEC;                 // K elements per 128-byte tile row
@@ -125,46 +124,6 @@ __global__ __launch_bounds__(NT) void conv_igemm_kernel(ConvArgs a) {
     // DENSE: whole tile inside one tap; track (kh, kw, c) incrementally.
     int t_kh = 0, t_kw = 0, t_c = 0;
     const T* xsafe = (const T*)a.x;
-
-    // Global -> registers for K tile kt (padding taps read a valid address and
-    // are zeroed by a select, so the loads stay branch-free and in registers).
-#define VD_LOAD_TILE(kt)                                                                   \
-    do {                                                                                  \
-        int dy, dx, c;                                                                    \
-        bool kval = true;                                                                 \
-        if constexpr (DENSE) {                                                            \
-            dy = t_kh; dx = t_kw; c = t_c + chunk * VEC;                                  \
-        } else {                                                                          \
-            const int kv = (kt) * 8 + chunk;                                              \
-            const int tap = kv / cvec;                                                    \
-            c = (kv - tap * cvec) * VEC;                                                  \
-            kval = tap < ntap;                                                            \
-            dy = tap / a.kw; dx = tap - dy * a.kw;                                        \
-        }                                                                                 \
-        const long toff = dy * tap_dy + (long)dx * a.ldx + c;                             \
-        _Pragma("unroll") for (int i = 0; i < A_IT; ++i) {                                \
-            const int iy = iy0[i] + dy, ix = ix0[i] + dx;                                 \
-            const bool ok = kval && (unsigned)iy < (unsigned)a.xh && (unsigned)ix < (unsigned)a.xw; \
-            const T* src = ok ? (const T*)a.x + (pix0[i] + toff) : xsafe;                 \
-            const u32x4 v = *(const u32x4*)src;                                           \
-            ra[i] = ok ? v : u32x4{0u, 0u, 0u, 0u};                                       \
-        }                                                                                 \
-        _Pragma("unroll") for (int i = 0; i < B_IT; ++i)                                  \
-            rb[i] = *(const u32x4*)(wbase + (size_t)(ROWS * i) * a.kpad + (size_t)(kt) * BKE); \
-        if constexpr (DENSE) {                                                            \
-            t_c += BKE;                                                                   \
-            if (t_c >= a.cin_pad) { t_c = 0; if (++t_kw == a.kw) { t_kw = 0; ++t_kh; } } \
-        }                                                                                 \
-    } while (0)
-#define VD_STORE_TILE(buf)                                                                 \
-    do {                                                                                  \
-        char* As_ = smem + (buf) * BUF;                                                   \
-        char* Bs_ = As_ + BM * 128;                                                       \
-        _Pragma("unroll") for (int i = 0; i < A_IT; ++i)                                  \
-            *(u32x4*)(As_ + lds_off(rbase + ROWS * i, chunk)) = ra[i];                    \
-        _Pragma("unroll") for (int i = 0; i < B_IT; ++i)                                  \
-            *(u32x4*)(Bs_ + lds_off(rbase + ROWS * i, chunk)) = rb[i];                    \
-    } while (0)
 
     // LDS-DMA form: every lane DMAs its 16-B chunk straight into the K buffer.
     // The destination is lane-linear (wave w, instruction i -> rows w*8+32i ..
@@ -277,7 +236,7 @@ __global__ __launch_bounds__(NT) void conv_igemm_kernel(ConvArgs a) {
         rpf[q] = *(const u32x4*)rp;
     }
 
-    if constexpr (GLDS) {
+    {
         // Two LDS buffers, tile kt+1 in flight while kt is consumed. Raw barriers
         // with counted vmcnt: __syncthreads() would add vmcnt(0) and drain the DMA.
         constexpr int LPT = A_IT + B_IT;                 // DMA instructions per lane per tile
@@ -291,17 +250,6 @@ __global__ __launch_bounds__(NT) void conv_igemm_kernel(ConvArgs a) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             if (kt + 2 < nk) VD_GLDS_TILE(kt + 2, kt & 1);
-        }
-    } else {
-        VD_LOAD_TILE(0);
-        VD_STORE_TILE(0);
-        __syncthreads();
-        for (int kt = 0; kt < nk; ++kt) {
-            const int cur = kt & 1;
-            if (kt + 1 < nk) VD_LOAD_TILE(kt + 1);
-            VD_COMPUTE(cur);
-            if (kt + 1 < nk) VD_STORE_TILE(cur ^ 1);
-            __syncthreads();
         }
     }
 
@@ -406,14 +354,11 @@ __global__ __launch_bounds__(NT) void conv_igemm_kernel(ConvArgs a) {
     }
 }
 
-#undef VD_LOAD_TILE
-#undef VD_STORE_TILE
 #undef VD_GLDS_TILE
 #undef VD_COMPUTE
 
 template <typename T, int BM, int BN, int NT = 256, int STAGES = 2>
 hipError_t launch_bn(const ConvArgs& a0, bool dense, hipStream_t s) {
-    static const bool glds = [] { const char* e = getenv("VD_CONV_GLDS"); return !e || atoi(e) != 0; }();
     ConvArgs a = a0;
     a.ntiles_n = (a.cout + BN - 1) / BN;
     const int mt = (a.M + BM - 1) / BM;
@@ -423,22 +368,23 @@ hipError_t launch_bn(const ConvArgs& a0, bool dense, hipStream_t s) {
     constexpr size_t BUF = (size_t)(BM + BN) * 128, EPI = (size_t)(BM / EP) * (BN + 4) * 4;
     const int nk = a.kpad / (8 * VEC);
     const size_t lds = std::max((nk > 1 ? STAGES : 1) * BUF, EPI);
-    if (glds) {
-        if (dense) hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, NT, 2, true, true>), grid, block, lds, s, a);
-        else hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, NT, 2, false, true>), grid, block, lds, s, a);
-    } else {
-        if (dense) hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, NT, 2, true, false>), grid, block, lds, s, a);
-        else hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, NT, 2, false, false>), grid, block, lds, s, a);
-    }
+    if (dense) hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, NT, 2, true>), grid, block, lds, s, a);
+    else hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, NT, 2, false>), grid, block, lds, s, a);
     return hipGetLastError();
 }
 
 }  // namespace
 
-// Tile selection: BN follows Cout (32 heads / 64 / 128), BM = 128; large dense
-// bf16 layers with Cout >= 128 take the 256 x 128, 8-wave, 3-stage form.
-// Weights must be packed with Npad a multiple of the chosen BN (runtime pads to 128).
-hipError_t vd_launch_conv(const ConvArgs& a, bool f32, hipStream_t s) {
+static const VdTune k_default_tune{};
+
+// Tile selection: BN follows Cout (32 heads / 64 / 128 / 192), BM = 128 (64 when the
+// 128-row grid is small); bf16 layers go to the streaming / phased / taps kernels
+// where those apply. Weights must be packed with Npad a multiple of the chosen BN
+// (runtime pads to 128).
+hipError_t vd_launch_conv(const ConvArgs& a0, bool f32, hipStream_t s) {
+    ConvArgs a = a0;
+    if (!a.tune) a.tune = &k_default_tune;
+    const VdTune& t = *a.tune;
     const int vec = f32 ? 4 : 8;
     const int bke = 8 * vec;
     const bool dense = (a.cin_pad % bke) == 0;
@@ -446,9 +392,9 @@ hipError_t vd_launch_conv(const ConvArgs& a, bool f32, hipStream_t s) {
         if (f32 || a.f16 || !vd_conv1x1_dual_ok(a)) return hipErrorInvalidValue;
         return vd_launch_conv1x1_stream(a, s);
     }
+    const int bn = a.cout <= 32 ? 32 : (a.cout <= 64 ? 64 : 128);
+    const long tiles128 = (long)((a.M + 127) / 128) * ((a.cout + bn - 1) / bn);
     if (a.f16) {   // fp16 mode (VD_PREC_FP16): the implicit GEMM on v_mfma_f32_16x16x32_f16
-        const int bn = a.cout <= 32 ? 32 : (a.cout <= 64 ? 64 : 128);
-        const long tiles128 = (long)((a.M + 127) / 128) * ((a.cout + bn - 1) / bn);
         if (tiles128 < 512) {
             if (bn == 32) return launch_bn<_Float16, 64, 32>(a, dense, s);
             if (bn == 64) return launch_bn<_Float16, 64, 64>(a, dense, s);
@@ -458,45 +404,27 @@ hipError_t vd_launch_conv(const ConvArgs& a, bool f32, hipStream_t s) {
         if (bn == 64) return launch_bn<_Float16, 128, 64>(a, dense, s);
         return launch_bn<_Float16, 128, 128>(a, dense, s);
     }
-    if (!f32 && vd_conv1x1_stream_ok(a)) return vd_launch_conv1x1_stream(a, s);
-    if (!f32 && vd_conv_big_ok(a)) return vd_launch_conv_big(a, s);
-    if (!f32 && vd_conv_big128_ok(a)) return vd_launch_conv_big128(a, s);
-    if (!f32 && vd_conv_taps_ok(a)) return vd_launch_conv_taps(a, s);
-    if (!f32 && dense && vd_conv_persist_ok(a)) return vd_launch_conv_persist(a, s);
     if (f32) {
         if (a.cout <= 32) return launch_bn<float, 128, 32>(a, dense, s);
         if (a.cout <= 64) return launch_bn<float, 128, 64>(a, dense, s);
         return launch_bn<float, 128, 128>(a, dense, s);
     }
+    if (vd_conv1x1_stream_ok(a)) return vd_launch_conv1x1_stream(a, s);
+    if (vd_conv_big_ok(a)) return vd_launch_conv_big(a, s);
+    if (vd_conv_taps_ok(a)) return vd_launch_conv_taps(a, s);
     // Small grids (YOLO's deep levels, RetinaFace level 3): 64-row tiles give
     // twice the workgroups, so the launch covers more of the 256 CUs.
-    const int bn = a.cout <= 32 ? 32 : (a.cout <= 64 ? 64 : 128);
-    const long tiles128 = (long)((a.M + 127) / 128) * ((a.cout + bn - 1) / bn);
-    const char* e = getenv("VD_CONV_SMALL");
-    const long small_lim = e ? atol(e) : 512;
     // Cout 129-192 (the fused SSH conv5X5_1 + conv3X3): one 192-wide N tile instead
-    // of two 128-wide ones, so each A tile is staged once (VD_CONV_N192=0: off)
-    const char* e192 = getenv("VD_CONV_N192");
-    const bool n192 = a.cout > 128 && a.cout <= 192 && !(e192 && atoi(e192) == 0);
-    if (tiles128 < small_lim) {
+    // of two 128-wide ones, so each A tile is staged once.
+    const bool n192 = a.cout > 128 && a.cout <= 192 && t.conv_n192;
+    if (tiles128 < t.conv_small) {
         if (n192) return launch_bn<__bf16, 64, 192>(a, dense, s);
         if (bn == 32) return launch_bn<__bf16, 64, 32>(a, dense, s);
         if (bn == 64) return launch_bn<__bf16, 64, 64>(a, dense, s);
         return launch_bn<__bf16, 64, 128>(a, dense, s);
     }
     if (bn == 32) return launch_bn<__bf16, 128, 32>(a, dense, s);
-    if (bn == 64) {
-        const char* t = getenv("VD_CONV_TALL");          // min 128-row tiles for 256-row tiles (0: off)
-        const long tall_min = t ? atol(t) : 0;   // measured slower than 128x64 (1 workgroup/CU): off
-        if (dense && tall_min > 0 && tiles128 >= tall_min) return launch_bn<__bf16, 256, 64>(a, dense, s);
-        return launch_bn<__bf16, 128, 64>(a, dense, s);
-    }
+    if (bn == 64) return launch_bn<__bf16, 128, 64>(a, dense, s);
     if (n192) return launch_bn<__bf16, 128, 192>(a, dense, s);
-    // Cout 65-128 on large grids: 192-row tiles (same operand footprint as 128x192).
-    // Off by default: 2-6 % slower than 128x128 on layer2's 3x3 (K 1152; fewer tiles,
-    // a worse last wave of the grid)
-    const char* em = getenv("VD_CONV_M192");   // min 128x128 tiles for 192x128 (0: off)
-    const long m192_min = em ? atol(em) : 0;
-    if (m192_min > 0 && tiles128 >= m192_min) return launch_bn<__bf16, 192, 128>(a, dense, s);
     return launch_bn<__bf16, 128, 128>(a, dense, s);
 }

@@ -348,10 +348,8 @@ bool mode_ok(const ConvArgs& a) {
 // Eligible: bf16, 1x1 taps without padding, K in {64,128,256}, Cout a multiple of
 // the channel slice, 16-B aligned channel offsets/strides for the residual and output.
 bool vd_conv1x1_stream_ok(const ConvArgs& a) {
-    const char* e = getenv("VD_CONV_STREAM");   // read per call (A/B and tests)
-    if ((e && atoi(e) == 0) || a.kh != 1 || a.kw != 1 || a.pad != 0) return false;
-    const char* e5 = getenv("VD_CONV_STREAM512");
-    const bool k512 = a.cin_pad == 512 && !(e5 && atoi(e5) == 0);
+    if (!a.tune->conv_stream || a.kh != 1 || a.kw != 1 || a.pad != 0) return false;
+    const bool k512 = a.cin_pad == 512 && a.tune->conv_stream512;
     if (a.cin_pad != 64 && a.cin_pad != 128 && a.cin_pad != 256 && !k512) return false;
     if (a.kpad < a.cin_pad || (a.cout % 64) != 0) return false;
     if ((a.ldx | a.xcoff) & 7) return false;
@@ -363,8 +361,7 @@ bool vd_conv1x1_stream_ok(const ConvArgs& a) {
 // DUAL (conv3 + downsample): instantiated for ResNet layer1.0 (K 64 + 64) and
 // layer2.0 (K 128 + 256 at stride 2), 128-channel slices, ReLU.
 bool vd_conv1x1_dual_ok(const ConvArgs& a) {
-    const char* e = getenv("VD_CONV_DUAL");
-    if ((e && atoi(e) == 0) || !a.x2) return false;
+    if (!a.x2 || (a.tune && !a.tune->conv_dual)) return false;
     if (a.kh != 1 || a.kw != 1 || a.pad != 0 || a.stride != 1 || a.act != VD_ACT_RELU || a.res_mode != VD_RES_NONE)
         return false;
     if (a.cout % 128 || a.kpad != a.cin_pad || a.kpad2 != a.cin2_pad) return false;
@@ -378,9 +375,9 @@ hipError_t vd_launch_conv1x1_stream(const ConvArgs& a, hipStream_t s) {
         return launch_stream<4, 8, VD_ACT_RELU, VD_RES_NONE, false, 8>(a, s);
     }
     // 256-channel slices at K 128/256 when Cout allows (bottleneck conv3 of layer2/3:
-    // 1.1-1.2x the 128-channel form, tools/convbench k512; VD_STREAM_NTT=8 keeps 128),
+    // 1.1-1.2x the 128-channel form, tools/convbench k512; option stream_ntt=8 keeps 128),
     // else 128-channel slices (64 when Cout is not a multiple of 128)
-    static const int ntt_env = [] { const char* e = getenv("VD_STREAM_NTT"); return e ? atoi(e) : 16; }();
+    const int ntt_env = a.tune ? a.tune->stream_ntt : 16;
     if (ntt_env == 16 && a.cout % 256 == 0 && a.cin_pad == 128) return launch_mode<4, 16, false>(a, s);
     if (ntt_env == 16 && a.cout % 256 == 0 && a.cin_pad == 256) return launch_mode<8, 16, false>(a, s);
     const bool wide = a.cout % 128 == 0;
@@ -393,11 +390,10 @@ hipError_t vd_launch_conv1x1_stream(const ConvArgs& a, hipStream_t s) {
 // General taps (any kh x kw, stride, pad; Cin a multiple of 8) for small layers:
 // K (padded to 64) <= TAPS_KMAX and Cout a multiple of 16 up to 128. Measured
 // (tools/convbench yolo): 1.2-2.4x the implicit GEMM at K <= 288 (YOLO's 16-64
-// channel layers), 0.6x at K = 576, hence the cut. VD_CONV_TAPS=0 disables.
+// channel layers), 0.6x at K = 576, hence the cut (option conv_taps=0 disables).
 constexpr int TAPS_KMAX = 320;
 bool vd_conv_taps_ok(const ConvArgs& a) {
-    const char* e = getenv("VD_CONV_TAPS");
-    if (e && atoi(e) == 0) return false;
+    if (!a.tune->conv_taps) return false;
     if ((a.cin_pad & 7) || a.kpad > TAPS_KMAX || (a.kpad & 63) || (a.cout & 15) || a.cout > 128) return false;
     if ((a.ldx | a.xcoff) & 7) return false;
     const int align = (a.cout % 32 == 0) ? 7 : 3;        // 16-B (or 8-B for 16-channel slices) stores

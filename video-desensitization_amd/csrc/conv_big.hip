@@ -12,15 +12,15 @@
 //     B0 (channels 0-127), B1, A1, staged by LDS-DMA (global_load_lds_dwordx4,
 //     source-side XOR swizzle) into two K stages (128 KB of LDS, 1 workgroup/CU).
 //   * Phases run (A0,B0) (A0,B1) (A1,B1) (A1,B0): A fragments are read once per
-//     half, B fragments at most three times per K tile. Half-tile h is issued
-//     5 phases before its first use, so 3 half-tiles (6 DMAs per lane) stay in
-//     flight across each phase's single raw s_barrier, retired by a counted
-//     s_waitcnt vmcnt (never 0 in steady state). A slot is refilled only after
-//     the barrier that follows its last read (see the schedule proof in DESIGN.md).
+//     half, B0 is kept in registers across the K tile. Two raw barriers per
+//     phase; waves 4-7 run one barrier behind waves 0-3, so on every SIMD one
+//     wave issues its fragment reads and DMA while the other multiplies.
+//     Half-tile h is issued 6 phases before its first use and retired by a
+//     counted s_waitcnt vmcnt (never 0 in steady state); a slot is refilled only
+//     two phases after its last read (the skew rule; proof in DESIGN.md).
 //   * Epilogue: the f32 tile goes through LDS 64 rows at a time, 16-B stores.
 #include "vd_common.h"
 #include <algorithm>
-#include <cstdlib>
 
 namespace {
 
@@ -82,7 +82,6 @@ __device__ __forceinline__ void wait_vm(int n) {
     }
 }
 
-template <int PH>   // 4: one quadrant per phase; 2: two per phase; 8: 4 phases, staggered wave groups
 __global__ __launch_bounds__(512) void conv_big_kernel(ConvArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -175,88 +174,9 @@ __global__ __launch_bounds__(512) void conv_big_kernel(ConvArgs a) {
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int j = 0; j < 2; ++j) acc[x][y][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    u32x4 af[4][2], bfr[2][2], bq[2][2][2], b0[2][2], b1[2][2];
+    u32x4 af[4][2], b0[2][2], b1[2][2];
 
-    // One phase: wait for its half-tiles, barrier, refill 5 ahead, read fragments, 16 MFMAs.
-#define VDB_PHASE(R, MH, NH, READ_A, READ_B, STEADY)                                           \
-    do {                                                                                       \
-        const int P = 4 * t + (R);                                                             \
-        const int need = 4 * t + ((R) == 0 ? 1 : ((R) == 1 ? 2 : 3));                          \
-        if (STEADY) {   /* P + 4 < nh_total - 1: 3 half-tiles in flight (4 after phase 3) */   \
-            if ((R) == 3) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");          \
-            else asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");                   \
-        } else {                                                                               \
-            wait_halves(min(P + 4, nh_total - 1) - need);                                      \
-        }                                                                                      \
-        __builtin_amdgcn_s_barrier();                                                          \
-        asm volatile("" ::: "memory");                                                         \
-        if (P + 5 < nh_total) VDB_ISSUE(P + 5);                                                \
-        const char* st_ = smem + (t & 1) * 4 * HT;                                             \
-        if (READ_A) {                                                                          \
-            const char* As_ = st_ + ((MH) ? 3 : 0) * HT;                                       \
-            _Pragma("unroll") for (int i = 0; i < 4; ++i)                                      \
-            _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                   \
-                af[i][ks] = *(const u32x4*)(As_ + lds_off(wr * 64 + i * 16 + (lane & 15), ks * 4 + (lane >> 4))); \
-        }                                                                                      \
-        if (READ_B) {                                                                          \
-            const char* Bs_ = st_ + ((NH) ? 2 : 1) * HT;                                       \
-            _Pragma("unroll") for (int j = 0; j < 2; ++j)                                      \
-            _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                   \
-                bfr[j][ks] = *(const u32x4*)(Bs_ + lds_off(wc * 32 + j * 16 + (lane & 15), ks * 4 + (lane >> 4))); \
-        }                                                                                      \
-        __builtin_amdgcn_s_setprio(1);                                                         \
-        _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                       \
-        _Pragma("unroll") for (int i = 0; i < 4; ++i)                                          \
-        _Pragma("unroll") for (int j = 0; j < 2; ++j)                                          \
-            acc[MH][NH][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(                       \
-                __builtin_bit_cast(bf16x8_t, af[i][ks]), __builtin_bit_cast(bf16x8_t, bfr[j][ks]), \
-                acc[MH][NH][i][j], 0, 0, 0);                                                   \
-        __builtin_amdgcn_s_setprio(0);                                                         \
-    } while (0)
-
-    // Two-phase form: phase 0 = quadrants (0,0),(0,1) from A0, B0, B1; phase 1 =
-    // (1,1),(1,0) from A1 and the B fragments still in registers. Half-tiles
-    // 2P+6 and 2P+7 are issued in phase P (3-4 half-tiles in flight at each wait).
-#define VDB_PHASE2(R, STEADY)                                                                  \
-    do {                                                                                       \
-        const int P = 2 * t + (R);                                                             \
-        const int need = 4 * t + ((R) == 0 ? 2 : 3);                                           \
-        if (STEADY) {                                                                          \
-            if ((R) == 1) asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");          \
-            else asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");                   \
-        } else {                                                                               \
-            wait_halves(min(2 * P + 5, nh_total - 1) - need);                                  \
-        }                                                                                      \
-        __builtin_amdgcn_s_barrier();                                                          \
-        asm volatile("" ::: "memory");                                                         \
-        if (2 * P + 6 < nh_total) VDB_ISSUE(2 * P + 6);                                        \
-        if (2 * P + 7 < nh_total) VDB_ISSUE(2 * P + 7);                                        \
-        const char* st_ = smem + (t & 1) * 4 * HT;                                             \
-        /* k-step-major read order: the k-step 0 MFMAs can start while k-step 1 reads land */ \
-        _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) {                                     \
-            const char* As_ = st_ + ((R) ? 3 : 0) * HT;                                        \
-            _Pragma("unroll") for (int i = 0; i < 4; ++i)                                      \
-                af[i][ks] = *(const u32x4*)(As_ + lds_off(wr * 64 + i * 16 + (lane & 15), ks * 4 + (lane >> 4))); \
-            if ((R) == 0) {                                                                    \
-                _Pragma("unroll") for (int nh = 0; nh < 2; ++nh) {                             \
-                    const char* Bs_ = st_ + (nh ? 2 : 1) * HT;                                 \
-                    _Pragma("unroll") for (int j = 0; j < 2; ++j)                              \
-                        bq[nh][j][ks] = *(const u32x4*)(Bs_ + lds_off(wc * 32 + j * 16 + (lane & 15), ks * 4 + (lane >> 4))); \
-                }                                                                              \
-            }                                                                                  \
-        }                                                                                      \
-        __builtin_amdgcn_s_setprio(1);                                                         \
-        _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                       \
-        _Pragma("unroll") for (int nh = 0; nh < 2; ++nh)                                       \
-        _Pragma("unroll") for (int i = 0; i < 4; ++i)                                          \
-        _Pragma("unroll") for (int j = 0; j < 2; ++j)                                          \
-            acc[R][nh][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(                        \
-                __builtin_bit_cast(bf16x8_t, af[i][ks]), __builtin_bit_cast(bf16x8_t, bq[nh][j][ks]), \
-                acc[R][nh][i][j], 0, 0, 0);                                                    \
-        __builtin_amdgcn_s_setprio(0);                                                         \
-    } while (0)
-
-    // Staggered form (PH == 8): two barriers per phase, L_p = {fragment reads of
+    // Staggered schedule: two barriers per phase, L_p = {fragment reads of
     // phase p, refill of half-tile p+6, vmcnt for what phase p+1 reads} | X_p |
     // C_p = {16 MFMAs} | Y_p. Waves 4-7 run one barrier behind waves 0-3, so on
     // every SIMD (waves s and s+4) one wave loads while the other multiplies.
@@ -318,7 +238,7 @@ __global__ __launch_bounds__(512) void conv_big_kernel(ConvArgs a) {
 #ifdef VD_STAMPS
     int sidx = 0;
 #endif
-    if constexpr (PH == 8) {
+    {
         for (int h = 0; h < 6 && h < nh_total; ++h) VDB_ISSUE(h);   // prologue: half-tiles 0..5
         wait_vm(min(5, nh_total - 1) - 1);                          // A0(0), B0(0) landed
         __builtin_amdgcn_s_barrier();
@@ -337,34 +257,8 @@ __global__ __launch_bounds__(512) void conv_big_kernel(ConvArgs a) {
             VDB_SPHASE(3, 1, 0, false, false, false, false);
         }
         if (wr == 0) __builtin_amdgcn_s_barrier();                  // undo the skew
-    } else if constexpr (PH == 4) {
-        for (int h = 0; h < 5 && h < nh_total; ++h) VDB_ISSUE(h);   // prologue: half-tiles 0..4
-        for (; t + 2 < nk; ++t) {            // steady state: every wait count is a constant
-            VDB_PHASE(0, 0, 0, true, true, true);
-            VDB_PHASE(1, 0, 1, false, true, true);
-            VDB_PHASE(2, 1, 1, true, false, true);
-            VDB_PHASE(3, 1, 0, false, true, true);
-        }
-        for (; t < nk; ++t) {                // last K tiles: the pipeline drains
-            VDB_PHASE(0, 0, 0, true, true, false);
-            VDB_PHASE(1, 0, 1, false, true, false);
-            VDB_PHASE(2, 1, 1, true, false, false);
-            VDB_PHASE(3, 1, 0, false, true, false);
-        }
-    } else {
-        for (int h = 0; h < 6 && h < nh_total; ++h) VDB_ISSUE(h);   // prologue: half-tiles 0..5
-        for (; t + 2 <= nk; ++t) {
-            VDB_PHASE2(0, true);
-            VDB_PHASE2(1, true);
-        }
-        for (; t < nk; ++t) {
-            VDB_PHASE2(0, false);
-            VDB_PHASE2(1, false);
-        }
     }
-#undef VDB_PHASE2
 #undef VDB_SPHASE
-#undef VDB_PHASE
 #undef VDB_ISSUE
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -429,274 +323,31 @@ __global__ __launch_bounds__(512) void conv_big_kernel(ConvArgs a) {
 }
 
 
-// ---------------------------------------------------------------------------
-// 256 x 128 form for Cout = 128-multiples (layer2 3x3, SSH 3x3 at 128 ch): the
-// K tile is three 16-KB half-tiles {A0, B, A1} in THREE LDS stages (144 KB),
-// 8 waves in the same two-barrier staggered schedule: phase 2t = A0 x B,
-// phase 2t+1 = A1 x B (B fragments kept in registers). Tile t+2 is issued in
-// the phases of tile t (A0 and B in the first, A1 in the second); its slot
-// last held tile t-1, whose reads ended >= 2 phases before (the skew rule).
-constexpr int STAGE3 = 3 * HT;
-constexpr int LDS_BYTES128 = 3 * STAGE3;
-constexpr int EPLD128 = 128 + 4;
-
-__global__ __launch_bounds__(512) void conv_big128_kernel(ConvArgs a) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int wr = wid >> 2, wc = wid & 3;
-
-    const int nwg = gridDim.x, bid = blockIdx.x;
-    const int q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
-    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-    const int tn = wg % a.ntiles_n, tm = wg / a.ntiles_n;
-    const int m0 = tm * 256, n0 = tn * 128;
-
-    const int rbase = tid >> 3;
-    const int lchunk = (tid & 7) ^ ((rbase >> 1) & 7);
-    const int ohw = a.yh * a.yw;
-    int iy0[4], ix0[4];
-    long pix0[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int m = m0 + rbase + 64 * i;
-        if (m < a.M) {
-            const int b = m / ohw, rem = m - b * ohw;
-            const int oy = rem / a.yw, ox = rem - oy * a.yw;
-            iy0[i] = oy * a.stride - a.pad;
-            ix0[i] = ox * a.stride - a.pad;
-            pix0[i] = (((long)b * a.xh + iy0[i]) * a.xw + ix0[i]) * a.ldx + a.xcoff + lchunk * 8;
-        } else {
-            iy0[i] = -(1 << 28); ix0[i] = 0; pix0[i] = 0;
-        }
-    }
-    const int nk = a.kpad / 64;
-    const __amdgpu_buffer_rsrc_t rsrc_x = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)a.x, 0, (int)((long)a.B * a.xh * a.xw * a.ldx * 2 < 0x7fffffffL ? (long)a.B * a.xh * a.xw * a.ldx * 2
-                                                                                 : 0x7fffffffL), 0x00020000);
-    const __amdgpu_buffer_rsrc_t rsrc_w = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7fffffff, 0x00020000);
-    const unsigned woff = (unsigned)(((long)(n0 + rbase) * a.kpad + lchunk * 8) * 2);
-    int a0_dy = 0, a0_dx = 0, a0_c = 0, a1_dy = 0, a1_dx = 0, a1_c = 0;
-    const long tap_dy = (long)a.xw * a.ldx;
-
-    // part j of K tile t: 0 = A0 (rows 0-127), 1 = B (channels n0 .. n0+127), 2 = A1
-#define VDC_ISSUE(T_, J_)                                                                      \
-    do {                                                                                       \
-        const int t_ = (T_), j_ = (J_);                                                        \
-        char* dst_ = smem + (t_ % 3) * STAGE3 + j_ * HT + wid * 8 * 128;                       \
-        if (j_ != 1) {                                                                         \
-            int& dy = j_ == 2 ? a1_dy : a0_dy;                                                 \
-            int& dx = j_ == 2 ? a1_dx : a0_dx;                                                 \
-            int& cc = j_ == 2 ? a1_c : a0_c;                                                   \
-            const long toff = dy * tap_dy + (long)dx * a.ldx + cc;                             \
-            const int i0 = j_ == 2 ? 2 : 0;                                                    \
-            _Pragma("unroll") for (int ii = 0; ii < 2; ++ii) {                                 \
-                const int i = i0 + ii;                                                         \
-                const bool ok = (unsigned)(iy0[i] + dy) < (unsigned)a.xh &&                   \
-                                (unsigned)(ix0[i] + dx) < (unsigned)a.xw;                      \
-                const unsigned off = ok ? (unsigned)((pix0[i] + toff) * 2) : 0x80000000u;      \
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_x, (lds_void_t*)(dst_ + ii * 64 * 128), 16, \
-                                                         off, 0, 0, 0);                        \
-            }                                                                                  \
-            cc += 64;                                                                          \
-            if (cc >= a.cin_pad) { cc = 0; if (++dx == a.kw) { dx = 0; ++dy; } }              \
-        } else {                                                                               \
-            _Pragma("unroll") for (int ii = 0; ii < 2; ++ii)                                   \
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_w, (lds_void_t*)(dst_ + ii * 64 * 128), 16, \
-                                                         woff + (unsigned)(64 * ii * a.kpad * 2), \
-                                                         (unsigned)(t_ * 64 * 2), 0, 0);       \
-        }                                                                                      \
-    } while (0)
-
-    f32x4_t acc[2][4][2];
-#pragma unroll
-    for (int x = 0; x < 2; ++x)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) acc[x][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    u32x4 af[4][2], bf[2][2];
-
-#define VDC_PHASE(R, STEADY)                                                                   \
-    do {                                                                                       \
-        const char* st_ = smem + (t % 3) * STAGE3;                                             \
-        if (t + 2 < nk) {                                                                      \
-            if ((R) == 0) { VDC_ISSUE(t + 2, 0); VDC_ISSUE(t + 2, 1); }                        \
-            else VDC_ISSUE(t + 2, 2);                                                          \
-        }                                                                                      \
-        _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) {                                     \
-            const char* As_ = st_ + ((R) ? 2 : 0) * HT;                                        \
-            _Pragma("unroll") for (int i = 0; i < 4; ++i)                                      \
-                af[i][ks] = *(const u32x4*)(As_ + lds_off(wr * 64 + i * 16 + (lane & 15), ks * 4 + (lane >> 4))); \
-            if ((R) == 0) {                                                                    \
-                _Pragma("unroll") for (int j = 0; j < 2; ++j)                                  \
-                    bf[j][ks] = *(const u32x4*)(st_ + HT + lds_off(wc * 32 + j * 16 + (lane & 15), ks * 4 + (lane >> 4))); \
-            }                                                                                  \
-        }                                                                                      \
-        if (STEADY) {                                                                          \
-            if ((R) == 0) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");                    \
-            else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");                              \
-        } else {                                                                               \
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                   \
-        }                                                                                      \
-        __builtin_amdgcn_s_barrier();                                                          \
-        __builtin_amdgcn_s_setprio(1);                                                         \
-        _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                       \
-        _Pragma("unroll") for (int i = 0; i < 4; ++i)                                          \
-        _Pragma("unroll") for (int j = 0; j < 2; ++j)                                          \
-            acc[R][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(                            \
-                __builtin_bit_cast(bf16x8_t, af[i][ks]), __builtin_bit_cast(bf16x8_t, bf[j][ks]), \
-                acc[R][i][j], 0, 0, 0);                                                        \
-        __builtin_amdgcn_s_setprio(0);                                                         \
-        asm volatile("" ::: "memory");                                                         \
-        __builtin_amdgcn_s_barrier();                                                          \
-        asm volatile("" ::: "memory");                                                         \
-    } while (0)
-
-    // prologue: K tiles 0 and 1, then A0(0) and B(0) landed
-    for (int tt = 0; tt < 2 && tt < nk; ++tt) { VDC_ISSUE(tt, 0); VDC_ISSUE(tt, 1); VDC_ISSUE(tt, 2); }
-    if (nk >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (wr == 1) __builtin_amdgcn_s_barrier();                     // the skew
-    asm volatile("" ::: "memory");
-    int t = 0;
-    for (; t + 2 < nk; ++t) {
-        VDC_PHASE(0, true);
-        VDC_PHASE(1, true);
-    }
-    for (; t < nk; ++t) {
-        VDC_PHASE(0, false);
-        VDC_PHASE(1, false);
-    }
-    if (wr == 0) __builtin_amdgcn_s_barrier();                     // undo the skew
-#undef VDC_PHASE
-#undef VDC_ISSUE
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-
-    float* ep = (float*)smem;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-        if (p) __syncthreads();
-        if (wr == (p & 1)) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        ep[(i * 16 + (lane >> 4) * 4 + r) * EPLD128 + wc * 32 + j * 16 + (lane & 15)] =
-                            acc[p >> 1][i][j][r];
-        }
-        __syncthreads();
-#pragma unroll
-        for (int qq = 0; qq < 2; ++qq) {
-            const int it = tid + 512 * qq;
-            const int row = it >> 4, cg = it & 15;
-            const int m = m0 + (p >> 1) * 128 + (p & 1) * 64 + row;
-            const int nb = n0 + cg * 8;
-            if (m >= a.M) continue;
-            const float* er = ep + row * EPLD128 + cg * 8;
-            const float4 e0 = *(const float4*)er, e1 = *(const float4*)(er + 4);
-            const float4 s0 = *(const float4*)(a.scale + nb), s1 = *(const float4*)(a.scale + nb + 4);
-            const float4 h0 = *(const float4*)(a.shift + nb), h1 = *(const float4*)(a.shift + nb + 4);
-            float v[8] = {e0.x * s0.x + h0.x, e0.y * s0.y + h0.y, e0.z * s0.z + h0.z, e0.w * s0.w + h0.w,
-                          e1.x * s1.x + h1.x, e1.y * s1.y + h1.y, e1.z * s1.z + h1.z, e1.w * s1.w + h1.w};
-            float rv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-            if (a.res_mode != VD_RES_NONE) {
-                size_t roff;
-                if (a.res_up) {
-                    const int b = m / ohw, rem = m - b * ohw;
-                    const int oy = rem / a.yw, ox = rem - oy * a.yw;
-                    roff = ((size_t)(b * a.rh + (oy >> 1)) * a.rw + (ox >> 1)) * a.res_ld + a.res_coff + nb;
-                } else {
-                    roff = (size_t)m * a.res_ld + a.res_coff + nb;
-                }
-                const bf16x8_t r8 = *(const bf16x8_t*)((const __bf16*)a.res + roff);
-#pragma unroll
-                for (int e = 0; e < 8; ++e) rv[e] = (float)r8[e];
-            }
-            bf16x8_t o;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                float t2 = v[e];
-                if (a.res_mode == VD_RES_PRE_ACT) t2 += rv[e];
-                t2 = act_apply(t2, a.act, a.slope);
-                if (a.res_mode == VD_RES_POST_ACT) t2 += rv[e];
-                o[e] = (__bf16)t2;
-            }
-            *(bf16x8_t*)((__bf16*)a.y + (size_t)m * a.ldy + a.ycoff + nb) = o;
-        }
-    }
-}
-
 }  // namespace
 
 // Eligible: bf16 dense taps (Cin a multiple of 64), Cout a multiple of 256, bf16
-// output with 16-B aligned channel offsets, at least `min_tiles` 256 x 256 tiles.
+// output with 16-B aligned channel offsets, at least tune.conv_big 256 x 256 tiles.
+// Measured (tools/convbench): at K = 512 ahead of the 128x128 GEMM by 14 % on the
+// 409600 x 256 layers (layer3.0 conv1, FPN output1), level on the 25600 x 2048 ones.
 bool vd_conv_big_ok(const ConvArgs& a) {
-    const char* e = getenv("VD_CONV_BIG");   // read per call: tests lower it to reach small shapes
-    const int min_tiles = e ? atoi(e) : 100;
+    const int min_tiles = a.tune->conv_big;
     if (min_tiles <= 0 || a.out_f32) return false;
-    // measured (tools/convbench): at K = 512 ahead of the 128x128 GEMM by 14 % on the
-    // 409600 x 256 layers (layer3.0 conv1, FPN output1), level on the 25600 x 2048 ones
-    const char* ek = getenv("VD_CONV_BIG_KMIN");
-    const int kmin = ek ? atoi(ek) : 512;
-    if ((a.cin_pad % 64) != 0 || (a.cout % 256) != 0 || a.kpad / 64 < 2 || a.kpad < kmin) return false;
+    if ((a.cin_pad % 64) != 0 || (a.cout % 256) != 0 || a.kpad / 64 < 2 || a.kpad < a.tune->conv_big_kmin) return false;
     if (((a.ldy | a.ycoff) & 7) || ((a.ldx | a.xcoff) & 7)) return false;
     if (a.res_mode != VD_RES_NONE && ((a.res_ld | a.res_coff) & 7)) return false;
     const long tiles = (long)((a.M + 255) / 256) * (a.cout / 256);
     return tiles >= min_tiles;
 }
 
-// 256 x 128 form: Cout a multiple of 128 (not of 256), same K rule
-// (VD_CONV_BIG128 = min tiles). Off by default: measured 10-12 % slower than
-// the 128x128 GEMM at 2 workgroups/CU on layer2 3x3 and SSH (tools/convbench).
-bool vd_conv_big128_ok(const ConvArgs& a) {
-    const char* e = getenv("VD_CONV_BIG128");
-    const int min_tiles = e ? atoi(e) : 0;
-    if (min_tiles <= 0 || a.out_f32) return false;
-    const char* ek = getenv("VD_CONV_BIG_KMIN");
-    const int kmin = ek ? atoi(ek) : 1024;
-    if ((a.cin_pad % 64) != 0 || (a.cout % 128) != 0 || a.kpad / 64 < 1 || a.kpad < kmin) return false;
-    if (((a.ldy | a.ycoff) & 7) || ((a.ldx | a.xcoff) & 7)) return false;
-    if (a.res_mode != VD_RES_NONE && ((a.res_ld | a.res_coff) & 7)) return false;
-    const long tiles = (long)((a.M + 255) / 256) * (a.cout / 128);
-    return tiles >= min_tiles;
-}
-
-hipError_t vd_launch_conv_big128(const ConvArgs& a0, hipStream_t s) {
-    static const bool attr = [] {
-        (void)hipFuncSetAttribute((const void*)conv_big128_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  LDS_BYTES128);
-        return true;
-    }();
-    (void)attr;
-    ConvArgs a = a0;
-    a.ntiles_n = a.cout / 128;
-    dim3 grid(((a.M + 255) / 256) * a.ntiles_n), block(512);
-    hipLaunchKernelGGL(conv_big128_kernel, grid, block, LDS_BYTES128, s, a);
-    return hipGetLastError();
-}
-
 hipError_t vd_launch_conv_big(const ConvArgs& a0, hipStream_t s) {
     static const bool attr = [] {
-        (void)hipFuncSetAttribute((const void*)conv_big_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  LDS_BYTES);
-        (void)hipFuncSetAttribute((const void*)conv_big_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  LDS_BYTES);
-        (void)hipFuncSetAttribute((const void*)conv_big_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)conv_big_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
         return true;
     }();
     (void)attr;
     ConvArgs a = a0;
     a.ntiles_n = a.cout / 256;
     dim3 grid(((a.M + 255) / 256) * a.ntiles_n), block(512);
-    const char* e = getenv("VD_CONV_BIG_PH");
-    // default: the staggered schedule (measured best once the A-address issue was made cheap)
-    if (e && atoi(e) == 4) hipLaunchKernelGGL(conv_big_kernel<4>, grid, block, LDS_BYTES, s, a);
-    else if (e && atoi(e) == 2) hipLaunchKernelGGL(conv_big_kernel<2>, grid, block, LDS_BYTES, s, a);
-    else hipLaunchKernelGGL(conv_big_kernel<8>, grid, block, LDS_BYTES, s, a);
+    hipLaunchKernelGGL(conv_big_kernel, grid, block, LDS_BYTES, s, a);
     return hipGetLastError();
 }

@@ -135,7 +135,7 @@ int vd_build_face(Ctx& c, const WMap& W) {
     if (rc) return rc;
     Act stem, pool;
     if ((rc = c.act(pool, H / 4, Wd / 4, 64))) return rc;
-    if (F.s2d && vd_stem_pool_ok(F.input.h, F.input.w, pool.h, pool.w)) {
+    if (F.s2d && c.tune.stem_pool && vd_stem_pool_ok(F.input.h, F.input.w, pool.h, pool.w)) {
         // conv1 + bn1 + relu + maxpool in one kernel (stem.hip): the stem map stays on chip
         if ((rc = c.add_stem_pool(F.net, ci, F.input, pool))) return rc;
     } else {
@@ -235,8 +235,7 @@ int vd_build_face(Ctx& c, const WMap& W) {
     const Act fpn_out[3] = {m1, m2, o3};
 
     // ---- SSH x3 + fused heads ----
-    const char* sfe = getenv("VD_SSH_FUSE");   // 0: conv3X3 and conv5X5_1 as two convs
-    const bool ssh_fuse = !(sfe && atoi(sfe) == 0);
+    const bool ssh_fuse = c.tune.ssh_fuse != 0;   // 0: conv3X3 and conv5X5_1 as two convs
     for (int l = 0; l < 3; ++l) {
         const std::string pre = "ssh" + std::to_string(l + 1);
         int s3, s51, s52, s72, s73;
@@ -321,12 +320,12 @@ int vd_build_face(Ctx& c, const WMap& W) {
     F.A = A;
     if ((rc = c.dalloc((void**)&F.anchors, anc.size() * 4))) return rc;
     VD_CHECK_HIP(hipMemcpy(F.anchors, anc.data(), anc.size() * 4, hipMemcpyHostToDevice));
-    if ((rc = vd_alloc_post(c, F.post, A))) return rc;
+    if ((rc = vd_alloc_post(c, F.post, A, A))) return rc;   // a frame keeps at most A faces
     F.loaded = true;
     return VD_OK;
 }
 
-int vd_alloc_post(Ctx& c, PostScratch& ps, int A) {
+int vd_alloc_post(Ctx& c, PostScratch& ps, int A, int kcap) {
     const size_t B = c.cfg.max_batch;
     int P = 1;
     while (P < A) P <<= 1;
@@ -340,5 +339,18 @@ int vd_alloc_post(Ctx& c, PostScratch& ps, int A) {
     if ((rc = c.dalloc((void**)&ps.area, B * A * 4))) return rc;
     if ((rc = c.dalloc((void**)&ps.sort, B * (size_t)P * 8))) return rc;
     if ((rc = c.dalloc((void**)&ps.supp, B * A))) return rc;
+    ps.kcap = kcap;
+    if ((rc = c.dalloc((void**)&ps.kcount, B * 4))) return rc;
+    if ((rc = c.dalloc((void**)&ps.kxyxy, B * kcap * 16))) return rc;
+    if ((rc = c.dalloc((void**)&ps.kxyxy_f, B * kcap * 16))) return rc;
+    if ((rc = c.dalloc((void**)&ps.kscore, B * kcap * 4))) return rc;
+    if ((rc = c.dalloc((void**)&ps.klabel, B * kcap * 4))) return rc;
+    VD_CHECK_HIP(hipMemset(ps.kcount, 0, B * 4));
     return VD_OK;
+}
+
+void vd_post_keep_args(PostScratch& ps, PostArgs& p, int n) {
+    p.kcap = ps.kcap;
+    p.k_count = ps.kcount; p.k_xyxy = ps.kxyxy; p.k_xyxy_f = ps.kxyxy_f; p.k_score = ps.kscore; p.k_label = ps.klabel;
+    ps.kn = n;
 }

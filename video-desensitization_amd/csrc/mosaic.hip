@@ -55,7 +55,7 @@ struct MosaicArgs {
     MBox* table; int tcap;                           // [n][tcap] prepared boxes
     int* cpref;                                      // [n][BOX_FAST+1] prefix sums of box cells sw*sh
     uint32_t* cells;                                 // [n][CELL_CAP] walked colour per cell
-    int map_on;                                      // fast path on (VD_MOSAIC_MAP=0 forces the generic path)
+    int map_on;                                      // fast path on (option mosaic_map=0 forces the generic path)
 };
 
 __device__ __forceinline__ int frame_boxes(const MosaicArgs& a, int f, int& n0) {
@@ -694,7 +694,7 @@ size_t vd_mosaic_table_bytes(int n, int tcap) {
 hipError_t vd_launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w, size_t pitch,
                             const int* cnt0, const int* xy0, int cap0,
                             const int* cnt1, const int* xy1, int cap1, int level, void* table,
-                            int stages, hipStream_t s) {
+                            int stages, int map_on, hipStream_t s) {
     if (n <= 0 || h <= 0 || w <= 0) return hipSuccess;
     const int vec_ok = (pitch % 16 == 0) && ((uintptr_t)in % 16 == 0) && ((uintptr_t)out % 16 == 0);
     const int tcap = (cnt0 ? cap0 : 0) + (cnt1 ? cap1 : 0);
@@ -703,8 +703,7 @@ hipError_t vd_launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w
     cel += (16 - ((uintptr_t)cel & 15)) & 15;
     MosaicArgs a{in, out, n, h, w, pitch, cnt0, xy0, cap0, cnt1, xy1, cap1, level, vec_ok, (MBox*)table, tcap,
                  (int*)cpre, (uint32_t*)cel, 1};
-    static const int map_env = [] { const char* e = getenv("VD_MOSAIC_MAP"); return e ? atoi(e) : 1; }();
-    a.map_on = map_env;
+    a.map_on = map_on;
     if (stages & 1) hipLaunchKernelGGL(mosaic_cell_kernel, dim3(CELL_BLOCKS, n), dim3(256), 0, s, a);
     if (stages & 2) hipLaunchKernelGGL(mosaic_out_kernel, dim3((h + ROWS - 1) / ROWS, n), dim3(256), 0, s, a);
     return hipGetLastError();

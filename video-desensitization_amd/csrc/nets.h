@@ -85,6 +85,16 @@ struct PostScratch {   // per-net candidate / NMS scratch sized for max_batch x 
     uint64_t* sort = nullptr;
     uint8_t* supp = nullptr;
     int sort_cap = 0;
+    // the last call's complete keep lists [max_batch][kcap] (library-owned): the
+    // mosaic reads these, never the caller's cap-limited copies; vd_read_boxes
+    // hands them out
+    int kcap = 0;
+    int* kcount = nullptr;
+    int* kxyxy = nullptr;
+    float* kxyxy_f = nullptr;
+    float* kscore = nullptr;
+    int* klabel = nullptr;
+    int kn = 0;                        // frames in the last call
 };
 
 struct FaceNet {
@@ -138,6 +148,7 @@ struct Ctx {
     int device = 0;
     bool f32 = false;
     bool f16 = false;                             // VD_PREC_FP16: fp16 operands/activations (GEMM path only)
+    VdTune tune;                                  // kernel-selection switches (vd_set_option)
     hipStream_t stream = nullptr, own_stream = nullptr;
     hipStream_t stream2 = nullptr;               // plate branch runs beside the face branch
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -194,6 +205,7 @@ struct Ctx {
     int check_frames(int n, int h, int w, size_t pitch);
     int box_targets(vd_boxes* out, int n, BoxTargets& t);
     int box_finish(vd_boxes* out, int n, const BoxTargets& t);
+    int host_box_staging(void** buf, size_t* have, int cap, int n, BoxTargets& t);
     int face_letterbox(const uint8_t* dframes, int n, int h, int w, size_t pitch);
     void face_letterbox_args(const uint8_t* dframes, int n, int h, int w, size_t pitch, LetterboxArgs* a);
     int face_forward(int n);
@@ -202,7 +214,8 @@ struct Ctx {
                       const int* xy0, int cap0, const int* cnt1, const int* xy1, int cap1, int level);
 };
 
-int vd_alloc_post(Ctx& ctx, PostScratch& ps, int A);
+int vd_alloc_post(Ctx& ctx, PostScratch& ps, int A, int kcap);
+void vd_post_keep_args(PostScratch& ps, PostArgs& p, int n);
 int vd_build_face(Ctx& ctx, const WMap& W);
 int vd_build_plate(Ctx& ctx, const WMap& W);
 // letterboxed: the canvas was already written (vd_launch_letterbox_pair in vd_process)

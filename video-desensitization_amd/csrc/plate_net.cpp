@@ -260,9 +260,8 @@ int vd_build_plate(Ctx& c, const WMap& W) {
         return vd_set_error(VD_ERR_WEIGHTS, "plate weights have %d classes, cfg.plate_nc = %d", cls0->shape[0], P.nc);
     int rc;
     static const int strides[] = {2, 2, 1, 2, 1, 2, 1, 2, 1};
-    // bf16: the letterbox writes the stem input in space-to-depth form (VD_PLATE_S2D=0: off)
-    const char* se = getenv("VD_PLATE_S2D");
-    P.s2d = !c.f32 && !c.f16 && !(se && atoi(se) == 0);
+    // bf16: the letterbox writes the stem input in space-to-depth form (option plate_s2d=0: off)
+    P.s2d = !c.f32 && !c.f16 && c.tune.plate_s2d;
     if (P.s2d && (rc = yconv_s2d(c, W, "model.0"))) return rc;
     for (int i : {0, 1, 3, 5, 7}) {
         if (i == 0 && P.s2d) continue;
@@ -303,7 +302,8 @@ int vd_build_plate(Ctx& c, const WMap& W) {
         if ((rc = c.act(P.head[i], s, s, P.hstride, true))) return rc;
         P.A_max += s * s;
     }
-    if ((rc = vd_alloc_post(c, P.post, P.A_max))) return rc;
+    const int kcap = c.cfg.plate_max_det > 0 ? std::min(P.A_max, c.cfg.plate_max_det) : P.A_max;
+    if ((rc = vd_alloc_post(c, P.post, P.A_max, kcap))) return rc;
     P.loaded = true;
     return VD_OK;
 }
@@ -404,6 +404,7 @@ int vd_plate_post(Ctx& c, int n, int img_h, int img_w, const BoxTargets& t) {
     p.inv_gain = 1.0f / (float)gain;   // torch divides a tensor by a Python scalar as x * (1/b)
     p.cap = t.cap; p.out_count = t.count; p.out_xyxy = t.xyxy; p.out_xyxy_f = t.xyxy_f;
     p.out_score = t.score; p.out_label = t.label;
+    vd_post_keep_args(P.post, p, n);
     c.t_begin(3, (double)n * P.A * P.hstride * 4);
     hipError_t e = vd_launch_post(p, c.stream);
     c.t_end();

@@ -124,8 +124,10 @@ __device__ __forceinline__ int trunc_i32(float v) {
 
 __device__ __forceinline__ float clampf(float v, float lo, float hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
+// Kept box `pos` of frame b: always into the library's complete keep list (what the
+// mosaic reads), and into the caller's arrays while pos < cap.
 __device__ void emit(const PostArgs& p, int b, int pos, float4 bx, uint64_t key) {
-    const size_t o = (size_t)b * p.cap + pos;
+    const size_t k = (size_t)b * p.kcap + pos;
     float X1, Y1, X2, Y2;
     const int a = (int)(key & 0xFFFFFFFFu);
     if (p.mode == POST_FACE) {
@@ -142,16 +144,25 @@ __device__ void emit(const PostArgs& p, int b, int pos, float4 bx, uint64_t key)
         X2 = clampf(VD_FMUL(VD_FSUB(bx.z, (float)p.padx), p.inv_gain), 0.f, (float)p.img_w);
         Y2 = clampf(VD_FMUL(VD_FSUB(bx.w, (float)p.pady), p.inv_gain), 0.f, (float)p.img_h);
     }
-    p.out_xyxy[4 * o + 0] = trunc_i32(X1);
-    p.out_xyxy[4 * o + 1] = trunc_i32(Y1);
-    p.out_xyxy[4 * o + 2] = trunc_i32(X2);
-    p.out_xyxy[4 * o + 3] = trunc_i32(Y2);
+    const int4 ib = make_int4(trunc_i32(X1), trunc_i32(Y1), trunc_i32(X2), trunc_i32(Y2));
+    const float4 fb = make_float4(X1, Y1, X2, Y2);
+    const float sc = __uint_as_float(0xFFFFFFFFu - (uint32_t)(key >> 32));
+    const int lab = p.mode == POST_FACE ? a : p.scratch_cls[(size_t)b * p.A + a];
+    ((int4*)p.k_xyxy)[k] = ib;
+    ((float4*)p.k_xyxy_f)[k] = fb;
+    p.k_score[k] = sc;
+    p.k_label[k] = lab;
+    if (pos >= p.cap || !p.out_xyxy) return;
+    const size_t o = (size_t)b * p.cap + pos;
+    // caller arrays: scalar stores (no alignment assumed)
+    p.out_xyxy[4 * o + 0] = ib.x; p.out_xyxy[4 * o + 1] = ib.y;
+    p.out_xyxy[4 * o + 2] = ib.z; p.out_xyxy[4 * o + 3] = ib.w;
     if (p.out_xyxy_f) {
         p.out_xyxy_f[4 * o + 0] = X1; p.out_xyxy_f[4 * o + 1] = Y1;
         p.out_xyxy_f[4 * o + 2] = X2; p.out_xyxy_f[4 * o + 3] = Y2;
     }
-    if (p.out_score) p.out_score[o] = __uint_as_float(0xFFFFFFFFu - (uint32_t)(key >> 32));
-    if (p.out_label) p.out_label[o] = p.mode == POST_FACE ? a : p.scratch_cls[(size_t)b * p.A + a];
+    if (p.out_score) p.out_score[o] = sc;
+    if (p.out_label) p.out_label[o] = lab;
 }
 
 __device__ void nms_frame(const PostArgs& p, int b, int M, uint64_t* keys, float4* box, float* area, uint8_t* supp,
@@ -189,7 +200,7 @@ __device__ void nms_frame(const PostArgs& p, int b, int M, uint64_t* keys, float
     if (tid == 0) *nkept_s = 0;
     __syncthreads();
 
-    const int limit = p.max_det > 0 ? min(p.max_det, p.cap) : p.cap;
+    const int limit = p.max_det > 0 ? min(p.max_det, p.kcap) : p.kcap;   // kcap >= every possible keep count
     for (int c0 = 0; c0 < M; c0 += 64) {
         if (wid == 0) {
             const int j = c0 + lane;
@@ -246,7 +257,9 @@ __device__ void nms_frame(const PostArgs& p, int b, int M, uint64_t* keys, float
     }
     if (tid == 0) {
         const int n = *nkept_s;
-        p.out_count[b] = p.max_det > 0 ? min(n, p.max_det) : n;   // i = i[:max_det]
+        const int kept = p.max_det > 0 ? min(n, p.max_det) : n;   // i = i[:max_det]
+        p.k_count[b] = kept;
+        if (p.out_count) p.out_count[b] = kept;
     }
 }
 
@@ -260,7 +273,10 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(PostArgs p) {
     const int b = blockIdx.x;
     const int M = p.cand_count[b];
     if (M == 0) {
-        if (threadIdx.x == 0) p.out_count[b] = 0;
+        if (threadIdx.x == 0) {
+            p.k_count[b] = 0;
+            if (p.out_count) p.out_count[b] = 0;
+        }
         return;
     }
     if (M <= LDS_CAND)

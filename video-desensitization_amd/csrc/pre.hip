@@ -355,8 +355,6 @@ __global__ __launch_bounds__(256) void upsample2x_kernel(const T* x, int xh, int
 // Same frames, both bf16 space-to-depth canvases, the same resize (nw, nh, filter)
 // and even relative offsets of the pasted images.
 bool vd_letterbox_pair_ok(const LetterboxArgs& a, const LetterboxArgs& b) {
-    const char* e = getenv("VD_LB_PAIR");
-    if (e && atoi(e) == 0) return false;
     return a.s2d && b.s2d && !a.out_f32 && !b.out_f32 && !a.out_f16 && !b.out_f16 && a.src == b.src && a.n == b.n &&
            a.ih == b.ih && a.iw == b.iw && a.pitch == b.pitch && a.iw * 3 <= LB_LDS_MAX && a.nw == b.nw &&
            a.nh == b.nh && a.mode == b.mode && a.scale_x == b.scale_x && a.scale_y == b.scale_y &&

@@ -319,7 +319,7 @@ bool Ctx::dual_ok(int ci, int c2, const Act& y) const {
     ConvArgs t{};
     t.kh = a.kh; t.kw = a.kw; t.pad = a.pad; t.stride = a.stride; t.cin_pad = a.cin_pad; t.kpad = a.kpad;
     t.cout = a.cout; t.act = a.act; t.res_mode = VD_RES_NONE; t.ldx = a.cin_pad; t.ldy = y.c; t.x2 = (const void*)1;
-    t.cin2_pad = b.cin_pad; t.kpad2 = b.kpad; t.ldx2 = b.cin_pad;
+    t.cin2_pad = b.cin_pad; t.kpad2 = b.kpad; t.ldx2 = b.cin_pad; t.tune = &tune;
     return b.kh == 1 && b.kw == 1 && b.pad == 0 && b.cout == a.cout && b.act == VD_ACT_NONE && vd_conv1x1_dual_ok(t);
 }
 
@@ -391,6 +391,7 @@ int Ctx::run_conv_op(const Op& op, int f0, int n, int fam) {
     a.M = n * op.y.h * op.y.w;
     a.act = cv.act; a.slope = cv.slope; a.out_f32 = op.y.f32 ? 1 : 0;
     a.f16 = f16 ? 1 : 0;
+    a.tune = &tune;
     double flops = cv.flops_per_px * a.M;
     if (op.conv2 >= 0) {
         const Conv& c2 = convs[op.conv2];
@@ -444,7 +445,7 @@ void Ctx::fuse_chains(Net& net, size_t begin) {
                                b.ycoff == 0 && !a.y.f32 && !b.y.f32 && c3.cin_pad == a.x.c &&
                                c1.cin_pad == c3.cout && a.r.h == a.y.h && a.r.w == a.y.w;
             const long M = (long)cfg.max_batch * a.y.h * a.y.w;
-            if (shape && vd_chain_ok(c3.cin_pad, c3.cout, c3.kpad, c1.kpad, a.x.c, a.r.c, a.y.c, b.y.c, M)) {
+            if (shape && tune.chain && vd_chain_ok(c3.cin_pad, c3.cout, c3.kpad, c1.kpad, a.x.c, a.r.c, a.y.c, b.y.c, M)) {
                 Op op = a;
                 op.kind = OP_CHAIN;
                 op.conv2 = b.conv;
@@ -553,19 +554,27 @@ int Ctx::check_frames(int n, int h, int w, size_t pitch) {
 }
 
 // Box outputs: kernels write straight into caller arrays when they are device
-// memory; host outputs go through ctx staging + one D2H at the end.
+// memory; host outputs go through ctx staging + one D2H at the end. `out` may be
+// NULL (no caller copy; the complete lists stay readable through vd_read_boxes).
 int Ctx::box_targets(vd_boxes* out, int n, BoxTargets& t) {
-    if (!out || !out->count || !out->xyxy || out->cap <= 0) return vd_set_error(VD_ERR_ARG, "vd_boxes needs count, xyxy, cap>0");
+    t = BoxTargets{};
+    if (!out) return VD_OK;
+    if (!out->count || !out->xyxy || out->cap <= 0) return vd_set_error(VD_ERR_ARG, "vd_boxes needs count, xyxy, cap>0");
     t.cap = out->cap;
     if (out->where == VD_DEVICE) {
         t.count = out->count; t.xyxy = out->xyxy; t.xyxy_f = out->xyxy_f; t.score = out->score; t.label = out->label;
         return VD_OK;
     }
-    size_t nb = (size_t)n * out->cap;
+    return host_box_staging(&stage_box, &stage_box_bytes, out->cap, n, t);
+}
+
+int Ctx::host_box_staging(void** buf, size_t* have, int cap, int n, BoxTargets& t) {
+    size_t nb = (size_t)n * cap;
     size_t need = n * 4 + nb * (16 + 16 + 4 + 4);
-    int rc = ensure_staging(&stage_box, &stage_box_bytes, need + 64);
+    int rc = ensure_staging(buf, have, need + 64);
     if (rc) return rc;
-    char* p = (char*)stage_box;
+    char* p = (char*)*buf;
+    t.cap = cap;
     t.count = (int*)p; p += ((n * 4 + 15) / 16) * 16;
     t.xyxy = (int*)p; p += nb * 16;
     t.xyxy_f = (float*)p; p += nb * 16;
@@ -574,8 +583,11 @@ int Ctx::box_targets(vd_boxes* out, int n, BoxTargets& t) {
     return VD_OK;
 }
 
+// Host outputs: one D2H of the staged arrays. count[f] is the complete keep count,
+// which may exceed cap: the arrays then hold the first cap boxes, the rest stay
+// readable through vd_read_boxes, and the mosaic used every box regardless.
 int Ctx::box_finish(vd_boxes* out, int n, const BoxTargets& t) {
-    if (out->where == VD_DEVICE) return VD_OK;
+    if (!out || out->where == VD_DEVICE) return VD_OK;
     size_t nb = (size_t)n * out->cap;
     VD_CHECK_HIP(hipMemcpyAsync(out->count, t.count, n * 4, hipMemcpyDeviceToHost, stream));
     VD_CHECK_HIP(hipMemcpyAsync(out->xyxy, t.xyxy, nb * 16, hipMemcpyDeviceToHost, stream));
@@ -583,9 +595,6 @@ int Ctx::box_finish(vd_boxes* out, int n, const BoxTargets& t) {
     if (out->score) VD_CHECK_HIP(hipMemcpyAsync(out->score, t.score, nb * 4, hipMemcpyDeviceToHost, stream));
     if (out->label) VD_CHECK_HIP(hipMemcpyAsync(out->label, t.label, nb * 4, hipMemcpyDeviceToHost, stream));
     VD_CHECK_HIP(hipStreamSynchronize(stream));
-    for (int i = 0; i < n; ++i)
-        if (out->count[i] > out->cap)
-            return vd_set_error(VD_ERR_CAPACITY, "frame %d kept %d boxes > cap %d", i, out->count[i], out->cap);
     return VD_OK;
 }
 
@@ -654,6 +663,7 @@ int Ctx::face_post(int n, int img_h, int img_w, const BoxTargets& t) {
     p.scx = inw / nw;
     p.cap = t.cap; p.out_count = t.count; p.out_xyxy = t.xyxy; p.out_xyxy_f = t.xyxy_f;
     p.out_score = t.score; p.out_label = t.label;
+    vd_post_keep_args(face.post, p, n);
     t_begin(3, (double)n * face.A * 32 * 4);
     hipError_t e = vd_launch_post(p, stream);
     t_end();
@@ -668,11 +678,12 @@ int Ctx::launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w, siz
     if (rc) return rc;
     t_begin(6, 0);
     hipError_t e = vd_launch_mosaic(in, out, n, h, w, pitch, cnt0, xy0, cap0, cnt1, xy1, cap1, level, mosaic_table,
-                                    1, stream);
+                                    1, tune.mosaic_map, stream);
     t_end();
     if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "mosaic: %s", hipGetErrorString(e));
     t_begin(1, 2.0 * n * (double)h * w * 3);
-    e = vd_launch_mosaic(in, out, n, h, w, pitch, cnt0, xy0, cap0, cnt1, xy1, cap1, level, mosaic_table, 2, stream);
+    e = vd_launch_mosaic(in, out, n, h, w, pitch, cnt0, xy0, cap0, cnt1, xy1, cap1, level, mosaic_table, 2, tune.mosaic_map,
+                         stream);
     t_end();
     if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "mosaic: %s", hipGetErrorString(e));
     return VD_OK;
@@ -735,13 +746,7 @@ int vd_create(const vd_cfg* cfg, int device, vd_ctx** out) {
         return vd_set_error(VD_ERR_HIP, "hipStreamCreate failed");
     }
     ctx->stream = ctx->own_stream;
-    // VD_PLATE_PRIO=1 puts the plate branch on a high-priority stream (so its small
-    // launches would take CUs the face convs leave idle first); measured neutral.
-    int prio_lo = 0, prio_hi = 0;
-    (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-    const char* pe = getenv("VD_PLATE_PRIO");
-    const int prio = (pe && atoi(pe) != 0) ? prio_hi : prio_lo;   // measured: no gain, default normal
-    if (hipStreamCreateWithPriority(&ctx->stream2, hipStreamNonBlocking, prio) != hipSuccess ||
+    if (hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming) != hipSuccess) {
         hipStreamDestroy(ctx->own_stream);
@@ -790,6 +795,30 @@ int vd_load_weights(vd_ctx* h, int net, const void* blob, size_t bytes, int fmt)
         return vd_build_plate(*ctx, W);
     }
     return vd_set_error(VD_ERR_ARG, "unknown net %d", net);
+}
+
+int vd_set_option(vd_ctx* h, const char* name, int value) {
+    Ctx* ctx = (Ctx*)h;
+    VD_ENTRY(ctx);
+    if (!name) return vd_set_error(VD_ERR_ARG, "null option name");
+    struct Opt { const char* n; int VdTune::*f; };
+    static const Opt opts[] = {
+        {"conv_stream", &VdTune::conv_stream}, {"conv_stream512", &VdTune::conv_stream512},
+        {"conv_dual", &VdTune::conv_dual}, {"conv_taps", &VdTune::conv_taps}, {"conv_n192", &VdTune::conv_n192},
+        {"conv_small", &VdTune::conv_small}, {"conv_big", &VdTune::conv_big},
+        {"conv_big_kmin", &VdTune::conv_big_kmin}, {"stream_ntt", &VdTune::stream_ntt},
+        {"lb_pair", &VdTune::lb_pair}, {"mosaic_map", &VdTune::mosaic_map}, {"block_fuse", &VdTune::block_fuse},
+        {"chain", &VdTune::chain}, {"stem_pool", &VdTune::stem_pool}, {"ssh_fuse", &VdTune::ssh_fuse},
+        {"plate_s2d", &VdTune::plate_s2d},
+    };
+    for (const Opt& o : opts)
+        if (strcmp(o.n, name) == 0) {
+            if (!strcmp(name, "stream_ntt") && value != 8 && value != 16)
+                return vd_set_error(VD_ERR_ARG, "stream_ntt must be 8 or 16");
+            ctx->tune.*(o.f) = value;
+            return VD_OK;
+        }
+    return vd_set_error(VD_ERR_ARG, "unknown option '%s'", name);
 }
 
 int vd_set_stream(vd_ctx* h, void* s) {
@@ -866,6 +895,11 @@ int vd_mosaic(vd_ctx* h, const uint8_t* in, uint8_t* out, int n, int fh, int fw,
     }
     const int* cnt = boxes->count;
     const int* xy = boxes->xyxy;
+    if (boxes->where == VD_HOST)   // a count past cap means boxes the caller does not hold: never skip them silently
+        for (int i = 0; i < n; ++i)
+            if (boxes->count[i] > boxes->cap)
+                return vd_set_error(VD_ERR_CAPACITY, "vd_mosaic: frame %d has count %d > cap %d (read the complete "
+                                    "list with vd_read_boxes)", i, boxes->count[i], boxes->cap);
     if (boxes->where == VD_HOST) {
         size_t nb = (size_t)n * boxes->cap;
         if ((rc = ctx->ensure_staging(&ctx->stage_box2, &ctx->stage_box2_bytes, n * 4 + nb * 16 + 16))) return rc;
@@ -901,21 +935,14 @@ int vd_process(vd_ctx* h, const uint8_t* in, uint8_t* out, int n, int fh, int fw
     if (rc) return rc;
     BoxTargets tf{}, tp{};
     if (do_faces && (rc = ctx->box_targets(faces, n, tf))) return rc;
-    if (do_plates) {
-        // plate box staging must not alias the face staging
+    if (do_plates && plates) {   // plate box staging must not alias the face staging
+        if (!plates->count || !plates->xyxy || plates->cap <= 0)
+            return vd_set_error(VD_ERR_ARG, "vd_boxes needs count, xyxy, cap>0");
         if (plates->where == VD_DEVICE) {
             tp.cap = plates->cap; tp.count = plates->count; tp.xyxy = plates->xyxy; tp.xyxy_f = plates->xyxy_f;
             tp.score = plates->score; tp.label = plates->label;
-        } else {
-            size_t nb = (size_t)n * plates->cap;
-            if ((rc = ctx->ensure_staging(&ctx->stage_box2, &ctx->stage_box2_bytes, n * 4 + nb * 40 + 64))) return rc;
-            char* p = (char*)ctx->stage_box2;
-            tp.cap = plates->cap;
-            tp.count = (int*)p; p += ((n * 4 + 15) / 16) * 16;
-            tp.xyxy = (int*)p; p += nb * 16;
-            tp.xyxy_f = (float*)p; p += nb * 16;
-            tp.score = (float*)p; p += nb * 4;
-            tp.label = (int*)p;
+        } else if ((rc = ctx->host_box_staging(&ctx->stage_box2, &ctx->stage_box2_bytes, plates->cap, n, tp))) {
+            return rc;
         }
     }
     const uint8_t* d = ctx->frames_to_device(in, n, fh, pitch, where, &rc);
@@ -929,7 +956,8 @@ int vd_process(vd_ctx* h, const uint8_t* in, uint8_t* out, int n, int fh, int fw
     if (fork) {
         LetterboxArgs fa, pa;
         ctx->face_letterbox_args(d, n, fh, fw, pitch, &fa);
-        if (vd_plate_letterbox_args(*ctx, d, n, fh, fw, pitch, &pa) == VD_OK && vd_letterbox_pair_ok(fa, pa)) {
+        if (ctx->tune.lb_pair && vd_plate_letterbox_args(*ctx, d, n, fh, fw, pitch, &pa) == VD_OK &&
+            vd_letterbox_pair_ok(fa, pa)) {
             ctx->t_begin(2, (double)n * (fa.nh * (double)fw * 3 + ((double)(fa.oh / 2 + 1) * (fa.ow / 2 + 1) +
                                                                     (double)(pa.oh / 2 + 1) * (pa.ow / 2 + 1)) * 32));
             hipError_t e = vd_launch_letterbox_pair(fa, pa, ctx->stream);
@@ -938,28 +966,15 @@ int vd_process(vd_ctx* h, const uint8_t* in, uint8_t* out, int n, int fh, int fw
             paired = true;
         }
     }
-    // VD_PLATE_FORK=s (1-4, experiment): the plate branch starts after face backbone
-    // stage s instead of beside the whole face forward (needs micro-batching off)
-    static const int fork_stage = [] { const char* e = getenv("VD_PLATE_FORK"); return e ? atoi(e) : 0; }();
-    const bool late_fork = fork && fork_stage >= 1 && fork_stage <= 4 && ctx->cfg.reserved[0] <= 0;
-    if (fork && !late_fork) {
+    if (fork) {
         VD_CHECK_HIP(hipEventRecord(ctx->ev_fork, ctx->stream));
         VD_CHECK_HIP(hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
     }
     if (do_faces) {
         if (!paired && (rc = ctx->face_letterbox(d, n, fh, fw, pitch))) return rc;
-        if (late_fork) {
-            const Net& fn = ctx->face.net;
-            const int split = fn.stage_end[fork_stage];
-            if ((rc = ctx->run_ops(fn, 0, split, 0, n))) return rc;
-            VD_CHECK_HIP(hipEventRecord(ctx->ev_fork, ctx->stream));
-            if ((rc = ctx->run_ops(fn, split, (int)fn.ops.size(), 0, n))) return rc;
-        } else if ((rc = ctx->face_forward(n))) {
-            return rc;
-        }
+        if ((rc = ctx->face_forward(n))) return rc;
         if ((rc = ctx->face_post(n, fh, fw, tf))) return rc;
     }
-    if (late_fork) VD_CHECK_HIP(hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
     if (do_plates) {
         hipStream_t main = ctx->stream;
         if (fork) ctx->stream = ctx->stream2;
@@ -979,10 +994,14 @@ int vd_process(vd_ctx* h, const uint8_t* in, uint8_t* out, int n, int fh, int fw
             if ((rc = ctx->ensure_staging(&ctx->stage_out, &ctx->stage_out_bytes, bytes))) return rc;
             dout = (uint8_t*)ctx->stage_out;
         }
-        if ((rc = ctx->launch_mosaic(d, dout, n, fh, fw, pitch, do_faces ? tf.count : nullptr,
-                                     do_faces ? tf.xyxy : nullptr, do_faces ? tf.cap : 0,
-                                     mosaic_plates ? tp.count : nullptr, mosaic_plates ? tp.xyxy : nullptr,
-                                     mosaic_plates ? tp.cap : 0, ctx->cfg.mosaic_level)))
+        // every kept box, from the library's complete keep lists (the caller's arrays
+        // may hold fewer: cap), faces in NMS order then plates (combine_detect.py:241-249)
+        const PostScratch& fp = ctx->face.post;
+        const PostScratch& pp = ctx->plate.post;
+        if ((rc = ctx->launch_mosaic(d, dout, n, fh, fw, pitch, do_faces ? fp.kcount : nullptr,
+                                     do_faces ? fp.kxyxy : nullptr, do_faces ? fp.kcap : 0,
+                                     mosaic_plates ? pp.kcount : nullptr, mosaic_plates ? pp.kxyxy : nullptr,
+                                     mosaic_plates ? pp.kcap : 0, ctx->cfg.mosaic_level)))
             return rc;
         if (where == VD_HOST) VD_CHECK_HIP(hipMemcpyAsync(out, dout, bytes, hipMemcpyDeviceToHost, ctx->stream));
     }
@@ -994,6 +1013,29 @@ int vd_process(vd_ctx* h, const uint8_t* in, uint8_t* out, int n, int fh, int fw
     }
     if (where == VD_HOST) VD_CHECK_HIP(hipStreamSynchronize(ctx->stream));
     return rc2;
+}
+
+int vd_read_boxes(vd_ctx* h, int net, int n, vd_boxes* out) {
+    Ctx* ctx = (Ctx*)h;
+    VD_ENTRY(ctx);
+    const PostScratch* ps = net == VD_NET_RETINAFACE ? &ctx->face.post : (net == VD_NET_YOLOV8N ? &ctx->plate.post : nullptr);
+    if (!ps) return vd_set_error(VD_ERR_ARG, "unknown net %d", net);
+    if (!ps->kcount) return vd_set_error(VD_ERR_STATE, "net %d not loaded", net);
+    if (!out || !out->count || !out->xyxy || out->cap <= 0) return vd_set_error(VD_ERR_ARG, "vd_boxes needs count, xyxy, cap>0");
+    if (n <= 0 || n > ps->kn) return vd_set_error(VD_ERR_ARG, "n=%d outside [1, %d frames of the last call]", n, ps->kn);
+    const hipMemcpyKind kind = out->where == VD_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    const int w = std::min(out->cap, ps->kcap);   // boxes per frame copied (beyond kcap nothing is ever kept)
+    const size_t dp = (size_t)out->cap, sp = (size_t)ps->kcap;
+    VD_CHECK_HIP(hipMemcpyAsync(out->count, ps->kcount, (size_t)n * 4, kind, ctx->stream));
+    VD_CHECK_HIP(hipMemcpy2DAsync(out->xyxy, dp * 16, ps->kxyxy, sp * 16, (size_t)w * 16, n, kind, ctx->stream));
+    if (out->xyxy_f)
+        VD_CHECK_HIP(hipMemcpy2DAsync(out->xyxy_f, dp * 16, ps->kxyxy_f, sp * 16, (size_t)w * 16, n, kind, ctx->stream));
+    if (out->score)
+        VD_CHECK_HIP(hipMemcpy2DAsync(out->score, dp * 4, ps->kscore, sp * 4, (size_t)w * 4, n, kind, ctx->stream));
+    if (out->label)
+        VD_CHECK_HIP(hipMemcpy2DAsync(out->label, dp * 4, ps->klabel, sp * 4, (size_t)w * 4, n, kind, ctx->stream));
+    if (out->where == VD_HOST) VD_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    return VD_OK;
 }
 
 int vd_timing_enable(vd_ctx* h, int on) {
@@ -1195,6 +1237,7 @@ int vdt_conv2d(vd_ctx* h, const float* x, int n, int xh, int xw, int cin, const 
     a.B = n; a.cin_pad = cv.cin_pad; a.cout = cout; a.kpad = cv.kpad;
     a.kh = kh; a.kw = kw; a.stride = stride; a.pad = pad; a.M = n * oh * ow;
     a.act = act; a.slope = slope; a.out_f32 = 1; a.f16 = ctx->f16 ? 1 : 0;
+    a.tune = &ctx->tune;
     hipError_t e = vd_launch_conv(a, ctx->f32, ctx->stream);
     if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "conv launch: %s", hipGetErrorString(e));
     VD_CHECK_HIP(hipStreamSynchronize(ctx->stream));

@@ -215,8 +215,6 @@ hipError_t launch_stem(const StemPoolArgs& a, hipStream_t s) {
 }  // namespace
 
 bool vd_stem_pool_ok(int xh, int xw, int ph, int pw) {
-    const char* e = getenv("VD_STEM_POOL");
-    if (e && atoi(e) == 0) return false;
     const int sh = xh - 1, sw = xw - 1;
     return xh >= 2 && xw >= 2 && ph == (sh - 1) / 2 + 1 && pw == (sw - 1) / 2 + 1 &&
            (double)xh * xw * 16 * 2 < 2147483647.0 && (double)ph * pw * 128 < 2147483647.0;
@@ -226,10 +224,6 @@ hipError_t vd_launch_stem_pool(const StemPoolArgs& a, hipStream_t s) {
     if (a.B <= 0) return hipSuccess;
     // one X' buffer and three workgroups per CU measured 9 % faster than two buffers
     // (DMA overlapping the whole tile) at two workgroups per CU: the kernel is
-    // latency-bound, occupancy wins (VD_STEM_NXB=2 selects the other form)
-    static const int nxb = [] {
-        const char* e = getenv("VD_STEM_NXB");
-        return e && atoi(e) == 2 ? 2 : 1;
-    }();
-    return nxb == 1 ? launch_stem<1>(a, s) : launch_stem<2>(a, s);
+    // latency-bound, occupancy wins
+    return launch_stem<1>(a, s);
 }

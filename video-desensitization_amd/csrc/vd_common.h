@@ -12,6 +12,31 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 enum VdAct { VD_ACT_NONE = 0, VD_ACT_RELU = 1, VD_ACT_LEAKY = 2, VD_ACT_SILU = 3 };
 enum VdResMode { VD_RES_NONE = 0, VD_RES_PRE_ACT = 1, VD_RES_POST_ACT = 2 };
 
+// Kernel-selection switches of one context. The defaults ARE the production plan;
+// vd_set_option (include/vdmi.h) changes them per context for A/B measurements and
+// for tests that force a kernel form onto small shapes. Plan-time switches
+// (block_fuse, chain, stem_pool, ssh_fuse, plate_s2d) take effect at the next
+// vd_load_weights; the others at the next launch. Nothing is read from the
+// environment.
+struct VdTune {
+    int conv_stream = 1;      // streaming 1x1 kernel (conv1x1.hip) for K in {64,128,256}
+    int conv_stream512 = 1;   //   ... and K = 512
+    int conv_dual = 1;        // conv3 + downsample as one streaming launch
+    int conv_taps = 1;        // streaming taps kernel for small K (YOLO)
+    int conv_n192 = 1;        // 192-wide N tile for Cout 129..192 (fused SSH conv)
+    int conv_small = 512;     // below this many 128-row tiles the GEMM takes 64-row tiles
+    int conv_big = 100;       // min 256x256 tiles for the phased kernel (0: off)
+    int conv_big_kmin = 512;  // min K for the phased kernel
+    int stream_ntt = 16;      // streaming 1x1: 256-channel slices where Cout allows (8: 128)
+    int lb_pair = 1;          // one letterbox launch for both canvases when geometry allows
+    int mosaic_map = 1;       // mosaic output pass: per-band vector maps (0: generic path)
+    int block_fuse = 1;       // plan: fused layer1 bottlenecks (block.hip)
+    int chain = 1;            // plan: layer2 conv3 + next conv1 (chain.hip)
+    int stem_pool = 1;        // plan: stem conv + maxpool (stem.hip)
+    int ssh_fuse = 1;         // plan: SSH conv3X3 + conv5X5_1 as one conv
+    int plate_s2d = 1;        // plan: YOLO space-to-depth stem input
+};
+
 // Implicit-GEMM convolution parameters (device side). Activations are NHWC with
 // an explicit channel stride (ld) and channel offset (coff) so a conv can read
 // a channel slice of a concat buffer and write into one (SSH concat,
@@ -33,6 +58,7 @@ struct ConvArgs {
     // downsample in one pass): y = act(acc*scale + shift + acc2*scale2 + shift2)
     const void* x2; int xh2, xw2, ldx2, xcoff2, stride2;
     const void* w2; const float* scale2; const float* shift2; int cin2_pad, kpad2;
+    const VdTune* tune;                          // host-side kernel selection (never read on the device)
 };
 
 // One fused layer1 bottleneck (block.hip): x [B][H][W][cin] -> y [B][H][W][256],
@@ -111,7 +137,13 @@ struct PostArgs {
     int img_h, img_w;        // source frame size (all frames of a call share it)
     float offx, offy, scx, scy;   // face correction (utils_bbox.py:118-132, float32)
     int padx, pady; float inv_gain;  // yolo scale_boxes
-    int cap;                 // output capacity per frame
+    int cap;                 // caller's capacity per frame (out_* may all be NULL)
+    int kcap;                // complete keep list capacity per frame (>= any keep count)
+    int* k_count;            // [B]          complete keep lists (library-owned; the mosaic's input)
+    int* k_xyxy;             // [B][kcap][4]
+    float* k_xyxy_f;         // [B][kcap][4]
+    float* k_score;          // [B][kcap]
+    int* k_label;            // [B][kcap]
     int* out_count;          // [B]
     int* out_xyxy;           // [B][cap][4]
     float* out_xyxy_f;       // [B][cap][4]
@@ -143,15 +175,11 @@ struct LetterboxArgs {
 bool vd_conv1x1_stream_ok(const ConvArgs& a);
 bool vd_conv_big_ok(const ConvArgs& a);
 hipError_t vd_launch_conv_big(const ConvArgs& a, hipStream_t s);
-bool vd_conv_big128_ok(const ConvArgs& a);
-hipError_t vd_launch_conv_big128(const ConvArgs& a, hipStream_t s);
 hipError_t vd_launch_conv1x1_stream(const ConvArgs& a, hipStream_t s);
 bool vd_conv_taps_ok(const ConvArgs& a);
 bool vd_conv1x1_dual_ok(const ConvArgs& a);
 hipError_t vd_launch_conv_taps(const ConvArgs& a, hipStream_t s);
 hipError_t vd_launch_conv(const ConvArgs& a, bool f32, hipStream_t s);
-bool vd_conv_persist_ok(const ConvArgs& a);
-hipError_t vd_launch_conv_persist(const ConvArgs& a, hipStream_t s);
 bool vd_block_ok(int cin, bool ds, int h, int w);
 bool vd_stem_pool_ok(int xh, int xw, int ph, int pw);
 hipError_t vd_launch_dwconv(const DwConvArgs& a, bool f32, bool f16, hipStream_t s);
@@ -171,7 +199,7 @@ hipError_t vd_launch_post(const PostArgs& p, hipStream_t s);
 hipError_t vd_launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w, size_t pitch,
                             const int* cnt0, const int* xy0, int cap0,
                             const int* cnt1, const int* xy1, int cap1, int level, void* table,
-                            int stages, hipStream_t s);   // stages: 1 = cell table, 2 = output pass
+                            int stages, int map_on, hipStream_t s);   // stages: 1 = cell table, 2 = output pass
 size_t vd_mosaic_table_bytes(int n, int tcap);
 
 #define VD_CHECK_HIP(expr)                                                     \

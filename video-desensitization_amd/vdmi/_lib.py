@@ -66,6 +66,7 @@ SIGNATURES = [
     ("vd_destroy", _I, [_P]),
     ("vd_load_weights", _I, [_P, _I, _P, _SZ, _I]),
     ("vd_set_stream", _I, [_P, _P]),
+    ("vd_set_option", _I, [_P, ctypes.c_char_p, _I]),
     ("vd_get_stream", _P, [_P]),
     ("vd_sync", _I, [_P]),
     ("vd_detect", _I, [_P, _P, _I, _I, _I, _SZ, _I, ctypes.POINTER(vd_boxes)]),
@@ -73,6 +74,7 @@ SIGNATURES = [
     ("vd_mosaic", _I, [_P, _P, _P, _I, _I, _I, _SZ, _I, ctypes.POINTER(vd_boxes), _I, _I]),
     ("vd_process", _I, [_P, _P, _P, _I, _I, _I, _SZ, _I, _I, ctypes.POINTER(vd_boxes),
                         ctypes.POINTER(vd_boxes)]),
+    ("vd_read_boxes", _I, [_P, _I, _I, ctypes.POINTER(vd_boxes)]),
     ("vd_timing_enable", _I, [_P, _I]),
     ("vd_timing_reset", _I, [_P]),
     ("vd_timing_read", _I, [_P, _I, ctypes.POINTER(_D), ctypes.POINTER(ctypes.c_int64),

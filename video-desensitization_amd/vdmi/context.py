@@ -57,7 +57,7 @@ class Context:
 
     def __init__(self, device=0, precision="bf16", max_batch=64, input_shape=(640, 640), confidence=0.5,
                  nms_iou=0.4, max_boxes=256, mosaic_level=8, plate_nc=1, plate_conf=0.5, plate_iou=0.7,
-                 plate_max_det=300, plate_imgsz=640, microbatch=0, microbatch_stage=2):
+                 plate_max_det=300, plate_imgsz=640, microbatch=0, microbatch_stage=2, options=None):
         lib = _lib.load()
         cfg = _lib.default_cfg()
         cfg.input_h, cfg.input_w = int(input_shape[0]), int(input_shape[1])
@@ -85,6 +85,8 @@ class Context:
         check(lib.vd_create(ctypes.byref(cfg), self.device, ctypes.byref(h)))
         self._h = h
         self._lib = lib
+        for k, v in dict(options or {}).items():   # kernel-selection switches (vd_set_option)
+            self.set_option(k, v)
 
     # -- lifecycle -------------------------------------------------------
     def close(self):
@@ -108,6 +110,9 @@ class Context:
         buf = ctypes.create_string_buffer(bytes(blob), len(blob))
         check(self._lib.vd_load_weights(self._h, net, buf, len(blob), _lib.VD_WEIGHTS_VDW1))
 
+    def set_option(self, name, value):
+        check(self._lib.vd_set_option(self._h, str(name).encode(), int(value)))
+
     def set_stream(self, stream_ptr):
         check(self._lib.vd_set_stream(self._h, stream_ptr))
 
@@ -123,19 +128,39 @@ class Context:
             boxes = _lib.HostBoxes(n, self.cfg.max_boxes)
         return boxes
 
+    def read_boxes(self, net, n, cap=None):
+        """The complete keep lists of the last call for frames [0, n) (vd_read_boxes) as
+        HostBoxes; cap defaults to the largest count."""
+        if cap is None:
+            cnt = _lib.HostBoxes(n, 1)
+            check(self._lib.vd_read_boxes(self._h, net, n, ctypes.byref(cnt.struct())))
+            cap = max(1, int(cnt.count.max()))
+        boxes = _lib.HostBoxes(n, cap)
+        check(self._lib.vd_read_boxes(self._h, net, n, ctypes.byref(boxes.struct())))
+        return boxes
+
+    def _complete(self, boxes, net, auto):
+        """Library-allocated host lists never come back truncated: a frame that kept
+        more than cfg.max_boxes boxes triggers a re-read of the complete lists."""
+        if auto and isinstance(boxes, _lib.HostBoxes) and boxes.n and int(boxes.count.max()) > boxes.cap:
+            return self.read_boxes(net, boxes.n, int(boxes.count.max()))
+        return boxes
+
     def detect(self, frames, boxes=None):
         p, n, h, w, pitch, where, keep = _frames_arg(frames)
+        auto = boxes is None
         boxes = self._boxes(boxes, n)
         s = boxes.struct()
         check(self._lib.vd_detect(self._h, p, n, h, w, pitch, where, ctypes.byref(s)))
-        return boxes
+        return self._complete(boxes, _lib.VD_NET_RETINAFACE, auto)
 
     def detect_plates(self, frames, boxes=None):
         p, n, h, w, pitch, where, keep = _frames_arg(frames)
+        auto = boxes is None
         boxes = self._boxes(boxes, n)
         s = boxes.struct()
         check(self._lib.vd_detect_plates(self._h, p, n, h, w, pitch, where, ctypes.byref(s)))
-        return boxes
+        return self._complete(boxes, _lib.VD_NET_YOLOV8N, auto)
 
     def mosaic(self, frames, boxes_xyxy, counts=None, level=None, out=None):
         """Out-of-place mosaic. boxes_xyxy: int32 [n][cap][4] (host numpy) or a
@@ -173,6 +198,7 @@ class Context:
                 import torch
                 out = torch.empty_like(frames)
         fs = ps = None
+        auto_f, auto_p = faces is None, plates is None
         if flags & _lib.VD_PROC_FACES:
             faces = self._boxes(faces, n)
             fs = faces.struct()
@@ -183,6 +209,10 @@ class Context:
         check(self._lib.vd_process(self._h, p, optr, n, h, w, pitch, where, flags,
                                    ctypes.byref(fs) if fs is not None else None,
                                    ctypes.byref(ps) if ps is not None else None))
+        if flags & _lib.VD_PROC_FACES:
+            faces = self._complete(faces, _lib.VD_NET_RETINAFACE, auto_f)
+        if flags & _lib.VD_PROC_PLATES:
+            plates = self._complete(plates, _lib.VD_NET_YOLOV8N, auto_p)
         return out, faces, plates
 
     # -- instrumentation ------------------------------------------------------
@@ -221,7 +251,7 @@ class Context:
         boxes = _lib.HostBoxes(n, cap or self.cfg.max_boxes)
         s = boxes.struct()
         check(self._lib.vdt_postprocess(self._h, ptr(loc), ptr(conf), n, ptr(hw), ctypes.byref(s)))
-        return boxes
+        return self._complete(boxes, _lib.VD_NET_RETINAFACE, cap is None)
 
     def plate_raw(self, frames):
         """Raw YOLO head outputs [n][64+nc][A] (DFL logits | class logits), f32."""

@@ -10,15 +10,18 @@ ResNet-50 (or MobileNet-0.25)/FPN/SSH forward, decode, NMS, correction — runs 
 Differences, all deliberate:
 * ``cuda=False`` raises: the product path has no CPU fallback (the reference's
   own CPU path crashes in retinaface_correct_boxes' ``.cuda()``, utils_bbox.py:118).
-* ``model_path`` missing on disk -> seeded random weights (reference keys), with a
-  warning, since the real checkpoint is not distributable here.
+* ``model_path`` missing on disk raises FileNotFoundError (a desensitisation run
+  on random weights would leave every face visible while appearing to succeed).
+  Seeded random weights with the reference keys are an explicit opt-in,
+  ``weights="random"`` (tests, benchmarks).
 * The returned image is the caller's array itself, not a copy (face.py:129 copies;
   the driver never reads it, combine_detect.py:237).
-* Extra keywords: ``precision`` ("bf16" default, "fp32" parity mode),
-  ``max_batch``, ``device_index``, ``seed``, ``weights`` (a state_dict).
+* Extra keywords: ``precision`` ("fp32" default = the reference's arithmetic,
+  exact-f32 MFMA; "bf16" / "fp16" trade box parity for 4-6x throughput, see
+  INTEGRATION.md), ``max_batch``, ``device_index``, ``seed``, ``weights``
+  (a state_dict, or "random").
 """
 import os
-import warnings
 
 import numpy as np
 
@@ -37,7 +40,7 @@ class Retinaface(object):
         "letterbox_image": True,
         "cuda": True,
         # vdmi extras
-        "precision": "bf16",
+        "precision": "fp32",
         "max_batch": 64,
         "device_index": 0,
         "seed": 0,
@@ -71,13 +74,15 @@ class Retinaface(object):
 
     def generate(self):
         """face.py:50-60: load weights once (device-resident; no DataParallel replicate)."""
-        if self.weights is not None:
+        if isinstance(self.weights, str) and self.weights == "random":   # explicit opt-in (tests, bench)
+            sd = (retinaface_mnet_state_dict if self.backbone == "mobilenet" else retinaface_state_dict)(self.seed)
+        elif self.weights is not None:
             sd = self.weights
         elif self.model_path and os.path.exists(self.model_path):
             sd = load_reference_checkpoint(self.model_path)
         else:
-            warnings.warn(f"{self.model_path} not found: using seeded random RetinaFace weights (seed={self.seed})")
-            sd = (retinaface_mnet_state_dict if self.backbone == "mobilenet" else retinaface_state_dict)(self.seed)
+            raise FileNotFoundError(f"RetinaFace checkpoint {self.model_path!r} not found (pass model_path=, "
+                                    "weights=<state_dict>, or weights='random' for seeded test weights)")
         self.ctx.load_weights(_lib.VD_NET_RETINAFACE, sd)
 
     def detect_boxes(self, images):

@@ -9,12 +9,15 @@ ultralytics does [ext]. Note the reference never uses them: its tuple check at
 combine_detect.py:239 always yields [] for Results objects. ``vdmi.pipeline``
 reproduces that by default and offers the intended behaviour as an option.
 
-Architecture: YOLOv8n. The weights (best.pt) are a
-pickled ultralytics object that cannot be loaded here without executing it; a
-converted state_dict (``model.<i>...`` keys) or seeded random weights are used.
+Architecture: YOLOv8n. The reference's ``best.pt`` is a
+pickled ultralytics object that is never unpickled here (it would execute code).
+Accepted weights: a state_dict file with ``model.<i>...`` keys loadable by
+``torch.load(weights_only=True)`` -- convert once where ultralytics is installed:
+``torch.save(YOLO("best.pt").model.float().state_dict(), "best_sd.pt")`` -- a VDW1
+file, or ``weights=<state_dict>``. A missing or unloadable file raises;
+``weights="random"`` (seeded, reference keys) is an explicit opt-in for tests.
 """
 import os
-import warnings
 
 import numpy as np
 
@@ -58,10 +61,34 @@ class _ModelProxy:
             yield type("P", (), {"device": self._device})()
 
 
+def load_plate_weights(path):
+    """A YOLOv8 state_dict file (torch weights_only) or a VDW1 file -> {name: array}."""
+    if not path or not os.path.exists(path):
+        raise FileNotFoundError(f"plate weights {path!r} not found (pass a converted state_dict / VDW1 file, "
+                                "weights=<state_dict>, or weights='random' for seeded test weights)")
+    with open(path, "rb") as f:
+        magic = f.read(4)
+    if magic == b"VDW1":
+        from .weights import unpack_vdw
+        return unpack_vdw(open(path, "rb").read())
+    import torch
+    try:
+        sd = torch.load(path, map_location="cpu", weights_only=True)
+    except Exception as e:   # a pickled ultralytics model object: refused by the safe loader
+        raise ValueError(f"{path}: not a weights-only state_dict (a pickled ultralytics checkpoint is never "
+                         "unpickled here). Convert it where ultralytics is installed: torch.save(YOLO(path)."
+                         "model.float().state_dict(), 'best_sd.pt')") from e
+    if isinstance(sd, dict) and isinstance(sd.get("model"), dict):
+        sd = sd["model"]
+    if not isinstance(sd, dict) or not any(k.startswith("model.") for k in sd):
+        raise ValueError(f"{path}: no 'model.<i>...' keys: not a YOLOv8 DetectionModel state_dict")
+    return {k: v.detach().float().cpu().numpy() for k, v in sd.items() if hasattr(v, "detach")}
+
+
 class YOLO:
     """ultralytics-style plate detector on libvdmi."""
 
-    def __init__(self, model="best.pt", nc=1, weights=None, precision="bf16", max_batch=64, device_index=0,
+    def __init__(self, model="best.pt", nc=1, weights=None, precision="fp32", max_batch=64, device_index=0,
                  seed=0, imgsz=640, iou=0.7, max_det=300, names=None):
         self.nc = nc
         self.names = names or {i: f"plate{i}" if nc > 1 else "plate" for i in range(nc)}
@@ -69,15 +96,10 @@ class YOLO:
         self.max_batch = max_batch
         self.ctx = Context(device=device_index, precision=precision, max_batch=max_batch, plate_nc=nc,
                            plate_iou=iou, plate_max_det=max_det, plate_imgsz=imgsz)
-        if weights is None:
-            if model and os.path.exists(model) and not model.endswith(".pt"):
-                from .weights import unpack_vdw
-                weights = unpack_vdw(open(model, "rb").read())
-            else:
-                if model and os.path.exists(model):
-                    warnings.warn(f"{model}: pickled ultralytics checkpoints are not loaded (they execute code); "
-                                  "convert to a state_dict / VDW1 file. Using seeded random weights.")
-                weights = yolov8n_state_dict(seed, nc)
+        if isinstance(weights, str) and weights == "random":   # explicit opt-in (tests, bench)
+            weights = yolov8n_state_dict(seed, nc)
+        elif weights is None:
+            weights = load_plate_weights(model)
         self.ctx.load_weights(_lib.VD_NET_YOLOV8N, weights)
         self.model = _ModelProxy(f"cuda:{device_index}")
         self._conf = 0.5
