@@ -55,6 +55,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP event timing")
     ap.add_argument("--faces", type=int, default=1, help="0: plates only, no mosaic (profiling the plate net)")
+    ap.add_argument("--host-pipeline", type=int, default=1, help="1: also time the host-frame pipeline (PCIe incl.)")
     return ap.parse_args()
 
 
@@ -244,8 +245,38 @@ def main():
             res.update(instrumented(mode, precision))
         res["faces_per_frame"] = round(float(mode.faces.count.float().mean().item()), 2)
         lists = frame_lists(mode.ctx, batches[-1][1]) if batches else []
+        if world == 1 and precision == a.precision and a.host_pipeline:
+            res["host_pipeline"] = host_pipeline(mode)
         mode.close()
         return res, lists
+
+    def host_pipeline(mode):
+        """The same workload from pinned HOST frames to pinned host output: H2D, the
+        vd_process and the D2H of frames and box lists on three streams
+        (vdmi.pipeline.FramePipeline), batch i's copies overlapping batch i+-1's
+        compute. The frames sit in the pinned slots a decoder would write into."""
+        from vdmi.pipeline import FramePipeline
+        pipe = FramePipeline(mode.ctx, H, W, max_batch=B, plates=plates)
+        for _ in range(pipe.depth):                       # both slots hold real frames
+            pipe.next_input(B)[...] = host[:B]
+            pipe.collect(pipe.submit_filled(B))
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        pending = None
+        for _ in range(a.steps):
+            pipe.next_input(B)
+            cur = pipe.submit_filled(B)
+            if pending is not None:
+                pipe.collect(pending)
+            pending = cur
+        pipe.collect(pending)
+        d = time.perf_counter() - t0
+        pipe.close()
+        mode.ctx.set_stream(stream.cuda_stream)
+        return {"value": round(B * a.steps / d, 2), "unit": "frames/s", "ms_per_step": round(d / a.steps * 1e3, 3),
+                "pcie_bytes_per_step": 2 * B * H * W * 3,
+                "what": "pinned host frames -> H2D -> vd_process -> D2H of mosaicked frames + box lists, "
+                        "copies and compute on separate streams (FramePipeline, depth 2)"}
 
     def instrumented(mode, precision):
         """Per-kernel-family durations: the same K steps again, each launch bracketed
@@ -312,7 +343,7 @@ def main():
                    "plates": plates},
     }
     for k in ("roofline", "blur_roofline", "faces_per_frame", "instrumented_ms_per_step", "plate_conv",
-              "ms_breakdown_per_step"):
+              "ms_breakdown_per_step", "host_pipeline"):
         if k in head:
             res[k] = head[k]
     parity = {}

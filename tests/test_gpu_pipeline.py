@@ -51,3 +51,67 @@ def test_batch_dropped_on_inference_error(gpu, tmp_path):
                                       loader=lambda p: synth.frame(64, 64, 0),
                                       saver=lambda img, p: saved.__setitem__(p, img))
     assert (n, nf, npl) == (0, 0, 0) and not saved
+
+
+def test_frame_pipeline_matches_unpipelined_process(gpu):
+    """FramePipeline (pinned double buffers, upload / compute / download streams,
+    results one batch behind) == one synchronous vd_process per batch: same
+    mosaicked pixels, complete counts and boxes, for faces and plates, incl. a
+    short last batch."""
+    import vdmi
+    from vdmi import _lib, synth, weights
+    from vdmi.pipeline import FramePipeline
+    ctx = vdmi.Context(precision="bf16", max_batch=4)
+    try:
+        ctx.load_weights(0, weights.retinaface_state_dict(0))
+        ctx.load_weights(1, weights.yolov8n_state_dict(0))
+        batches = [synth.frames(4, 540, 960, seed=40, start=4 * i) for i in range(4)] + \
+                  [synth.frames(2, 540, 960, seed=41)]
+        pipe = FramePipeline(ctx, 540, 960, max_batch=4, mosaic_plates=True)
+        got = [(o.copy(), fc.copy(), [b.copy() for b in fb], pc.copy(), [b.copy() for b in pb])
+               for o, fc, fb, pc, pb in pipe.run(iter(batches))]
+        pipe.close()
+        flags = _lib.VD_PROC_FACES | _lib.VD_PROC_PLATES | _lib.VD_PROC_MOSAIC | _lib.VD_PROC_MOSAIC_PLATES
+        assert len(got) == len(batches)
+        nf = 0
+        for fr, (o, fc, fb, pc, pb) in zip(batches, got):
+            out, faces, plates = ctx.process(fr, flags=flags)
+            np.testing.assert_array_equal(o, out)
+            np.testing.assert_array_equal(fc, faces.count)
+            np.testing.assert_array_equal(pc, plates.count)
+            for j in range(fr.shape[0]):
+                np.testing.assert_array_equal(fb[j], faces.frame(j)[0])
+                np.testing.assert_array_equal(pb[j], plates.frame(j)[0])
+            nf += int(fc.sum())
+        assert nf > 0
+    finally:
+        ctx.close()
+
+
+def test_batch_process_images_fused_mosaic_plates(gpu, tmp_path):
+    """The fused path with mosaic_plates=True (intended mode): plates are counted and
+    blurred after the faces, exactly as the oracle's sequential mosaic of the drop-in
+    detectors' boxes (faces in NMS order, then plates)."""
+    import vdmi
+    from vdmi import synth, weights
+    from vdmi.pipeline import batch_process_images
+    frames = {f"g{i:02d}.png": synth.frame(1080, 1920, i, seed=8) for i in range(3)}
+    for name in frames:
+        (tmp_path / name).write_bytes(b"")
+    saved = {}
+    face = vdmi.Retinaface(input_shape=[640, 640, 3], nms_iou=0.4, max_batch=4,
+                           weights=weights.retinaface_state_dict(0))
+    plate = vdmi.YOLO(weights="random", max_batch=4)
+    n, nf, npl = batch_process_images(str(tmp_path), str(tmp_path / "out"), face, plate, batch_size=2,
+                                      loader=lambda p: frames[os.path.basename(p)], mosaic_plates=True,
+                                      saver=lambda img, p: saved.__setitem__(os.path.basename(p), img))
+    assert n == 3 and len(saved) == 3
+    tf = tp = 0
+    for name, img in frames.items():
+        fb = face.detect_images([img])[0][1]
+        pb = plate([img])[0].boxes.xyxy.tolist()
+        tf += len(fb)
+        tp += len(pb)
+        boxes = [tuple(int(v) for v in b) for b in fb] + [tuple(int(v) for v in b) for b in pb]
+        np.testing.assert_array_equal(saved[f"processed_{name}"], omosaic.mosaic_frame(img, boxes, 8))
+    assert (nf, npl) == (tf, tp) and tp > 0

@@ -83,6 +83,7 @@ class Retinaface(object):
         else:
             raise FileNotFoundError(f"RetinaFace checkpoint {self.model_path!r} not found (pass model_path=, "
                                     "weights=<state_dict>, or weights='random' for seeded test weights)")
+        self.state_dict = sd           # kept for a fused face+plate context (vdmi.pipeline)
         self.ctx.load_weights(_lib.VD_NET_RETINAFACE, sd)
 
     def detect_boxes(self, images):

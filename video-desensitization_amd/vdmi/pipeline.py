@@ -1,19 +1,24 @@
 """Hot-loop body of the reference driver on the MI355X path.
 
 ``batch_process_images`` mirrors combine_detect.py:183-277 (same signature, same
-per-batch semantics): list the frame files, load a batch, run the face detector
-and the plate detector, take face boxes from ``face_results[j][1]`` and plate
-boxes from ``plate_results[j][1] if isinstance(..., tuple) else []``
-(combine_detect.py:237-239 — Results objects yield [], so plates are discarded
-exactly as in the reference unless ``mosaic_plates=True``), truncate with int()
-(:243-244), mosaic sequentially per box (:246-249), save, count faces/plates, and
-drop a batch whose inference raises (:226-228).
+per-batch semantics): list the frame files, load a batch, detect faces and
+plates, take face boxes from ``face_results[j][1]`` and plate boxes from
+``plate_results[j][1] if isinstance(..., tuple) else []`` (combine_detect.py:237-239
+-- Results objects yield [], so plate boxes are discarded exactly as in the
+reference unless ``mosaic_plates=True``), int() them (:243-244), mosaic every box
+in order (:246-249), save, count, and drop a batch whose inference raises
+(:226-228).
 
-``process_batch`` is the same body on device-resident frames through one
-``vd_process`` call (letterbox, both forwards, NMS, mosaic), which is what the
-benchmark times. Image I/O (cv2.imread/imwrite, combine_detect.py:167-180) is
-outside the hot path; it is used when cv2 is importable and can be replaced by
-``loader`` / ``saver`` callables.
+When both detectors are the vdmi drop-ins, the batch body is ONE ``vd_process``
+on one context (letterbox, both forwards, NMS, mosaic of every kept box) driven
+by ``FramePipeline``: pinned host buffers, double-buffered device slots and
+three HIP streams (host->device copy, compute, device->host copy), so batch
+i's upload and batch i-1's download overlap batch i's compute; file decode and
+encode run on worker threads beside it. Other detector objects take the
+reference's two-thread path unchanged.
+
+File I/O uses cv2 when importable (combine_detect.py:167-180: imread + BGR->RGB,
+imwrite of RGB->BGR) and Pillow otherwise; ``loader`` / ``saver`` override both.
 """
 import logging
 import os
@@ -31,27 +36,191 @@ def _cv2():
     try:
         import cv2
         return cv2
-    except Exception as e:  # pragma: no cover - cv2 is absent in this image
-        raise RuntimeError("cv2 is needed for file I/O; pass loader=/saver= callables instead") from e
+    except Exception:
+        return None
 
 
 def load_image_rgb(path):
-    """combine_detect.py:167-172."""
+    """combine_detect.py:167-172 (cv2.imread + BGR->RGB); Pillow when cv2 is absent."""
     cv2 = _cv2()
-    img = cv2.imread(path)
-    if img is None:
-        raise ValueError(f"cannot read image: {path}")
-    return cv2.cvtColor(img, cv2.COLOR_BGR2RGB)
+    if cv2 is not None:
+        img = cv2.imread(path)
+        if img is None:
+            raise ValueError(f"cannot read image: {path}")
+        return cv2.cvtColor(img, cv2.COLOR_BGR2RGB)
+    from PIL import Image
+    with Image.open(path) as im:
+        return np.asarray(im.convert("RGB"))
 
 
 def save_output_image(image_array, output_path):
-    """combine_detect.py:177-180."""
+    """combine_detect.py:177-180 (cv2.imwrite, JPEG quality 95 by default); Pillow
+    (quality 95) when cv2 is absent."""
     cv2 = _cv2()
-    cv2.imwrite(output_path, cv2.cvtColor(image_array, cv2.COLOR_RGB2BGR))
+    if cv2 is not None:
+        cv2.imwrite(output_path, cv2.cvtColor(image_array, cv2.COLOR_RGB2BGR))
+        return
+    from PIL import Image
+    Image.fromarray(np.ascontiguousarray(image_array)).save(output_path, quality=95)
 
 
 def _boxes_of(result):
     return result[1] if isinstance(result, tuple) else []
+
+
+class FramePipeline:
+    """Pipelined ``vd_process`` over host frame batches on one context.
+
+    Per batch i (slot i % depth): host frames -> pinned slot (CPU copy), then on
+    the upload stream an async H2D into the device slot, on the compute stream
+    (the context's stream) one vd_process (faces | plates | mosaic) into the
+    device output slot, on the download stream the D2H of the mosaicked frames
+    and of the box counts / lists. Events order the three streams; a slot is
+    reused only after its previous batch's download completed. ``run`` yields
+    each batch's results one batch behind the submission, so the next batch's
+    upload and compute are already queued while the caller consumes a result.
+    """
+
+    def __init__(self, ctx, h, w, max_batch=None, depth=2, plates=True, mosaic_plates=False, cap=256):
+        import torch
+        self.torch = torch
+        self.ctx = ctx
+        self.h, self.w = int(h), int(w)
+        self.B = int(max_batch or ctx.cfg.max_batch)
+        self.depth = max(2, int(depth))
+        self.cap = int(cap)
+        dev = torch.device(f"cuda:{ctx.device}")
+        self.dev = dev
+        flags = _lib.VD_PROC_FACES | _lib.VD_PROC_MOSAIC
+        if plates:
+            flags |= _lib.VD_PROC_PLATES
+            if mosaic_plates:
+                flags |= _lib.VD_PROC_MOSAIC_PLATES
+        self.flags = flags
+        self.plates = bool(plates)
+        shp = (self.depth, self.B, self.h, self.w, 3)
+        self.h_in = torch.empty(shp, dtype=torch.uint8).pin_memory()
+        self.h_out = torch.empty(shp, dtype=torch.uint8).pin_memory()
+        self.d_in = torch.empty(shp, dtype=torch.uint8, device=dev)
+        self.d_out = torch.empty(shp, dtype=torch.uint8, device=dev)
+        from .context import DeviceBoxes
+        self.d_faces = [DeviceBoxes(self.B, self.cap, dev) for _ in range(self.depth)]
+        self.d_plates = [DeviceBoxes(self.B, self.cap, dev) for _ in range(self.depth)] if plates else None
+        nb = 2 if plates else 1
+        self.h_cnt = torch.empty((self.depth, nb, self.B), dtype=torch.int32).pin_memory()
+        self.h_xy = torch.empty((self.depth, nb, self.B, self.cap, 4), dtype=torch.int32).pin_memory()
+        self.s_up = torch.cuda.Stream(dev)
+        self.s_comp = torch.cuda.Stream(dev)
+        self.s_down = torch.cuda.Stream(dev)
+        ctx.set_stream(self.s_comp.cuda_stream)
+        ev = lambda: [torch.cuda.Event() for _ in range(self.depth)]
+        self.ev_up, self.ev_comp, self.ev_down = ev(), ev(), ev()
+        self.used = [False] * self.depth
+        self.seq = 0
+
+    def next_input(self, n):
+        """Pinned host buffer [n,h,w,3] of the next slot, free to be written (a decoder
+        can write frames straight into it); then call submit_filled(n)."""
+        if n <= 0 or n > self.B:
+            raise ValueError(f"batch of {n} outside [1, {self.B}]")
+        k = self.seq % self.depth
+        if self.used[k]:
+            self.ev_down[k].synchronize()        # the slot's previous batch has left the device
+        return self.h_in[k, :n].numpy()
+
+    def submit(self, frames):
+        """Queue one batch (numpy uint8 [n,h,w,3]) on the three streams; returns a
+        ticket for collect(). Raises (VdError / ValueError) when the batch is rejected."""
+        frames = np.ascontiguousarray(frames, np.uint8)
+        if frames.ndim != 4 or frames.shape[1:] != (self.h, self.w, 3):
+            raise ValueError(f"batch {frames.shape} does not fit the pipeline ({self.B}, {self.h}, {self.w}, 3)")
+        self.next_input(frames.shape[0])[...] = frames   # host copy into pinned memory
+        return self.submit_filled(frames.shape[0])
+
+    def submit_filled(self, n):
+        """Queue the batch already written into next_input(n)'s buffer."""
+        torch = self.torch
+        k = self.seq % self.depth
+        with torch.cuda.stream(self.s_up):
+            if self.used[k]:
+                self.s_up.wait_event(self.ev_comp[k])      # device input slot no longer read
+            self.d_in[k, :n].copy_(self.h_in[k, :n], non_blocking=True)
+            self.ev_up[k].record(self.s_up)
+        self.s_comp.wait_event(self.ev_up[k])
+        if self.used[k]:
+            self.s_comp.wait_event(self.ev_down[k])
+        faces = self.d_faces[k]
+        plates = self.d_plates[k] if self.plates else None
+        self.ctx.process(self.d_in[k, :n], self.d_out[k, :n], faces=faces, plates=plates, flags=self.flags)
+        self.ev_comp[k].record(self.s_comp)
+        with torch.cuda.stream(self.s_down):
+            self.s_down.wait_event(self.ev_comp[k])
+            self.h_out[k, :n].copy_(self.d_out[k, :n], non_blocking=True)
+            self.h_cnt[k, 0, :n].copy_(faces.count[:n], non_blocking=True)
+            self.h_xy[k, 0, :n].copy_(faces.xyxy[:n], non_blocking=True)
+            if self.plates:
+                self.h_cnt[k, 1, :n].copy_(plates.count[:n], non_blocking=True)
+                self.h_xy[k, 1, :n].copy_(plates.xyxy[:n], non_blocking=True)
+            self.ev_down[k].record(self.s_down)
+        self.used[k] = True
+        self.seq += 1
+        return (k, n)
+
+    def collect(self, ticket):
+        """Wait for a submitted batch: (out uint8 [n,h,w,3], face_counts [n], face_boxes,
+        plate_counts, plate_boxes). `out` and the boxes are views of pinned buffers,
+        valid until `depth` more batches are submitted. Counts are complete (they may
+        exceed cap; the mosaic always covers every kept box)."""
+        k, n = ticket
+        self.ev_down[k].synchronize()
+        cnt = self.h_cnt[k].numpy()
+        xy = self.h_xy[k].numpy()
+        out = self.h_out[k, :n].numpy()
+        faces = [xy[0, j, :min(int(cnt[0, j]), self.cap)] for j in range(n)]
+        plates = [xy[1, j, :min(int(cnt[1, j]), self.cap)] for j in range(n)] if self.plates else [None] * n
+        return out, cnt[0, :n].copy(), faces, (cnt[1, :n].copy() if self.plates else None), plates
+
+    def run(self, batches):
+        """Yield collect() of every batch, one batch behind the submission, so the next
+        batch's upload and compute are queued while the caller consumes a result."""
+        pending = None
+        for frames in batches:
+            cur = self.submit(frames)
+            if pending is not None:
+                yield self.collect(pending)
+            pending = cur
+        if pending is not None:
+            yield self.collect(pending)
+
+    def close(self):
+        self.torch.cuda.synchronize(self.dev)
+        self.ctx.set_stream(None)
+
+
+def fused_context(face_detector, plate_detector, batch_size):
+    """One context holding both drop-ins' weights and the face detector's knobs
+    (cached on the face detector)."""
+    from .context import Context
+    key = (id(plate_detector), int(batch_size))
+    cache = getattr(face_detector, "_fused", None)
+    if cache and cache[0] == key:
+        return cache[1]
+    fd, pd = face_detector, plate_detector
+    ctx = Context(device=fd.device_index, precision=fd.precision, max_batch=max(int(batch_size), 1),
+                  input_shape=fd.input_shape[:2], confidence=fd.confidence, nms_iou=fd.nms_iou,
+                  max_boxes=fd.max_boxes, plate_nc=pd.nc, plate_conf=pd.ctx.cfg.plate_conf,
+                  plate_iou=pd.ctx.cfg.plate_iou, plate_max_det=pd.ctx.cfg.plate_max_det,
+                  plate_imgsz=pd.ctx.cfg.plate_imgsz)
+    ctx.load_weights(_lib.VD_NET_RETINAFACE, fd.state_dict)
+    ctx.load_weights(_lib.VD_NET_YOLOV8N, pd.state_dict)
+    face_detector._fused = (key, ctx)
+    return ctx
+
+
+def _is_vdmi_pair(face_detector, plate_detector):
+    from .face import Retinaface
+    from .plate import YOLO
+    return isinstance(face_detector, Retinaface) and isinstance(plate_detector, YOLO)
 
 
 def batch_process_images(input_dir, output_dir, face_detector, plate_detector, batch_size=16,
@@ -62,13 +231,103 @@ def batch_process_images(input_dir, output_dir, face_detector, plate_detector, b
     saver = saver or save_output_image
     image_paths = [os.path.join(input_dir, f) for f in os.listdir(input_dir) if f.lower().endswith(IMAGE_EXT)]
     os.makedirs(output_dir, exist_ok=True)
-    total_processed = total_faces = total_plates = 0
-    executor = ThreadPoolExecutor(max_workers=num_workers)
-    save_futures = []
-    for i in range(0, len(image_paths), batch_size):
-        batch_files = image_paths[i:i + batch_size]
-        with ThreadPoolExecutor(max_workers=num_workers) as pool:
-            batch_images = list(pool.map(loader, batch_files))
+    batches = [image_paths[i:i + batch_size] for i in range(0, len(image_paths), batch_size)]
+    io = ThreadPoolExecutor(max_workers=num_workers)
+    try:
+        if _is_vdmi_pair(face_detector, plate_detector) and mosaic_level == face_detector.ctx.cfg.mosaic_level:
+            res = _fused_batches(batches, output_dir, face_detector, plate_detector, batch_size, loader, saver,
+                                 mosaic_plates, io, logger)
+        else:
+            res = _threaded_batches(batches, output_dir, face_detector, plate_detector, loader, saver,
+                                    mosaic_plates, mosaic_level, io, logger)
+    finally:
+        io.shutdown(wait=True)
+    logger.info(f"processed {res[0]} images: {res[1]} faces, {res[2]} plates")
+    return res
+
+
+def _save_all(futs, logger):
+    for f in futs:
+        try:
+            f.result()
+        except Exception as e:
+            logger.error(f"saving failed: {e}")
+
+
+def _fused_batches(batches, output_dir, face_detector, plate_detector, batch_size, loader, saver, mosaic_plates,
+                   io, logger):
+    """The vdmi path, streaming: decode batch b+1 (threads) while batch b is on the
+    GPU (FramePipeline: one vd_process per batch), collect batch b-1 and hand its
+    frames to the encoder threads. Frames of another size get their own pipeline;
+    a batch whose load or inference fails is dropped (combine_detect.py:226-228)."""
+    totals = [0, 0, 0]
+    save_futs = []
+    ctx = fused_context(face_detector, plate_detector, batch_size)
+    pipes = {}
+    load = lambda files: list(io.map(loader, files))
+
+    def finish(p):
+        pipe, ticket, files = p
+        try:
+            out, fcnt, _, pcnt, _ = pipe.collect(ticket)
+        except Exception as e:           # a fault surfacing at the sync: the batch is dropped
+            logger.error(f"parallel inference failed: {e}")
+            return
+        for path, img in zip(files, out):
+            dst = os.path.join(output_dir, f"processed_{os.path.basename(path)}")
+            save_futs.append(io.submit(saver, img.copy(), dst))
+        totals[0] += len(files)
+        totals[1] += int(fcnt.sum())
+        if mosaic_plates:                # the reference's tuple check discards plate boxes otherwise
+            totals[2] += int(pcnt.sum())
+
+    pending = None
+    fut = io.submit(load, batches[0]) if batches else None
+    for bi, files in enumerate(batches):
+        try:
+            imgs = fut.result()
+        except Exception as e:
+            logger.error(f"loading failed: {e}")
+            imgs = None
+        fut = io.submit(load, batches[bi + 1]) if bi + 1 < len(batches) else None
+        if imgs is None:
+            continue
+        groups = {}
+        for f, im in zip(files, imgs):
+            groups.setdefault(im.shape, []).append((f, im))
+        for shape, items in groups.items():
+            if shape not in pipes:
+                pipes[shape] = FramePipeline(ctx, shape[0], shape[1], max_batch=batch_size, plates=True,
+                                             mosaic_plates=mosaic_plates)
+            try:
+                cur = (pipes[shape], pipes[shape].submit(np.stack([im for _, im in items])),
+                       [f for f, _ in items])
+            except Exception as e:       # combine_detect.py:226-228: the batch is dropped
+                logger.error(f"parallel inference failed: {e}")
+                cur = None
+            if pending is not None:
+                finish(pending)
+            pending = cur
+    if pending is not None:
+        finish(pending)
+    for pipe in pipes.values():
+        pipe.close()
+    _save_all(save_futs, logger)
+    return tuple(totals)
+
+
+def _threaded_batches(batches, output_dir, face_detector, plate_detector, loader, saver, mosaic_plates,
+                      mosaic_level, io, logger):
+    """Generic detectors: the reference's two-thread face || plate submission, then
+    one batched mosaic launch per same-size group."""
+    total = faces = plates = 0
+    save_futs = []
+    for files in batches:
+        try:
+            batch_images = list(io.map(loader, files))
+        except Exception as e:
+            logger.error(f"loading failed: {e}")
+            continue
         with ThreadPoolExecutor(max_workers=2) as infer:   # face || plate, as the reference does
             ff = infer.submit(face_detector.detect_images, batch_images.copy())
             fp = infer.submit(plate_detector, batch_images.copy(), verbose=False, conf=0.5)
@@ -88,21 +347,15 @@ def batch_process_images(input_dir, output_dir, face_detector, plate_detector, b
             boxes = [(int(x1), int(y1), int(x2), int(y2)) for x1, y1, x2, y2 in face_boxes]
             boxes += [(int(x1), int(y1), int(x2), int(y2)) for x1, y1, x2, y2 in plate_boxes]
             per_frame.append(boxes)
-            total_faces += len(face_boxes)
-            total_plates += len(plate_boxes)
+            faces += len(face_boxes)
+            plates += len(plate_boxes)
         processed = _mosaic_grouped(batch_images, per_frame, mosaic_level)
-        for path, img in zip(batch_files, processed):
+        for path, img in zip(files, processed):
             out = os.path.join(output_dir, f"processed_{os.path.basename(path)}")
-            save_futures.append(executor.submit(saver, img, out))
-        total_processed += len(batch_files)
-    for f in save_futures:
-        try:
-            f.result()
-        except Exception as e:
-            logger.error(f"saving failed: {e}")
-    executor.shutdown()
-    logger.info(f"processed {total_processed} images: {total_faces} faces, {total_plates} plates")
-    return total_processed, total_faces, total_plates
+            save_futs.append(io.submit(saver, img, out))
+        total += len(files)
+    _save_all(save_futs, logger)
+    return total, faces, plates
 
 
 def _mosaic_grouped(images, boxes, level):

@@ -100,6 +100,7 @@ class YOLO:
             weights = yolov8n_state_dict(seed, nc)
         elif weights is None:
             weights = load_plate_weights(model)
+        self.state_dict = weights      # kept for a fused face+plate context (vdmi.pipeline)
         self.ctx.load_weights(_lib.VD_NET_YOLOV8N, weights)
         self.model = _ModelProxy(f"cuda:{device_index}")
         self._conf = 0.5
