@@ -5,11 +5,14 @@ through the whole hot path on each GPU: letterbox -> RetinaFace-R50+FPN+SSH ->
 decode/NMS -> box correction -> int() -> mosaic write-back, with the YOLOv8n
 plate forward + NMS beside it (BASELINE config 3).
 
-The headline runs in fp32 -- the reference's arithmetic (exact-f32 MFMA), the
+The headline runs in fp32 -- the reference's arithmetic: f32 activations and
+weights; every conv multiplies f32 operands split exactly into three bf16 terms
+(six products on the bf16 matrix cores, f32 accumulation: conv_x6.hip), the
 mode whose boxes are parity-checked against the oracle. The same frames are then
-run in bf16 and fp16 (`modes`), and `parity` reports, over the B bench frames,
-the fraction whose complete keep lists and int boxes equal the fp32 GPU path's
-(and, from the cpu_baseline leg, the fp32 GPU path's agreement with the oracle).
+run on exact-f32 MFMA (`fp32_exact`), bf16 and fp16 (`modes`), and `parity`
+reports, over the B bench frames, the fraction whose complete keep lists and int
+boxes equal the headline's (and, from the cpu_baseline leg, each fp32 path's
+agreement with the oracle).
 
 Multi-GPU (one process per GPU, torchrun): `--scaling weak` (default) gives every
 rank its own B frames; `--scaling strong --frames N` shards ONE list of N frames
@@ -32,7 +35,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "video-desensitization_amd"))
 sys.path.insert(0, ROOT)
 
-PEAK_TFLOPS = {"bf16": 2500.0, "fp16": 2500.0, "fp32": 157.3}   # MI355X_MICROARCH.md: dense MFMA peaks
+# MI355X_MICROARCH.md dense MFMA peaks. fp32 (default plan, conv_x6.hip): f32 FLOPs on the bf16
+# matrix cores at six products per multiply-add -> 2500 / 6; fp32_exact: v_mfma_f32_16x16x4_f32.
+PEAK_TFLOPS = {"bf16": 2500.0, "fp16": 2500.0, "fp32": 2500.0 / 6, "fp32_exact": 157.3}
 PEAK_HBM_GBS = 8000.0                           # MI355X_MICROARCH.md: HBM3E spec
 
 
@@ -44,8 +49,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--precision", default="fp32", choices=["bf16", "fp16", "fp32"])
-    ap.add_argument("--compare", default="bf16,fp16",
+    ap.add_argument("--precision", default="fp32", choices=["bf16", "fp16", "fp32", "fp32_exact"])
+    ap.add_argument("--compare", default="fp32_exact,bf16,fp16",
                     help="extra precisions measured on the same frames at N=1 (',' separated; '' = none)")
     ap.add_argument("--plates", type=int, default=1, help="1: run YOLOv8n beside RetinaFace (BASELINE config 3)")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
@@ -144,9 +149,11 @@ class Mode:
     def __init__(self, a, precision, dev, sd, plates):
         import vdmi
         from vdmi import _lib, weights
-        opts = dict(o.split("=", 1) for o in a.option)
-        self.ctx = vdmi.Context(device=dev.index or 0, precision=precision, max_batch=a.batch,
-                                options={k: int(v) for k, v in opts.items()})
+        opts = {k: int(v) for k, v in (o.split("=", 1) for o in a.option)}
+        if precision == "fp32_exact":     # fp32 plan on exact-f32 MFMA instead of the 3-term bf16 split
+            opts["f32_split"] = 0
+        self.ctx = vdmi.Context(device=dev.index or 0, precision=precision.replace("_exact", ""),
+                                max_batch=a.batch, options=opts)
         self.ctx.load_weights(_lib.VD_NET_RETINAFACE, sd)
         if plates:
             self.ctx.load_weights(_lib.VD_NET_YOLOV8N, weights.yolov8n_state_dict(0))
@@ -297,7 +304,9 @@ def main():
         ach = cflop / (cms * 1e-3) / 1e12 if cms > 0 else 0.0
         traffic, tsrc, blur_traffic = pmc_traffic(precision)
         peak = PEAK_TFLOPS[precision]
-        kern = ("conv_igemm_kernel<float> launches (exact-f32 v_mfma_f32_16x16x4_f32)" if precision == "fp32" else
+        kern = ("conv_x6_kernel launches (f32 operands split exactly into 3 bf16 terms, 6 products on "
+                "v_mfma_f32_16x16x32_bf16, f32 accumulate; peak = 2500/6)" if precision == "fp32" else
+                "conv_igemm_kernel<float> launches (exact-f32 v_mfma_f32_16x16x4_f32)" if precision == "fp32_exact" else
                 "conv_igemm_kernel<_Float16> launches" if precision == "fp16" else
                 "stem_pool + bottleneck (fused layer1) + chain (layer2) + conv_big + conv_igemm + conv1x1_stream")
         r["roofline"] = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
@@ -333,7 +342,7 @@ def main():
         "metric": "end-to-end detect+blur FPS on 1920x1080 frames",
         "value": head["value"], "unit": "frames/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": head["ms_per_step"], "higher_is_better": True, "scaling": a.scaling,
-        "vs_baseline": None, "dtype": a.precision,
+        "vs_baseline": None, "dtype": "fp32" if a.precision.startswith("fp32") else a.precision,
         "data": "synthetic (counter-hash frames, seeded random weights)",
         "config": {"workload": f"RetinaFace-R50+FPN+SSH{' + YOLOv8n plates' if plates else ''} detect + mosaic "
                                f"write-back, {total} frames of {W}x{H} per step over {world} GPU(s) "
@@ -347,10 +356,12 @@ def main():
         if k in head:
             res[k] = head[k]
     parity = {}
+    mode_lists = {}
     if world == 1:
         modes = {}
         for p in [x for x in a.compare.split(",") if x and x != a.precision]:
             m, lists = measure(p)
+            mode_lists[p] = lists
             keep, boxes = agreement(lists, head_lists)
             parity[f"{p}_vs_{a.precision}"] = {"keep_lists": keep, "int_boxes": boxes, "frames": len(lists)}
             m["parity_vs_" + a.precision] = parity[f"{p}_vs_{a.precision}"]
@@ -364,9 +375,10 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         base, ref = cpu_baseline(host[:64], sd, a.cpu_baseline_seconds)
         res["cpu_baseline"] = base
-        if a.precision == "fp32":
-            keep, boxes = agreement(head_lists, ref)
-            parity["fp32_vs_oracle"] = {"keep_lists": keep, "int_boxes": boxes, "frames": len(ref)}
+        for p, lists in [(a.precision, head_lists)] + list(mode_lists.items()):
+            if p.startswith("fp32"):
+                keep, boxes = agreement(lists, ref)
+                parity[f"{p}_vs_oracle"] = {"keep_lists": keep, "int_boxes": boxes, "frames": len(ref)}
     if parity:
         parity["definition"] = ("fraction of bench frames whose complete keep lists (anchor indices in NMS "
                                 "order) / keep lists and int boxes are identical")

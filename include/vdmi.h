@@ -58,7 +58,9 @@ extern "C" {
 #define VD_DEVICE 1
 
 #define VD_PREC_BF16 0       /* bf16 operands, f32 accumulate (performance mode) */
-#define VD_PREC_FP32 1       /* f32 operands, exact-f32 MFMA (parity mode)       */
+#define VD_PREC_FP32 1       /* f32 operands and activations (parity mode): convs on
+                              * bf16 MFMA by exact 3-term operand split (6 products,
+                              * f32 accumulate; option f32_split=0: exact-f32 MFMA) */
 #define VD_PREC_FP16 2       /* fp16 operands, f32 accumulate (implicit GEMM on   *
                               * v_mfma_f32_16x16x32_f16; no bf16-only fusions)    */
 
@@ -126,7 +128,7 @@ int   vd_set_stream(vd_ctx* ctx, void* hip_stream);   /* NULL -> library-owned s
  * chain, stem_pool, ssh_fuse, plate_s2d) apply to weights loaded afterwards, the
  * rest to the next launch. Names: conv_stream conv_stream512 conv_dual conv_taps
  * conv_n192 conv_small conv_big conv_big_kmin stream_ntt lb_pair mosaic_map
- * block_fuse chain stem_pool ssh_fuse plate_s2d. VD_ERR_ARG for unknown names. */
+ * block_fuse chain stem_pool ssh_fuse plate_s2d f32_split. VD_ERR_ARG for unknown names. */
 int   vd_set_option(vd_ctx* ctx, const char* name, int value);
 void* vd_get_stream(vd_ctx* ctx);
 int   vd_sync(vd_ctx* ctx);

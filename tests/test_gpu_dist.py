@@ -17,7 +17,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-N_FRAMES, H, W, CAP = 7, 720, 1280, 64
+N_FRAMES, H, W, CAP = 7, 1080, 1920, 64
 
 
 def _free_port():

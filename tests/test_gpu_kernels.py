@@ -194,13 +194,17 @@ CONV_CASES = [
 ]
 
 
-@pytest.mark.parametrize("prec", ["fp32", "bf16", "fp16", "bf16-gemm64", "bf16-gemm128"])
+@pytest.mark.parametrize("prec", ["fp32", "fp32-exact", "bf16", "fp16", "bf16-gemm64", "bf16-gemm128"])
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv_matches_torch(gpu, face_ctx_factory, prec, case, options=None):
-    """bf16: the default dispatch (streaming 1x1 / streaming taps / phased / GEMM);
-    bf16-gemm64 / -gemm128: the implicit GEMM with 64- and 128-row tiles forced
-    through vd_set_option."""
+    """fp32: the default fp32 plan (conv_x6.hip, exact 3-term bf16 split);
+    fp32-exact: exact-f32 MFMA (option f32_split=0); bf16: the default dispatch
+    (streaming 1x1 / streaming taps / phased / GEMM); bf16-gemm64 / -gemm128: the
+    implicit GEMM with 64- and 128-row tiles forced through vd_set_option."""
     options = dict(options or {})
+    if prec == "fp32-exact":
+        options.update(f32_split=0)
+        prec = "fp32"
     if prec.startswith("bf16-gemm"):
         options.update(conv_taps=0, conv_stream=0, conv_big=0, conv_small=100000000 if prec == "bf16-gemm64" else 0)
         prec = "bf16"
@@ -232,6 +236,27 @@ def test_conv_matches_torch(gpu, face_ctx_factory, prec, case, options=None):
     err = np.abs(got - y).max() / (np.abs(y).max() + 1e-6)
     assert got.shape == y.shape
     assert err < tol, f"rel err {err}"
+
+
+@pytest.mark.parametrize("case", [(2, 20, 24, 256, 256, 3, 1, 1, 0, 0), (1, 40, 40, 512, 128, 1, 1, 0, 0, 0),
+                                  (3, 17, 23, 3, 64, 7, 2, 3, 0, 0)])
+def test_conv_fp32_split_error_matches_exact_f32(gpu, face_ctx_factory, case):
+    """The split path's error against a float64 convolution is at the level of the
+    exact-f32 MFMA path's (both ~1e-7 of max|y|): the 3-term bf16 split is fp32
+    arithmetic, not a reduced precision (conv_x6.hip)."""
+    n, h, w, cin, cout, k, s, p, _, _ = case
+    rng = np.random.default_rng(cin + cout + k)
+    x = np.maximum(rng.standard_normal((n, h, w, cin)), 0).astype(F32) * F32(3.0)
+    wt = (rng.standard_normal((cout, cin, k, k)) * np.sqrt(2.0 / (cin * k * k))).astype(F32)
+    y = torch.nn.functional.conv2d(torch.from_numpy(x).permute(0, 3, 1, 2).double(), torch.from_numpy(wt).double(),
+                                   stride=s, padding=p).permute(0, 2, 3, 1).numpy()
+    errs = {}
+    for opts in ((), (("f32_split", 0),)):
+        ctx = face_ctx_factory("fp32", 8, options=opts)
+        got = ctx.conv2d(x, wt, s, p)
+        errs[opts] = np.abs(got - y).max() / np.abs(y).max()
+    split, exact = errs[()], errs[(("f32_split", 0),)]
+    assert split < 1e-6 and split < 3 * exact + 1e-7, (split, exact)
 
 
 BIG_CASES = [

@@ -65,9 +65,9 @@ def test_frame_pipeline_matches_unpipelined_process(gpu):
     try:
         ctx.load_weights(0, weights.retinaface_state_dict(0))
         ctx.load_weights(1, weights.yolov8n_state_dict(0))
-        batches = [synth.frames(4, 540, 960, seed=40, start=4 * i) for i in range(4)] + \
-                  [synth.frames(2, 540, 960, seed=41)]
-        pipe = FramePipeline(ctx, 540, 960, max_batch=4, mosaic_plates=True)
+        batches = [synth.frames(4, 1080, 1920, seed=40, start=4 * i) for i in range(3)] + \
+                  [synth.frames(2, 1080, 1920, seed=41)]
+        pipe = FramePipeline(ctx, 1080, 1920, max_batch=4, mosaic_plates=True)
         got = [(o.copy(), fc.copy(), [b.copy() for b in fb], pc.copy(), [b.copy() for b in pb])
                for o, fc, fb, pc, pb in pipe.run(iter(batches))]
         pipe.close()

@@ -405,6 +405,7 @@ hipError_t vd_launch_conv(const ConvArgs& a0, bool f32, hipStream_t s) {
         return launch_bn<_Float16, 128, 128>(a, dense, s);
     }
     if (f32) {
+        if (vd_conv_x6_ok(a)) return vd_launch_conv_x6(a, s);
         if (a.cout <= 32) return launch_bn<float, 128, 32>(a, dense, s);
         if (a.cout <= 64) return launch_bn<float, 128, 64>(a, dense, s);
         return launch_bn<float, 128, 128>(a, dense, s);

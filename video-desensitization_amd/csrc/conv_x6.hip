@@ -1,0 +1,345 @@
+// conv_x6.hip — fp32 convolution on the bf16 matrix cores by exact operand
+// decomposition (VD_PREC_FP32 with option f32_split = 1, the default).
+//
+// Every f32 operand is split EXACTLY into three bf16 terms, x = x0 + x1 + x2
+// (x0 = the top 8 significand bits, x1 the next 8, x2 the last 8: each residual
+// is exact in f32 and fits the next term), and the product is the sum of the six
+// cross terms with i + j <= 2:
+//     a*b ~= a0 b0 + a0 b1 + a1 b0 + a0 b2 + a1 b1 + a2 b0
+// Each term is an exact 16-bit product accumulated in f32 by
+// v_mfma_f32_16x16x32_bf16; the dropped terms (a1 b2, a2 b1, a2 b2) are below
+// 2^-22 |ab|, so a K-long dot product carries the same error as an f32 fma chain
+// (measured in tests/test_gpu_kernels.py against float64: error at the level of
+// the exact-f32 MFMA path). Six bf16 MFMAs (96 cycles per 16x16x32 block) replace
+// eight exact-f32 v_mfma_f32_16x16x4_f32 (256 cycles): 2.67x the f32 MFMA rate.
+//
+// Same conv contract as conv.hip (NHWC f32 activations, K = (kh, kw, c) with c
+// fastest, fused BN scale/shift + residual + activation, channel-sliced
+// in/out); replaces the same reference layers (retinaface.py:71-92 via
+// torchvision resnet50 [ext], layers.py:10-114, the YOLOv8n convs).
+//
+// Schedule: 256 x 128 tile (M pixels x N channels), 8 waves (4 x 2, each a
+// 64 x 64 wave tile of 16 MFMA blocks), K tile 32, two LDS stages of
+// {A planes 3 x 256 x 64 B, B planes 3 x 128 x 64 B} = 72 KB each.
+//   * A (f32 pixels): global -> registers (two 16-B loads per 8 k), split by
+//     bit masking + exact f32 subtraction, written as three 16-B bf16 chunks;
+//     loads for tile t+2 are issued while tile t computes.
+//   * B (weights): split once at weight load into [Npad][Kpad/32][3 planes][32]
+//     bf16; LDS-DMA straight into the stage (source-side swizzle).
+//   * 64-B LDS rows, chunk' = chunk ^ (((row >> 3) & 1) * 3): conflict-free
+//     ds_read_b128 fragment reads for the 16-row MFMA operand pattern.
+#include "vd_common.h"
+#include <algorithm>
+#include <cstring>
+
+namespace {
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+constexpr int BM = 256, BN = 128, NT = 512;
+constexpr int KT = 32;                          // K per tile (one bf16 MFMA k-step)
+constexpr int PL_A = BM * 64, PL_B = BN * 64;   // bytes per plane
+constexpr int STAGE = 3 * PL_A + 3 * PL_B;      // 73 728 B
+constexpr int LDS_BYTES = 2 * STAGE;            // 147 456 B
+constexpr int EPLD = BN + 4;                    // f32 epilogue row stride
+
+__device__ __forceinline__ int swz(int row, int chunk) { return row * 64 + ((chunk ^ (((row >> 3) & 1) * 3)) << 4); }
+
+__device__ __forceinline__ float act_apply(float v, int act, float slope) {
+    if (act == VD_ACT_RELU) return v > 0.f ? v : 0.f;
+    if (act == VD_ACT_LEAKY) return v > 0.f ? v : v * slope;
+    if (act == VD_ACT_SILU) return v / (1.0f + __expf(-v));
+    return v;
+}
+
+// x = hi + mid + lo exactly (truncation split: each term keeps 8 significand bits)
+__device__ __forceinline__ void split3(float x, unsigned& h, unsigned& m, unsigned& l) {
+    const unsigned u = __float_as_uint(x);
+    const float x0 = __uint_as_float(u & 0xFFFF0000u);
+    const float r1 = x - x0;                       // exact
+    const unsigned v = __float_as_uint(r1);
+    const float x1 = __uint_as_float(v & 0xFFFF0000u);
+    const float r2 = r1 - x1;                      // exact, <= 8 significand bits
+    h = u >> 16;
+    m = v >> 16;
+    l = __float_as_uint(r2) >> 16;
+}
+
+__global__ __launch_bounds__(NT) void conv_x6_kernel(ConvArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 1, wn = wid & 1;          // 4 x 2 waves, 64 x 64 each
+
+    // XCD-aware bijective remap (blocks b, b+8, ... share an XCD)
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
+    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    const int tn = wg % a.ntiles_n, tm = wg / a.ntiles_n;
+    const int m0 = tm * BM, n0 = tn * BN;
+
+    // ---- A staging: thread = (row, k-pair) items; item i: row = (tid >> 2) + 128 i, pair = tid & 3 (k 8p..8p+7)
+    const int apair = tid & 3, arow = tid >> 2;
+    const int ohw = a.yh * a.yw;
+    long pix0[2];
+    int iy0[2], ix0[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int m = m0 + arow + 128 * i;
+        if (m < a.M) {
+            const int b = m / ohw, rem = m - b * ohw;
+            const int oy = rem / a.yw, ox = rem - oy * a.yw;
+            iy0[i] = oy * a.stride - a.pad;
+            ix0[i] = ox * a.stride - a.pad;
+            pix0[i] = (((long)b * a.xh + iy0[i]) * a.xw + ix0[i]) * a.ldx + a.xcoff;
+        } else {
+            iy0[i] = -(1 << 28); ix0[i] = 0; pix0[i] = 0;
+        }
+    }
+    const long tap_dy = (long)a.xw * a.ldx;
+    const int cvec = a.cin_pad >> 2, ntap = a.kh * a.kw;   // 4-channel chunks per tap
+    const int nk = a.kpad / KT;
+    const float* xf = (const float*)a.x;
+
+    float4 ra[2][2];                                // [item][half]: 8 f32 of one row
+    auto load_a = [&](int kt) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int kv = kt * 8 + apair * 2 + h;          // 4-channel chunk index within K
+            const int tap = kv / cvec;
+            const int c = (kv - tap * cvec) * 4;
+            const bool kval = tap < ntap;
+            const int dy = tap / a.kw, dx = tap - (tap / a.kw) * a.kw;
+            const long toff = dy * tap_dy + (long)dx * a.ldx + c;
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int iy = iy0[i] + dy, ix = ix0[i] + dx;
+                const bool ok = kval && (unsigned)iy < (unsigned)a.xh && (unsigned)ix < (unsigned)a.xw;
+                const float4 v = *(const float4*)(ok ? xf + (pix0[i] + toff) : xf);
+                ra[i][h] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+    };
+    auto store_a = [&](int st) {
+        char* A = smem + st * STAGE;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const float e[8] = {ra[i][0].x, ra[i][0].y, ra[i][0].z, ra[i][0].w,
+                                ra[i][1].x, ra[i][1].y, ra[i][1].z, ra[i][1].w};
+            unsigned hv[8], mv[8], lv[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) split3(e[j], hv[j], mv[j], lv[j]);
+            const int off = swz(arow + 128 * i, apair);
+            *(u32x4*)(A + off) = u32x4{hv[0] | (hv[1] << 16), hv[2] | (hv[3] << 16), hv[4] | (hv[5] << 16),
+                                       hv[6] | (hv[7] << 16)};
+            *(u32x4*)(A + PL_A + off) = u32x4{mv[0] | (mv[1] << 16), mv[2] | (mv[3] << 16), mv[4] | (mv[5] << 16),
+                                              mv[6] | (mv[7] << 16)};
+            *(u32x4*)(A + 2 * PL_A + off) = u32x4{lv[0] | (lv[1] << 16), lv[2] | (lv[3] << 16),
+                                                  lv[4] | (lv[5] << 16), lv[6] | (lv[7] << 16)};
+        }
+    };
+
+    // ---- B: LDS-DMA, one instruction = 1 KB = 16 rows of one plane; 24 per tile, 3 per wave
+    // instruction j (0..23): plane j / 8, rows 16 * (j % 8) .. +15; lane -> row + lane / 4, slot lane & 3
+    const __amdgpu_buffer_rsrc_t rsrc_w = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7fffffff, 0x00020000);
+    auto dma_b = [&](int kt, int st) {
+        char* Bs = smem + st * STAGE + 3 * PL_A;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const int j = wid * 3 + q;
+            const int p = j >> 3, r0 = (j & 7) * 16;
+            const int row = r0 + (lane >> 2), slot = lane & 3;
+            const int chunk = slot ^ (((row >> 3) & 1) * 3);
+            const unsigned off = (unsigned)((((long)(n0 + row) * nk + kt) * 3 + p) * 64 + chunk * 16);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_w, (lds_void_t*)(Bs + p * PL_B + r0 * 64), 16, off, 0, 0, 0);
+        }
+    };
+
+    f32x4_t acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    auto compute = [&](int st) {
+        const char* A = smem + st * STAGE;
+        const char* Bs = A + 3 * PL_A;
+        const int ch = lane >> 4;
+        u32x4 bf[4][3];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) bf[j][p] = *(const u32x4*)(Bs + p * PL_B + swz(wn * 64 + j * 16 + (lane & 15), ch));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            u32x4 af[3];
+#pragma unroll
+            for (int p = 0; p < 3; ++p) af[p] = *(const u32x4*)(A + p * PL_A + swz(wm * 64 + i * 16 + (lane & 15), ch));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+#define VDX_MFMA(pa, pb)                                                                     \
+    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[pa]), \
+                                                        __builtin_bit_cast(bf16x8_t, bf[j][pb]), acc[i][j], 0, 0, 0)
+                // small terms first
+                VDX_MFMA(2, 0);
+                VDX_MFMA(1, 1);
+                VDX_MFMA(0, 2);
+                VDX_MFMA(1, 0);
+                VDX_MFMA(0, 1);
+                VDX_MFMA(0, 0);
+#undef VDX_MFMA
+            }
+        }
+    };
+
+    // ---- main loop: stage kt & 1 holds tile kt; A(kt+1) split/written during compute(kt),
+    // A(kt+2) loads and B(kt+2) DMA issued after it (vmcnt bookkeeping: 4 A loads then
+    // 3 B DMAs per thread per tile)
+    load_a(0);
+    store_a(0);
+    dma_b(0, 0);
+    if (nk > 1) {
+        load_a(1);
+        dma_b(1, 1);
+    }
+    // Raw barriers with counted waits: __syncthreads() would add vmcnt(0) and drain
+    // the prefetch. Per thread, tile kt+1's A loads (4) and B DMA (3) are the
+    // youngest VMEM ops at the top of iteration kt: vmcnt(3) retires B(kt) and A(kt+1).
+    for (int kt = 0; kt < nk; ++kt) {
+        if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this thread's A(kt) ds_writes
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        compute(kt & 1);
+        if (kt + 1 < nk) store_a((kt + 1) & 1);      // the other stage: its tile kt-1 was consumed
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();                // everyone done reading stage kt & 1
+        asm volatile("" ::: "memory");
+        if (kt + 2 < nk) {
+            load_a(kt + 2);
+            dma_b(kt + 2, kt & 1);
+        }
+    }
+    __syncthreads();
+
+    // ---- fused epilogue: 2 passes of 128 rows through LDS ([128][BN+4] f32)
+    float* ep = (float*)smem;
+    const bool vec_ok = ((a.cout & 7) == 0) && ((a.ldy & 7) == 0) && ((a.ycoff & 7) == 0) &&
+                        (a.res_mode == VD_RES_NONE || (((a.res_ld | a.res_coff) & 7) == 0));
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        if (h) __syncthreads();
+        if ((wm >> 1) == h) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        ep[((wm & 1) * 64 + i * 16 + (lane >> 4) * 4 + r) * EPLD + wn * 64 + j * 16 + (lane & 15)] =
+                            acc[i][j][r];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {                   // 128 rows x 16 groups of 8 channels / 512 threads
+            const int it = tid + NT * q;
+            const int rr = it >> 4, cg = it & 15;
+            const int m = m0 + h * 128 + rr;
+            const int nb = n0 + cg * 8;
+            if (m >= a.M || nb >= a.cout) continue;
+            const float* er = ep + rr * EPLD + cg * 8;
+            const size_t yo = (size_t)m * a.ldy + a.ycoff + nb;
+            size_t roff = 0;
+            if (a.res_mode != VD_RES_NONE) {
+                if (a.res_up) {
+                    const int b = m / ohw, rem = m - b * ohw;
+                    const int oy = rem / a.yw, ox = rem - oy * a.yw;
+                    roff = ((size_t)(b * a.rh + (oy >> 1)) * a.rw + (ox >> 1)) * a.res_ld + a.res_coff + nb;
+                } else {
+                    roff = (size_t)m * a.res_ld + a.res_coff + nb;
+                }
+            }
+            if (vec_ok) {
+                const float4 s0 = *(const float4*)(a.scale + nb), s1 = *(const float4*)(a.scale + nb + 4);
+                const float4 h0 = *(const float4*)(a.shift + nb), h1 = *(const float4*)(a.shift + nb + 4);
+                const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+                const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+                const float4 e0 = *(const float4*)er, e1 = *(const float4*)(er + 4);
+                const float ev[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+                float rv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+                if (a.res_mode != VD_RES_NONE) {
+                    const float4 r0 = *(const float4*)((const float*)a.res + roff);
+                    const float4 r1 = *(const float4*)((const float*)a.res + roff + 4);
+                    rv[0] = r0.x; rv[1] = r0.y; rv[2] = r0.z; rv[3] = r0.w;
+                    rv[4] = r1.x; rv[5] = r1.y; rv[6] = r1.z; rv[7] = r1.w;
+                }
+                float v[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    float t = ev[e] * sc[e] + sh[e];
+                    if (a.res_mode == VD_RES_PRE_ACT) t += rv[e];
+                    t = act_apply(t, a.act, a.slope);
+                    if (a.res_mode == VD_RES_POST_ACT) t += rv[e];
+                    v[e] = t;
+                }
+                *(float4*)((float*)a.y + yo) = make_float4(v[0], v[1], v[2], v[3]);
+                *(float4*)((float*)a.y + yo + 4) = make_float4(v[4], v[5], v[6], v[7]);
+            } else {
+                for (int e = 0; e < 8 && nb + e < a.cout; ++e) {
+                    const int n = nb + e;
+                    float t = er[e] * a.scale[n] + a.shift[n];
+                    const float rv = a.res_mode != VD_RES_NONE ? ((const float*)a.res)[roff + e] : 0.f;
+                    if (a.res_mode == VD_RES_PRE_ACT) t += rv;
+                    t = act_apply(t, a.act, a.slope);
+                    if (a.res_mode == VD_RES_POST_ACT) t += rv;
+                    ((float*)a.y)[yo + e] = t;
+                }
+            }
+        }
+    }
+}
+
+}  // namespace
+
+// Eligible: f32 activations with Cin padded to 4, K padded to 32, split weights present.
+bool vd_conv_x6_ok(const ConvArgs& a) {
+    return a.wx3 != nullptr && (a.kpad % KT) == 0 && (a.cin_pad % 4) == 0 && ((a.ldx | a.xcoff) & 3) == 0;
+}
+
+hipError_t vd_launch_conv_x6(const ConvArgs& a0, hipStream_t s) {
+    static const bool attr = [] {
+        (void)hipFuncSetAttribute((const void*)conv_x6_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        return true;
+    }();
+    (void)attr;
+    ConvArgs a = a0;
+    a.w = a.wx3;                                   // the kernel reads the split planes
+    a.ntiles_n = (a.cout + BN - 1) / BN;
+    const int mt = (a.M + BM - 1) / BM;
+    hipLaunchKernelGGL(conv_x6_kernel, dim3(mt * a.ntiles_n), dim3(NT), LDS_BYTES, s, a);
+    return hipGetLastError();
+}
+
+// Host: pack f32 weights [npad][kpad] (k = tap * cin_pad + c) into the split layout
+// [npad][kpad / 32][3][32] bf16 (plane 0 = top 8 significand bits; same truncation
+// split as the kernel's activations).
+static inline unsigned f2u(float f) { unsigned u; std::memcpy(&u, &f, 4); return u; }
+static inline float u2f(unsigned u) { float f; std::memcpy(&f, &u, 4); return f; }
+
+void vd_pack_x6(const float* w, int npad, int kpad, uint16_t* out) {
+    const int nk = kpad / KT;
+    for (int n = 0; n < npad; ++n)
+        for (int t = 0; t < nk; ++t)
+            for (int k = 0; k < KT; ++k) {
+                const float x = w[(size_t)n * kpad + t * KT + k];
+                const unsigned u = f2u(x);
+                const float r1 = x - u2f(u & 0xFFFF0000u);
+                const unsigned v = f2u(r1);
+                const float r2 = r1 - u2f(v & 0xFFFF0000u);
+                uint16_t* o = out + (((size_t)n * nk + t) * 3) * KT + k;
+                o[0] = (uint16_t)(u >> 16);
+                o[KT] = (uint16_t)(v >> 16);
+                o[2 * KT] = (uint16_t)(f2u(r2) >> 16);
+            }
+}

@@ -28,6 +28,7 @@ struct Conv {
     int cin = 0, cin_pad = 0, cout = 0, npad = 0, kh = 0, kw = 0, stride = 1, pad = 0, kpad = 0, act = 0;
     float slope = 0.f;
     void* w = nullptr;
+    void* wx3 = nullptr;       // fp32 + f32_split: [npad][kpad/32][3][32] bf16 planes (conv_x6.hip)
     float* scale = nullptr;
     float* shift = nullptr;
     double flops_per_px = 0;   // algorithmic FLOPs per output pixel (real Cin, no padding)

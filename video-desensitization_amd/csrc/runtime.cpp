@@ -160,6 +160,12 @@ int Ctx::upload_conv(Conv& cv, const std::vector<float>& w_oihw, const std::vect
         rc = dalloc(&cv.w, packed.size() * 4);
         if (rc) return rc;
         VD_CHECK_HIP(hipMemcpy(cv.w, packed.data(), packed.size() * 4, hipMemcpyHostToDevice));
+        if (tune.f32_split) {   // the same weights as three exact bf16 planes for conv_x6.hip
+            std::vector<uint16_t> sp(packed.size() * 3);
+            vd_pack_x6(packed.data(), cv.npad, cv.kpad, sp.data());
+            if ((rc = dalloc(&cv.wx3, sp.size() * 2))) return rc;
+            VD_CHECK_HIP(hipMemcpy(cv.wx3, sp.data(), sp.size() * 2, hipMemcpyHostToDevice));
+        }
     } else {
         std::vector<uint16_t> h(packed.size());
         for (size_t i = 0; i < packed.size(); ++i) h[i] = to_half(f16, packed[i]);
@@ -392,6 +398,7 @@ int Ctx::run_conv_op(const Op& op, int f0, int n, int fam) {
     a.act = cv.act; a.slope = cv.slope; a.out_f32 = op.y.f32 ? 1 : 0;
     a.f16 = f16 ? 1 : 0;
     a.tune = &tune;
+    a.wx3 = cv.wx3;
     double flops = cv.flops_per_px * a.M;
     if (op.conv2 >= 0) {
         const Conv& c2 = convs[op.conv2];
@@ -809,7 +816,7 @@ int vd_set_option(vd_ctx* h, const char* name, int value) {
         {"conv_big_kmin", &VdTune::conv_big_kmin}, {"stream_ntt", &VdTune::stream_ntt},
         {"lb_pair", &VdTune::lb_pair}, {"mosaic_map", &VdTune::mosaic_map}, {"block_fuse", &VdTune::block_fuse},
         {"chain", &VdTune::chain}, {"stem_pool", &VdTune::stem_pool}, {"ssh_fuse", &VdTune::ssh_fuse},
-        {"plate_s2d", &VdTune::plate_s2d},
+        {"plate_s2d", &VdTune::plate_s2d}, {"f32_split", &VdTune::f32_split},
     };
     for (const Opt& o : opts)
         if (strcmp(o.n, name) == 0) {
@@ -1238,6 +1245,7 @@ int vdt_conv2d(vd_ctx* h, const float* x, int n, int xh, int xw, int cin, const 
     a.kh = kh; a.kw = kw; a.stride = stride; a.pad = pad; a.M = n * oh * ow;
     a.act = act; a.slope = slope; a.out_f32 = 1; a.f16 = ctx->f16 ? 1 : 0;
     a.tune = &ctx->tune;
+    a.wx3 = cv.wx3;
     hipError_t e = vd_launch_conv(a, ctx->f32, ctx->stream);
     if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "conv launch: %s", hipGetErrorString(e));
     VD_CHECK_HIP(hipStreamSynchronize(ctx->stream));

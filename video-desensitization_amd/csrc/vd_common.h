@@ -35,6 +35,8 @@ struct VdTune {
     int stem_pool = 1;        // plan: stem conv + maxpool (stem.hip)
     int ssh_fuse = 1;         // plan: SSH conv3X3 + conv5X5_1 as one conv
     int plate_s2d = 1;        // plan: YOLO space-to-depth stem input
+    int f32_split = 1;        // plan (fp32): convs on bf16 MFMA by exact 3-term operand split
+                              //   (conv_x6.hip); 0: exact-f32 v_mfma_f32_16x16x4_f32 (conv.hip)
 };
 
 // Implicit-GEMM convolution parameters (device side). Activations are NHWC with
@@ -59,6 +61,7 @@ struct ConvArgs {
     const void* x2; int xh2, xw2, ldx2, xcoff2, stride2;
     const void* w2; const float* scale2; const float* shift2; int cin2_pad, kpad2;
     const VdTune* tune;                          // host-side kernel selection (never read on the device)
+    const void* wx3;                             // fp32: weights split into 3 bf16 planes (conv_x6.hip), or NULL
 };
 
 // One fused layer1 bottleneck (block.hip): x [B][H][W][cin] -> y [B][H][W][256],
@@ -180,6 +183,9 @@ bool vd_conv_taps_ok(const ConvArgs& a);
 bool vd_conv1x1_dual_ok(const ConvArgs& a);
 hipError_t vd_launch_conv_taps(const ConvArgs& a, hipStream_t s);
 hipError_t vd_launch_conv(const ConvArgs& a, bool f32, hipStream_t s);
+bool vd_conv_x6_ok(const ConvArgs& a);
+hipError_t vd_launch_conv_x6(const ConvArgs& a, hipStream_t s);
+void vd_pack_x6(const float* w, int npad, int kpad, uint16_t* out);   // host: f32 [npad][kpad] -> split planes
 bool vd_block_ok(int cin, bool ds, int h, int w);
 bool vd_stem_pool_ok(int xh, int xw, int ph, int pw);
 hipError_t vd_launch_dwconv(const DwConvArgs& a, bool f32, bool f16, hipStream_t s);
