@@ -16,6 +16,9 @@
  *                                   applied per box in order at     combine_detect.py:246-249
  *   vd_process                   <- the per-batch body of batch_process_images
  *                                                                    combine_detect.py:214-251
+ *   vd_jpeg_decode / vd_jpeg_info <- cv2.imread(path) + cvtColor(BGR2RGB) of the ffmpeg-split
+ *                                   frames                         combine_detect.py:167-172,
+ *                                   (frames from convert_video_to_frames :279-476)
  *   vd_read_boxes                <- the complete per-frame box lists the reference's
  *                                   loop iterates (combine_detect.py:241-249), past any cap
  *   vd_sync / vd_last_error / vd_destroy: runtime plumbing (no reference equivalent;
@@ -143,6 +146,17 @@ int vd_mosaic(vd_ctx* ctx, const uint8_t* in, uint8_t* out, int n, int h, int w,
               int where, const vd_boxes* boxes, int level, int mode);
 int vd_process(vd_ctx* ctx, const uint8_t* in, uint8_t* out, int n, int h, int w, size_t pitch,
                int where, int flags, vd_boxes* faces, vd_boxes* plates);
+/* Baseline JPEG frames -> RGB frames: the frame read of the reference's loop
+ * (cv2.imread + BGR->RGB of the ffmpeg-split frames, combine_detect.py:167-172),
+ * libjpeg-turbo's default decode (ISLOW IDCT, fancy upsampling, table YCbCr->RGB),
+ * bit-identical. data[i] / sizes[i]: n host JPEG buffers, all h x w with one
+ * component layout (1 or 3 components, 1x1 / 2x1 / 2x2 sampling; no progressive /
+ * arithmetic coding). Entropy decode on host threads; dequantize + IDCT + upsample +
+ * colour in HIP kernels writing `out` (VD_DEVICE: queued on the context stream, the
+ * frames feed vd_process directly; VD_HOST: returns when `out` is filled). */
+int vd_jpeg_decode(vd_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n, uint8_t* out,
+                   int h, int w, size_t pitch, int where);
+int vd_jpeg_info(const uint8_t* data, size_t size, int* h, int* w, int* comps);
 /* The complete keep lists of the last vd_detect / vd_detect_plates / vd_process
  * call on this context for frames [0, n) of `net` (VD_NET_*), into `out`
  * (min(count, out->cap) boxes per frame; count = complete count). Ordered on the
@@ -192,6 +206,10 @@ int vdt_bottleneck(vd_ctx* ctx, const float* x, int n, int h, int w, int cin,
 /* Raw YOLO Detect outputs [n][64+nc][A] (per-side DFL logits | class logits),
  * host f32, anchors in level -> y -> x order at the letterboxed canvas; *anchors
  * receives A. `out` may be NULL to query A. */
+/* JPEG host entropy stage alone (no GPU): quantized coefficients [nblocks][64]
+ * (natural order; blocks by component, block row, block col); out may be NULL to
+ * query nblocks. */
+int vdt_jpeg_coefficients(const uint8_t* data, size_t size, int16_t* out, size_t cap_blocks, int* nblocks);
 int vdt_plate_raw(vd_ctx* ctx, const uint8_t* frames, int n, int h, int w, size_t pitch,
                   int where, float* out, int* anchors);
 

@@ -242,7 +242,7 @@ def test_conv_matches_torch(gpu, face_ctx_factory, prec, case, options=None):
                                   (3, 17, 23, 3, 64, 7, 2, 3, 0, 0)])
 def test_conv_fp32_split_error_matches_exact_f32(gpu, face_ctx_factory, case):
     """The split path's error against a float64 convolution is at the level of the
-    exact-f32 MFMA path's (both ~1e-7 of max|y|): the 3-term bf16 split is fp32
+    exact-f32 MFMA path's (both ~1.6e-6 of max|y| at K = 2304): the 3-term bf16 split is fp32
     arithmetic, not a reduced precision (conv_x6.hip)."""
     n, h, w, cin, cout, k, s, p, _, _ = case
     rng = np.random.default_rng(cin + cout + k)
@@ -256,7 +256,7 @@ def test_conv_fp32_split_error_matches_exact_f32(gpu, face_ctx_factory, case):
         got = ctx.conv2d(x, wt, s, p)
         errs[opts] = np.abs(got - y).max() / np.abs(y).max()
     split, exact = errs[()], errs[(("f32_split", 0),)]
-    assert split < 1e-6 and split < 3 * exact + 1e-7, (split, exact)
+    assert split < 4e-6 and split < 2 * exact + 1e-7, (split, exact)
 
 
 BIG_CASES = [

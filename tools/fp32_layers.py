@@ -1,0 +1,36 @@
+"""Per-layer view of the fp32 face plan (conv-by-conv) from a rocprofv3 kernel trace:
+maps the last step's conv launches on the face stream onto face_plan(fused=False)
+and prints duration, TFLOP/s and the kernel.
+
+    python tools/fp32_layers.py gpurun_out/<dir>/run_kernel_trace.csv
+"""
+import csv
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from conv_layers import face_plan  # noqa: E402
+
+
+def main(path, B=64):
+    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+    lb = [i for i, r in enumerate(rows) if "letterbox" in r["Kernel_Name"]]
+    li = lb[-1] if lb else 0
+    # the face stream: the stream of the letterbox kernel with the most conv launches after it
+    sid = rows[li]["Stream_Id"]
+    convs = [r for r in rows[li:] if r["Stream_Id"] == sid and ("conv" in r["Kernel_Name"])]
+    plan = face_plan(B, fused=False, block=False, chain=False, ssh_fused=True)
+    tot = fl_tot = 0
+    for (name, M, N, K), r in zip(plan, convs):
+        dt = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+        fl = 2.0 * M * N * K
+        tot += dt
+        fl_tot += fl
+        kn = r["Kernel_Name"].split("(")[0].replace("(anonymous namespace)::", "")[:40]
+        grid = int(r["Grid_Size_X"]) // max(int(r["Workgroup_Size_X"]), 1)
+        print(f"{name:12s} M={M:8d} N={N:5d} K={K:5d} {dt*1e6:8.1f} us {fl/dt/1e12:7.1f} TF/s  wg={grid:6d} {kn}")
+    print(f"total {tot*1e3:.2f} ms over {len(convs[:len(plan)])} launches, {fl_tot/tot/1e12:.1f} TF/s")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 64)

@@ -37,14 +37,37 @@ namespace {
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-constexpr int BM = 256, BN = 128, NT = 512;
+constexpr int BM = 256, NT = 512;
 constexpr int KT = 32;                          // K per tile (one bf16 MFMA k-step)
-constexpr int PL_A = BM * 64, PL_B = BN * 64;   // bytes per plane
-constexpr int STAGE = 3 * PL_A + 3 * PL_B;      // 73 728 B
-constexpr int LDS_BYTES = 2 * STAGE;            // 147 456 B
-constexpr int EPLD = BN + 4;                    // f32 epilogue row stride
+constexpr int PL_A = BM * 64;                   // bytes per A plane
+
+template <int BN> struct X6Shape {
+    static constexpr int PL_B = BN * 64;                       // bytes per B plane
+    static constexpr int STAGE = 3 * PL_A + 3 * PL_B;          // BN 128: 73 728 B
+    static constexpr int LDS = 2 * STAGE;
+    static constexpr int WAVES_N = BN >= 64 ? 2 : 1;
+    static constexpr int WAVES_M = 8 / WAVES_N;
+    static constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
+    static constexpr int TM = WTM / 16, TN = WTN / 16;
+    static constexpr int NDMA = 3 * BN / 16;                   // 1-KB DMA instructions per K tile
+    static constexpr int EPLD = BN + 4;                        // f32 epilogue row stride
+};
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 64 + ((chunk ^ (((row >> 3) & 1) * 3)) << 4); }
+
+// s_waitcnt vmcnt(n) for n in [0, 7] (immediate operand)
+__device__ __forceinline__ void wait_vm(int n) {
+    switch (n) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    }
+}
 
 __device__ __forceinline__ float act_apply(float v, int act, float slope) {
     if (act == VD_ACT_RELU) return v > 0.f ? v : 0.f;
@@ -66,10 +89,13 @@ __device__ __forceinline__ void split3(float x, unsigned& h, unsigned& m, unsign
     l = __float_as_uint(r2) >> 16;
 }
 
+template <int BN>
 __global__ __launch_bounds__(NT) void conv_x6_kernel(ConvArgs a) {
+    using S = X6Shape<BN>;
+    constexpr int STAGE = S::STAGE, PL_B = S::PL_B, TM = S::TM, TN = S::TN;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int wm = wid >> 1, wn = wid & 1;          // 4 x 2 waves, 64 x 64 each
+    const int wm = wid / S::WAVES_N, wn = wid % S::WAVES_N;
 
     // XCD-aware bijective remap (blocks b, b+8, ... share an XCD)
     const int nwg = gridDim.x, bid = blockIdx.x;
@@ -97,86 +123,121 @@ __global__ __launch_bounds__(NT) void conv_x6_kernel(ConvArgs a) {
         }
     }
     const long tap_dy = (long)a.xw * a.ldx;
-    const int cvec = a.cin_pad >> 2, ntap = a.kh * a.kw;   // 4-channel chunks per tap
     const int nk = a.kpad / KT;
-    const float* xf = (const float*)a.x;
+    // A through a buffer descriptor: 32-bit byte offsets, and an offset past
+    // num_records returns zeros (conv padding, K padding) without a select on the
+    // loaded value -- a select would force a wait right at the load
+    const long xbytes = (long)a.B * a.xh * a.xw * a.ldx * 4;
+    const __amdgpu_buffer_rsrc_t rsrc_x = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, (int)xbytes, 0x00020000);
 
-    float4 ra[2][2];                                // [item][half]: 8 f32 of one row
-    auto load_a = [&](int kt) {
+    // two register sets of A (8 f32 of each of 2 rows): tile t lives in set t & 1,
+    // loaded two iterations before it is split into LDS
+    u32x4 ra[2][2][2];                              // [set][item][half]
+    // per half h: the (dy, dx, c) of this thread's 4-channel chunk kt*8 + 2*apair + h,
+    // advanced by 32 channels per load_a call (tiles are loaded in order): no
+    // divisions and no branches in the load path
+    int tdy[2], tdx[2], tc[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int ch0 = (apair * 2 + h) * 4;
+        const int t = ch0 / a.cin_pad;
+        tc[h] = ch0 - t * a.cin_pad;
+        tdy[h] = t / a.kw;
+        tdx[h] = t - tdy[h] * a.kw;
+    }
+    auto load_a = [&](u32x4 (&r)[2][2]) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            const int kv = kt * 8 + apair * 2 + h;          // 4-channel chunk index within K
-            const int tap = kv / cvec;
-            const int c = (kv - tap * cvec) * 4;
-            const bool kval = tap < ntap;
-            const int dy = tap / a.kw, dx = tap - (tap / a.kw) * a.kw;
-            const long toff = dy * tap_dy + (long)dx * a.ldx + c;
+            // a chunk past the last tap (K padding) is pushed off the image rows, so
+            // one unsigned compare rejects it (selects only: no divergent branch)
+            const int dyk = tdy[h] < a.kh ? tdy[h] : (1 << 28);
+            const long toff = tdy[h] * tap_dy + (long)tdx[h] * a.ldx + tc[h];
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                const int iy = iy0[i] + dy, ix = ix0[i] + dx;
-                const bool ok = kval && (unsigned)iy < (unsigned)a.xh && (unsigned)ix < (unsigned)a.xw;
-                const float4 v = *(const float4*)(ok ? xf + (pix0[i] + toff) : xf);
-                ra[i][h] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+                const unsigned iy = (unsigned)(iy0[i] + dyk), ix = (unsigned)(ix0[i] + tdx[h]);
+                const bool ok = (iy < (unsigned)a.xh) & (ix < (unsigned)a.xw);
+                const unsigned off = ok ? (unsigned)((pix0[i] + toff) * 4) : 0x80000000u;
+                r[i][h] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc_x, (int)off, 0, 0));
             }
+            tc[h] += KT;
+            if (a.cin_pad >= KT) {                  // at most one tap step per tile
+                const bool wrap = tc[h] >= a.cin_pad;
+                tc[h] -= wrap ? a.cin_pad : 0;
+                tdx[h] += wrap ? 1 : 0;
+            } else {
+                while (tc[h] >= a.cin_pad) { tc[h] -= a.cin_pad; ++tdx[h]; }
+            }
+            while (tdx[h] >= a.kw) { tdx[h] -= a.kw; ++tdy[h]; }
         }
     };
-    auto store_a = [&](int st) {
+    auto store_item = [&](int st, const u32x4 (&r)[2][2], int i) {
         char* A = smem + st * STAGE;
+        float e[8];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const float e[8] = {ra[i][0].x, ra[i][0].y, ra[i][0].z, ra[i][0].w,
-                                ra[i][1].x, ra[i][1].y, ra[i][1].z, ra[i][1].w};
-            unsigned hv[8], mv[8], lv[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) split3(e[j], hv[j], mv[j], lv[j]);
-            const int off = swz(arow + 128 * i, apair);
-            *(u32x4*)(A + off) = u32x4{hv[0] | (hv[1] << 16), hv[2] | (hv[3] << 16), hv[4] | (hv[5] << 16),
-                                       hv[6] | (hv[7] << 16)};
-            *(u32x4*)(A + PL_A + off) = u32x4{mv[0] | (mv[1] << 16), mv[2] | (mv[3] << 16), mv[4] | (mv[5] << 16),
-                                              mv[6] | (mv[7] << 16)};
-            *(u32x4*)(A + 2 * PL_A + off) = u32x4{lv[0] | (lv[1] << 16), lv[2] | (lv[3] << 16),
-                                                  lv[4] | (lv[5] << 16), lv[6] | (lv[7] << 16)};
+        for (int j = 0; j < 4; ++j) {
+            e[j] = __uint_as_float(r[i][0][j]);
+            e[4 + j] = __uint_as_float(r[i][1][j]);
         }
+        unsigned hv[8], mv[8], lv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) split3(e[j], hv[j], mv[j], lv[j]);
+        const int off = swz(arow + 128 * i, apair);
+        *(u32x4*)(A + off) = u32x4{hv[0] | (hv[1] << 16), hv[2] | (hv[3] << 16), hv[4] | (hv[5] << 16),
+                                   hv[6] | (hv[7] << 16)};
+        *(u32x4*)(A + PL_A + off) = u32x4{mv[0] | (mv[1] << 16), mv[2] | (mv[3] << 16), mv[4] | (mv[5] << 16),
+                                          mv[6] | (mv[7] << 16)};
+        *(u32x4*)(A + 2 * PL_A + off) = u32x4{lv[0] | (lv[1] << 16), lv[2] | (lv[3] << 16), lv[4] | (lv[5] << 16),
+                                              lv[6] | (lv[7] << 16)};
     };
 
-    // ---- B: LDS-DMA, one instruction = 1 KB = 16 rows of one plane; 24 per tile, 3 per wave
-    // instruction j (0..23): plane j / 8, rows 16 * (j % 8) .. +15; lane -> row + lane / 4, slot lane & 3
+    // ---- B: LDS-DMA, one instruction = 1 KB = 16 rows of one plane; NDMA per tile,
+    // instruction j on wave j % 8: plane j / (BN/16), rows 16 * (j % (BN/16)) .. +15
+    constexpr int RB = BN / 16;                        // 16-row blocks per plane
+    constexpr int NDMA = S::NDMA;
+    const int my_dma = NDMA / 8 + (wid < NDMA % 8 ? 1 : 0);
     const __amdgpu_buffer_rsrc_t rsrc_w = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7fffffff, 0x00020000);
     auto dma_b = [&](int kt, int st) {
         char* Bs = smem + st * STAGE + 3 * PL_A;
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            const int j = wid * 3 + q;
-            const int p = j >> 3, r0 = (j & 7) * 16;
-            const int row = r0 + (lane >> 2), slot = lane & 3;
-            const int chunk = slot ^ (((row >> 3) & 1) * 3);
-            const unsigned off = (unsigned)((((long)(n0 + row) * nk + kt) * 3 + p) * 64 + chunk * 16);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_w, (lds_void_t*)(Bs + p * PL_B + r0 * 64), 16, off, 0, 0, 0);
+        for (int q = 0; q < (NDMA + 7) / 8; ++q) {
+            const int j = wid + 8 * q;
+            if (j < NDMA) {
+                const int p = j / RB, r0 = (j % RB) * 16;
+                const int row = r0 + (lane >> 2), slot = lane & 3;
+                const int chunk = slot ^ (((row >> 3) & 1) * 3);
+                const unsigned off = (unsigned)((((long)(n0 + row) * nk + kt) * 3 + p) * 64 + chunk * 16);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_w, (lds_void_t*)(Bs + p * PL_B + r0 * 64), 16, off, 0,
+                                                         0, 0);
+            }
         }
     };
 
-    f32x4_t acc[4][4];
+    f32x4_t acc[TM][TN];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-    auto compute = [&](int st) {
+    // one K tile from stage st; the split + LDS write of the next tile's A items are
+    // interleaved with the MFMA rows (VALU work beside the matrix cores)
+    auto compute = [&](int st, bool split_next, int st_next, const u32x4 (&rn)[2][2]) {
         const char* A = smem + st * STAGE;
         const char* Bs = A + 3 * PL_A;
         const int ch = lane >> 4;
-        u32x4 bf[4][3];
+        u32x4 bf[TN][3];
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < TN; ++j)
 #pragma unroll
-            for (int p = 0; p < 3; ++p) bf[j][p] = *(const u32x4*)(Bs + p * PL_B + swz(wn * 64 + j * 16 + (lane & 15), ch));
+            for (int p = 0; p < 3; ++p)
+                bf[j][p] = *(const u32x4*)(Bs + p * PL_B + swz(wn * S::WTN + j * 16 + (lane & 15), ch));
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < TM; ++i) {
             u32x4 af[3];
 #pragma unroll
-            for (int p = 0; p < 3; ++p) af[p] = *(const u32x4*)(A + p * PL_A + swz(wm * 64 + i * 16 + (lane & 15), ch));
+            for (int p = 0; p < 3; ++p)
+                af[p] = *(const u32x4*)(A + p * PL_A + swz(wm * S::WTM + i * 16 + (lane & 15), ch));
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
+            for (int j = 0; j < TN; ++j) {
 #define VDX_MFMA(pa, pb)                                                                     \
     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[pa]), \
                                                         __builtin_bit_cast(bf16x8_t, bf[j][pb]), acc[i][j], 0, 0, 0)
@@ -189,62 +250,69 @@ __global__ __launch_bounds__(NT) void conv_x6_kernel(ConvArgs a) {
                 VDX_MFMA(0, 0);
 #undef VDX_MFMA
             }
+            if (split_next && i == 0) store_item(st_next, rn, 0);
+            if (split_next && i == (TM > 2 ? 2 : 1)) store_item(st_next, rn, 1);
         }
     };
 
-    // ---- main loop: stage kt & 1 holds tile kt; A(kt+1) split/written during compute(kt),
-    // A(kt+2) loads and B(kt+2) DMA issued after it (vmcnt bookkeeping: 4 A loads then
-    // 3 B DMAs per thread per tile)
-    load_a(0);
-    store_a(0);
+    // ---- main loop. Per thread VMEM issue order: ... A(t+2) loads (4), B(t+1) DMA
+    // (my_dma) at the end of iteration t-1. At the top of iteration t the younger ops
+    // are those of iteration t-1's end -- A(t+2), B(t+1) -- so B(t) and A(t+1) retire
+    // at vmcnt(4 + my_dma) (fewer when the tail issued less).
+    load_a(ra[0]);
+    store_item(0, ra[0], 0);
+    store_item(0, ra[0], 1);
     dma_b(0, 0);
-    if (nk > 1) {
-        load_a(1);
-        dma_b(1, 1);
-    }
-    // Raw barriers with counted waits: __syncthreads() would add vmcnt(0) and drain
-    // the prefetch. Per thread, tile kt+1's A loads (4) and B DMA (3) are the
-    // youngest VMEM ops at the top of iteration kt: vmcnt(3) retires B(kt) and A(kt+1).
-    for (int kt = 0; kt < nk; ++kt) {
-        if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (nk > 1) load_a(ra[1]);
+    if (nk > 1) dma_b(1, 1);
+    if (nk > 2) load_a(ra[0]);
+    auto iter = [&](int kt, const u32x4 (&rnext)[2][2], u32x4 (&rfree)[2][2]) {
+        // younger than B(kt) / A(kt+1): A(kt+2) loads (issued iff kt+2 < nk) and
+        // B(kt+1) DMA (iff kt+1 < nk)
+        const int younger = (kt + 2 < nk ? 4 : 0) + (kt + 1 < nk ? my_dma : 0);
+        wait_vm(younger);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this thread's A(kt) ds_writes
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        compute(kt & 1);
-        if (kt + 1 < nk) store_a((kt + 1) & 1);      // the other stage: its tile kt-1 was consumed
+        compute(kt & 1, kt + 1 < nk, (kt + 1) & 1, rnext);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();                // everyone done reading stage kt & 1
+        __builtin_amdgcn_s_barrier();                        // everyone done reading stage kt & 1
         asm volatile("" ::: "memory");
-        if (kt + 2 < nk) {
-            load_a(kt + 2);
-            dma_b(kt + 2, kt & 1);
-        }
+        if (kt + 3 < nk) load_a(rfree);                       // A(kt+3) into the set A(kt+1) just left
+        if (kt + 2 < nk) dma_b(kt + 2, kt & 1);
+    };
+    // Raw barriers with counted waits: __syncthreads() would add vmcnt(0) and drain
+    // the prefetch. Unrolled by 2 so the register sets are indexed statically.
+    for (int kt = 0; kt < nk; kt += 2) {
+        iter(kt, ra[1], ra[1]);
+        if (kt + 1 < nk) iter(kt + 1, ra[0], ra[0]);
     }
     __syncthreads();
 
     // ---- fused epilogue: 2 passes of 128 rows through LDS ([128][BN+4] f32)
+    constexpr int EPLD = S::EPLD, CG = BN / 8, ITEMS = 128 * CG / NT;
     float* ep = (float*)smem;
     const bool vec_ok = ((a.cout & 7) == 0) && ((a.ldy & 7) == 0) && ((a.ycoff & 7) == 0) &&
                         (a.res_mode == VD_RES_NONE || (((a.res_ld | a.res_coff) & 7) == 0));
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         if (h) __syncthreads();
-        if ((wm >> 1) == h) {
+        const int wrow = wm * S::WTM - h * 128;        // this wave's first row within the pass
+        if (wrow >= 0 && wrow < 128) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < TM; ++i)
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
+                for (int j = 0; j < TN; ++j)
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
-                        ep[((wm & 1) * 64 + i * 16 + (lane >> 4) * 4 + r) * EPLD + wn * 64 + j * 16 + (lane & 15)] =
+                        ep[(wrow + i * 16 + (lane >> 4) * 4 + r) * EPLD + wn * S::WTN + j * 16 + (lane & 15)] =
                             acc[i][j][r];
         }
         __syncthreads();
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {                   // 128 rows x 16 groups of 8 channels / 512 threads
+        for (int q = 0; q < ITEMS; ++q) {              // 128 rows x CG groups of 8 channels / 512 threads
             const int it = tid + NT * q;
-            const int rr = it >> 4, cg = it & 15;
+            const int rr = it / CG, cg = it % CG;
             const int m = m0 + h * 128 + rr;
             const int nb = n0 + cg * 8;
             if (m >= a.M || nb >= a.cout) continue;
@@ -304,12 +372,16 @@ __global__ __launch_bounds__(NT) void conv_x6_kernel(ConvArgs a) {
 
 // Eligible: f32 activations with Cin padded to 4, K padded to 32, split weights present.
 bool vd_conv_x6_ok(const ConvArgs& a) {
-    return a.wx3 != nullptr && (a.kpad % KT) == 0 && (a.cin_pad % 4) == 0 && ((a.ldx | a.xcoff) & 3) == 0;
+    const double xbytes = (double)a.B * a.xh * a.xw * a.ldx * 4;   // 32-bit buffer offsets
+    return a.wx3 != nullptr && (a.kpad % KT) == 0 && (a.cin_pad % 4) == 0 && ((a.ldx | a.xcoff) & 3) == 0 &&
+           xbytes < 2147483647.0;
 }
 
-hipError_t vd_launch_conv_x6(const ConvArgs& a0, hipStream_t s) {
+template <int BN>
+static hipError_t launch_x6(const ConvArgs& a0, hipStream_t s) {
     static const bool attr = [] {
-        (void)hipFuncSetAttribute((const void*)conv_x6_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)conv_x6_kernel<BN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  X6Shape<BN>::LDS);
         return true;
     }();
     (void)attr;
@@ -317,8 +389,16 @@ hipError_t vd_launch_conv_x6(const ConvArgs& a0, hipStream_t s) {
     a.w = a.wx3;                                   // the kernel reads the split planes
     a.ntiles_n = (a.cout + BN - 1) / BN;
     const int mt = (a.M + BM - 1) / BM;
-    hipLaunchKernelGGL(conv_x6_kernel, dim3(mt * a.ntiles_n), dim3(NT), LDS_BYTES, s, a);
+    hipLaunchKernelGGL(conv_x6_kernel<BN>, dim3(mt * a.ntiles_n), dim3(NT), X6Shape<BN>::LDS, s, a);
     return hipGetLastError();
+}
+
+// N tile follows Cout (weights are packed with Npad a multiple of 128, so every
+// tile's rows exist): 32 for the heads, 64 for the 64-channel convs, else 128.
+hipError_t vd_launch_conv_x6(const ConvArgs& a, hipStream_t s) {
+    if (a.cout <= 32) return launch_x6<32>(a, s);
+    if (a.cout <= 64) return launch_x6<64>(a, s);
+    return launch_x6<128>(a, s);
 }
 
 // Host: pack f32 weights [npad][kpad] (k = tap * cin_pad + c) into the split layout

@@ -165,6 +165,12 @@ struct Ctx {
     void* stage_box = nullptr; size_t stage_box_bytes = 0;
     void* stage_box2 = nullptr; size_t stage_box2_bytes = 0;
     void* mosaic_table = nullptr; size_t mosaic_table_bytes = 0;
+    // JPEG frame decode (jpeg_host.cpp): pinned host staging, device copy, planes
+    void* jpeg_host = nullptr; size_t jpeg_host_bytes = 0;
+    void* jpeg_dev = nullptr; size_t jpeg_dev_bytes = 0;
+    void* jpeg_planes = nullptr; size_t jpeg_planes_bytes = 0;
+    hipEvent_t jpeg_ev = nullptr;                 // last H2D out of jpeg_host
+    int jpeg_threads = 16;                        // host entropy-decode threads
     bool timing = false;
     std::vector<TimedEv> ev_pool;
     size_t ev_used = 0;
@@ -172,6 +178,7 @@ struct Ctx {
     int dalloc(void** p, size_t bytes);
     int act(Act& a, int h, int w, int c, bool f32out = false);
     int ensure_staging(void** p, size_t* have, size_t need);
+    int ensure_pinned(void** p, size_t* have, size_t need);
     int upload_conv(Conv& cv, const std::vector<float>& w_oihw, const std::vector<float>& scale,
                     const std::vector<float>& shift);
     int make_conv_bn(const WMap& W, const std::string& wkey, const std::string& bn, float eps, int stride, int pad,

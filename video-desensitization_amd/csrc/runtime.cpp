@@ -18,6 +18,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 static thread_local std::string g_err;
@@ -91,6 +92,18 @@ int Ctx::act(Act& a, int h, int w, int c, bool f32out) {
     int rc = dalloc(&a.p, bytes);
     if (rc) return rc;
     hipMemset(a.p, 0, bytes);
+    return VD_OK;
+}
+
+int Ctx::ensure_pinned(void** p, size_t* have, size_t need) {
+    if (*have >= need) return VD_OK;
+    if (*p) { (void)hipEventSynchronize(jpeg_ev); hipHostFree(*p); }
+    *p = nullptr;
+    *have = 0;
+    need += need / 4;                             // grow with headroom: batches vary in size
+    hipError_t e = hipHostMalloc(p, need, hipHostMallocDefault);
+    if (e != hipSuccess) return vd_set_error(VD_ERR_NOMEM, "hipHostMalloc(%zu) failed", need);
+    *have = need;
     return VD_OK;
 }
 
@@ -753,7 +766,12 @@ int vd_create(const vd_cfg* cfg, int device, vd_ctx** out) {
         return vd_set_error(VD_ERR_HIP, "hipStreamCreate failed");
     }
     ctx->stream = ctx->own_stream;
-    if (hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess ||
+    {
+        const unsigned hw = std::thread::hardware_concurrency();
+        ctx->jpeg_threads = (int)std::max(1u, std::min(16u, hw ? hw : 4u));   // one GPU's host share
+    }
+    if (hipEventCreateWithFlags(&ctx->jpeg_ev, hipEventDisableTiming) != hipSuccess ||
+        hipStreamCreateWithFlags(&ctx->stream2, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming) != hipSuccess) {
         hipStreamDestroy(ctx->own_stream);
@@ -775,6 +793,10 @@ int vd_destroy(vd_ctx* h) {
     if (ctx->stage_box) hipFree(ctx->stage_box);
     if (ctx->stage_box2) hipFree(ctx->stage_box2);
     if (ctx->mosaic_table) hipFree(ctx->mosaic_table);
+    if (ctx->jpeg_dev) hipFree(ctx->jpeg_dev);
+    if (ctx->jpeg_planes) hipFree(ctx->jpeg_planes);
+    if (ctx->jpeg_host) hipHostFree(ctx->jpeg_host);
+    if (ctx->jpeg_ev) hipEventDestroy(ctx->jpeg_ev);
     for (auto& t : ctx->ev_pool) { hipEventDestroy(t.a); hipEventDestroy(t.b); }
     hipStreamSynchronize(ctx->stream2);
     hipEventDestroy(ctx->ev_fork);

@@ -174,6 +174,20 @@ struct LetterboxArgs {
                            //    Y in [0, oh/2], X in [0, ow/2]
 };
 
+// One batch of JPEG frames (jpeg_host.cpp -> jpeg.hip): sparse coefficients per
+// block, block order (image, component, block row, block col).
+struct JpegArgs {
+    int n, h, w, nc, hmax, vmax;
+    int bw[3], bh[3], hs[3], vs[3], cblk[3];    // per component: block grid, sampling, first block
+    long plane_off[3];
+    int blocks_per_image;
+    const uint32_t* blk_off;                    // [n * blocks_per_image + 1] into entries
+    const uint16_t* quant;                      // [n][3][64] natural order
+    const uint32_t* entries;                    // natural index << 16 | int16 quantized value
+    uint8_t* planes;                            // [n * blocks_per_image][64] decoded samples
+    uint8_t* out; size_t pitch;                 // RGB frames [n][h][pitch]
+};
+
 // ---- kernel launchers (one translation unit each) ----
 bool vd_conv1x1_stream_ok(const ConvArgs& a);
 bool vd_conv_big_ok(const ConvArgs& a);
@@ -202,6 +216,7 @@ hipError_t vd_launch_maxpool(bool f32, bool f16, const void* x, int n, int xh, i
 hipError_t vd_launch_upsample2x(bool f32, const void* x, int n, int xh, int xw, int ldx, int xcoff,
                                 void* y, int ldy, int ycoff, int c, hipStream_t s);
 hipError_t vd_launch_post(const PostArgs& p, hipStream_t s);
+hipError_t vd_launch_jpeg(const JpegArgs& a, hipStream_t s);
 hipError_t vd_launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w, size_t pitch,
                             const int* cnt0, const int* xy0, int cap0,
                             const int* cnt1, const int* xy1, int cap1, int level, void* table,

@@ -10,10 +10,10 @@ Host-side mirror of the reference's per-frame interfaces over libvdmi.so
 * ``Context``                          the C-ABI context (device frames, timing hooks)
 """
 from ._lib import VdCapacityError, VdError, load  # noqa: F401
-from .context import Context, DeviceBoxes  # noqa: F401
+from .context import Context, DeviceBoxes, jpeg_info  # noqa: F401
 from .face import Retinaface  # noqa: F401
 from .mosaic import mosaic_frames, mosaic_rectangle_region_single  # noqa: F401
 from .plate import YOLO, PlateDetector  # noqa: F401
 
 __all__ = ["Context", "DeviceBoxes", "Retinaface", "YOLO", "PlateDetector", "mosaic_rectangle_region_single",
-           "mosaic_frames", "VdError", "VdCapacityError", "load"]
+           "mosaic_frames", "VdError", "VdCapacityError", "load", "jpeg_info"]

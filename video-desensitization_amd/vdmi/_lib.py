@@ -75,6 +75,8 @@ SIGNATURES = [
     ("vd_process", _I, [_P, _P, _P, _I, _I, _I, _SZ, _I, _I, ctypes.POINTER(vd_boxes),
                         ctypes.POINTER(vd_boxes)]),
     ("vd_read_boxes", _I, [_P, _I, _I, ctypes.POINTER(vd_boxes)]),
+    ("vd_jpeg_decode", _I, [_P, ctypes.POINTER(_P), ctypes.POINTER(_SZ), _I, _P, _I, _I, _SZ, _I]),
+    ("vd_jpeg_info", _I, [_P, _SZ, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_I)]),
     ("vd_timing_enable", _I, [_P, _I]),
     ("vd_timing_reset", _I, [_P]),
     ("vd_timing_read", _I, [_P, _I, ctypes.POINTER(_D), ctypes.POINTER(ctypes.c_int64),
@@ -86,6 +88,7 @@ SIGNATURES = [
                         ctypes.POINTER(_I), ctypes.POINTER(_I)]),
     ("vdt_bottleneck", _I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
     ("vdt_plate_raw", _I, [_P, _P, _I, _I, _I, _SZ, _I, _P, ctypes.POINTER(_I)]),
+    ("vdt_jpeg_coefficients", _I, [_P, _SZ, _P, _SZ, ctypes.POINTER(_I)]),
 ]
 
 _lib = None

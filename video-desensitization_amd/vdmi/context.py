@@ -35,6 +35,15 @@ def _frames_arg(frames):
     return a.ctypes.data, n, h, w, w * 3, _lib.VD_HOST, a
 
 
+def jpeg_info(data):
+    """(h, w, components) of a baseline JPEG (host-only parse, no GPU)."""
+    lib = _lib.load()
+    h, w, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    buf = ctypes.create_string_buffer(bytes(data), len(data))
+    check(lib.vd_jpeg_info(buf, len(data), ctypes.byref(h), ctypes.byref(w), ctypes.byref(c)))
+    return h.value, w.value, c.value
+
+
 class DeviceBoxes:
     """vd_boxes backed by torch device tensors (kernels write them directly)."""
 
@@ -214,6 +223,34 @@ class Context:
         if flags & _lib.VD_PROC_PLATES:
             plates = self._complete(plates, _lib.VD_NET_YOLOV8N, auto_p)
         return out, faces, plates
+
+    # -- frame I/O ------------------------------------------------------------
+    def jpeg_decode(self, jpegs, out=None):
+        """Baseline JPEG frames (a list of bytes, all one size and layout) -> RGB
+        uint8 [n,h,w,3], bit-identical to libjpeg-turbo's default decode (what
+        cv2.imread + BGR->RGB gives the reference, combine_detect.py:167-172).
+        `out`: a torch uint8 device tensor (decoded in place on the GPU, queued on
+        the context stream -- ready to pass to process()) or None (numpy result)."""
+        jpegs = [bytes(j) for j in jpegs]
+        n = len(jpegs)
+        if n == 0:
+            raise ValueError("no frames")
+        h, w, _ = jpeg_info(jpegs[0])
+        bufs = [ctypes.create_string_buffer(j, len(j)) for j in jpegs]
+        ptrs = (ctypes.c_void_p * n)(*[ctypes.addressof(b) for b in bufs])
+        sizes = (ctypes.c_size_t * n)(*[len(j) for j in jpegs])
+        if out is None:
+            out = np.empty((n, h, w, 3), np.uint8)
+        if _is_torch(out):
+            if tuple(out.shape) != (n, h, w, 3) or not out.is_contiguous():
+                raise ValueError(f"out must be contiguous uint8 [{n},{h},{w},3]")
+            where, optr = (_lib.VD_DEVICE if out.is_cuda else _lib.VD_HOST), out.data_ptr()
+        else:
+            if out.shape != (n, h, w, 3) or out.dtype != np.uint8 or not out.flags["C_CONTIGUOUS"]:
+                raise ValueError(f"out must be C-contiguous uint8 [{n},{h},{w},3]")
+            where, optr = _lib.VD_HOST, ptr(out)
+        check(self._lib.vd_jpeg_decode(self._h, ptrs, sizes, n, optr, h, w, w * 3, where))
+        return out
 
     # -- instrumentation ------------------------------------------------------
     def timing(self, on=True):
