@@ -37,20 +37,27 @@ namespace {
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-constexpr int BM = 256, NT = 512;
 constexpr int KT = 32;                          // K per tile (one bf16 MFMA k-step)
-constexpr int PL_A = BM * 64;                   // bytes per A plane
 
-template <int BN> struct X6Shape {
+// Two forms: the big tile (256 x BN, 8 waves, two LDS stages, one workgroup per CU)
+// for the compute-heavy layers, and the small tile (128 x BN, 4 waves, ONE stage,
+// three workgroups per CU) for small-K / small-M layers, where a workgroup's
+// load -> compute -> epilogue phases are short and neighbours on the CU overlap them.
+template <int BM_, int BN, int NT_, int NST> struct X6Shape {
+    static constexpr int BM = BM_, NT = NT_, WAVES = NT / 64;
+    static constexpr int PL_A = BM * 64;                       // bytes per A plane
     static constexpr int PL_B = BN * 64;                       // bytes per B plane
-    static constexpr int STAGE = 3 * PL_A + 3 * PL_B;          // BN 128: 73 728 B
-    static constexpr int LDS = 2 * STAGE;
+    static constexpr int STAGE = 3 * PL_A + 3 * PL_B;          // 256 x 128: 73 728 B
+    static constexpr int EPR = NST == 2 ? 128 : 64;            // epilogue rows per pass
+    static constexpr int EPLD = BN + 4;                        // f32 epilogue row stride
+    static constexpr int LDS = NST * STAGE > EPR * EPLD * 4 ? NST * STAGE : EPR * EPLD * 4;
     static constexpr int WAVES_N = BN >= 64 ? 2 : 1;
-    static constexpr int WAVES_M = 8 / WAVES_N;
+    static constexpr int WAVES_M = WAVES / WAVES_N;
     static constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
     static constexpr int TM = WTM / 16, TN = WTN / 16;
     static constexpr int NDMA = 3 * BN / 16;                   // 1-KB DMA instructions per K tile
-    static constexpr int EPLD = BN + 4;                        // f32 epilogue row stride
+    static constexpr int AROWS = NT / 4;                       // A rows per staging pass (2 passes)
+    static_assert(BM == 2 * AROWS, "two A items per thread");
 };
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 64 + ((chunk ^ (((row >> 3) & 1) * 3)) << 4); }
@@ -89,10 +96,11 @@ __device__ __forceinline__ void split3(float x, unsigned& h, unsigned& m, unsign
     l = __float_as_uint(r2) >> 16;
 }
 
-template <int BN>
+template <int BM, int BN, int NT, int NST>
 __global__ __launch_bounds__(NT) void conv_x6_kernel(ConvArgs a) {
-    using S = X6Shape<BN>;
-    constexpr int STAGE = S::STAGE, PL_B = S::PL_B, TM = S::TM, TN = S::TN;
+    using S = X6Shape<BM, BN, NT, NST>;
+    constexpr int STAGE = S::STAGE, PL_A = S::PL_A, PL_B = S::PL_B, TM = S::TM, TN = S::TN, WAVES = S::WAVES;
+    constexpr int AROWS = S::AROWS;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid / S::WAVES_N, wn = wid % S::WAVES_N;
@@ -104,14 +112,14 @@ __global__ __launch_bounds__(NT) void conv_x6_kernel(ConvArgs a) {
     const int tn = wg % a.ntiles_n, tm = wg / a.ntiles_n;
     const int m0 = tm * BM, n0 = tn * BN;
 
-    // ---- A staging: thread = (row, k-pair) items; item i: row = (tid >> 2) + 128 i, pair = tid & 3 (k 8p..8p+7)
+    // ---- A staging: thread = (row, k-pair) items; item i: row = (tid >> 2) + AROWS i, pair = tid & 3 (k 8p..8p+7)
     const int apair = tid & 3, arow = tid >> 2;
     const int ohw = a.yh * a.yw;
     long pix0[2];
     int iy0[2], ix0[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-        const int m = m0 + arow + 128 * i;
+        const int m = m0 + arow + AROWS * i;
         if (m < a.M) {
             const int b = m / ohw, rem = m - b * ohw;
             const int oy = rem / a.yw, ox = rem - oy * a.yw;
@@ -181,7 +189,7 @@ __global__ __launch_bounds__(NT) void conv_x6_kernel(ConvArgs a) {
         unsigned hv[8], mv[8], lv[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) split3(e[j], hv[j], mv[j], lv[j]);
-        const int off = swz(arow + 128 * i, apair);
+        const int off = swz(arow + AROWS * i, apair);
         *(u32x4*)(A + off) = u32x4{hv[0] | (hv[1] << 16), hv[2] | (hv[3] << 16), hv[4] | (hv[5] << 16),
                                    hv[6] | (hv[7] << 16)};
         *(u32x4*)(A + PL_A + off) = u32x4{mv[0] | (mv[1] << 16), mv[2] | (mv[3] << 16), mv[4] | (mv[5] << 16),
@@ -191,16 +199,16 @@ __global__ __launch_bounds__(NT) void conv_x6_kernel(ConvArgs a) {
     };
 
     // ---- B: LDS-DMA, one instruction = 1 KB = 16 rows of one plane; NDMA per tile,
-    // instruction j on wave j % 8: plane j / (BN/16), rows 16 * (j % (BN/16)) .. +15
+    // instruction j on wave j % WAVES: plane j / (BN/16), rows 16 * (j % (BN/16)) .. +15
     constexpr int RB = BN / 16;                        // 16-row blocks per plane
     constexpr int NDMA = S::NDMA;
-    const int my_dma = NDMA / 8 + (wid < NDMA % 8 ? 1 : 0);
+    const int my_dma = NDMA / WAVES + (wid < NDMA % WAVES ? 1 : 0);
     const __amdgpu_buffer_rsrc_t rsrc_w = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7fffffff, 0x00020000);
     auto dma_b = [&](int kt, int st) {
         char* Bs = smem + st * STAGE + 3 * PL_A;
 #pragma unroll
-        for (int q = 0; q < (NDMA + 7) / 8; ++q) {
-            const int j = wid + 8 * q;
+        for (int q = 0; q < (NDMA + WAVES - 1) / WAVES; ++q) {
+            const int j = wid + WAVES * q;
             if (j < NDMA) {
                 const int p = j / RB, r0 = (j % RB) * 16;
                 const int row = r0 + (lane >> 2), slot = lane & 3;
@@ -255,6 +263,7 @@ __global__ __launch_bounds__(NT) void conv_x6_kernel(ConvArgs a) {
         }
     };
 
+    if constexpr (NST == 2) {
     // ---- main loop. Per thread VMEM issue order: ... A(t+2) loads (4), B(t+1) DMA
     // (my_dma) at the end of iteration t-1. At the top of iteration t the younger ops
     // are those of iteration t-1's end -- A(t+2), B(t+1) -- so B(t) and A(t+1) retire
@@ -287,18 +296,42 @@ __global__ __launch_bounds__(NT) void conv_x6_kernel(ConvArgs a) {
         iter(kt, ra[1], ra[1]);
         if (kt + 1 < nk) iter(kt + 1, ra[0], ra[0]);
     }
+    } else {
+    // ---- one LDS stage: per tile, B(kt) DMA and the split A(kt) write, then
+    // compute; A(kt+1)'s loads run under it (registers), B waits for the stage
+    load_a(ra[0]);
+    auto iter1 = [&](int kt, const u32x4 (&rcur)[2][2], u32x4 (&rnext)[2][2]) {
+        dma_b(kt, 0);
+        store_item(0, rcur, 0);                               // compiler waits for A(kt)'s loads
+        store_item(0, rcur, 1);
+        if (kt + 1 < nk) load_a(rnext);
+        wait_vm(kt + 1 < nk ? 4 : 0);                         // B(kt) landed (older than A(kt+1))
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        compute(0, false, 0, rcur);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();                        // the stage is free again
+        asm volatile("" ::: "memory");
+    };
+    for (int kt = 0; kt < nk; kt += 2) {
+        iter1(kt, ra[0], ra[1]);
+        if (kt + 1 < nk) iter1(kt + 1, ra[1], ra[0]);
+    }
+    }
     __syncthreads();
 
-    // ---- fused epilogue: 2 passes of 128 rows through LDS ([128][BN+4] f32)
-    constexpr int EPLD = S::EPLD, CG = BN / 8, ITEMS = 128 * CG / NT;
+    // ---- fused epilogue: BM / EPR passes of EPR rows through LDS ([EPR][BN+4] f32)
+    constexpr int EPLD = S::EPLD, EPR = S::EPR, CG = BN / 8, ITEMS = EPR * CG / NT;
+    static_assert(ITEMS >= 1 && (EPR * CG) % NT == 0, "epilogue items");
     float* ep = (float*)smem;
     const bool vec_ok = ((a.cout & 7) == 0) && ((a.ldy & 7) == 0) && ((a.ycoff & 7) == 0) &&
                         (a.res_mode == VD_RES_NONE || (((a.res_ld | a.res_coff) & 7) == 0));
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < BM / EPR; ++h) {
         if (h) __syncthreads();
-        const int wrow = wm * S::WTM - h * 128;        // this wave's first row within the pass
-        if (wrow >= 0 && wrow < 128) {
+        const int wrow = wm * S::WTM - h * EPR;        // this wave's first row within the pass
+        if (wrow >= 0 && wrow < EPR) {
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -310,10 +343,10 @@ __global__ __launch_bounds__(NT) void conv_x6_kernel(ConvArgs a) {
         }
         __syncthreads();
 #pragma unroll
-        for (int q = 0; q < ITEMS; ++q) {              // 128 rows x CG groups of 8 channels / 512 threads
+        for (int q = 0; q < ITEMS; ++q) {              // EPR rows x CG groups of 8 channels / NT threads
             const int it = tid + NT * q;
             const int rr = it / CG, cg = it % CG;
-            const int m = m0 + h * 128 + rr;
+            const int m = m0 + h * EPR + rr;
             const int nb = n0 + cg * 8;
             if (m >= a.M || nb >= a.cout) continue;
             const float* er = ep + rr * EPLD + cg * 8;
@@ -377,11 +410,12 @@ bool vd_conv_x6_ok(const ConvArgs& a) {
            xbytes < 2147483647.0;
 }
 
-template <int BN>
+template <int BM, int BN, int NT, int NST>
 static hipError_t launch_x6(const ConvArgs& a0, hipStream_t s) {
+    using S = X6Shape<BM, BN, NT, NST>;
     static const bool attr = [] {
-        (void)hipFuncSetAttribute((const void*)conv_x6_kernel<BN>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  X6Shape<BN>::LDS);
+        (void)hipFuncSetAttribute((const void*)conv_x6_kernel<BM, BN, NT, NST>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS);
         return true;
     }();
     (void)attr;
@@ -389,16 +423,30 @@ static hipError_t launch_x6(const ConvArgs& a0, hipStream_t s) {
     a.w = a.wx3;                                   // the kernel reads the split planes
     a.ntiles_n = (a.cout + BN - 1) / BN;
     const int mt = (a.M + BM - 1) / BM;
-    hipLaunchKernelGGL(conv_x6_kernel<BN>, dim3(mt * a.ntiles_n), dim3(NT), X6Shape<BN>::LDS, s, a);
+    hipLaunchKernelGGL((conv_x6_kernel<BM, BN, NT, NST>), dim3(mt * a.ntiles_n), dim3(NT), S::LDS, s, a);
     return hipGetLastError();
 }
 
 // N tile follows Cout (weights are packed with Npad a multiple of 128, so every
 // tile's rows exist): 32 for the heads, 64 for the 64-channel convs, else 128.
+// The small single-stage tile takes the narrow (N <= 64) layers with K <= 256 or
+// a grid of fewer than 512 big tiles (measured: stem 2.16 -> 1.87 ms, layer1 conv1
+// 640 -> 580 us, SSH level 1/2 and heads 15-25 % faster); at N = 128 it measured
+// 30-45 % slower than the big tile (one wave per SIMD at 198 VGPRs) and is not used.
 hipError_t vd_launch_conv_x6(const ConvArgs& a, hipStream_t s) {
-    if (a.cout <= 32) return launch_x6<32>(a, s);
-    if (a.cout <= 64) return launch_x6<64>(a, s);
-    return launch_x6<128>(a, s);
+    const int bn = a.cout <= 32 ? 32 : (a.cout <= 64 ? 64 : 128);
+    const long big_tiles = (long)((a.M + 255) / 256) * ((a.cout + bn - 1) / bn);
+    const int small_k = a.tune ? a.tune->x6_small_k : 256, small_tiles = a.tune ? a.tune->x6_small_tiles : 512;
+    const bool force_small = small_k >= (1 << 30);       // test hook: every layer on the small tile
+    const bool small = force_small || (bn <= 64 && (a.kpad <= small_k || big_tiles < small_tiles));
+    if (small) {
+        if (bn == 32) return launch_x6<128, 32, 256, 1>(a, s);
+        if (bn == 64) return launch_x6<128, 64, 256, 1>(a, s);
+        return launch_x6<128, 128, 256, 1>(a, s);
+    }
+    if (bn == 32) return launch_x6<256, 32, 512, 2>(a, s);
+    if (bn == 64) return launch_x6<256, 64, 512, 2>(a, s);
+    return launch_x6<256, 128, 512, 2>(a, s);
 }
 
 // Host: pack f32 weights [npad][kpad] (k = tap * cin_pad + c) into the split layout

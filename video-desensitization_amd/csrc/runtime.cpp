@@ -839,6 +839,7 @@ int vd_set_option(vd_ctx* h, const char* name, int value) {
         {"lb_pair", &VdTune::lb_pair}, {"mosaic_map", &VdTune::mosaic_map}, {"block_fuse", &VdTune::block_fuse},
         {"chain", &VdTune::chain}, {"stem_pool", &VdTune::stem_pool}, {"ssh_fuse", &VdTune::ssh_fuse},
         {"plate_s2d", &VdTune::plate_s2d}, {"f32_split", &VdTune::f32_split},
+        {"x6_small_k", &VdTune::x6_small_k}, {"x6_small_tiles", &VdTune::x6_small_tiles},
     };
     for (const Opt& o : opts)
         if (strcmp(o.n, name) == 0) {
