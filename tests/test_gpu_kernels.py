@@ -198,8 +198,9 @@ CONV_CASES = [
                                   "bf16-gemm128"])
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv_matches_torch(gpu, face_ctx_factory, prec, case, options=None):
-    """fp32: the default fp32 plan (conv_x6.hip, exact 3-term bf16 split; -big / -small
-    force its 256-row two-stage / 128-row one-stage tile);
+    """fp32: the default fp32 plan (conv_x6.hip, exact 3-term bf16 split: streaming 1x1
+    for K in {64,128,256}, else the tiled GEMM; -big / -small force its 256-row
+    two-stage / 128-row one-stage tile);
     fp32-exact: exact-f32 MFMA (option f32_split=0); bf16: the default dispatch
     (streaming 1x1 / streaming taps / phased / GEMM); bf16-gemm64 / -gemm128: the
     implicit GEMM with 64- and 128-row tiles forced through vd_set_option."""
@@ -208,8 +209,8 @@ def test_conv_matches_torch(gpu, face_ctx_factory, prec, case, options=None):
         options.update(f32_split=0)
         prec = "fp32"
     if prec in ("fp32-big", "fp32-small"):    # force one x6 tile form (conv_x6.hip)
-        options.update(x6_small_k=0, x6_small_tiles=0) if prec == "fp32-big" else \
-            options.update(x6_small_k=1 << 30)
+        options.update(x6_small_k=0, x6_small_tiles=0, x6_stream=0) if prec == "fp32-big" else \
+            options.update(x6_small_k=1 << 30, x6_stream=0)
         prec = "fp32"
     if prec.startswith("bf16-gemm"):
         options.update(conv_taps=0, conv_stream=0, conv_big=0, conv_small=100000000 if prec == "bf16-gemm64" else 0)

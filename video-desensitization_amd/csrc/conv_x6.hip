@@ -401,6 +401,176 @@ __global__ __launch_bounds__(NT) void conv_x6_kernel(ConvArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Streaming 1x1 form for the memory-bound bottleneck convs (K = Cin in {64, 128,
+// 256}): the split weight slice of NCH output channels sits in LDS for the whole
+// (persistent) workgroup, and every wave streams groups of 16 output pixels with
+// no workgroup barrier, so loads, MFMAs and stores of the CU's waves interleave.
+// D^T[n][p] = sum_k W[n][k] X[p][k]: A = weight rows (LDS, split planes), B = the
+// 16 pixels' 8 channels per lane loaded as 2 x 16 B f32 straight from NHWC and
+// split in registers; weight rows are permuted so tiles 2i, 2i+1 give a lane 8
+// consecutive output channels (two 16-B f32 stores, residual read in the same shape).
+template <int KS, int NTT, int ACT, int RES>
+__global__ __launch_bounds__(512) void conv1x1_x6_kernel(ConvArgs a, int nchunks, int groups) {
+    constexpr int NCH = 16 * NTT, PL = KS * NCH * 64;     // bytes per weight plane
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* s_scale = (float*)(smem + 3 * PL);
+    float* s_shift = s_scale + NCH;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int bid = blockIdx.x, xcd = bid & 7, local = bid >> 3;
+    const int chunk = local % nchunks;
+    const int mblk = (local / nchunks) * 8 + xcd;
+    const int nmblk = gridDim.x / nchunks;
+    const int n0 = chunk * NCH;
+    {   // split weights [n0, n0 + NCH) x K -> LDS [plane][ks][row][64 B]; row 16j + i holds
+        // channel 32(j>>1) + 8(i>>2) + 4(j&1) + (i&3)
+        const int nk = a.kpad / KT;
+        for (int i = tid; i < 3 * KS * NCH * 4; i += 512) {
+            const int c = i & 3, row = (i >> 2) % NCH, pk = (i >> 2) / NCH, ks = pk % KS, p = pk / KS;
+            const int j = row >> 4, ii = row & 15;
+            const int chn = NTT == 1 ? row : 32 * (j >> 1) + 8 * (ii >> 2) + 4 * (j & 1) + (ii & 3);
+            const u32x4 v = *(const u32x4*)((const char*)a.wx3 + ((((size_t)(n0 + chn) * nk + ks) * 3 + p) * 64 + c * 16));
+            *(u32x4*)(smem + p * PL + ks * NCH * 64 + swz(row, c)) = v;
+        }
+        for (int i = tid; i < NCH; i += 512) {
+            s_scale[i] = a.scale[n0 + i];
+            s_shift[i] = a.shift[n0 + i];
+        }
+    }
+    __syncthreads();
+    const int p_lane = lane & 15, q = lane >> 4;
+    const int ohw = a.yh * a.yw;
+    const int wstride = nmblk * 8;
+    auto load = [&](int g, u32x4 (&xf)[KS][2]) {
+        const int mu = g * 16 + p_lane;
+        const int m = mu < a.M ? mu : a.M - 1;
+        const int b = m / ohw, rem = m - b * ohw;
+        const int oy = rem / a.yw, ox = rem - oy * a.yw;
+        const float* xp = (const float*)a.x + (((size_t)b * a.xh + oy * a.stride) * a.xw + ox * a.stride) * a.ldx +
+                          a.xcoff + q * 8;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            xf[ks][0] = *(const u32x4*)(xp + ks * 32);
+            xf[ks][1] = *(const u32x4*)(xp + ks * 32 + 4);
+        }
+    };
+    u32x4 xf[KS][2];
+    int g = mblk * 8 + wid;
+    if (g < groups) load(g, xf);
+    for (; g < groups; g += wstride) {
+        asm volatile("" ::: "memory");
+        u32x4 xn[KS][2];
+        const int gn = g + wstride;
+        if (gn < groups) load(gn, xn);
+        f32x4_t acc[NTT];
+#pragma unroll
+        for (int j = 0; j < NTT; ++j) acc[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            unsigned hv[8], mv[8], lv[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) split3(__uint_as_float(xf[ks][e >> 2][e & 3]), hv[e], mv[e], lv[e]);
+            u32x4 xb[3];
+            xb[0] = u32x4{hv[0] | (hv[1] << 16), hv[2] | (hv[3] << 16), hv[4] | (hv[5] << 16), hv[6] | (hv[7] << 16)};
+            xb[1] = u32x4{mv[0] | (mv[1] << 16), mv[2] | (mv[3] << 16), mv[4] | (mv[5] << 16), mv[6] | (mv[7] << 16)};
+            xb[2] = u32x4{lv[0] | (lv[1] << 16), lv[2] | (lv[3] << 16), lv[4] | (lv[5] << 16), lv[6] | (lv[7] << 16)};
+#pragma unroll
+            for (int j = 0; j < NTT; ++j) {
+                u32x4 wf[3];
+#pragma unroll
+                for (int p = 0; p < 3; ++p) wf[p] = *(const u32x4*)(smem + p * PL + ks * NCH * 64 + swz(16 * j + p_lane, q));
+#define VDS_MFMA(pw, px)                                                                              \
+    acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, wf[pw]),         \
+                                                     __builtin_bit_cast(bf16x8_t, xb[px]), acc[j], 0, 0, 0)
+                VDS_MFMA(2, 0);
+                VDS_MFMA(1, 1);
+                VDS_MFMA(0, 2);
+                VDS_MFMA(1, 0);
+                VDS_MFMA(0, 1);
+                VDS_MFMA(0, 0);
+#undef VDS_MFMA
+            }
+        }
+        const int mu = g * 16 + p_lane;
+        if (mu < a.M) {
+            const int m = mu;
+            size_t roff = 0;
+            if constexpr (RES != VD_RES_NONE) {
+                if (a.res_up) {
+                    const int b = m / ohw, rem = m - b * ohw;
+                    const int oy = rem / a.yw, ox = rem - oy * a.yw;
+                    roff = ((size_t)(b * a.rh + (oy >> 1)) * a.rw + (ox >> 1)) * a.res_ld;
+                } else {
+                    roff = (size_t)m * a.res_ld;
+                }
+                roff += a.res_coff + n0 + q * 8;
+            }
+            const size_t yo = (size_t)m * a.ldy + a.ycoff + n0 + q * 8;
+#pragma unroll
+            for (int i = 0; i < NTT / 2; ++i) {
+                const int c = 32 * i + q * 8;
+                const float4 s0 = *(const float4*)(s_scale + c), s1 = *(const float4*)(s_scale + c + 4);
+                const float4 h0 = *(const float4*)(s_shift + c), h1 = *(const float4*)(s_shift + c + 4);
+                const f32x4_t& lo = acc[2 * i];
+                const f32x4_t& hi = acc[2 * i + 1];
+                float v[8] = {lo[0] * s0.x + h0.x, lo[1] * s0.y + h0.y, lo[2] * s0.z + h0.z, lo[3] * s0.w + h0.w,
+                              hi[0] * s1.x + h1.x, hi[1] * s1.y + h1.y, hi[2] * s1.z + h1.z, hi[3] * s1.w + h1.w};
+                float rv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+                if constexpr (RES != VD_RES_NONE) {
+                    const float4 r0 = *(const float4*)((const float*)a.res + roff + 32 * i);
+                    const float4 r1 = *(const float4*)((const float*)a.res + roff + 32 * i + 4);
+                    rv[0] = r0.x; rv[1] = r0.y; rv[2] = r0.z; rv[3] = r0.w;
+                    rv[4] = r1.x; rv[5] = r1.y; rv[6] = r1.z; rv[7] = r1.w;
+                }
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    float t = v[e];
+                    if constexpr (RES == VD_RES_PRE_ACT) t += rv[e];
+                    t = act_apply(t, ACT, a.slope);
+                    if constexpr (RES == VD_RES_POST_ACT) t += rv[e];
+                    v[e] = t;
+                }
+                *(float4*)((float*)a.y + yo + 32 * i) = make_float4(v[0], v[1], v[2], v[3]);
+                *(float4*)((float*)a.y + yo + 32 * i + 4) = make_float4(v[4], v[5], v[6], v[7]);
+            }
+        }
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) { xf[ks][0] = xn[ks][0]; xf[ks][1] = xn[ks][1]; }
+    }
+}
+
+template <int KS, int NTT, int ACT, int RES>
+hipError_t launch_stream_x6(const ConvArgs& a, hipStream_t s) {
+    constexpr int NCH = 16 * NTT;
+    constexpr int lds = 3 * KS * NCH * 64 + 2 * NCH * 4;
+    static const int resident = [] {
+        (void)hipFuncSetAttribute((const void*)conv1x1_x6_kernel<KS, NTT, ACT, RES>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        int dev = 0, cus = 256, per_cu = 1;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv1x1_x6_kernel<KS, NTT, ACT, RES>, 512, lds);
+        return std::max(1, cus * std::max(1, per_cu));
+    }();
+    const int nchunks = a.cout / NCH;
+    const int groups = (a.M + 15) / 16;
+    int k = std::max(1, resident / (8 * nchunks));
+    k = std::min(k, std::max(1, (groups + 63) / 64));
+    hipLaunchKernelGGL((conv1x1_x6_kernel<KS, NTT, ACT, RES>), dim3(8 * nchunks * k), dim3(512), lds, s, a, nchunks,
+                       groups);
+    return hipGetLastError();
+}
+
+template <int KS, int NTT>
+hipError_t stream_mode_x6(const ConvArgs& a, hipStream_t s) {
+    if (a.act == VD_ACT_RELU) {
+        if (a.res_mode == VD_RES_PRE_ACT) return launch_stream_x6<KS, NTT, VD_ACT_RELU, VD_RES_PRE_ACT>(a, s);
+        if (a.res_mode == VD_RES_NONE) return launch_stream_x6<KS, NTT, VD_ACT_RELU, VD_RES_NONE>(a, s);
+    }
+    if (a.act == VD_ACT_NONE && a.res_mode == VD_RES_NONE) return launch_stream_x6<KS, NTT, VD_ACT_NONE, VD_RES_NONE>(a, s);
+    return hipErrorInvalidValue;   // excluded by vd_conv1x1_x6_ok
+}
+
 }  // namespace
 
 // Eligible: f32 activations with Cin padded to 4, K padded to 32, split weights present.
@@ -433,7 +603,27 @@ static hipError_t launch_x6(const ConvArgs& a0, hipStream_t s) {
 // a grid of fewer than 512 big tiles (measured: stem 2.16 -> 1.87 ms, layer1 conv1
 // 640 -> 580 us, SSH level 1/2 and heads 15-25 % faster); at N = 128 it measured
 // 30-45 % slower than the big tile (one wave per SIMD at 198 VGPRs) and is not used.
+// Streaming 1x1 (conv1x1_x6_kernel): 1x1 taps without padding, K = Cin in {64, 128,
+// 256} (one channel slice of 128, or 64 at K = 256, fits 96 KB of LDS in three split
+// planes), ReLU with / without the pre-activation residual, or no activation.
+static int stream_x6_nch(const ConvArgs& a) {
+    if (!a.tune || !a.tune->x6_stream || a.kh != 1 || a.kw != 1 || a.pad != 0 || a.kpad != a.cin_pad) return 0;
+    if (a.cin_pad != 64 && a.cin_pad != 128 && a.cin_pad != 256) return 0;
+    const bool mode = (a.act == VD_ACT_RELU && (a.res_mode == VD_RES_NONE || a.res_mode == VD_RES_PRE_ACT)) ||
+                      (a.act == VD_ACT_NONE && a.res_mode == VD_RES_NONE);
+    if (!mode || ((a.ldx | a.xcoff | a.ldy | a.ycoff) & 7)) return 0;
+    if (a.res_mode != VD_RES_NONE && ((a.res_ld | a.res_coff) & 7)) return 0;
+    const int nch = a.cin_pad == 256 ? 64 : 128;
+    if (a.cout % nch == 0) return nch;
+    return a.cout % 64 == 0 && a.cin_pad <= 128 ? 64 : 0;
+}
+
 hipError_t vd_launch_conv_x6(const ConvArgs& a, hipStream_t s) {
+    if (const int nch = stream_x6_nch(a)) {
+        if (a.cin_pad == 64) return nch == 128 ? stream_mode_x6<2, 8>(a, s) : stream_mode_x6<2, 4>(a, s);
+        if (a.cin_pad == 128) return nch == 128 ? stream_mode_x6<4, 8>(a, s) : stream_mode_x6<4, 4>(a, s);
+        return stream_mode_x6<8, 4>(a, s);
+    }
     const int bn = a.cout <= 32 ? 32 : (a.cout <= 64 ? 64 : 128);
     const long big_tiles = (long)((a.M + 255) / 256) * ((a.cout + bn - 1) / bn);
     const int small_k = a.tune ? a.tune->x6_small_k : 256, small_tiles = a.tune ? a.tune->x6_small_tiles : 512;
