@@ -11,7 +11,7 @@ wide coalesced read, so bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024. Counters
 also include Infinity-Cache hits. Face convs = conv dispatches on the face stream
 (the stream of the face letterbox), matched to the counter rows by Dispatch_Id.
 
-    python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write [out.json]
+    python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write [out.json] [precision]
 """
 import csv
 import json
@@ -40,13 +40,15 @@ def per_launch_named(d, counter, name):
     return sum(vals) / max(len(vals), 1), len(vals)
 
 
-def main(fetch_dir, write_dir, out=None):
+def main(fetch_dir, write_dir, out=None, precision="bf16"):
     f_kib, nf = per_launch(fetch_dir, "FETCH_SIZE")
     w_kib, nw = per_launch(write_dir, "WRITE_SIZE")
     mf, mnf = per_launch_named(fetch_dir, "FETCH_SIZE", "mosaic_out_kernel")
     mw, mnw = per_launch_named(write_dir, "WRITE_SIZE", "mosaic_out_kernel")
     res = {
-        "kernel": "RetinaFace conv launches (stem_pool / bottleneck / chain / conv_big / conv_igemm / conv1x1_stream), face stream",
+        "precision": precision,
+        "kernel": "RetinaFace conv launches on the face stream (" + ("conv_x6 / conv1x1_x6, fp32 split" if precision == "fp32"
+                  else "stem_pool / bottleneck / chain / conv_big / conv_igemm / conv1x1_stream") + ")",
         "launches": {"fetch_pass": nf, "write_pass": nw},
         "fetch_size_kib_per_launch": round(f_kib, 1),
         "write_size_kib_per_launch": round(w_kib, 1),
@@ -64,4 +66,5 @@ def main(fetch_dir, write_dir, out=None):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None)
+    main(sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None,
+         sys.argv[4] if len(sys.argv) > 4 else "bf16")

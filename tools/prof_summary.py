@@ -12,9 +12,10 @@ import os
 import sys
 
 FAMILIES = [("conv", ("conv_igemm_kernel", "conv1x1_stream_kernel", "conv_big_kernel", "bottleneck_kernel",
-                       "stem_pool_kernel", "chain_kernel", "dwconv")),
+                       "stem_pool_kernel", "chain_kernel", "dwconv", "conv_x6_kernel", "conv1x1_x6_kernel")),
             ("mosaic", ("mosaic_",)), ("letterbox", ("letterbox_kernel", "letterbox_s2d")),
-            ("post", ("candidates_kernel", "nms_kernel")), ("other", ("maxpool", "upsample"))]
+            ("post", ("candidates_kernel", "nms_kernel")), ("other", ("maxpool", "upsample")),
+            ("jpeg", ("jpeg_idct_kernel", "jpeg_color_kernel"))]
 CONV = FAMILIES[0][1]
 
 
