@@ -6,13 +6,15 @@ decode/NMS -> box correction -> int() -> mosaic write-back, with the YOLOv8n
 plate forward + NMS beside it (BASELINE config 3).
 
 The headline runs in fp32 -- the reference's arithmetic: f32 activations and
-weights; every conv multiplies f32 operands split exactly into three bf16 terms
-(six products on the bf16 matrix cores, f32 accumulation: conv_x6.hip), the
-mode whose boxes are parity-checked against the oracle. The same frames are then
-run on exact-f32 MFMA (`fp32_exact`), bf16 and fp16 (`modes`), and `parity`
-reports, over the B bench frames, the fraction whose complete keep lists and int
-boxes equal the headline's (and, from the cpu_baseline leg, each fp32 path's
-agreement with the oracle).
+weights. Every conv scales its f32 operands by powers of two (per frame from the
+producer's running max |x|, per output channel for the weights) and splits them
+into fp16 pairs: three products on the f16 matrix cores, f32 accumulation
+(conv_x6.hip), error at f32 level; this is the mode whose boxes are parity-checked
+against the oracle. The same frames are then run on the exact 3-term bf16 split
+(`fp32_x6`, 6 products), exact-f32 MFMA (`fp32_exact`), bf16 and fp16 (`modes`),
+and `parity` reports, over the B bench frames, the fraction whose complete keep
+lists and int boxes equal the headline's (and, from the cpu_baseline leg, each fp32
+path's agreement with the oracle).
 
 Multi-GPU (one process per GPU, torchrun): `--scaling weak` (default) gives every
 rank its own B frames; `--scaling strong --frames N` shards ONE list of N frames
@@ -37,7 +39,7 @@ sys.path.insert(0, ROOT)
 
 # MI355X_MICROARCH.md dense MFMA peaks. fp32 (default plan, conv_x6.hip): f32 FLOPs on the bf16
 # matrix cores at six products per multiply-add -> 2500 / 6; fp32_exact: v_mfma_f32_16x16x4_f32.
-PEAK_TFLOPS = {"bf16": 2500.0, "fp16": 2500.0, "fp32": 2500.0 / 6, "fp32_exact": 157.3}
+PEAK_TFLOPS = {"bf16": 2500.0, "fp16": 2500.0, "fp32": 2500.0 / 3, "fp32_x6": 2500.0 / 6, "fp32_exact": 157.3}
 PEAK_HBM_GBS = 8000.0                           # MI355X_MICROARCH.md: HBM3E spec
 
 
@@ -49,8 +51,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--precision", default="fp32", choices=["bf16", "fp16", "fp32", "fp32_exact"])
-    ap.add_argument("--compare", default="fp32_exact,bf16,fp16",
+    ap.add_argument("--precision", default="fp32", choices=["bf16", "fp16", "fp32", "fp32_x6", "fp32_exact"])
+    ap.add_argument("--compare", default="fp32_x6,fp32_exact,bf16,fp16",
                     help="extra precisions measured on the same frames at N=1 (',' separated; '' = none)")
     ap.add_argument("--plates", type=int, default=1, help="1: run YOLOv8n beside RetinaFace (BASELINE config 3)")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
@@ -150,9 +152,11 @@ class Mode:
         import vdmi
         from vdmi import _lib, weights
         opts = {k: int(v) for k, v in (o.split("=", 1) for o in a.option)}
-        if precision == "fp32_exact":     # fp32 plan on exact-f32 MFMA instead of the 3-term bf16 split
+        if precision == "fp32_exact":     # fp32 plan on exact-f32 MFMA
             opts["f32_split"] = 0
-        self.ctx = vdmi.Context(device=dev.index or 0, precision=precision.replace("_exact", ""),
+        if precision == "fp32_x6":        # fp32 plan on the exact 3-term bf16 split (6 products)
+            opts["f32_split"] = 1
+        self.ctx = vdmi.Context(device=dev.index or 0, precision=precision.split("_")[0],
                                 max_batch=a.batch, options=opts)
         self.ctx.load_weights(_lib.VD_NET_RETINAFACE, sd)
         if plates:
@@ -304,8 +308,11 @@ def main():
         ach = cflop / (cms * 1e-3) / 1e12 if cms > 0 else 0.0
         traffic, tsrc, blur_traffic = pmc_traffic(precision)
         peak = PEAK_TFLOPS[precision]
-        kern = ("conv_x6_kernel launches (f32 operands split exactly into 3 bf16 terms, 6 products on "
-                "v_mfma_f32_16x16x32_bf16, f32 accumulate; peak = 2500/6)" if precision == "fp32" else
+        kern = ("conv_x6_kernel<..., 3> launches (f32 operands split exactly into 3 bf16 terms, 6 products on "
+                "v_mfma_f32_16x16x32_bf16, f32 accumulate; peak = 2500/6)" if precision == "fp32_x6" else
+                "conv_x6_kernel<..., 2> / conv1x1_x6_kernel<..., 2> launches (f32 operands scaled per frame / per "
+                "channel by powers of two and split into fp16 pairs, 3 products on v_mfma_f32_16x16x32_f16, f32 "
+                "accumulate; peak = 2500/3)" if precision == "fp32" else
                 "conv_igemm_kernel<float> launches (exact-f32 v_mfma_f32_16x16x4_f32)" if precision == "fp32_exact" else
                 "conv_igemm_kernel<_Float16> launches" if precision == "fp16" else
                 "stem_pool + bottleneck (fused layer1) + chain (layer2) + conv_big + conv_igemm + conv1x1_stream")

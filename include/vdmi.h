@@ -61,9 +61,12 @@ extern "C" {
 #define VD_DEVICE 1
 
 #define VD_PREC_BF16 0       /* bf16 operands, f32 accumulate (performance mode) */
-#define VD_PREC_FP32 1       /* f32 operands and activations (parity mode): convs on
-                              * bf16 MFMA by exact 3-term operand split (6 products,
-                              * f32 accumulate; option f32_split=0: exact-f32 MFMA) */
+#define VD_PREC_FP32 1       /* f32 operands and activations (parity mode): operands
+                              * scaled by powers of two (per frame / per output
+                              * channel) and split into fp16 pairs, 3 products on
+                              * the f16 matrix cores, f32 accumulate; option
+                              * f32_split=1: exact 3-term bf16 split (6 products),
+                              * 0: exact-f32 MFMA */
 #define VD_PREC_FP16 2       /* fp16 operands, f32 accumulate (implicit GEMM on   *
                               * v_mfma_f32_16x16x32_f16; no bf16-only fusions)    */
 
@@ -128,7 +131,7 @@ int   vd_load_weights(vd_ctx* ctx, int net, const void* blob, size_t bytes, int 
 int   vd_set_stream(vd_ctx* ctx, void* hip_stream);   /* NULL -> library-owned stream */
 /* Kernel-selection switches (A/B measurement, tests that force a kernel form onto
  * small shapes); the defaults are the production plan. Plan switches (block_fuse,
- * chain, stem_pool, ssh_fuse, plate_s2d) apply to weights loaded afterwards, the
+ * chain, stem_pool, ssh_fuse, plate_s2d, f32_split) apply to weights loaded afterwards, the
  * rest to the next launch. Names: conv_stream conv_stream512 conv_dual conv_taps
  * conv_n192 conv_small conv_big conv_big_kmin stream_ntt lb_pair mosaic_map
  * block_fuse chain stem_pool ssh_fuse plate_s2d f32_split x6_small_k x6_small_tiles x6_stream.

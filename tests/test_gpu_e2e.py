@@ -49,10 +49,15 @@ def _rel(a, b):
     return np.abs(a - b).max() / (np.abs(b).max() + 1e-12)
 
 
+# fp32 plans: 1 = 3-term bf16 split (6 products), 2 = scaled fp16 pairs (3 products), 0 = exact-f32 MFMA
+SPLITS = [1, 2, 0]
+
+
+@pytest.mark.parametrize("split", SPLITS)
 @pytest.mark.parametrize("h,w,wkind", [(1080, 1920, "default"), (720, 1280, "default"), (1080, 1920, "mnet"),
                                         (720, 1280, "mnet")])
-def test_heads_fp32_match_oracle(gpu, face_ctx_factory, h, w, wkind):
-    ctx = face_ctx_factory("fp32", 8, wkind)
+def test_heads_fp32_match_oracle(gpu, face_ctx_factory, h, w, wkind, split):
+    ctx = face_ctx_factory("fp32", 8, wkind, options=(("f32_split", split),))
     fr = _frames(2, h, w)
     loc, conf, ldm = ctx.forward_heads(fr)
     eloc, econf, eldm = _oracle_heads(fr, wkind)
@@ -182,9 +187,10 @@ def _near_decision(conf_b, boxes_norm, thr=0.5, iou=0.4, eps=1e-4):
     return near
 
 
+@pytest.mark.parametrize("split", SPLITS)
 @pytest.mark.parametrize("wkind", ["default", "mnet"])
-def test_detect_fp32_matches_oracle(gpu, face_ctx_factory, wkind):
-    ctx = face_ctx_factory("fp32", 8, wkind)
+def test_detect_fp32_matches_oracle(gpu, face_ctx_factory, wkind, split):
+    ctx = face_ctx_factory("fp32", 8, wkind, options=(("f32_split", split),))
     fr = _frames(3, 1080, 1920, seed=2)
     got = ctx.detect(fr)
     eloc, econf, _ = _oracle_heads(fr, wkind)

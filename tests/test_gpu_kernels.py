@@ -194,17 +194,22 @@ CONV_CASES = [
 ]
 
 
-@pytest.mark.parametrize("prec", ["fp32", "fp32-big", "fp32-small", "fp32-exact", "bf16", "fp16", "bf16-gemm64",
-                                  "bf16-gemm128"])
+@pytest.mark.parametrize("prec", ["fp32", "fp32-big", "fp32-small", "fp32-exact", "fp32-x6", "fp32-x6-big",
+                                  "fp32-x6-small", "bf16", "fp16", "bf16-gemm64", "bf16-gemm128"])
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv_matches_torch(gpu, face_ctx_factory, prec, case, options=None):
-    """fp32: the default fp32 plan (conv_x6.hip, exact 3-term bf16 split: streaming 1x1
-    for K in {64,128,256}, else the tiled GEMM; -big / -small force its 256-row
-    two-stage / 128-row one-stage tile);
-    fp32-exact: exact-f32 MFMA (option f32_split=0); bf16: the default dispatch
+    """fp32: the default fp32 plan (conv_x6.hip, scaled fp16 pairs on the f16 matrix
+    cores: streaming 1x1 for K in {64,128,256}, else the tiled GEMM; -big / -small
+    force its 256-row two-stage / 128-row one-stage tile; the hook also checks the
+    kernel's per-frame output max slots against the host max of the result);
+    fp32-exact: exact-f32 MFMA (option f32_split=0); fp32-x6(-big/-small): the exact
+    3-term bf16 split (option f32_split=1); bf16: the default dispatch
     (streaming 1x1 / streaming taps / phased / GEMM); bf16-gemm64 / -gemm128: the
     implicit GEMM with 64- and 128-row tiles forced through vd_set_option."""
     options = dict(options or {})
+    if prec.startswith("fp32-x6"):
+        options.update(f32_split=1)
+        prec = prec.replace("-x6", "")
     if prec == "fp32-exact":
         options.update(f32_split=0)
         prec = "fp32"
@@ -248,9 +253,9 @@ def test_conv_matches_torch(gpu, face_ctx_factory, prec, case, options=None):
 @pytest.mark.parametrize("case", [(2, 20, 24, 256, 256, 3, 1, 1, 0, 0), (1, 40, 40, 512, 128, 1, 1, 0, 0, 0),
                                   (3, 17, 23, 3, 64, 7, 2, 3, 0, 0)])
 def test_conv_fp32_split_error_matches_exact_f32(gpu, face_ctx_factory, case):
-    """The split path's error against a float64 convolution is at the level of the
-    exact-f32 MFMA path's (both ~1.6e-6 of max|y| at K = 2304): the 3-term bf16 split is fp32
-    arithmetic, not a reduced precision (conv_x6.hip)."""
+    """Both split paths' errors against a float64 convolution are at the level of the
+    exact-f32 MFMA path's (~1.6e-6 of max|y| at K = 2304): the 3-term bf16 split and the
+    scaled fp16 pair are fp32 arithmetic, not a reduced precision (conv_x6.hip)."""
     n, h, w, cin, cout, k, s, p, _, _ = case
     rng = np.random.default_rng(cin + cout + k)
     x = np.maximum(rng.standard_normal((n, h, w, cin)), 0).astype(F32) * F32(3.0)
@@ -258,12 +263,13 @@ def test_conv_fp32_split_error_matches_exact_f32(gpu, face_ctx_factory, case):
     y = torch.nn.functional.conv2d(torch.from_numpy(x).permute(0, 3, 1, 2).double(), torch.from_numpy(wt).double(),
                                    stride=s, padding=p).permute(0, 2, 3, 1).numpy()
     errs = {}
-    for opts in ((), (("f32_split", 0),)):
+    for opts in ((("f32_split", 1),), (("f32_split", 0),), (("f32_split", 2),)):
         ctx = face_ctx_factory("fp32", 8, options=opts)
         got = ctx.conv2d(x, wt, s, p)
         errs[opts] = np.abs(got - y).max() / np.abs(y).max()
-    split, exact = errs[()], errs[(("f32_split", 0),)]
+    split, exact, pair = errs[(("f32_split", 1),)], errs[(("f32_split", 0),)], errs[(("f32_split", 2),)]
     assert split < 4e-6 and split < 2 * exact + 1e-7, (split, exact)
+    assert pair < 4e-6 and pair < 2 * exact + 1e-7, (pair, exact)
 
 
 BIG_CASES = [

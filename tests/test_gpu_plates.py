@@ -19,10 +19,12 @@ _CTX = {}
 
 
 def _ctx(precision):
+    """precision 'fp32-x6': the fp32 plan on the exact 3-term bf16 split (option f32_split=1)."""
     import vdmi
     from vdmi import weights
     if precision not in _CTX:
-        c = vdmi.Context(precision=precision, max_batch=4)
+        opts = {"f32_split": 1} if precision == "fp32-x6" else {}
+        c = vdmi.Context(precision=precision.replace("-x6", ""), max_batch=4, options=opts)
         c.load_weights(0, weights.retinaface_state_dict(0))
         c.load_weights(1, weights.yolov8n_state_dict(0))
         _CTX[precision] = c
@@ -42,11 +44,12 @@ def _rel(a, b):
     return np.abs(a - b).max() / (np.abs(b).max() + 1e-12)
 
 
+@pytest.mark.parametrize("prec", ["fp32", "fp32-x6"])
 @pytest.mark.parametrize("h,w", [(1080, 1920), (720, 1280), (640, 640), (480, 640)])
-def test_plate_raw_fp32(gpu, h, w):
+def test_plate_raw_fp32(gpu, h, w, prec):
     from vdmi import synth
     fr = synth.frames(2, h, w, seed=5)
-    got = _ctx("fp32").plate_raw(fr)
+    got = _ctx(prec).plate_raw(fr)
     exp, _, _ = _oracle_raw(fr)
     assert got.shape == exp.shape
     assert _rel(got, exp) < 1e-4
@@ -68,7 +71,7 @@ def test_plate_raw_bf16_close(gpu):
     assert _rel(got[:, 64:], exp[:, 64:]) < 8e-2
 
 
-@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+@pytest.mark.parametrize("prec", ["fp32", "fp32-x6", "bf16"])
 def test_plate_post_exact_given_raw(gpu, prec):
     from vdmi import synth
     ctx = _ctx(prec)

@@ -14,12 +14,14 @@ from conv_layers import face_plan  # noqa: E402
 
 def main(path, B=64):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-    lb = [i for i, r in enumerate(rows) if "letterbox" in r["Kernel_Name"]]
-    li = lb[-1] if lb else 0
-    # the face stream: the stream of the letterbox kernel with the most conv launches after it
-    sid = rows[li]["Stream_Id"]
-    convs = [r for r in rows[li:] if r["Stream_Id"] == sid and ("conv" in r["Kernel_Name"])]
     plan = face_plan(B, fused=False, block=False, chain=False, ssh_fused=True)
+    # the face stream: the stream with the most conv launches (73 per step vs the plate net's 60);
+    # its last len(plan) conv launches are the last step's layers
+    per = {}
+    for r in rows:
+        if "conv" in r["Kernel_Name"]:
+            per.setdefault(r["Stream_Id"], []).append(r)
+    convs = max(per.values(), key=len)[-len(plan):]
     tot = fl_tot = 0
     for (name, M, N, K), r in zip(plan, convs):
         dt = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9

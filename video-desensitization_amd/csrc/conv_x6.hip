@@ -30,6 +30,7 @@
 //     ds_read_b128 fragment reads for the 16-row MFMA operand pattern.
 #include "vd_common.h"
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 
 namespace {
@@ -38,16 +39,17 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void_t;
 
 constexpr int KT = 32;                          // K per tile (one bf16 MFMA k-step)
+constexpr int kAmaxFrames = 1024;               // LDS reserved for per-frame max slots (frames per launch)
 
 // Two forms: the big tile (256 x BN, 8 waves, two LDS stages, one workgroup per CU)
 // for the compute-heavy layers, and the small tile (128 x BN, 4 waves, ONE stage,
 // three workgroups per CU) for small-K / small-M layers, where a workgroup's
 // load -> compute -> epilogue phases are short and neighbours on the CU overlap them.
-template <int BM_, int BN, int NT_, int NST> struct X6Shape {
+template <int BM_, int BN, int NT_, int NST, int TERMS> struct X6Shape {
     static constexpr int BM = BM_, NT = NT_, WAVES = NT / 64;
     static constexpr int PL_A = BM * 64;                       // bytes per A plane
     static constexpr int PL_B = BN * 64;                       // bytes per B plane
-    static constexpr int STAGE = 3 * PL_A + 3 * PL_B;          // 256 x 128: 73 728 B
+    static constexpr int STAGE = TERMS * (PL_A + PL_B);        // 256 x 128: 73 728 B (3 terms), 49 152 B (2)
     static constexpr int EPR = NST == 2 ? 128 : 64;            // epilogue rows per pass
     static constexpr int EPLD = BN + 4;                        // f32 epilogue row stride
     static constexpr int LDS = NST * STAGE > EPR * EPLD * 4 ? NST * STAGE : EPR * EPLD * 4;
@@ -55,7 +57,7 @@ template <int BM_, int BN, int NT_, int NST> struct X6Shape {
     static constexpr int WAVES_M = WAVES / WAVES_N;
     static constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
     static constexpr int TM = WTM / 16, TN = WTN / 16;
-    static constexpr int NDMA = 3 * BN / 16;                   // 1-KB DMA instructions per K tile
+    static constexpr int NDMA = TERMS * BN / 16;               // 1-KB DMA instructions per K tile
     static constexpr int AROWS = NT / 4;                       // A rows per staging pass (2 passes)
     static_assert(BM == 2 * AROWS, "two A items per thread");
 };
@@ -96,9 +98,64 @@ __device__ __forceinline__ void split3(float x, unsigned& h, unsigned& m, unsign
     l = __float_as_uint(r2) >> 16;
 }
 
-template <int BM, int BN, int NT, int NST>
+// x = hi + lo (+ below 2^-24 |x|) with both terms fp16, round to nearest: the
+// scaled operand (|x| < 2^15, see act_scale) keeps 22-24 significand bits
+__device__ __forceinline__ void split2h(float x, unsigned& h, unsigned& l) {
+    const _Float16 x0 = (_Float16)x;
+    const _Float16 x1 = (_Float16)(x - (float)x0);    // the residual is exact in f32
+    h = __builtin_bit_cast(unsigned short, x0);
+    l = __builtin_bit_cast(unsigned short, x1);
+}
+
+template <int TERMS>
+__device__ __forceinline__ f32x4_t mfma_terms(const u32x4 (&a)[3], const u32x4 (&b)[3], f32x4_t acc);
+
+template <>
+__device__ __forceinline__ f32x4_t mfma_terms<3>(const u32x4 (&a)[3], const u32x4 (&b)[3], f32x4_t acc) {
+#define VDX_MFMA(pa, pb)                                                                                 \
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a[pa]),                  \
+                                                  __builtin_bit_cast(bf16x8_t, b[pb]), acc, 0, 0, 0)
+    // small terms first
+    VDX_MFMA(2, 0);
+    VDX_MFMA(1, 1);
+    VDX_MFMA(0, 2);
+    VDX_MFMA(1, 0);
+    VDX_MFMA(0, 1);
+    VDX_MFMA(0, 0);
+#undef VDX_MFMA
+    return acc;
+}
+
+template <>
+__device__ __forceinline__ f32x4_t mfma_terms<2>(const u32x4 (&a)[3], const u32x4 (&b)[3], f32x4_t acc) {
+#define VDH_MFMA(pa, pb)                                                                                 \
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, a[pa]),                    \
+                                                 __builtin_bit_cast(f16x8_t, b[pb]), acc, 0, 0, 0)
+    VDH_MFMA(1, 0);
+    VDH_MFMA(0, 1);
+    VDH_MFMA(0, 0);
+#undef VDH_MFMA
+    return acc;
+}
+
+// 8 f32 -> TERMS packed 16-B planes (bf16 truncation split, or scaled fp16 pair)
+template <int TERMS>
+__device__ __forceinline__ void split_pack(const float (&e)[8], float sa, u32x4 (&o)[3]) {
+    unsigned hv[8], mv[8], lv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        if constexpr (TERMS == 3) split3(e[j], hv[j], mv[j], lv[j]);
+        else { split2h(e[j] * sa, hv[j], mv[j]); lv[j] = 0; }
+    }
+    o[0] = u32x4{hv[0] | (hv[1] << 16), hv[2] | (hv[3] << 16), hv[4] | (hv[5] << 16), hv[6] | (hv[7] << 16)};
+    o[1] = u32x4{mv[0] | (mv[1] << 16), mv[2] | (mv[3] << 16), mv[4] | (mv[5] << 16), mv[6] | (mv[7] << 16)};
+    if constexpr (TERMS == 3)
+        o[2] = u32x4{lv[0] | (lv[1] << 16), lv[2] | (lv[3] << 16), lv[4] | (lv[5] << 16), lv[6] | (lv[7] << 16)};
+}
+
+template <int BM, int BN, int NT, int NST, int TERMS>
 __global__ __launch_bounds__(NT) void conv_x6_kernel(ConvArgs a) {
-    using S = X6Shape<BM, BN, NT, NST>;
+    using S = X6Shape<BM, BN, NT, NST, TERMS>;
     constexpr int STAGE = S::STAGE, PL_A = S::PL_A, PL_B = S::PL_B, TM = S::TM, TN = S::TN, WAVES = S::WAVES;
     constexpr int AROWS = S::AROWS;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -117,6 +174,7 @@ __global__ __launch_bounds__(NT) void conv_x6_kernel(ConvArgs a) {
     const int ohw = a.yh * a.yw;
     long pix0[2];
     int iy0[2], ix0[2];
+    float sa[2] = {1.f, 1.f};                       // fp16 pair: the row's frame scale 2^k
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int m = m0 + arow + AROWS * i;
@@ -126,6 +184,7 @@ __global__ __launch_bounds__(NT) void conv_x6_kernel(ConvArgs a) {
             iy0[i] = oy * a.stride - a.pad;
             ix0[i] = ox * a.stride - a.pad;
             pix0[i] = (((long)b * a.xh + iy0[i]) * a.xw + ix0[i]) * a.ldx + a.xcoff;
+            if constexpr (TERMS == 2) sa[i] = __builtin_ldexpf(1.f, act_scale_exp(a, b));
         } else {
             iy0[i] = -(1 << 28); ix0[i] = 0; pix0[i] = 0;
         }
@@ -186,16 +245,11 @@ __global__ __launch_bounds__(NT) void conv_x6_kernel(ConvArgs a) {
             e[j] = __uint_as_float(r[i][0][j]);
             e[4 + j] = __uint_as_float(r[i][1][j]);
         }
-        unsigned hv[8], mv[8], lv[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) split3(e[j], hv[j], mv[j], lv[j]);
+        u32x4 o[3];
+        split_pack<TERMS>(e, sa[i], o);
         const int off = swz(arow + AROWS * i, apair);
-        *(u32x4*)(A + off) = u32x4{hv[0] | (hv[1] << 16), hv[2] | (hv[3] << 16), hv[4] | (hv[5] << 16),
-                                   hv[6] | (hv[7] << 16)};
-        *(u32x4*)(A + PL_A + off) = u32x4{mv[0] | (mv[1] << 16), mv[2] | (mv[3] << 16), mv[4] | (mv[5] << 16),
-                                          mv[6] | (mv[7] << 16)};
-        *(u32x4*)(A + 2 * PL_A + off) = u32x4{lv[0] | (lv[1] << 16), lv[2] | (lv[3] << 16), lv[4] | (lv[5] << 16),
-                                              lv[6] | (lv[7] << 16)};
+#pragma unroll
+        for (int p = 0; p < TERMS; ++p) *(u32x4*)(A + p * PL_A + off) = o[p];
     };
 
     // ---- B: LDS-DMA, one instruction = 1 KB = 16 rows of one plane; NDMA per tile,
@@ -205,7 +259,7 @@ __global__ __launch_bounds__(NT) void conv_x6_kernel(ConvArgs a) {
     const int my_dma = NDMA / WAVES + (wid < NDMA % WAVES ? 1 : 0);
     const __amdgpu_buffer_rsrc_t rsrc_w = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7fffffff, 0x00020000);
     auto dma_b = [&](int kt, int st) {
-        char* Bs = smem + st * STAGE + 3 * PL_A;
+        char* Bs = smem + st * STAGE + TERMS * PL_A;
 #pragma unroll
         for (int q = 0; q < (NDMA + WAVES - 1) / WAVES; ++q) {
             const int j = wid + WAVES * q;
@@ -213,7 +267,7 @@ __global__ __launch_bounds__(NT) void conv_x6_kernel(ConvArgs a) {
                 const int p = j / RB, r0 = (j % RB) * 16;
                 const int row = r0 + (lane >> 2), slot = lane & 3;
                 const int chunk = slot ^ (((row >> 3) & 1) * 3);
-                const unsigned off = (unsigned)((((long)(n0 + row) * nk + kt) * 3 + p) * 64 + chunk * 16);
+                const unsigned off = (unsigned)((((long)(n0 + row) * nk + kt) * TERMS + p) * 64 + chunk * 16);
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_w, (lds_void_t*)(Bs + p * PL_B + r0 * 64), 16, off, 0,
                                                          0, 0);
             }
@@ -225,39 +279,29 @@ __global__ __launch_bounds__(NT) void conv_x6_kernel(ConvArgs a) {
     for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    if (a.ymax)   // beyond the stages / epilogue image; ordered before use by the main loop's barriers
+        for (int f = tid; f < a.B; f += NT) ((unsigned*)(smem + S::LDS))[f] = 0u;
 
     // one K tile from stage st; the split + LDS write of the next tile's A items are
     // interleaved with the MFMA rows (VALU work beside the matrix cores)
     auto compute = [&](int st, bool split_next, int st_next, const u32x4 (&rn)[2][2]) {
         const char* A = smem + st * STAGE;
-        const char* Bs = A + 3 * PL_A;
+        const char* Bs = A + TERMS * PL_A;
         const int ch = lane >> 4;
         u32x4 bf[TN][3];
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
-            for (int p = 0; p < 3; ++p)
+            for (int p = 0; p < TERMS; ++p)
                 bf[j][p] = *(const u32x4*)(Bs + p * PL_B + swz(wn * S::WTN + j * 16 + (lane & 15), ch));
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
             u32x4 af[3];
 #pragma unroll
-            for (int p = 0; p < 3; ++p)
+            for (int p = 0; p < TERMS; ++p)
                 af[p] = *(const u32x4*)(A + p * PL_A + swz(wm * S::WTM + i * 16 + (lane & 15), ch));
 #pragma unroll
-            for (int j = 0; j < TN; ++j) {
-#define VDX_MFMA(pa, pb)                                                                     \
-    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, af[pa]), \
-                                                        __builtin_bit_cast(bf16x8_t, bf[j][pb]), acc[i][j], 0, 0, 0)
-                // small terms first
-                VDX_MFMA(2, 0);
-                VDX_MFMA(1, 1);
-                VDX_MFMA(0, 2);
-                VDX_MFMA(1, 0);
-                VDX_MFMA(0, 1);
-                VDX_MFMA(0, 0);
-#undef VDX_MFMA
-            }
+            for (int j = 0; j < TN; ++j) acc[i][j] = mfma_terms<TERMS>(af, bf[j], acc[i][j]);
             if (split_next && i == 0) store_item(st_next, rn, 0);
             if (split_next && i == (TM > 2 ? 2 : 1)) store_item(st_next, rn, 1);
         }
@@ -327,6 +371,7 @@ __global__ __launch_bounds__(NT) void conv_x6_kernel(ConvArgs a) {
     float* ep = (float*)smem;
     const bool vec_ok = ((a.cout & 7) == 0) && ((a.ldy & 7) == 0) && ((a.ycoff & 7) == 0) &&
                         (a.res_mode == VD_RES_NONE || (((a.res_ld | a.res_coff) & 7) == 0));
+    unsigned* s_amax = (unsigned*)(smem + S::LDS);     // per-frame max |y| of this tile (a.ymax)
 #pragma unroll
     for (int h = 0; h < BM / EPR; ++h) {
         if (h) __syncthreads();
@@ -348,9 +393,13 @@ __global__ __launch_bounds__(NT) void conv_x6_kernel(ConvArgs a) {
             const int rr = it / CG, cg = it % CG;
             const int m = m0 + h * EPR + rr;
             const int nb = n0 + cg * 8;
-            if (m >= a.M || nb >= a.cout) continue;
+            const bool valid = m < a.M && nb < a.cout;
+            const int fb = valid ? m / ohw : -1;
+            float vmax = 0.f;
+            if (valid) {
             const float* er = ep + rr * EPLD + cg * 8;
             const size_t yo = (size_t)m * a.ldy + a.ycoff + nb;
+            const float inv_sa = TERMS == 2 ? __builtin_ldexpf(1.f, -act_scale_exp(a, fb)) : 1.f;
             size_t roff = 0;
             if (a.res_mode != VD_RES_NONE) {
                 if (a.res_up) {
@@ -378,26 +427,34 @@ __global__ __launch_bounds__(NT) void conv_x6_kernel(ConvArgs a) {
                 float v[8];
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
-                    float t = ev[e] * sc[e] + sh[e];
+                    float t = (ev[e] * inv_sa) * sc[e] + sh[e];
                     if (a.res_mode == VD_RES_PRE_ACT) t += rv[e];
                     t = act_apply(t, a.act, a.slope);
                     if (a.res_mode == VD_RES_POST_ACT) t += rv[e];
                     v[e] = t;
+                    vmax = fmaxf(vmax, fabsf(t));
                 }
                 *(float4*)((float*)a.y + yo) = make_float4(v[0], v[1], v[2], v[3]);
                 *(float4*)((float*)a.y + yo + 4) = make_float4(v[4], v[5], v[6], v[7]);
             } else {
                 for (int e = 0; e < 8 && nb + e < a.cout; ++e) {
                     const int n = nb + e;
-                    float t = er[e] * a.scale[n] + a.shift[n];
+                    float t = (er[e] * inv_sa) * a.scale[n] + a.shift[n];
                     const float rv = a.res_mode != VD_RES_NONE ? ((const float*)a.res)[roff + e] : 0.f;
                     if (a.res_mode == VD_RES_PRE_ACT) t += rv;
                     t = act_apply(t, a.act, a.slope);
                     if (a.res_mode == VD_RES_POST_ACT) t += rv;
                     ((float*)a.y)[yo + e] = t;
+                    vmax = fmaxf(vmax, fabsf(t));
                 }
             }
+            }   // valid
+            if (a.ymax) amax_lds_add(s_amax, fb, vmax);
         }
+    }
+    if (a.ymax) {
+        __syncthreads();
+        amax_lds_flush(s_amax, a.ymax, a.B);
     }
 }
 
@@ -410,11 +467,11 @@ __global__ __launch_bounds__(NT) void conv_x6_kernel(ConvArgs a) {
 // 16 pixels' 8 channels per lane loaded as 2 x 16 B f32 straight from NHWC and
 // split in registers; weight rows are permuted so tiles 2i, 2i+1 give a lane 8
 // consecutive output channels (two 16-B f32 stores, residual read in the same shape).
-template <int KS, int NTT, int ACT, int RES>
+template <int KS, int NTT, int ACT, int RES, int TERMS>
 __global__ __launch_bounds__(512) void conv1x1_x6_kernel(ConvArgs a, int nchunks, int groups) {
     constexpr int NCH = 16 * NTT, PL = KS * NCH * 64;     // bytes per weight plane
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    float* s_scale = (float*)(smem + 3 * PL);
+    float* s_scale = (float*)(smem + TERMS * PL);
     float* s_shift = s_scale + NCH;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int bid = blockIdx.x, xcd = bid & 7, local = bid >> 3;
@@ -425,11 +482,11 @@ __global__ __launch_bounds__(512) void conv1x1_x6_kernel(ConvArgs a, int nchunks
     {   // split weights [n0, n0 + NCH) x K -> LDS [plane][ks][row][64 B]; row 16j + i holds
         // channel 32(j>>1) + 8(i>>2) + 4(j&1) + (i&3)
         const int nk = a.kpad / KT;
-        for (int i = tid; i < 3 * KS * NCH * 4; i += 512) {
+        for (int i = tid; i < TERMS * KS * NCH * 4; i += 512) {
             const int c = i & 3, row = (i >> 2) % NCH, pk = (i >> 2) / NCH, ks = pk % KS, p = pk / KS;
             const int j = row >> 4, ii = row & 15;
             const int chn = NTT == 1 ? row : 32 * (j >> 1) + 8 * (ii >> 2) + 4 * (j & 1) + (ii & 3);
-            const u32x4 v = *(const u32x4*)((const char*)a.wx3 + ((((size_t)(n0 + chn) * nk + ks) * 3 + p) * 64 + c * 16));
+            const u32x4 v = *(const u32x4*)((const char*)a.wx3 + ((((size_t)(n0 + chn) * nk + ks) * TERMS + p) * 64 + c * 16));
             *(u32x4*)(smem + p * PL + ks * NCH * 64 + swz(row, c)) = v;
         }
         for (int i = tid; i < NCH; i += 512) {
@@ -437,6 +494,9 @@ __global__ __launch_bounds__(512) void conv1x1_x6_kernel(ConvArgs a, int nchunks
             s_shift[i] = a.shift[n0 + i];
         }
     }
+    unsigned* s_amax = (unsigned*)(s_shift + NCH);        // per-frame max |y| (a.ymax)
+    if (a.ymax)
+        for (int f = tid; f < a.B; f += 512) s_amax[f] = 0u;
     __syncthreads();
     const int p_lane = lane & 15, q = lane >> 4;
     const int ohw = a.yh * a.yw;
@@ -465,33 +525,27 @@ __global__ __launch_bounds__(512) void conv1x1_x6_kernel(ConvArgs a, int nchunks
         f32x4_t acc[NTT];
 #pragma unroll
         for (int j = 0; j < NTT; ++j) acc[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        const int mu = g * 16 + p_lane;
+        const int fb = (mu < a.M ? mu : a.M - 1) / ohw;     // this lane's pixel's frame
+        const int kexp = TERMS == 2 ? act_scale_exp(a, fb) : 0;
+        const float sa = __builtin_ldexpf(1.f, kexp), inv_sa = __builtin_ldexpf(1.f, -kexp);
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
-            unsigned hv[8], mv[8], lv[8];
+            float e8[8];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) split3(__uint_as_float(xf[ks][e >> 2][e & 3]), hv[e], mv[e], lv[e]);
+            for (int e = 0; e < 8; ++e) e8[e] = __uint_as_float(xf[ks][e >> 2][e & 3]);
             u32x4 xb[3];
-            xb[0] = u32x4{hv[0] | (hv[1] << 16), hv[2] | (hv[3] << 16), hv[4] | (hv[5] << 16), hv[6] | (hv[7] << 16)};
-            xb[1] = u32x4{mv[0] | (mv[1] << 16), mv[2] | (mv[3] << 16), mv[4] | (mv[5] << 16), mv[6] | (mv[7] << 16)};
-            xb[2] = u32x4{lv[0] | (lv[1] << 16), lv[2] | (lv[3] << 16), lv[4] | (lv[5] << 16), lv[6] | (lv[7] << 16)};
+            split_pack<TERMS>(e8, sa, xb);
 #pragma unroll
             for (int j = 0; j < NTT; ++j) {
                 u32x4 wf[3];
 #pragma unroll
-                for (int p = 0; p < 3; ++p) wf[p] = *(const u32x4*)(smem + p * PL + ks * NCH * 64 + swz(16 * j + p_lane, q));
-#define VDS_MFMA(pw, px)                                                                              \
-    acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, wf[pw]),         \
-                                                     __builtin_bit_cast(bf16x8_t, xb[px]), acc[j], 0, 0, 0)
-                VDS_MFMA(2, 0);
-                VDS_MFMA(1, 1);
-                VDS_MFMA(0, 2);
-                VDS_MFMA(1, 0);
-                VDS_MFMA(0, 1);
-                VDS_MFMA(0, 0);
-#undef VDS_MFMA
+                for (int p = 0; p < TERMS; ++p)
+                    wf[p] = *(const u32x4*)(smem + p * PL + ks * NCH * 64 + swz(16 * j + p_lane, q));
+                acc[j] = mfma_terms<TERMS>(wf, xb, acc[j]);
             }
         }
-        const int mu = g * 16 + p_lane;
+        float vmax = 0.f;
         if (mu < a.M) {
             const int m = mu;
             size_t roff = 0;
@@ -513,8 +567,10 @@ __global__ __launch_bounds__(512) void conv1x1_x6_kernel(ConvArgs a, int nchunks
                 const float4 h0 = *(const float4*)(s_shift + c), h1 = *(const float4*)(s_shift + c + 4);
                 const f32x4_t& lo = acc[2 * i];
                 const f32x4_t& hi = acc[2 * i + 1];
-                float v[8] = {lo[0] * s0.x + h0.x, lo[1] * s0.y + h0.y, lo[2] * s0.z + h0.z, lo[3] * s0.w + h0.w,
-                              hi[0] * s1.x + h1.x, hi[1] * s1.y + h1.y, hi[2] * s1.z + h1.z, hi[3] * s1.w + h1.w};
+                float v[8] = {(lo[0] * inv_sa) * s0.x + h0.x, (lo[1] * inv_sa) * s0.y + h0.y,
+                              (lo[2] * inv_sa) * s0.z + h0.z, (lo[3] * inv_sa) * s0.w + h0.w,
+                              (hi[0] * inv_sa) * s1.x + h1.x, (hi[1] * inv_sa) * s1.y + h1.y,
+                              (hi[2] * inv_sa) * s1.z + h1.z, (hi[3] * inv_sa) * s1.w + h1.w};
                 float rv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
                 if constexpr (RES != VD_RES_NONE) {
                     const float4 r0 = *(const float4*)((const float*)a.res + roff + 32 * i);
@@ -529,49 +585,69 @@ __global__ __launch_bounds__(512) void conv1x1_x6_kernel(ConvArgs a, int nchunks
                     t = act_apply(t, ACT, a.slope);
                     if constexpr (RES == VD_RES_POST_ACT) t += rv[e];
                     v[e] = t;
+                    vmax = fmaxf(vmax, fabsf(t));
                 }
                 *(float4*)((float*)a.y + yo + 32 * i) = make_float4(v[0], v[1], v[2], v[3]);
                 *(float4*)((float*)a.y + yo + 32 * i + 4) = make_float4(v[4], v[5], v[6], v[7]);
             }
         }
+        if (a.ymax) amax_lds_add(s_amax, mu < a.M ? fb : -1, vmax);
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) { xf[ks][0] = xn[ks][0]; xf[ks][1] = xn[ks][1]; }
     }
+    if (a.ymax) {
+        __syncthreads();
+        amax_lds_flush(s_amax, a.ymax, a.B);
+    }
 }
 
-template <int KS, int NTT, int ACT, int RES>
+template <int KS, int NTT, int ACT, int RES, int TERMS>
 hipError_t launch_stream_x6(const ConvArgs& a, hipStream_t s) {
     constexpr int NCH = 16 * NTT;
-    constexpr int lds = 3 * KS * NCH * 64 + 2 * NCH * 4;
+    constexpr int lds = TERMS * KS * NCH * 64 + 2 * NCH * 4;
     static const int resident = [] {
-        (void)hipFuncSetAttribute((const void*)conv1x1_x6_kernel<KS, NTT, ACT, RES>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        (void)hipFuncSetAttribute((const void*)conv1x1_x6_kernel<KS, NTT, ACT, RES, TERMS>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds + 4 * kAmaxFrames);
         int dev = 0, cus = 256, per_cu = 1;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv1x1_x6_kernel<KS, NTT, ACT, RES>, 512, lds);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv1x1_x6_kernel<KS, NTT, ACT, RES, TERMS>, 512,
+                                                           lds);
         return std::max(1, cus * std::max(1, per_cu));
     }();
     const int nchunks = a.cout / NCH;
     const int groups = (a.M + 15) / 16;
     int k = std::max(1, resident / (8 * nchunks));
     k = std::min(k, std::max(1, (groups + 63) / 64));
-    hipLaunchKernelGGL((conv1x1_x6_kernel<KS, NTT, ACT, RES>), dim3(8 * nchunks * k), dim3(512), lds, s, a, nchunks,
-                       groups);
+    hipLaunchKernelGGL((conv1x1_x6_kernel<KS, NTT, ACT, RES, TERMS>), dim3(8 * nchunks * k), dim3(512),
+                       lds + (a.ymax ? 4 * a.B : 0), s, a, nchunks, groups);
     return hipGetLastError();
 }
 
-template <int KS, int NTT>
+template <int KS, int NTT, int TERMS>
 hipError_t stream_mode_x6(const ConvArgs& a, hipStream_t s) {
     if (a.act == VD_ACT_RELU) {
-        if (a.res_mode == VD_RES_PRE_ACT) return launch_stream_x6<KS, NTT, VD_ACT_RELU, VD_RES_PRE_ACT>(a, s);
-        if (a.res_mode == VD_RES_NONE) return launch_stream_x6<KS, NTT, VD_ACT_RELU, VD_RES_NONE>(a, s);
+        if (a.res_mode == VD_RES_PRE_ACT) return launch_stream_x6<KS, NTT, VD_ACT_RELU, VD_RES_PRE_ACT, TERMS>(a, s);
+        if (a.res_mode == VD_RES_NONE) return launch_stream_x6<KS, NTT, VD_ACT_RELU, VD_RES_NONE, TERMS>(a, s);
     }
-    if (a.act == VD_ACT_NONE && a.res_mode == VD_RES_NONE) return launch_stream_x6<KS, NTT, VD_ACT_NONE, VD_RES_NONE>(a, s);
-    return hipErrorInvalidValue;   // excluded by vd_conv1x1_x6_ok
+    if (a.act == VD_ACT_NONE && a.res_mode == VD_RES_NONE)
+        return launch_stream_x6<KS, NTT, VD_ACT_NONE, VD_RES_NONE, TERMS>(a, s);
+    return hipErrorInvalidValue;   // excluded by stream_x6_nch
+}
+
+__global__ void amax_merge_kernel(unsigned* dst, const unsigned* src, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = max(dst[i], src[i]);
 }
 
 }  // namespace
+
+// max-pool / upsample outputs of the fp16-pair plan: the output's per-frame range is
+// within the input's (plate_net.cpp SPPF / Upsample, the f32 face stem's pool)
+hipError_t vd_launch_amax_merge(unsigned* dst, const unsigned* src, int n, hipStream_t s) {
+    hipLaunchKernelGGL(amax_merge_kernel, dim3((n + 63) / 64), dim3(64), 0, s, dst, src, n);
+    return hipGetLastError();
+}
 
 // Eligible: f32 activations with Cin padded to 4, K padded to 32, split weights present.
 bool vd_conv_x6_ok(const ConvArgs& a) {
@@ -580,12 +656,12 @@ bool vd_conv_x6_ok(const ConvArgs& a) {
            xbytes < 2147483647.0;
 }
 
-template <int BM, int BN, int NT, int NST>
+template <int BM, int BN, int NT, int NST, int TERMS>
 static hipError_t launch_x6(const ConvArgs& a0, hipStream_t s) {
-    using S = X6Shape<BM, BN, NT, NST>;
+    using S = X6Shape<BM, BN, NT, NST, TERMS>;
     static const bool attr = [] {
-        (void)hipFuncSetAttribute((const void*)conv_x6_kernel<BM, BN, NT, NST>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS);
+        (void)hipFuncSetAttribute((const void*)conv_x6_kernel<BM, BN, NT, NST, TERMS>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS + 4 * kAmaxFrames);
         return true;
     }();
     (void)attr;
@@ -593,7 +669,8 @@ static hipError_t launch_x6(const ConvArgs& a0, hipStream_t s) {
     a.w = a.wx3;                                   // the kernel reads the split planes
     a.ntiles_n = (a.cout + BN - 1) / BN;
     const int mt = (a.M + BM - 1) / BM;
-    hipLaunchKernelGGL((conv_x6_kernel<BM, BN, NT, NST>), dim3(mt * a.ntiles_n), dim3(NT), S::LDS, s, a);
+    const int lds = S::LDS + (a.ymax ? 4 * a.B : 0);
+    hipLaunchKernelGGL((conv_x6_kernel<BM, BN, NT, NST, TERMS>), dim3(mt * a.ntiles_n), dim3(NT), lds, s, a);
     return hipGetLastError();
 }
 
@@ -606,23 +683,27 @@ static hipError_t launch_x6(const ConvArgs& a0, hipStream_t s) {
 // Streaming 1x1 (conv1x1_x6_kernel): 1x1 taps without padding, K = Cin in {64, 128,
 // 256} (one channel slice of 128, or 64 at K = 256, fits 96 KB of LDS in three split
 // planes), ReLU with / without the pre-activation residual, or no activation.
-static int stream_x6_nch(const ConvArgs& a) {
+static int stream_x6_nch(const ConvArgs& a, int terms) {
     if (!a.tune || !a.tune->x6_stream || a.kh != 1 || a.kw != 1 || a.pad != 0 || a.kpad != a.cin_pad) return 0;
     if (a.cin_pad != 64 && a.cin_pad != 128 && a.cin_pad != 256) return 0;
     const bool mode = (a.act == VD_ACT_RELU && (a.res_mode == VD_RES_NONE || a.res_mode == VD_RES_PRE_ACT)) ||
                       (a.act == VD_ACT_NONE && a.res_mode == VD_RES_NONE);
     if (!mode || ((a.ldx | a.xcoff | a.ldy | a.ycoff) & 7)) return 0;
     if (a.res_mode != VD_RES_NONE && ((a.res_ld | a.res_coff) & 7)) return 0;
-    const int nch = a.cin_pad == 256 ? 64 : 128;
+    const int nch = (a.cin_pad == 256 && terms == 3) ? 64 : 128;
     if (a.cout % nch == 0) return nch;
     return a.cout % 64 == 0 && a.cin_pad <= 128 ? 64 : 0;
 }
 
-hipError_t vd_launch_conv_x6(const ConvArgs& a, hipStream_t s) {
-    if (const int nch = stream_x6_nch(a)) {
-        if (a.cin_pad == 64) return nch == 128 ? stream_mode_x6<2, 8>(a, s) : stream_mode_x6<2, 4>(a, s);
-        if (a.cin_pad == 128) return nch == 128 ? stream_mode_x6<4, 8>(a, s) : stream_mode_x6<4, 4>(a, s);
-        return stream_mode_x6<8, 4>(a, s);
+template <int TERMS>
+static hipError_t launch_terms(const ConvArgs& a0, hipStream_t s) {
+    ConvArgs a = a0;
+    if (TERMS == 2) a.scale = a.scale_x;              // the fp16 pair's per-channel rescaled BN scale
+    if (const int nch = stream_x6_nch(a, TERMS)) {
+        if (a.cin_pad == 64) return nch == 128 ? stream_mode_x6<2, 8, TERMS>(a, s) : stream_mode_x6<2, 4, TERMS>(a, s);
+        if (a.cin_pad == 128) return nch == 128 ? stream_mode_x6<4, 8, TERMS>(a, s) : stream_mode_x6<4, 4, TERMS>(a, s);
+        if constexpr (TERMS == 2) return stream_mode_x6<8, 8, TERMS>(a, s);
+        return stream_mode_x6<8, 4, TERMS>(a, s);
     }
     const int bn = a.cout <= 32 ? 32 : (a.cout <= 64 ? 64 : 128);
     const long big_tiles = (long)((a.M + 255) / 256) * ((a.cout + bn - 1) / bn);
@@ -630,13 +711,23 @@ hipError_t vd_launch_conv_x6(const ConvArgs& a, hipStream_t s) {
     const bool force_small = small_k >= (1 << 30);       // test hook: every layer on the small tile
     const bool small = force_small || (bn <= 64 && (a.kpad <= small_k || big_tiles < small_tiles));
     if (small) {
-        if (bn == 32) return launch_x6<128, 32, 256, 1>(a, s);
-        if (bn == 64) return launch_x6<128, 64, 256, 1>(a, s);
-        return launch_x6<128, 128, 256, 1>(a, s);
+        if (bn == 32) return launch_x6<128, 32, 256, 1, TERMS>(a, s);
+        if (bn == 64) return launch_x6<128, 64, 256, 1, TERMS>(a, s);
+        return launch_x6<128, 128, 256, 1, TERMS>(a, s);
     }
-    if (bn == 32) return launch_x6<256, 32, 512, 2>(a, s);
-    if (bn == 64) return launch_x6<256, 64, 512, 2>(a, s);
-    return launch_x6<256, 128, 512, 2>(a, s);
+    if (bn == 32) return launch_x6<256, 32, 512, 2, TERMS>(a, s);
+    if (bn == 64) return launch_x6<256, 64, 512, 2, TERMS>(a, s);
+    return launch_x6<256, 128, 512, 2, TERMS>(a, s);
+}
+
+hipError_t vd_launch_conv_x6(const ConvArgs& a, hipStream_t s) {
+    if (a.f32_split == 2) {
+        if (!a.scale_x || (a.ymax && a.B > kAmaxFrames)) return hipErrorInvalidValue;
+        return launch_terms<2>(a, s);
+    }
+    ConvArgs b = a;
+    b.xmax = nullptr;                                   // the bf16 triple needs no operand scaling
+    return launch_terms<3>(b, s);
 }
 
 // Host: pack f32 weights [npad][kpad] (k = tap * cin_pad + c) into the split layout
@@ -660,4 +751,30 @@ void vd_pack_x6(const float* w, int npad, int kpad, uint16_t* out) {
                 o[KT] = (uint16_t)(v >> 16);
                 o[2 * KT] = (uint16_t)(f2u(r2) >> 16);
             }
+}
+
+// Host: the fp16-pair layout [npad][kpad / 32][2][32] fp16 for f32_split = 2. Row n
+// is scaled by 2^e[n] so its largest |w| lies in [2^14, 2^15) (hi = RNE(w 2^e),
+// lo = RNE(w 2^e - hi)); row_inv[n] = 2^-e[n] is folded into the BN scale.
+void vd_pack_x3h(const float* w, int npad, int kpad, uint16_t* out, float* row_inv) {
+    const int nk = kpad / KT;
+    for (int n = 0; n < npad; ++n) {
+        float m = 0.f;
+        for (int k = 0; k < kpad; ++k) m = std::max(m, std::fabs(w[(size_t)n * kpad + k]));
+        int e = 0;
+        if (m > 0.f) {
+            (void)std::frexp(m, &e);
+            e = std::min(100, std::max(-100, 15 - e));
+        }
+        row_inv[n] = std::ldexp(1.f, -e);
+        for (int t = 0; t < nk; ++t)
+            for (int k = 0; k < KT; ++k) {
+                const float x = std::ldexp(w[(size_t)n * kpad + t * KT + k], e);
+                const _Float16 h = (_Float16)x;
+                const _Float16 l = (_Float16)(x - (float)h);
+                uint16_t* o = out + (((size_t)n * nk + t) * 2) * KT + k;
+                std::memcpy(o, &h, 2);
+                std::memcpy(o + KT, &l, 2);
+            }
+    }
 }

@@ -32,9 +32,10 @@ __global__ __launch_bounds__(256) void dwconv3x3_kernel(DwConvArgs a) {
     const int cv = a.c / N;
     const long idx = (long)blockIdx.x * 256 + threadIdx.x;
     const long total = (long)a.B * a.yh * a.yw * cv;
-    if (idx >= total) return;
-    const int g = (int)(idx % cv);
-    long pix = idx / cv;
+    const bool valid = idx < total;          // no early exit: the wave merges its output max
+    const long ic = valid ? idx : total - 1;
+    const int g = (int)(ic % cv);
+    long pix = ic / cv;
     const int ox = (int)(pix % a.yw);
     pix /= a.yw;
     const int oy = (int)(pix % a.yh);
@@ -62,9 +63,19 @@ __global__ __launch_bounds__(256) void dwconv3x3_kernel(DwConvArgs a) {
         }
     }
     T o[N];
+    float vmax = 0.f;
 #pragma unroll
-    for (int e = 0; e < N; ++e) o[e] = (T)act_apply(acc[e] * a.scale[c0 + e] + a.shift[c0 + e], a.act, a.slope);
-    *(u32x4*)((T*)a.y + (((size_t)b * a.yh + oy) * a.yw + ox) * a.ldy + a.ycoff + c0) = *(const u32x4*)o;
+    for (int e = 0; e < N; ++e) {
+        const float v = act_apply(acc[e] * a.scale[c0 + e] + a.shift[c0 + e], a.act, a.slope);
+        o[e] = (T)v;
+        vmax = fmaxf(vmax, fabsf(v));
+    }
+    if (a.ymax) {
+        AmaxTrack t;
+        if (valid) t.add(a.ymax, b, vmax);
+        t.publish(a.ymax);
+    }
+    if (valid) *(u32x4*)((T*)a.y + (((size_t)b * a.yh + oy) * a.yw + ox) * a.ldy + a.ycoff + c0) = *(const u32x4*)o;
 }
 
 }  // namespace

@@ -120,9 +120,12 @@ int vd_build_face(Ctx& c, const WMap& W) {
     int rc;
     F.mnet = find_t(W, "body.stage1.0.0.weight") != nullptr;   // cfg_mnet (face.py:35, retinaface.py:60)
     F.s2d = !c.f32 && !c.f16 && !F.mnet && H % 2 == 0 && Wd % 2 == 0;
+    c.amax_begin(0);
     if (F.s2d) rc = c.act(F.input, H / 2 + 1, Wd / 2 + 1, 16);
     else rc = c.act(F.input, H, Wd, cpad);
     if (rc) return rc;
+    F.input.amax = nullptr;            // letterboxed canvas: |pixel - mean| <= 255
+    F.input.bound = 255.f;
 
     Act feats[3];
     if (F.mnet) {
@@ -321,6 +324,8 @@ int vd_build_face(Ctx& c, const WMap& W) {
     if ((rc = c.dalloc((void**)&F.anchors, anc.size() * 4))) return rc;
     VD_CHECK_HIP(hipMemcpy(F.anchors, anc.data(), anc.size() * 4, hipMemcpyHostToDevice));
     if ((rc = vd_alloc_post(c, F.post, A, A))) return rc;   // a frame keeps at most A faces
+    F.net.amax = c.amax_region(0);
+    F.net.amax_bytes = F.net.amax ? c.amax_region_bytes() : 0;
     F.loaded = true;
     return VD_OK;
 }

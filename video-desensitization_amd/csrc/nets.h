@@ -22,13 +22,20 @@ struct Act {          // NHWC activation buffer sized for cfg.max_batch frames
     void* p = nullptr;
     int h = 0, w = 0, c = 0;   // c = channel stride
     bool f32 = false;
+    // fp16-pair plan (f32_split = 2): per-frame running max |x| [max_batch] that every
+    // producer folds its outputs into (conv_x6.hip AmaxTrack), or a static bound
+    // for the letterboxed canvas (amax NULL)
+    unsigned* amax = nullptr;
+    float bound = 0.f;
 };
 
 struct Conv {
     int cin = 0, cin_pad = 0, cout = 0, npad = 0, kh = 0, kw = 0, stride = 1, pad = 0, kpad = 0, act = 0;
     float slope = 0.f;
     void* w = nullptr;
-    void* wx3 = nullptr;       // fp32 + f32_split: [npad][kpad/32][3][32] bf16 planes (conv_x6.hip)
+    void* wx3 = nullptr;       // fp32 + f32_split: [npad][kpad/32][3][32] bf16 / [..][2][32] fp16 planes (conv_x6.hip)
+    float* scale_x = nullptr;  // fp16 pairs: BN scale times the row's 2^-e
+    int split = 0;             // fp32: VdTune::f32_split when the weights were packed
     float* scale = nullptr;
     float* shift = nullptr;
     double flops_per_px = 0;   // algorithmic FLOPs per output pixel (real Cin, no padding)
@@ -72,6 +79,8 @@ struct Op {
 
 struct Net {
     std::vector<Op> ops;
+    unsigned* amax = nullptr;                        // fp16-pair plan: this net's max slots, zeroed per run
+    size_t amax_bytes = 0;
     int stage_end[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // op index after each backbone stage (face: 0=stem,1..4=layerN)
     int conv_fam = 0;                                // timing family of its convs (0 face, 5 plate)
 };
@@ -171,6 +180,15 @@ struct Ctx {
     void* jpeg_planes = nullptr; size_t jpeg_planes_bytes = 0;
     hipEvent_t jpeg_ev = nullptr;                 // last H2D out of jpeg_host
     int jpeg_threads = 16;                        // host entropy-decode threads
+    // fp16-pair plan: per-frame activation max slots, one region per network (face 0,
+    // plates 1) of kAmaxActs activations x max_batch frames
+    static constexpr int kAmaxActs = 256;
+    unsigned* amax_pool = nullptr;
+    int amax_owner = 0;
+    int amax_next[2] = {0, 0};
+    int amax_begin(int owner);                    // builders: slots of `owner` restart
+    unsigned* amax_region(int owner) const { return amax_pool ? amax_pool + (size_t)owner * kAmaxActs * cfg.max_batch : nullptr; }
+    size_t amax_region_bytes() const { return (size_t)kAmaxActs * cfg.max_batch * 4; }
     bool timing = false;
     std::vector<TimedEv> ev_pool;
     size_t ev_used = 0;

@@ -206,6 +206,8 @@ struct Planner {
 int build_plan(Ctx& c, int ch, int cw, Net& net) {
     PlateNet& P = c.plate;
     Planner p{c, net, ch, cw};
+    net.amax = c.amax_region(1);
+    net.amax_bytes = net.amax ? c.amax_region_bytes() : 0;
     Act in = P.input;
     in.h = P.s2d ? ch / 2 + 1 : ch;
     in.w = P.s2d ? cw / 2 + 1 : cw;
@@ -287,9 +289,12 @@ int vd_build_plate(Ctx& c, const WMap& W) {
     }
     // buffers for the imgsz x imgsz canvas
     const int cpad = c.f32 ? 4 : 8;
+    c.amax_begin(1);
     if (P.s2d) rc = c.act(P.input, P.imgsz / 2 + 1, P.imgsz / 2 + 1, 16);
     else rc = c.act(P.input, P.imgsz, P.imgsz, cpad);
     if (rc) return rc;
+    P.input.amax = nullptr;            // letterboxed canvas / 255: in [0, 1]
+    P.input.bound = 1.f;
     for (const Buf& b : kBufs) {
         Act a;
         if ((rc = c.act(a, P.imgsz / b.div, P.imgsz / b.div, b.c))) return rc;

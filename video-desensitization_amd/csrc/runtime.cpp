@@ -92,6 +92,19 @@ int Ctx::act(Act& a, int h, int w, int c, bool f32out) {
     int rc = dalloc(&a.p, bytes);
     if (rc) return rc;
     hipMemset(a.p, 0, bytes);
+    a.amax = nullptr;
+    a.bound = 0.f;
+    if (f32 && tune.f32_split == 2) {
+        if (!amax_pool && (rc = dalloc((void**)&amax_pool, 2 * amax_region_bytes()))) return rc;
+        if (amax_next[amax_owner] >= kAmaxActs) return vd_set_error(VD_ERR_NOMEM, "activation range slots exhausted");
+        a.amax = amax_region(amax_owner) + (size_t)amax_next[amax_owner]++ * cfg.max_batch;
+    }
+    return VD_OK;
+}
+
+int Ctx::amax_begin(int owner) {
+    amax_owner = owner;
+    amax_next[owner] = 0;
     return VD_OK;
 }
 
@@ -173,11 +186,21 @@ int Ctx::upload_conv(Conv& cv, const std::vector<float>& w_oihw, const std::vect
         rc = dalloc(&cv.w, packed.size() * 4);
         if (rc) return rc;
         VD_CHECK_HIP(hipMemcpy(cv.w, packed.data(), packed.size() * 4, hipMemcpyHostToDevice));
-        if (tune.f32_split) {   // the same weights as three exact bf16 planes for conv_x6.hip
+        if (tune.f32_split == 2) {   // scaled fp16 pairs (conv_x6.hip, 3 products)
+            std::vector<uint16_t> sp(packed.size() * 2);
+            std::vector<float> row_inv(cv.npad), sx(cv.npad, 0.f);
+            vd_pack_x3h(packed.data(), cv.npad, cv.kpad, sp.data(), row_inv.data());
+            for (int n = 0; n < cv.cout; ++n) sx[n] = scale[n] * row_inv[n];
+            if ((rc = dalloc(&cv.wx3, sp.size() * 2)) || (rc = dalloc((void**)&cv.scale_x, cv.npad * 4))) return rc;
+            VD_CHECK_HIP(hipMemcpy(cv.wx3, sp.data(), sp.size() * 2, hipMemcpyHostToDevice));
+            VD_CHECK_HIP(hipMemcpy(cv.scale_x, sx.data(), cv.npad * 4, hipMemcpyHostToDevice));
+            cv.split = 2;
+        } else if (tune.f32_split) {   // the same weights as three exact bf16 planes for conv_x6.hip
             std::vector<uint16_t> sp(packed.size() * 3);
             vd_pack_x6(packed.data(), cv.npad, cv.kpad, sp.data());
             if ((rc = dalloc(&cv.wx3, sp.size() * 2))) return rc;
             VD_CHECK_HIP(hipMemcpy(cv.wx3, sp.data(), sp.size() * 2, hipMemcpyHostToDevice));
+            cv.split = 1;
         }
     } else {
         std::vector<uint16_t> h(packed.size());
@@ -412,6 +435,13 @@ int Ctx::run_conv_op(const Op& op, int f0, int n, int fam) {
     a.f16 = f16 ? 1 : 0;
     a.tune = &tune;
     a.wx3 = cv.wx3;
+    a.scale_x = cv.scale_x;
+    a.f32_split = cv.split;
+    a.xmax = op.x.amax ? op.x.amax + f0 : nullptr;
+    a.xbound = op.x.bound;
+    a.ymax = op.y.amax ? op.y.amax + f0 : nullptr;
+    if (cv.split == 2 && !a.xmax && !(a.xbound > 0.f))
+        return vd_set_error(VD_ERR_ARG, "internal: conv input without a range (fp16-pair plan)");
     double flops = cv.flops_per_px * a.M;
     if (op.conv2 >= 0) {
         const Conv& c2 = convs[op.conv2];
@@ -487,11 +517,19 @@ int Ctx::run_dwconv_op(const Op& op, int f0, int n) {
     a.w = d.w; a.scale = d.scale; a.shift = d.shift;
     a.y = (void*)foff(op.y, f0); a.yh = op.y.h; a.yw = op.y.w; a.ldy = op.y.c; a.ycoff = 0;
     a.B = n; a.c = d.c; a.stride = d.stride; a.act = d.act; a.slope = d.slope;
+    a.ymax = op.y.amax ? op.y.amax + f0 : nullptr;
     t_begin(4, 0);
     hipError_t e = vd_launch_dwconv(a, f32, f16, stream);
     t_end();
     if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "depthwise conv: %s", hipGetErrorString(e));
     return VD_OK;
+}
+
+// max-pool / upsample: the output's per-frame range is within the input's
+static hipError_t amax_follow_impl(const Op& op, int f0, int n, hipStream_t s) {
+    if (!op.y.amax) return hipSuccess;
+    if (!op.x.amax) return op.x.bound > 0.f ? hipErrorInvalidValue : hipSuccess;
+    return vd_launch_amax_merge(op.y.amax + f0, op.x.amax + f0, n, s);
 }
 
 int Ctx::run_ops(const Net& net, int b, int e, int f0, int n) {
@@ -514,12 +552,14 @@ int Ctx::run_ops(const Net& net, int b, int e, int f0, int n) {
                                               (void*)foff(op.y, f0), op.y.h, op.y.w, op.y.c, op.ycoff, op.ch, op.k,
                                               op.s, op.p, stream);
             t_end();
+            if (er == hipSuccess) er = amax_follow_impl(op, f0, n, stream);
             if (er != hipSuccess) rc = vd_set_error(VD_ERR_HIP, "maxpool: %s", hipGetErrorString(er));
         } else if (op.kind == OP_UPSAMPLE) {
             t_begin(4, 0);
             hipError_t er = vd_launch_upsample2x(f32, foff(op.x, f0), n, op.x.h, op.x.w, op.x.c, op.xcoff,
                                                  (void*)foff(op.y, f0), op.y.c, op.ycoff, op.ch, stream);
             t_end();
+            if (er == hipSuccess) er = amax_follow_impl(op, f0, n, stream);
             if (er != hipSuccess) rc = vd_set_error(VD_ERR_HIP, "upsample: %s", hipGetErrorString(er));
         }
         if (rc) return rc;
@@ -533,6 +573,7 @@ int Ctx::run_ops(const Net& net, int b, int e, int f0, int n) {
 // over the whole batch (the small late layers need the whole batch to fill 256 CUs).
 int Ctx::run_net(const Net& net, int n, int mb, int split) {
     const int ne = (int)net.ops.size();
+    if (net.amax) VD_CHECK_HIP(hipMemsetAsync(net.amax, 0, net.amax_bytes, stream));
     if (mb <= 0 || mb >= n || split <= 0) return run_ops(net, 0, ne, 0, n);
     for (int f0 = 0; f0 < n; f0 += mb) {
         int rc = run_ops(net, 0, split, f0, std::min(mb, n - f0));
@@ -1270,6 +1311,24 @@ int vdt_conv2d(vd_ctx* h, const float* x, int n, int xh, int xw, int cin, const 
     a.act = act; a.slope = slope; a.out_f32 = 1; a.f16 = ctx->f16 ? 1 : 0;
     a.tune = &ctx->tune;
     a.wx3 = cv.wx3;
+    a.scale_x = cv.scale_x;
+    a.f32_split = cv.split;
+    // fp16-pair plan: the input's per-frame max |x| as a producer would have left it,
+    // and the output's slots, checked below against the host max of the result
+    unsigned* dm = nullptr;
+    const bool ranged = cv.split == 2;
+    if (ranged) {
+        std::vector<unsigned> xm(2 * n, 0u);
+        for (int b = 0; b < n; ++b) {
+            float m = 0.f;
+            for (size_t i = (size_t)b * xh * xw * cin; i < (size_t)(b + 1) * xh * xw * cin; ++i) m = std::max(m, std::fabs(x[i]));
+            memcpy(&xm[b], &m, 4);
+        }
+        if ((rc = ctx->dalloc((void**)&dm, xm.size() * 4))) return rc;
+        VD_CHECK_HIP(hipMemcpy(dm, xm.data(), xm.size() * 4, hipMemcpyHostToDevice));
+        a.xmax = dm;
+        a.ymax = dm + n;
+    }
     hipError_t e = vd_launch_conv(a, ctx->f32, ctx->stream);
     if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "conv launch: %s", hipGetErrorString(e));
     VD_CHECK_HIP(hipStreamSynchronize(ctx->stream));
@@ -1277,6 +1336,19 @@ int vdt_conv2d(vd_ctx* h, const float* x, int n, int xh, int xw, int cin, const 
     VD_CHECK_HIP(hipMemcpy(yb.data(), dy, yb.size() * 4, hipMemcpyDeviceToHost));
     for (size_t p = 0; p < (size_t)n * oh * ow; ++p)
         for (int c = 0; c < cout; ++c) y[p * cout + c] = yb[p * ldy + c];
+    if (ranged && cv.wx3) {
+        std::vector<float> ym(n);
+        VD_CHECK_HIP(hipMemcpy(ym.data(), dm + n, n * 4, hipMemcpyDeviceToHost));
+        for (int b = 0; b < n; ++b) {
+            float m = 0.f;
+            for (size_t i = (size_t)b * oh * ow * cout; i < (size_t)(b + 1) * oh * ow * cout; ++i) m = std::max(m, std::fabs(y[i]));
+            if (m != ym[b]) {
+                for (size_t i = nalloc; i < ctx->allocs.size(); ++i) hipFree(ctx->allocs[i]);
+                ctx->allocs.resize(nalloc);
+                return vd_set_error(VD_ERR_HIP, "frame %d: output max slot %g, host max %g", b, ym[b], m);
+            }
+        }
+    }
     if (oh_out) *oh_out = oh;
     if (ow_out) *ow_out = ow;
     // release this call's temporaries

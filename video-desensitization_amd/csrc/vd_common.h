@@ -38,8 +38,10 @@ struct VdTune {
     int x6_stream = 1;        // fp32 split: streaming 1x1 kernel for K in {64, 128, 256}
     int x6_small_k = 256;     // fp32 split: K at or below which the small single-stage tile runs
     int x6_small_tiles = 512; //   ... and big-tile grids smaller than this (0 / 0: big tile always)
-    int f32_split = 1;        // plan (fp32): convs on bf16 MFMA by exact 3-term operand split
-                              //   (conv_x6.hip); 0: exact-f32 v_mfma_f32_16x16x4_f32 (conv.hip)
+    int f32_split = 2;        // plan (fp32, at weight load): 2 = operands scaled by powers of two
+                              //   and split into fp16 pairs, 3 products on the f16 matrix cores;
+                              //   1 = exact 3-term bf16 split, 6 products (conv_x6.hip);
+                              //   0 = exact-f32 v_mfma_f32_16x16x4_f32 (conv.hip)
 };
 
 // Implicit-GEMM convolution parameters (device side). Activations are NHWC with
@@ -64,7 +66,14 @@ struct ConvArgs {
     const void* x2; int xh2, xw2, ldx2, xcoff2, stride2;
     const void* w2; const float* scale2; const float* shift2; int cin2_pad, kpad2;
     const VdTune* tune;                          // host-side kernel selection (never read on the device)
-    const void* wx3;                             // fp32: weights split into 3 bf16 planes (conv_x6.hip), or NULL
+    const void* wx3;                             // fp32: split weights (conv_x6.hip: 3 bf16 / 2 fp16 planes), or NULL
+    // f32_split = 2 (fp16 pair): per-channel BN scale with the weight rows' 2^-e folded in,
+    // the input's running max |x| (device slot, or a static bound when NULL) and the
+    // output's slot (atomic max of |y|; NULL: not tracked)
+    const float* scale_x;
+    int f32_split;                               // the conv's weight format (Conv::split at load)
+    const unsigned* xmax; float xbound;
+    unsigned* ymax;
 };
 
 // One fused layer1 bottleneck (block.hip): x [B][H][W][cin] -> y [B][H][W][256],
@@ -103,6 +112,7 @@ struct DwConvArgs {
     const float* scale; const float* shift;
     void* y; int yh, yw, ldy, ycoff;
     int B, c, stride, act; float slope;
+    unsigned* ymax;                              // fp16-pair plan: per-frame max |y| slots, or NULL
 };
 
 // RetinaFace stem conv (space-to-depth form) + maxpool in one kernel (stem.hip):
@@ -191,7 +201,73 @@ struct JpegArgs {
     uint8_t* out; size_t pitch;                 // RGB frames [n][h][pitch]
 };
 
+// TERMS = 2 (fp16 pair): each frame's activations are scaled by a power of two so
+// their largest magnitude (the producer's per-frame running max, or a static bound
+// for the letterboxed canvas) lands in [2^14, 2^15): fp16 never overflows and the
+// low term stays normal down to 2^-2 of that. A row (pixel) keeps one scale over
+// all of K, so the accumulator is scaled back per row in the epilogue (exact:
+// powers of two), and a frame's result does not depend on the rest of its batch.
+// Returns the exponent k (operand * 2^k) for frame b.
+__device__ __forceinline__ int act_scale_exp(const ConvArgs& a, int b) {
+    const float m = a.xmax ? __uint_as_float(a.xmax[b]) : a.xbound;
+    if (!(m > 0.f) || !(m < 3.0e38f)) return 0;
+    int e;
+    (void)frexpf(m, &e);                              // m < 2^e
+    const int k = 15 - e;
+    return k < -100 ? -100 : (k > 100 ? 100 : k);
+}
+
+// Per-frame running max |y| into the output's slots (non-negative floats order as
+// their bit patterns; NaNs are ignored). A lane folds its outputs into (frame, max)
+// and flushes on a frame change (rows only ascend, so rarely); at the end the wave
+// merges the lanes of its lowest frame into one atomic.
+struct AmaxTrack {
+    int b = -1;
+    float m = 0.f;
+    __device__ __forceinline__ void add(unsigned* slot, int fb, float v) {
+        if (fb != b) {
+            if (b >= 0 && m > 0.f) atomicMax(slot + b, __float_as_uint(m));
+            b = fb;
+            m = 0.f;
+        }
+        m = fmaxf(m, v);
+    }
+    __device__ __forceinline__ void publish(unsigned* slot) {
+        int lo = b >= 0 ? b : 0x7fffffff;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) lo = min(lo, __shfl_xor(lo, o));
+        float v = (b == lo) ? m : 0.f;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+        if ((threadIdx.x & 63) == 0 && lo != 0x7fffffff && v > 0.f) atomicMax(slot + lo, __float_as_uint(v));
+        if (b >= 0 && b != lo && m > 0.f) atomicMax(slot + b, __float_as_uint(m));
+    }
+};
+
+// Workgroup-local form for the conv kernels (one launch touches every frame, so
+// per-lane global atomics would serialise on 64 addresses): every lane of a wave
+// calls amax_lds_add convergently with its output's frame (-1: none) and max |y|;
+// the wave merges its lowest frame into one LDS atomic (other frames: rare, per
+// lane), and amax_lds_flush moves the workgroup's nonzero slots to global.
+__device__ __forceinline__ void amax_lds_add(unsigned* s, int fb, float v) {
+    int lo = fb >= 0 ? fb : 0x7fffffff;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) lo = min(lo, __shfl_xor(lo, o));
+    if (lo == 0x7fffffff) return;                     // wave-uniform
+    float m = (fb == lo) ? v : 0.f;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0 && m > 0.f) atomicMax(s + lo, __float_as_uint(m));
+    if (fb >= 0 && fb != lo && v > 0.f) atomicMax(s + fb, __float_as_uint(v));
+}
+
+__device__ __forceinline__ void amax_lds_flush(const unsigned* s, unsigned* g, int nframes) {
+    for (int f = threadIdx.x; f < nframes; f += blockDim.x)
+        if (s[f]) atomicMax(g + f, s[f]);
+}
+
 // ---- kernel launchers (one translation unit each) ----
+hipError_t vd_launch_amax_merge(unsigned* dst, const unsigned* src, int n, hipStream_t s);
 bool vd_conv1x1_stream_ok(const ConvArgs& a);
 bool vd_conv_big_ok(const ConvArgs& a);
 hipError_t vd_launch_conv_big(const ConvArgs& a, hipStream_t s);
@@ -203,6 +279,7 @@ hipError_t vd_launch_conv(const ConvArgs& a, bool f32, hipStream_t s);
 bool vd_conv_x6_ok(const ConvArgs& a);
 hipError_t vd_launch_conv_x6(const ConvArgs& a, hipStream_t s);
 void vd_pack_x6(const float* w, int npad, int kpad, uint16_t* out);   // host: f32 [npad][kpad] -> split planes
+void vd_pack_x3h(const float* w, int npad, int kpad, uint16_t* out, float* row_inv);   // ... fp16 pairs
 bool vd_block_ok(int cin, bool ds, int h, int w);
 bool vd_stem_pool_ok(int xh, int xw, int ph, int pw);
 hipError_t vd_launch_dwconv(const DwConvArgs& a, bool f32, bool f16, hipStream_t s);
