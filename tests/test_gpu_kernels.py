@@ -171,6 +171,7 @@ CONV_CASES = [
     (1, 12, 10, 256, 32, 1, 1, 0, 0, 0),      # heads (BN=32 tile)
     (1, 9, 11, 512, 200, 3, 1, 1, 2, 1),      # cout not a tile multiple, leaky
     (2, 23, 21, 256, 192, 3, 1, 1, 1, 0),     # 192-wide N tile: fused SSH conv5X5_1 + conv3X3
+    (2, 13, 11, 256, 512, 3, 1, 1, 1, 1),     # fp32 pairs: 256 x 256 tile, two N tiles, residual, M tail
     (1, 15, 17, 64, 160, 3, 1, 1, 2, 1),      # 192-wide N tile, cout 160, leaky + residual
     # 1x1 streaming kernel (bf16, K 64/128/256/512): bottleneck conv3 / conv1 / downsample shapes
     (2, 21, 23, 64, 256, 1, 1, 0, 1, 1),      # conv3 + residual, M not a multiple of 16
@@ -214,7 +215,7 @@ def test_conv_matches_torch(gpu, face_ctx_factory, prec, case, options=None):
         options.update(f32_split=0)
         prec = "fp32"
     if prec in ("fp32-big", "fp32-small"):    # force one x6 tile form (conv_x6.hip)
-        options.update(x6_small_k=0, x6_small_tiles=0, x6_stream=0) if prec == "fp32-big" else \
+        options.update(x6_small_k=0, x6_small_k2=0, x6_small_tiles=0, x6_stream=0) if prec == "fp32-big" else \
             options.update(x6_small_k=1 << 30, x6_stream=0)
         prec = "fp32"
     if prec.startswith("bf16-gemm"):

@@ -288,22 +288,42 @@ __global__ __launch_bounds__(NT) void conv_x6_kernel(ConvArgs a) {
         const char* A = smem + st * STAGE;
         const char* Bs = A + TERMS * PL_A;
         const int ch = lane >> 4;
-        u32x4 bf[TN][3];
+        if constexpr (TN > TM) {   // wide wave tile: all A fragments resident, B fragments streamed
+            u32x4 af[TM][3];
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
+            for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int p = 0; p < TERMS; ++p)
-                bf[j][p] = *(const u32x4*)(Bs + p * PL_B + swz(wn * S::WTN + j * 16 + (lane & 15), ch));
+                for (int p = 0; p < TERMS; ++p)
+                    af[i][p] = *(const u32x4*)(A + p * PL_A + swz(wm * S::WTM + i * 16 + (lane & 15), ch));
 #pragma unroll
-        for (int i = 0; i < TM; ++i) {
-            u32x4 af[3];
+            for (int j = 0; j < TN; ++j) {
+                u32x4 bf[3];
 #pragma unroll
-            for (int p = 0; p < TERMS; ++p)
-                af[p] = *(const u32x4*)(A + p * PL_A + swz(wm * S::WTM + i * 16 + (lane & 15), ch));
+                for (int p = 0; p < TERMS; ++p)
+                    bf[p] = *(const u32x4*)(Bs + p * PL_B + swz(wn * S::WTN + j * 16 + (lane & 15), ch));
 #pragma unroll
-            for (int j = 0; j < TN; ++j) acc[i][j] = mfma_terms<TERMS>(af, bf[j], acc[i][j]);
-            if (split_next && i == 0) store_item(st_next, rn, 0);
-            if (split_next && i == (TM > 2 ? 2 : 1)) store_item(st_next, rn, 1);
+                for (int i = 0; i < TM; ++i) acc[i][j] = mfma_terms<TERMS>(af[i], bf, acc[i][j]);
+                if (split_next && j == 0) store_item(st_next, rn, 0);
+                if (split_next && j == TN / 2) store_item(st_next, rn, 1);
+            }
+        } else {
+            u32x4 bf[TN][3];
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int p = 0; p < TERMS; ++p)
+                    bf[j][p] = *(const u32x4*)(Bs + p * PL_B + swz(wn * S::WTN + j * 16 + (lane & 15), ch));
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                u32x4 af[3];
+#pragma unroll
+                for (int p = 0; p < TERMS; ++p)
+                    af[p] = *(const u32x4*)(A + p * PL_A + swz(wm * S::WTM + i * 16 + (lane & 15), ch));
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[i][j] = mfma_terms<TERMS>(af, bf[j], acc[i][j]);
+                if (split_next && i == 0) store_item(st_next, rn, 0);
+                if (split_next && i == (TM > 2 ? 2 : 1)) store_item(st_next, rn, 1);
+            }
         }
     };
 
@@ -372,6 +392,8 @@ __global__ __launch_bounds__(NT) void conv_x6_kernel(ConvArgs a) {
     const bool vec_ok = ((a.cout & 7) == 0) && ((a.ldy & 7) == 0) && ((a.ycoff & 7) == 0) &&
                         (a.res_mode == VD_RES_NONE || (((a.res_ld | a.res_coff) & 7) == 0));
     unsigned* s_amax = (unsigned*)(smem + S::LDS);     // per-frame max |y| of this tile (a.ymax)
+    int tfb = -1;                                      // this thread's first frame and its running max;
+    float tmax = 0.f;                                  // items of a later frame go to LDS directly (rare)
 #pragma unroll
     for (int h = 0; h < BM / EPR; ++h) {
         if (h) __syncthreads();
@@ -449,10 +471,15 @@ __global__ __launch_bounds__(NT) void conv_x6_kernel(ConvArgs a) {
                 }
             }
             }   // valid
-            if (a.ymax) amax_lds_add(s_amax, fb, vmax);
+            if (valid && a.ymax) {
+                if (tfb < 0) tfb = fb;
+                if (fb == tfb) tmax = fmaxf(tmax, vmax);
+                else if (vmax > 0.f) atomicMax(s_amax + fb, __float_as_uint(vmax));
+            }
         }
     }
     if (a.ymax) {
+        amax_lds_add(s_amax, tfb, tmax);
         __syncthreads();
         amax_lds_flush(s_amax, a.ymax, a.B);
     }
@@ -708,8 +735,12 @@ static hipError_t launch_terms(const ConvArgs& a0, hipStream_t s) {
     const int bn = a.cout <= 32 ? 32 : (a.cout <= 64 ? 64 : 128);
     const long big_tiles = (long)((a.M + 255) / 256) * ((a.cout + bn - 1) / bn);
     const int small_k = a.tune ? a.tune->x6_small_k : 256, small_tiles = a.tune ? a.tune->x6_small_tiles : 512;
+    const int small_k2 = a.tune ? a.tune->x6_small_k2 : (1 << 20);
     const bool force_small = small_k >= (1 << 30);       // test hook: every layer on the small tile
-    const bool small = force_small || (bn <= 64 && (a.kpad <= small_k || big_tiles < small_tiles));
+    // fp16 pairs: the 4-wave one-stage tile wins for every N <= 64 layer measured
+    // (layer1 conv2 831 -> 603 us, SSH level-0 conv7X7 229 -> 163 us)
+    const bool small = force_small || (bn <= 64 && (a.kpad <= (TERMS == 2 ? small_k2 : small_k) ||
+                                                    big_tiles < small_tiles));
     if (small) {
         if (bn == 32) return launch_x6<128, 32, 256, 1, TERMS>(a, s);
         if (bn == 64) return launch_x6<128, 64, 256, 1, TERMS>(a, s);
@@ -717,6 +748,13 @@ static hipError_t launch_terms(const ConvArgs& a0, hipStream_t s) {
     }
     if (bn == 32) return launch_x6<256, 32, 512, 2, TERMS>(a, s);
     if (bn == 64) return launch_x6<256, 64, 512, 2, TERMS>(a, s);
+    if constexpr (TERMS == 2) {   // 64 x 128 wave tiles: 2/3 of the LDS fragment reads per MFMA
+        // (layer3/4 and FPN 12-20 % faster than 256 x 128; not below ~200 tiles: FPN output3,
+        // 100 tiles, 137 -> 199 us)
+        const long t256 = (long)((a.M + 255) / 256) * (a.cout / 256);
+        if (a.tune && a.tune->x6_bn256 && a.cout % 256 == 0 && t256 >= 192)
+            return launch_x6<256, 256, 512, 2, TERMS>(a, s);
+    }
     return launch_x6<256, 128, 512, 2, TERMS>(a, s);
 }
 

@@ -881,7 +881,7 @@ int vd_set_option(vd_ctx* h, const char* name, int value) {
         {"chain", &VdTune::chain}, {"stem_pool", &VdTune::stem_pool}, {"ssh_fuse", &VdTune::ssh_fuse},
         {"plate_s2d", &VdTune::plate_s2d}, {"f32_split", &VdTune::f32_split},
         {"x6_small_k", &VdTune::x6_small_k}, {"x6_small_tiles", &VdTune::x6_small_tiles},
-        {"x6_stream", &VdTune::x6_stream},
+        {"x6_stream", &VdTune::x6_stream}, {"x6_small_k2", &VdTune::x6_small_k2}, {"x6_bn256", &VdTune::x6_bn256},
     };
     for (const Opt& o : opts)
         if (strcmp(o.n, name) == 0) {

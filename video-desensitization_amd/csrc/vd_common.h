@@ -38,6 +38,8 @@ struct VdTune {
     int x6_stream = 1;        // fp32 split: streaming 1x1 kernel for K in {64, 128, 256}
     int x6_small_k = 256;     // fp32 split: K at or below which the small single-stage tile runs
     int x6_small_tiles = 512; //   ... and big-tile grids smaller than this (0 / 0: big tile always)
+    int x6_small_k2 = 1 << 20;//   fp16 pairs: K at or below which N <= 64 layers take the small tile
+    int x6_bn256 = 1;         // fp16 pairs: 256 x 256 tile for Cout % 256 == 0
     int f32_split = 2;        // plan (fp32, at weight load): 2 = operands scaled by powers of two
                               //   and split into fp16 pairs, 3 products on the f16 matrix cores;
                               //   1 = exact 3-term bf16 split, 6 products (conv_x6.hip);
