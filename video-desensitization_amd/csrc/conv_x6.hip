@@ -754,6 +754,11 @@ static hipError_t launch_terms(const ConvArgs& a0, hipStream_t s) {
         const long t256 = (long)((a.M + 255) / 256) * (a.cout / 256);
         if (a.tune && a.tune->x6_bn256 && a.cout % 256 == 0 && t256 >= 192)
             return launch_x6<256, 256, 512, 2, TERMS>(a, s);
+        // Cout 192 (the fused SSH conv5X5_1 + conv3X3): one 192-wide N tile instead of two
+        // 128-wide ones with a quarter of the MFMAs on padding rows (level 0 1716 -> 1264 us,
+        // level 1 526 -> 396; not for level 2's 100 tiles: 137 -> 178)
+        if (a.tune && a.tune->x6_bn256 && a.cout == 192 && (a.M + 255) / 256 >= 192)
+            return launch_x6<256, 192, 512, 2, TERMS>(a, s);
     }
     return launch_x6<256, 128, 512, 2, TERMS>(a, s);
 }
