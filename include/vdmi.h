@@ -162,6 +162,16 @@ int vd_process(vd_ctx* ctx, const uint8_t* in, uint8_t* out, int n, int h, int w
 int vd_jpeg_decode(vd_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n, uint8_t* out,
                    int h, int w, size_t pitch, int where);
 int vd_jpeg_info(const uint8_t* data, size_t size, int* h, int* w, int* comps);
+/* RGB frames -> baseline JFIF: the frame write of the reference's loop (cv2.imwrite
+ * of the processed frames, combine_detect.py:174-180, :259-262; cv2's defaults are
+ * quality 95, 4:2:0), libjpeg-turbo's compressor with its defaults bit-identical
+ * (Pillow Image.save(..., quality, subsampling) bytes). frames: n frames h x w x 3
+ * RGB at `where`; subsampling 0 = 4:4:4, 1 = 4:2:2, 2 = 4:2:0. Colour conversion,
+ * downsampling, ISLOW FDCT and quantisation in a HIP kernel, Huffman coding on host
+ * threads. Frame i goes to out + i * cap, its length to sizes[i]; VD_ERR_CAPACITY
+ * if a frame needs more than cap bytes. Returns when every frame is written. */
+int vd_jpeg_encode(vd_ctx* ctx, const uint8_t* frames, int n, int h, int w, size_t pitch, int where,
+                   int quality, int subsampling, uint8_t* out, size_t cap, size_t* sizes);
 /* The complete keep lists of the last vd_detect / vd_detect_plates / vd_process
  * call on this context for frames [0, n) of `net` (VD_NET_*), into `out`
  * (min(count, out->cap) boxes per frame; count = complete count). Ordered on the

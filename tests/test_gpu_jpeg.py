@@ -1,4 +1,4 @@
-"""vd_jpeg_decode on the GPU: bit-exact against Pillow's libjpeg-turbo (and the
+"""vd_jpeg_decode / vd_jpeg_encode on the GPU: bit-exact against Pillow's libjpeg-turbo (and the
 oracle) for every supported layout, batched 1080p frames decoded straight into
 device memory, and those frames through vd_process identical to host-decoded ones."""
 import io
@@ -68,3 +68,42 @@ def test_batch_1080p_device_decode_and_process(jctx):
             np.testing.assert_array_equal(lists_d.frame(b)[0], lists_h.frame(b)[0])
     finally:
         jctx.set_stream(None)
+
+
+# ------------------------------------------------------------------ encode (vd_jpeg_encode)
+from test_jpeg_enc import ENC_CASES, frame as enc_frame, pillow_jpeg  # noqa: E402
+
+
+@pytest.mark.parametrize("case", ENC_CASES)
+def test_encode_matches_pillow_bytes(jctx, case):
+    h, w, q, sub = case
+    imgs = np.stack([enc_frame(h, w, seed=s) for s in range(3)])
+    got = jctx.jpeg_encode(imgs, quality=q, subsampling=sub)
+    for img, g in zip(imgs, got):
+        assert g == pillow_jpeg(img, q, sub)
+
+
+def test_encode_noise_needs_the_retry_capacity(jctx):
+    rng = np.random.default_rng(11)
+    noise = rng.integers(0, 256, (2, 48, 64, 3), dtype=np.uint8)
+    got = jctx.jpeg_encode(noise, quality=100, subsampling=0)       # > 3 B/pixel: second capacity pass
+    for img, g in zip(noise, got):
+        assert g == pillow_jpeg(img, 100, 0)
+
+
+def test_encode_1080p_from_device_frames_after_process(jctx):
+    """The reference's per-frame write (cv2.imwrite, q95, 4:2:0) of mosaicked frames
+    that never leave the GPU: vd_process output -> vd_jpeg_encode from device memory;
+    bytes equal Pillow's encode of the same frames, and decode back bit-exactly."""
+    import torch
+    from vdmi import synth
+    dev = torch.device("cuda:0")
+    fr = torch.from_numpy(synth.frames(4, 1080, 1920, seed=9)).to(dev)
+    out, _, _ = jctx.process(fr)
+    torch.cuda.synchronize()
+    got = jctx.jpeg_encode(out, quality=95, subsampling=2)
+    host = out.cpu().numpy()
+    for img, g in zip(host, got):
+        assert g == pillow_jpeg(img, 95, 2)
+    back = jctx.jpeg_decode(got)
+    np.testing.assert_array_equal(back, np.stack([pillow_rgb(g) for g in got]))

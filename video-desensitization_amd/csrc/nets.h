@@ -178,7 +178,10 @@ struct Ctx {
     void* jpeg_host = nullptr; size_t jpeg_host_bytes = 0;
     void* jpeg_dev = nullptr; size_t jpeg_dev_bytes = 0;
     void* jpeg_planes = nullptr; size_t jpeg_planes_bytes = 0;
-    hipEvent_t jpeg_ev = nullptr;                 // last H2D out of jpeg_host
+    hipEvent_t jpeg_ev = nullptr;                 // last H2D out of jpeg_host / jenc_host
+    // JPEG frame encode (jpeg_enc.cpp): device coefficients + tables, pinned host copy
+    void* jenc_dev = nullptr; size_t jenc_dev_bytes = 0;
+    void* jenc_host = nullptr; size_t jenc_host_bytes = 0;
     int jpeg_threads = 16;                        // host entropy-decode threads
     // fp16-pair plan: per-frame activation max slots, one region per network (face 0,
     // plates 1) of kAmaxActs activations x max_batch frames

@@ -837,6 +837,8 @@ int vd_destroy(vd_ctx* h) {
     if (ctx->jpeg_dev) hipFree(ctx->jpeg_dev);
     if (ctx->jpeg_planes) hipFree(ctx->jpeg_planes);
     if (ctx->jpeg_host) hipHostFree(ctx->jpeg_host);
+    if (ctx->jenc_dev) hipFree(ctx->jenc_dev);
+    if (ctx->jenc_host) hipHostFree(ctx->jenc_host);
     if (ctx->jpeg_ev) hipEventDestroy(ctx->jpeg_ev);
     for (auto& t : ctx->ev_pool) { hipEventDestroy(t.a); hipEventDestroy(t.b); }
     hipStreamSynchronize(ctx->stream2);

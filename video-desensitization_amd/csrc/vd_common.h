@@ -268,7 +268,18 @@ __device__ __forceinline__ void amax_lds_flush(const unsigned* s, unsigned* g, i
         if (s[f]) atomicMax(g + f, s[f]);
 }
 
+// One batch of RGB frames -> quantized coefficient blocks (jpeg_enc.hip -> jpeg_enc.cpp).
+struct JpegEncArgs {
+    const uint8_t* src; size_t pitch; int n, h, w;
+    int hl, vl;                                 // luma sampling factors (chroma 1x1)
+    int bw[3], bh[3];                           // blocks per component (width/height_in_blocks)
+    long cblk[3], blocks_per_frame;             // first block of each component within a frame
+    const uint16_t* recip; const uint16_t* corr; const uint8_t* shift;   // [2 tables][64], natural order
+    int16_t* coef;                              // [n][blocks_per_frame][64] natural order
+};
+
 // ---- kernel launchers (one translation unit each) ----
+hipError_t vd_launch_jpeg_fdct(const JpegEncArgs& a, hipStream_t s);
 hipError_t vd_launch_amax_merge(unsigned* dst, const unsigned* src, int n, hipStream_t s);
 bool vd_conv1x1_stream_ok(const ConvArgs& a);
 bool vd_conv_big_ok(const ConvArgs& a);

@@ -77,6 +77,7 @@ SIGNATURES = [
     ("vd_read_boxes", _I, [_P, _I, _I, ctypes.POINTER(vd_boxes)]),
     ("vd_jpeg_decode", _I, [_P, ctypes.POINTER(_P), ctypes.POINTER(_SZ), _I, _P, _I, _I, _SZ, _I]),
     ("vd_jpeg_info", _I, [_P, _SZ, ctypes.POINTER(_I), ctypes.POINTER(_I), ctypes.POINTER(_I)]),
+    ("vd_jpeg_encode", _I, [_P, _P, _I, _I, _I, _SZ, _I, _I, _I, _P, _SZ, ctypes.POINTER(_SZ)]),
     ("vd_timing_enable", _I, [_P, _I]),
     ("vd_timing_reset", _I, [_P]),
     ("vd_timing_read", _I, [_P, _I, ctypes.POINTER(_D), ctypes.POINTER(ctypes.c_int64),

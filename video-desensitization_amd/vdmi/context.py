@@ -252,6 +252,26 @@ class Context:
         check(self._lib.vd_jpeg_decode(self._h, ptrs, sizes, n, optr, h, w, w * 3, where))
         return out
 
+    def jpeg_encode(self, frames, quality=95, subsampling=2):
+        """RGB uint8 frames [n,h,w,3] (numpy, or a torch tensor on the GPU: encoded
+        from device memory, no D2H of pixels) -> list of JFIF bytes, bit-identical to
+        libjpeg-turbo's compressor (Pillow ``Image.save(..., quality=quality,
+        subsampling=subsampling)``; cv2.imwrite's defaults are quality 95, 4:2:0 --
+        the reference's frame write, combine_detect.py:174-180)."""
+        p, n, h, w, pitch, where, keep = _frames_arg(frames)
+        sizes = (ctypes.c_size_t * n)()
+        # typical frames need < 3 B/pixel; the retry bound covers any baseline block
+        # (63 AC codes of 26 bits + DC, every byte stuffed) at 1.5-3 samples/pixel
+        for cap in (h * w * 3 + 65536, h * w * 20 + 65536):
+            out = np.empty(n * cap, np.uint8)
+            rc = self._lib.vd_jpeg_encode(self._h, p, n, h, w, pitch, where, int(quality), int(subsampling),
+                                          ptr(out), cap, sizes)
+            if rc != _lib.VD_ERR_CAPACITY:
+                break
+        check(rc)
+        del keep
+        return [out[i * cap:i * cap + sizes[i]].tobytes() for i in range(n)]
+
     # -- instrumentation ------------------------------------------------------
     def timing(self, on=True):
         check(self._lib.vd_timing_enable(self._h, 1 if on else 0))
