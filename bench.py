@@ -258,6 +258,7 @@ def main():
         lists = frame_lists(mode.ctx, batches[-1][1]) if batches else []
         if world == 1 and precision == a.precision and a.host_pipeline:
             res["host_pipeline"] = host_pipeline(mode)
+            res["jpeg_pipeline"] = jpeg_pipeline(mode)
         mode.close()
         return res, lists
 
@@ -288,6 +289,35 @@ def main():
                 "pcie_bytes_per_step": 2 * B * H * W * 3,
                 "what": "pinned host frames -> H2D -> vd_process -> D2H of mosaicked frames + box lists, "
                         "copies and compute on separate streams (FramePipeline, depth 2)"}
+
+    def jpeg_pipeline(mode):
+        """Frame I/O included: the B frames as in-memory JPEG files
+        (q95 4:2:0, what the reference's ffmpeg split and cv2.imwrite produce) ->
+        vd_jpeg_decode (host Huffman threads + HIP IDCT) into device frames ->
+        vd_process -> vd_jpeg_encode (HIP FDCT + host Huffman threads) -> JPEG bytes."""
+        ctx = mode.ctx
+        ctx.set_stream(stream.cuda_stream)
+        jp = ctx.jpeg_encode(frames[:B], quality=95, subsampling=2)
+        d_in = torch.empty_like(frames[:B])
+        d_out = torch.empty_like(frames[:B])
+        steps = max(1, min(a.steps, 5))
+
+        def one():
+            ctx.jpeg_decode(jp, out=d_in)
+            mode.process(d_in, d_out)
+            return ctx.jpeg_encode(d_out, quality=95, subsampling=2)
+        one()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            outj = one()
+        d = time.perf_counter() - t0
+        return {"value": round(B * steps / d, 2), "unit": "frames/s", "ms_per_step": round(d / steps * 1e3, 3),
+                "steps": steps, "jpeg_bytes_in_per_frame": int(np.mean([len(j) for j in jp])),
+                "jpeg_bytes_out_per_frame": int(np.mean([len(j) for j in outj])),
+                "huffman_threads": 16,
+                "what": "in-memory q95 4:2:0 JPEG frames -> GPU decode -> vd_process -> GPU encode -> JPEG "
+                        "bytes (entropy coding on host threads)"}
 
     def instrumented(mode, precision):
         """Per-kernel-family durations: the same K steps again, each launch bracketed
@@ -359,7 +389,7 @@ def main():
                    "plates": plates},
     }
     for k in ("roofline", "blur_roofline", "faces_per_frame", "instrumented_ms_per_step", "plate_conv",
-              "ms_breakdown_per_step", "host_pipeline"):
+              "ms_breakdown_per_step", "host_pipeline", "jpeg_pipeline"):
         if k in head:
             res[k] = head[k]
     parity = {}

@@ -115,3 +115,39 @@ def test_batch_process_images_fused_mosaic_plates(gpu, tmp_path):
         boxes = [tuple(int(v) for v in b) for b in fb] + [tuple(int(v) for v in b) for b in pb]
         np.testing.assert_array_equal(saved[f"processed_{name}"], omosaic.mosaic_frame(img, boxes, 8))
     assert (nf, npl) == (tf, tp) and tp > 0
+
+
+def test_batch_process_images_gpu_jpeg_codec(gpu, tmp_path):
+    """The reference's real file loop: a directory of ffmpeg-style JPEG frames (q95
+    4:2:0) -> batch_process_images with vdmi detectors and no custom I/O takes the GPU
+    codec path (vd_jpeg_decode -> vd_process -> vd_jpeg_encode). Every written file is
+    byte-identical to libjpeg-turbo's encode (Pillow, q95, 4:2:0) of the oracle mosaic
+    of the host-decoded frame with the detector's boxes; a progressive JPEG among them
+    takes the host decoder and is still processed."""
+    import io
+    from PIL import Image
+    import vdmi
+    from vdmi import synth, weights
+    from vdmi.pipeline import batch_process_images
+    src = {}
+    for i in range(7):
+        img = np.repeat(np.repeat(synth.frame(180, 320, i, seed=5), 2, 0), 2, 1)   # 360x640, real structure
+        b = io.BytesIO()
+        Image.fromarray(img).save(b, "JPEG", quality=95, progressive=(i == 6))
+        (tmp_path / f"f{i:03d}.jpg").write_bytes(b.getvalue())
+        src[f"f{i:03d}.jpg"] = np.asarray(Image.open(io.BytesIO(b.getvalue())).convert("RGB"))
+    face = vdmi.Retinaface(input_shape=[640, 640, 3], nms_iou=0.4, max_batch=4,
+                           weights=weights.retinaface_state_dict(0))
+    plate = vdmi.YOLO(weights="random", max_batch=4)
+    out_dir = tmp_path / "out"
+    n, nf, npl = batch_process_images(str(tmp_path), str(out_dir), face, plate, batch_size=3)
+    assert n == 7 and npl == 0
+    total = 0
+    for name, img in src.items():
+        boxes = face.detect_images([img])[0][1]
+        total += len(boxes)
+        exp = omosaic.mosaic_frame(img, [tuple(int(v) for v in b) for b in boxes], 8)
+        b = io.BytesIO()
+        Image.fromarray(exp).save(b, "JPEG", quality=95, subsampling=2)
+        assert (out_dir / f"processed_{name}").read_bytes() == b.getvalue(), name
+    assert nf == total and total > 0

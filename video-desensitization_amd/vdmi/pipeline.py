@@ -224,9 +224,17 @@ def _is_vdmi_pair(face_detector, plate_detector):
 
 
 def batch_process_images(input_dir, output_dir, face_detector, plate_detector, batch_size=16,
-                         loader=None, saver=None, mosaic_plates=False, mosaic_level=8, num_workers=6):
-    """combine_detect.py:183-277. Returns (total_processed, total_faces, total_plates)."""
+                         loader=None, saver=None, mosaic_plates=False, mosaic_level=8, num_workers=6,
+                         gpu_codec="auto", jpeg_quality=95):
+    """combine_detect.py:183-277. Returns (total_processed, total_faces, total_plates).
+
+    gpu_codec ("auto" | True | False): with vdmi detectors, no custom loader/saver and
+    only .jpg/.jpeg frames (what the reference's ffmpeg split writes), the frames are
+    read as bytes, decoded on the GPU (vd_jpeg_decode), processed and encoded on the
+    GPU (vd_jpeg_encode, cv2.imwrite's quality 95 / 4:2:0), so pixels never cross
+    PCIe; the bytes written equal libjpeg-turbo's encode of the processed frames."""
     logger = logging.getLogger("VideoProcessor.batch_process_images")
+    custom_io = loader is not None or saver is not None
     loader = loader or load_image_rgb
     saver = saver or save_output_image
     image_paths = [os.path.join(input_dir, f) for f in os.listdir(input_dir) if f.lower().endswith(IMAGE_EXT)]
@@ -234,7 +242,12 @@ def batch_process_images(input_dir, output_dir, face_detector, plate_detector, b
     batches = [image_paths[i:i + batch_size] for i in range(0, len(image_paths), batch_size)]
     io = ThreadPoolExecutor(max_workers=num_workers)
     try:
-        if _is_vdmi_pair(face_detector, plate_detector) and mosaic_level == face_detector.ctx.cfg.mosaic_level:
+        fused = _is_vdmi_pair(face_detector, plate_detector) and mosaic_level == face_detector.ctx.cfg.mosaic_level
+        all_jpeg = all(p.lower().endswith((".jpg", ".jpeg")) for p in image_paths)
+        if fused and gpu_codec and (gpu_codec is True or (not custom_io and all_jpeg)):
+            res = _gpu_codec_batches(batches, output_dir, face_detector, plate_detector, batch_size, mosaic_plates,
+                                     io, logger, jpeg_quality)
+        elif fused:
             res = _fused_batches(batches, output_dir, face_detector, plate_detector, batch_size, loader, saver,
                                  mosaic_plates, io, logger)
         else:
@@ -312,6 +325,77 @@ def _fused_batches(batches, output_dir, face_detector, plate_detector, batch_siz
         finish(pending)
     for pipe in pipes.values():
         pipe.close()
+    _save_all(save_futs, logger)
+    return tuple(totals)
+
+
+def _read_bytes(path):
+    with open(path, "rb") as f:
+        return f.read()
+
+
+def _write_bytes(data, path):
+    with open(path, "wb") as f:
+        f.write(data)
+
+
+def _gpu_codec_batches(batches, output_dir, face_detector, plate_detector, batch_size, mosaic_plates, io, logger,
+                       quality):
+    """Frame I/O on the GPU: file bytes (reader threads, next batch prefetched) ->
+    vd_jpeg_decode into device frames -> one vd_process (faces | plates | mosaic) ->
+    vd_jpeg_encode from device memory -> writer threads. A frame the GPU decoder
+    does not take (progressive, other layout) is decoded by the host loader; a
+    batch whose inference fails is dropped (combine_detect.py:226-228)."""
+    import torch
+    from .context import DeviceBoxes, jpeg_info
+    ctx = fused_context(face_detector, plate_detector, batch_size)
+    dev = torch.device(f"cuda:{ctx.device}")
+    flags = _lib.VD_PROC_FACES | _lib.VD_PROC_MOSAIC | _lib.VD_PROC_PLATES
+    if mosaic_plates:
+        flags |= _lib.VD_PROC_MOSAIC_PLATES
+    faces = DeviceBoxes(batch_size, 256, dev)
+    plates = DeviceBoxes(batch_size, 256, dev)
+    totals = [0, 0, 0]
+    save_futs = []
+    read = lambda files: list(io.map(_read_bytes, files))
+    fut = io.submit(read, batches[0]) if batches else None
+    for bi, files in enumerate(batches):
+        try:
+            blobs = fut.result()
+        except Exception as e:
+            logger.error(f"loading failed: {e}")
+            blobs = None
+        fut = io.submit(read, batches[bi + 1]) if bi + 1 < len(batches) else None
+        if blobs is None:
+            continue
+        groups = {}
+        for f, b in zip(files, blobs):
+            try:
+                key = jpeg_info(b)[:2]
+            except Exception:
+                key = load_image_rgb(f).shape[:2]
+            groups.setdefault(key, []).append((f, b))
+        for (h, w), items in groups.items():
+            try:
+                d_in = torch.empty((len(items), h, w, 3), dtype=torch.uint8, device=dev)
+                try:
+                    ctx.jpeg_decode([b for _, b in items], out=d_in)
+                except Exception:            # not a layout the GPU decoder takes: host decode
+                    d_in.copy_(torch.from_numpy(np.stack([load_image_rgb(f) for f, _ in items])))
+                    torch.cuda.synchronize(dev)  # the copy ran on torch's stream, not the context's
+                out, fc, pc = ctx.process(d_in, faces=faces, plates=plates, flags=flags)
+                jpgs = ctx.jpeg_encode(out, quality=quality, subsampling=2)
+            except Exception as e:           # combine_detect.py:226-228: the batch is dropped
+                logger.error(f"parallel inference failed: {e}")
+                continue
+            n = len(items)
+            for (path, _), data in zip(items, jpgs):
+                save_futs.append(io.submit(_write_bytes, data,
+                                           os.path.join(output_dir, f"processed_{os.path.basename(path)}")))
+            totals[0] += n
+            totals[1] += int(fc.count[:n].sum().item())
+            if mosaic_plates:
+                totals[2] += int(pc.count[:n].sum().item())
     _save_all(save_futs, logger)
     return tuple(totals)
 
