@@ -312,3 +312,23 @@ def test_heads_bf16_ssh_fused_matches_unfused(gpu):
             ctx.close()
     for a, b in zip(out["1"], out["0"]):
         np.testing.assert_array_equal(a, b)
+
+
+def test_heads_fp32_dual_downsample_bit_identical(gpu):
+    """fp32 (fp16-pair) plans run layer1.0 / layer2.0's conv3 + downsample as one
+    streaming pass (conv1x1_x6_dual_kernel); option conv_dual=0 at weight load stores
+    the downsample output and adds it as conv3's residual. Same operand scales, same
+    products, the downsample term rounded to f32 before the add in both: the heads
+    are bit-identical."""
+    import vdmi
+    fr = _frames(2, 1080, 1920, seed=13)
+    out = {}
+    for dual in (1, 0):
+        ctx = vdmi.Context(precision="fp32", max_batch=2, options={"conv_dual": dual})
+        try:
+            ctx.load_weights(0, face_weights("default"))
+            out[dual] = ctx.forward_heads(fr)
+        finally:
+            ctx.close()
+    for a, b in zip(out[1], out[0]):
+        np.testing.assert_array_equal(a, b)

@@ -1,0 +1,13 @@
+# fp32 dual conv3+downsample: bit-identity + fp32 parity tests, faces-only layer profile, bench
+set -u
+cd "${GRAFT_REPO_ROOT}"
+mkdir -p gpurun_out/g22
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_e2e.py -k "fp32" -p no:cacheprovider > gpurun_out/g22/tests.log 2>&1; rc=$?
+tail -5 gpurun_out/g22/tests.log
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/g22/p -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-timing --compare "" --host-pipeline 0 --plates 0 > $GRAFT_REPO_ROOT/gpurun_out/g22/p.log 2>&1 || exit $?
+cd $GRAFT_REPO_ROOT
+timeout -k 10 200 python bench.py --compare "" --host-pipeline 0 --no-cpu-baseline > gpurun_out/g22/bench.json 2> gpurun_out/g22/bench.err || exit $?
+python -c "import json;d=json.load(open('gpurun_out/g22/bench.json'));print(d['value'],d['ms_per_step'],d['roofline']['frac'])"

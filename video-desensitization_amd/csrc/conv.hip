@@ -388,8 +388,9 @@ hipError_t vd_launch_conv(const ConvArgs& a0, bool f32, hipStream_t s) {
     const int vec = f32 ? 4 : 8;
     const int bke = 8 * vec;
     const bool dense = (a.cin_pad % bke) == 0;
-    if (a.x2) {   // fused conv3 + downsample: planned only where the dual streaming kernel applies
-        if (f32 || a.f16 || !vd_conv1x1_dual_ok(a)) return hipErrorInvalidValue;
+    if (a.x2) {   // fused conv3 + downsample: planned only where a dual streaming kernel applies
+        if (f32) return vd_launch_conv_x6(a, s);
+        if (a.f16 || !vd_conv1x1_dual_ok(a)) return hipErrorInvalidValue;
         return vd_launch_conv1x1_stream(a, s);
     }
     const int bn = a.cout <= 32 ? 32 : (a.cout <= 64 ? 64 : 128);

@@ -628,6 +628,171 @@ __global__ __launch_bounds__(512) void conv1x1_x6_kernel(ConvArgs a, int nchunks
     }
 }
 
+// Dual streaming form (fp16 pairs): a bottleneck's conv3 (+bn3) and its downsample
+// (+bn, strided 1x1 over the block input) for the same output pixels in one pass,
+// y = relu((bn3(conv3(t2))) + bn_d(ds(x))): the downsample output never goes
+// through HBM. The two products keep their own per-frame operand scales (t2's and
+// x's producers' max), and the downsample term is rounded to f32 before the add as
+// the unfused plan stores it, so the result is bit-identical to conv_ds followed by
+// conv3 with a pre-activation residual. Layer1.0 (K 64 + 64) and layer2.0 (K 128 +
+// 256, stride 2).
+template <int KS, int KS2, int NTT>
+__global__ __launch_bounds__(512) void conv1x1_x6_dual_kernel(ConvArgs a, int nchunks, int groups) {
+    constexpr int NCH = 16 * NTT, PL = KS * NCH * 64, PL2 = KS2 * NCH * 64;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* w2s = smem + 2 * PL;
+    float* s_scale = (float*)(w2s + 2 * PL2);
+    float* s_shift = s_scale + NCH;
+    float* s_scale2 = s_shift + NCH;
+    float* s_shift2 = s_scale2 + NCH;
+    unsigned* s_amax = (unsigned*)(s_shift2 + NCH);
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int bid = blockIdx.x, xcd = bid & 7, local = bid >> 3;
+    const int chunk = local % nchunks;
+    const int mblk = (local / nchunks) * 8 + xcd;
+    const int nmblk = gridDim.x / nchunks;
+    const int n0 = chunk * NCH;
+    auto stage_w = [&](const void* wsrc, int kpad, int ks_n, char* dst, int pl) {
+        const int nk = kpad / KT;
+        for (int i = tid; i < 2 * ks_n * NCH * 4; i += 512) {
+            const int c = i & 3, row = (i >> 2) % NCH, pk = (i >> 2) / NCH, ks = pk % ks_n, p = pk / ks_n;
+            const int j = row >> 4, ii = row & 15;
+            const int chn = 32 * (j >> 1) + 8 * (ii >> 2) + 4 * (j & 1) + (ii & 3);
+            const u32x4 v = *(const u32x4*)((const char*)wsrc + ((((size_t)(n0 + chn) * nk + ks) * 2 + p) * 64 + c * 16));
+            *(u32x4*)(dst + p * pl + ks * NCH * 64 + swz(row, c)) = v;
+        }
+    };
+    stage_w(a.wx3, a.kpad, KS, smem, PL);
+    stage_w(a.wx3_2, a.kpad2, KS2, w2s, PL2);
+    for (int i = tid; i < NCH; i += 512) {
+        s_scale[i] = a.scale[n0 + i];
+        s_shift[i] = a.shift[n0 + i];
+        s_scale2[i] = a.scale2[n0 + i];
+        s_shift2[i] = a.shift2[n0 + i];
+    }
+    if (a.ymax)
+        for (int f = tid; f < a.B; f += 512) s_amax[f] = 0u;
+    __syncthreads();
+    const int p_lane = lane & 15, q = lane >> 4;
+    const int ohw = a.yh * a.yw;
+    const int wstride = nmblk * 8;
+    auto load = [&](int g, u32x4 (&xf)[KS][2], u32x4 (&xf2)[KS2][2]) {
+        const int mu = g * 16 + p_lane;
+        const int m = mu < a.M ? mu : a.M - 1;
+        const int b = m / ohw, rem = m - b * ohw;
+        const int oy = rem / a.yw, ox = rem - oy * a.yw;
+        const float* xp = (const float*)a.x + (((size_t)b * a.xh + oy * a.stride) * a.xw + ox * a.stride) * a.ldx +
+                          a.xcoff + q * 8;
+        const float* xp2 = (const float*)a.x2 +
+                           (((size_t)b * a.xh2 + oy * a.stride2) * a.xw2 + ox * a.stride2) * a.ldx2 + a.xcoff2 + q * 8;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            xf[ks][0] = *(const u32x4*)(xp + ks * 32);
+            xf[ks][1] = *(const u32x4*)(xp + ks * 32 + 4);
+        }
+#pragma unroll
+        for (int ks = 0; ks < KS2; ++ks) {
+            xf2[ks][0] = *(const u32x4*)(xp2 + ks * 32);
+            xf2[ks][1] = *(const u32x4*)(xp2 + ks * 32 + 4);
+        }
+    };
+    auto gemm = [&](f32x4_t (&acc)[NTT], const auto& xf, const char* wl, int pl, float sa) {
+        constexpr int ks_n = sizeof(xf) / sizeof(xf[0]);
+#pragma unroll
+        for (int ks = 0; ks < ks_n; ++ks) {
+            float e8[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) e8[e] = __uint_as_float(xf[ks][e >> 2][e & 3]);
+            u32x4 xb[3];
+            split_pack<2>(e8, sa, xb);
+#pragma unroll
+            for (int j = 0; j < NTT; ++j) {
+                u32x4 wf[3];
+#pragma unroll
+                for (int p = 0; p < 2; ++p) wf[p] = *(const u32x4*)(wl + p * pl + ks * NCH * 64 + swz(16 * j + p_lane, q));
+                acc[j] = mfma_terms<2>(wf, xb, acc[j]);
+            }
+        }
+    };
+    ConvArgs a2 = a;                                       // the downsample input's range slots
+    a2.xmax = a.x2max;
+    a2.xbound = a.x2bound;
+    u32x4 xf[KS][2], xf2[KS2][2];
+    int g = mblk * 8 + wid;
+    if (g < groups) load(g, xf, xf2);
+    for (; g < groups; g += wstride) {
+        asm volatile("" ::: "memory");
+        u32x4 xn[KS][2], xn2[KS2][2];
+        const int gn = g + wstride;
+        if (gn < groups) load(gn, xn, xn2);
+        const int mu = g * 16 + p_lane;
+        const int fb = (mu < a.M ? mu : a.M - 1) / ohw;
+        const int k1 = act_scale_exp(a, fb), k2 = act_scale_exp(a2, fb);
+        f32x4_t acc[NTT], acc2[NTT];
+#pragma unroll
+        for (int j = 0; j < NTT; ++j) acc[j] = acc2[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        gemm(acc, xf, smem, PL, __builtin_ldexpf(1.f, k1));
+        gemm(acc2, xf2, w2s, PL2, __builtin_ldexpf(1.f, k2));
+        const float inv1 = __builtin_ldexpf(1.f, -k1), inv2 = __builtin_ldexpf(1.f, -k2);
+        float vmax = 0.f;
+        if (mu < a.M) {
+            const size_t yo = (size_t)mu * a.ldy + a.ycoff + n0 + q * 8;
+#pragma unroll
+            for (int i = 0; i < NTT / 2; ++i) {
+                const int c = 32 * i + q * 8;
+                float v[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const float a1 = (e < 4 ? acc[2 * i][e] : acc[2 * i + 1][e - 4]);
+                    const float a2v = (e < 4 ? acc2[2 * i][e] : acc2[2 * i + 1][e - 4]);
+                    const float r = (a2v * inv2) * s_scale2[c + e] + s_shift2[c + e];   // the stored ds value
+                    float t = (a1 * inv1) * s_scale[c + e] + s_shift[c + e];
+                    t += r;
+                    t = t > 0.f ? t : 0.f;
+                    v[e] = t;
+                    vmax = fmaxf(vmax, t);
+                }
+                *(float4*)((float*)a.y + yo + 32 * i) = make_float4(v[0], v[1], v[2], v[3]);
+                *(float4*)((float*)a.y + yo + 32 * i + 4) = make_float4(v[4], v[5], v[6], v[7]);
+            }
+        }
+        if (a.ymax) amax_lds_add(s_amax, mu < a.M ? fb : -1, vmax);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) { xf[ks][0] = xn[ks][0]; xf[ks][1] = xn[ks][1]; }
+#pragma unroll
+        for (int ks = 0; ks < KS2; ++ks) { xf2[ks][0] = xn2[ks][0]; xf2[ks][1] = xn2[ks][1]; }
+    }
+    if (a.ymax) {
+        __syncthreads();
+        amax_lds_flush(s_amax, a.ymax, a.B);
+    }
+}
+
+template <int KS, int KS2, int NTT>
+hipError_t launch_dual_x6(const ConvArgs& a0, hipStream_t s) {
+    constexpr int NCH = 16 * NTT;
+    constexpr int lds = 2 * (KS + KS2) * NCH * 64 + 4 * NCH * 4;
+    static const int resident = [] {
+        (void)hipFuncSetAttribute((const void*)conv1x1_x6_dual_kernel<KS, KS2, NTT>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds + 4 * kAmaxFrames);
+        int dev = 0, cus = 256, per_cu = 1;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv1x1_x6_dual_kernel<KS, KS2, NTT>, 512, lds);
+        return std::max(1, cus * std::max(1, per_cu));
+    }();
+    ConvArgs a = a0;
+    a.scale = a.scale_x;                                   // per-channel rescaled BN scales of the pairs
+    a.scale2 = a.scale2_x;
+    const int nchunks = a.cout / NCH;
+    const int groups = (a.M + 15) / 16;
+    int k = std::max(1, resident / (8 * nchunks));
+    k = std::min(k, std::max(1, (groups + 63) / 64));
+    hipLaunchKernelGGL((conv1x1_x6_dual_kernel<KS, KS2, NTT>), dim3(8 * nchunks * k), dim3(512),
+                       lds + (a.ymax ? 4 * a.B : 0), s, a, nchunks, groups);
+    return hipGetLastError();
+}
+
 template <int KS, int NTT, int ACT, int RES, int TERMS>
 hipError_t launch_stream_x6(const ConvArgs& a, hipStream_t s) {
     constexpr int NCH = 16 * NTT;
@@ -763,7 +928,24 @@ static hipError_t launch_terms(const ConvArgs& a0, hipStream_t s) {
     return launch_x6<256, 128, 512, 2, TERMS>(a, s);
 }
 
+// fp16 pairs: bottleneck conv3 (1x1, K 64 / 128, ReLU) + downsample (1x1, K 64 / 256,
+// strided, no activation) as conv1x1_x6_dual_kernel
+bool vd_conv1x1_x6_dual_ok(const ConvArgs& a) {
+    if (a.f32_split != 2 || !a.wx3 || !a.wx3_2 || !a.scale_x || !a.scale2_x) return false;
+    if (a.kh != 1 || a.kw != 1 || a.pad != 0 || a.stride != 1 || a.kpad != a.cin_pad || a.kpad2 != a.cin2_pad) return false;
+    if (a.act != VD_ACT_RELU || a.res_mode != VD_RES_NONE) return false;
+    if (((a.ldx | a.xcoff | a.ldy | a.ycoff | a.ldx2 | a.xcoff2) & 7)) return false;
+    if (a.cin_pad == 64 && a.kpad2 == 64) return a.cout % 128 == 0;
+    if (a.cin_pad == 128 && a.kpad2 == 256) return a.cout % 64 == 0;
+    return false;
+}
+
 hipError_t vd_launch_conv_x6(const ConvArgs& a, hipStream_t s) {
+    if (a.x2) {
+        if (!vd_conv1x1_x6_dual_ok(a) || (a.ymax && a.B > kAmaxFrames)) return hipErrorInvalidValue;
+        if (a.cin_pad == 64) return launch_dual_x6<2, 2, 8>(a, s);
+        return launch_dual_x6<4, 8, 4>(a, s);
+    }
     if (a.f32_split == 2) {
         if (!a.scale_x || (a.ymax && a.B > kAmaxFrames)) return hipErrorInvalidValue;
         return launch_terms<2>(a, s);

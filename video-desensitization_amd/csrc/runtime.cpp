@@ -355,9 +355,18 @@ int Ctx::make_conv_cat(const WMap& W, const std::vector<std::string>& wkeys, con
 
 // Bottleneck conv3 (ci on x) + downsample (c2 on x2, strided 1x1) in one op.
 bool Ctx::dual_ok(int ci, int c2, const Act& y) const {
-    if (f32 || f16) return false;
+    if (f16) return false;
     const Conv& a = convs[ci];
     const Conv& b = convs[c2];
+    if (f32) {   // fp16-pair plan: conv1x1_x6_dual_kernel
+        if (!tune.conv_dual || a.split != 2 || b.split != 2 || b.cout != a.cout || b.act != VD_ACT_NONE) return false;
+        ConvArgs t{};
+        t.kh = a.kh; t.kw = a.kw; t.pad = a.pad; t.stride = a.stride; t.cin_pad = a.cin_pad; t.kpad = a.kpad;
+        t.cout = a.cout; t.act = a.act; t.res_mode = VD_RES_NONE; t.ldx = a.cin_pad; t.ldy = y.c;
+        t.ldx2 = b.cin_pad; t.cin2_pad = b.cin_pad; t.kpad2 = b.kpad; t.f32_split = 2;
+        t.wx3 = a.wx3; t.wx3_2 = b.wx3; t.scale_x = a.scale_x; t.scale2_x = b.scale_x;
+        return b.kh == 1 && b.kw == 1 && b.pad == 0 && vd_conv1x1_x6_dual_ok(t);
+    }
     ConvArgs t{};
     t.kh = a.kh; t.kw = a.kw; t.pad = a.pad; t.stride = a.stride; t.cin_pad = a.cin_pad; t.kpad = a.kpad;
     t.cout = a.cout; t.act = a.act; t.res_mode = VD_RES_NONE; t.ldx = a.cin_pad; t.ldy = y.c; t.x2 = (const void*)1;
@@ -448,6 +457,9 @@ int Ctx::run_conv_op(const Op& op, int f0, int n, int fam) {
         a.x2 = foff(op.x2, f0); a.xh2 = op.x2.h; a.xw2 = op.x2.w; a.ldx2 = op.x2.c; a.xcoff2 = 0;
         a.stride2 = c2.stride; a.w2 = c2.w; a.scale2 = c2.scale; a.shift2 = c2.shift;
         a.cin2_pad = c2.cin_pad; a.kpad2 = c2.kpad;
+        a.wx3_2 = c2.wx3; a.scale2_x = c2.scale_x;
+        a.x2max = op.x2.amax ? op.x2.amax + f0 : nullptr;
+        a.x2bound = op.x2.bound;
         flops += c2.flops_per_px * a.M;
     }
     t_begin(fam, flops);

@@ -76,6 +76,9 @@ struct ConvArgs {
     int f32_split;                               // the conv's weight format (Conv::split at load)
     const unsigned* xmax; float xbound;
     unsigned* ymax;
+    // fp16 pairs, fused downsample (x2): its split weights, rescaled BN scale, input range
+    const void* wx3_2; const float* scale2_x;
+    const unsigned* x2max; float x2bound;
 };
 
 // One fused layer1 bottleneck (block.hip): x [B][H][W][cin] -> y [B][H][W][256],
@@ -290,6 +293,7 @@ bool vd_conv1x1_dual_ok(const ConvArgs& a);
 hipError_t vd_launch_conv_taps(const ConvArgs& a, hipStream_t s);
 hipError_t vd_launch_conv(const ConvArgs& a, bool f32, hipStream_t s);
 bool vd_conv_x6_ok(const ConvArgs& a);
+bool vd_conv1x1_x6_dual_ok(const ConvArgs& a);
 hipError_t vd_launch_conv_x6(const ConvArgs& a, hipStream_t s);
 void vd_pack_x6(const float* w, int npad, int kpad, uint16_t* out);   // host: f32 [npad][kpad] -> split planes
 void vd_pack_x3h(const float* w, int npad, int kpad, uint16_t* out, float* row_inv);   // ... fp16 pairs
