@@ -634,8 +634,7 @@ __global__ __launch_bounds__(512) void conv1x1_x6_kernel(ConvArgs a, int nchunks
 // through HBM. The two products keep their own per-frame operand scales (t2's and
 // x's producers' max), and the downsample term is rounded to f32 before the add as
 // the unfused plan stores it, so the result is bit-identical to conv_ds followed by
-// conv3 with a pre-activation residual. Layer1.0 (K 64 + 64) and layer2.0 (K 128 +
-// 256, stride 2).
+// conv3 with a pre-activation residual. Layer1.0 (K 64 + 64).
 template <int KS, int KS2, int NTT>
 __global__ __launch_bounds__(512) void conv1x1_x6_dual_kernel(ConvArgs a, int nchunks, int groups) {
     constexpr int NCH = 16 * NTT, PL = KS * NCH * 64, PL2 = KS2 * NCH * 64;
@@ -935,16 +934,16 @@ bool vd_conv1x1_x6_dual_ok(const ConvArgs& a) {
     if (a.kh != 1 || a.kw != 1 || a.pad != 0 || a.stride != 1 || a.kpad != a.cin_pad || a.kpad2 != a.cin2_pad) return false;
     if (a.act != VD_ACT_RELU || a.res_mode != VD_RES_NONE) return false;
     if (((a.ldx | a.xcoff | a.ldy | a.ycoff | a.ldx2 | a.xcoff2) & 7)) return false;
-    if (a.cin_pad == 64 && a.kpad2 == 64) return a.cout % 128 == 0;
-    if (a.cin_pad == 128 && a.kpad2 == 256) return a.cout % 64 == 0;
-    return false;
+    // layer1.0 only: at layer2.0 (K 128 + 256) the weights of both fit LDS only as
+    // 64-channel slices, every pixel is then split for 8 slices instead of 4 and the
+    // pass measured level with the two launches (839 vs 424 + 433 us)
+    return a.cin_pad == 64 && a.kpad2 == 64 && a.cout % 128 == 0;
 }
 
 hipError_t vd_launch_conv_x6(const ConvArgs& a, hipStream_t s) {
     if (a.x2) {
         if (!vd_conv1x1_x6_dual_ok(a) || (a.ymax && a.B > kAmaxFrames)) return hipErrorInvalidValue;
-        if (a.cin_pad == 64) return launch_dual_x6<2, 2, 8>(a, s);
-        return launch_dual_x6<4, 8, 4>(a, s);
+        return launch_dual_x6<2, 2, 8>(a, s);
     }
     if (a.f32_split == 2) {
         if (!a.scale_x || (a.ymax && a.B > kAmaxFrames)) return hipErrorInvalidValue;
