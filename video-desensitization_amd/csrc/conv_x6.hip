@@ -100,9 +100,11 @@ __device__ __forceinline__ void split3(float x, unsigned& h, unsigned& m, unsign
 
 // x = hi + lo (+ below 2^-24 |x|) with both terms fp16, round to nearest: the
 // scaled operand (|x| < 2^15, see act_scale) keeps 22-24 significand bits
-__device__ __forceinline__ void split2h(float x, unsigned& h, unsigned& l) {
-    const _Float16 x0 = (_Float16)x;
-    const _Float16 x1 = (_Float16)(x - (float)x0);    // the residual is exact in f32
+__device__ __forceinline__ void split2h(float x, float sa, unsigned& h, unsigned& l) {
+    // x * sa is exact (a power of two), so each term is ONE rounding of a fused
+    // multiply-add to fp16 (v_fma_mixlo_f16): hi = RNE(x sa), lo = RNE(x sa - hi)
+    const _Float16 x0 = (_Float16)__builtin_fmaf(x, sa, 0.f);
+    const _Float16 x1 = (_Float16)__builtin_fmaf(x, sa, -(float)x0);   // the residual is exact in f32
     h = __builtin_bit_cast(unsigned short, x0);
     l = __builtin_bit_cast(unsigned short, x1);
 }
@@ -145,7 +147,7 @@ __device__ __forceinline__ void split_pack(const float (&e)[8], float sa, u32x4 
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         if constexpr (TERMS == 3) split3(e[j], hv[j], mv[j], lv[j]);
-        else { split2h(e[j] * sa, hv[j], mv[j]); lv[j] = 0; }
+        else { split2h(e[j], sa, hv[j], mv[j]); lv[j] = 0; }
     }
     o[0] = u32x4{hv[0] | (hv[1] << 16), hv[2] | (hv[3] << 16), hv[4] | (hv[5] << 16), hv[6] | (hv[7] << 16)};
     o[1] = u32x4{mv[0] | (mv[1] << 16), mv[2] | (mv[3] << 16), mv[4] | (mv[5] << 16), mv[6] | (mv[7] << 16)};
@@ -154,7 +156,7 @@ __device__ __forceinline__ void split_pack(const float (&e)[8], float sa, u32x4 
 }
 
 template <int BM, int BN, int NT, int NST, int TERMS>
-__global__ __launch_bounds__(NT) void conv_x6_kernel(ConvArgs a) {
+__global__ __launch_bounds__(NT, 2) void conv_x6_kernel(ConvArgs a) {
     using S = X6Shape<BM, BN, NT, NST, TERMS>;
     constexpr int STAGE = S::STAGE, PL_A = S::PL_A, PL_B = S::PL_B, TM = S::TM, TN = S::TN, WAVES = S::WAVES;
     constexpr int AROWS = S::AROWS;
@@ -172,7 +174,7 @@ __global__ __launch_bounds__(NT) void conv_x6_kernel(ConvArgs a) {
     // ---- A staging: thread = (row, k-pair) items; item i: row = (tid >> 2) + AROWS i, pair = tid & 3 (k 8p..8p+7)
     const int apair = tid & 3, arow = tid >> 2;
     const int ohw = a.yh * a.yw;
-    long pix0[2];
+    int pix0[2];                                    // element offsets (xbytes < 2^31: vd_conv_x6_ok)
     int iy0[2], ix0[2];
     float sa[2] = {1.f, 1.f};                       // fp16 pair: the row's frame scale 2^k
 #pragma unroll
@@ -183,13 +185,13 @@ __global__ __launch_bounds__(NT) void conv_x6_kernel(ConvArgs a) {
             const int oy = rem / a.yw, ox = rem - oy * a.yw;
             iy0[i] = oy * a.stride - a.pad;
             ix0[i] = ox * a.stride - a.pad;
-            pix0[i] = (((long)b * a.xh + iy0[i]) * a.xw + ix0[i]) * a.ldx + a.xcoff;
+            pix0[i] = ((b * a.xh + iy0[i]) * a.xw + ix0[i]) * a.ldx + a.xcoff;
             if constexpr (TERMS == 2) sa[i] = __builtin_ldexpf(1.f, act_scale_exp(a, b));
         } else {
             iy0[i] = -(1 << 28); ix0[i] = 0; pix0[i] = 0;
         }
     }
-    const long tap_dy = (long)a.xw * a.ldx;
+    const int tap_dy = a.xw * a.ldx;
     const int nk = a.kpad / KT;
     // A through a buffer descriptor: 32-bit byte offsets, and an offset past
     // num_records returns zeros (conv padding, K padding) without a select on the
@@ -218,23 +220,26 @@ __global__ __launch_bounds__(NT) void conv_x6_kernel(ConvArgs a) {
             // a chunk past the last tap (K padding) is pushed off the image rows, so
             // one unsigned compare rejects it (selects only: no divergent branch)
             const int dyk = tdy[h] < a.kh ? tdy[h] : (1 << 28);
-            const long toff = tdy[h] * tap_dy + (long)tdx[h] * a.ldx + tc[h];
+            const int toff = tdy[h] * tap_dy + tdx[h] * a.ldx + tc[h];
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 const unsigned iy = (unsigned)(iy0[i] + dyk), ix = (unsigned)(ix0[i] + tdx[h]);
                 const bool ok = (iy < (unsigned)a.xh) & (ix < (unsigned)a.xw);
-                const unsigned off = ok ? (unsigned)((pix0[i] + toff) * 4) : 0x80000000u;
+                const unsigned off = ok ? (unsigned)(pix0[i] + toff) * 4u : 0x80000000u;
                 r[i][h] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc_x, (int)off, 0, 0));
             }
             tc[h] += KT;
-            if (a.cin_pad >= KT) {                  // at most one tap step per tile
+            if (a.cin_pad >= KT) {                  // at most one tap step per tile: selects only
                 const bool wrap = tc[h] >= a.cin_pad;
                 tc[h] -= wrap ? a.cin_pad : 0;
                 tdx[h] += wrap ? 1 : 0;
+                const bool wrap2 = tdx[h] >= a.kw;
+                tdx[h] -= wrap2 ? a.kw : 0;
+                tdy[h] += wrap2 ? 1 : 0;
             } else {
                 while (tc[h] >= a.cin_pad) { tc[h] -= a.cin_pad; ++tdx[h]; }
+                while (tdx[h] >= a.kw) { tdx[h] -= a.kw; ++tdy[h]; }
             }
-            while (tdx[h] >= a.kw) { tdx[h] -= a.kw; ++tdy[h]; }
         }
     };
     auto store_item = [&](int st, const u32x4 (&r)[2][2], int i) {
