@@ -12,13 +12,14 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from prof_summary import face_stream  # noqa: E402
 
 
-def face_plan(B=64, H=640, W=640, fused=True, block=True, chain=True, ssh_fused=True):
+def face_plan(B=64, H=640, W=640, fused=True, block=True, chain=True, ssh_fused=True, dual=(0, 1)):
     """(name, M, N, K) of every conv launch in face_net.cpp order; with `block` the
     three layer1 bottlenecks are one launch each (block.hip), K = their summed
     reduction depth per output channel of 256 (same FLOPs); with `chain`
     layer2.1/2.2's conv3 runs with the next block's conv1 (chain.hip, N=512 K=256
     carries both layers' FLOPs); with `ssh_fused` each SSH's conv5X5_1 and conv3X3
-    are one 192-channel conv."""
+    are one 192-channel conv; `dual`: the layers whose block 0 runs conv3 + downsample
+    as one launch (bf16: layer1/2; fp32: layer1)."""
     L = []
     h, w = H // 2, W // 2
     L.append(("stem7x7", B * h * w, 64, 3 * 49))
@@ -38,7 +39,7 @@ def face_plan(B=64, H=640, W=640, fused=True, block=True, chain=True, ssh_fused=
                 L.append((f"l{li+1}.{bi}.c1", B * h * w, planes, cin))
             oh, ow = h // s, w // s
             L.append((f"l{li+1}.{bi}.c2", B * oh * ow, planes, planes * 9))
-            if bi == 0 and fused and li < 2:     # bf16 plan: conv3 + downsample in one pass
+            if bi == 0 and fused and li in dual:  # conv3 + downsample in one pass
                 L.append((f"l{li+1}.{bi}.c3+ds", B * oh * ow, planes * 4, planes + cin))
             else:
                 if bi == 0:

@@ -14,7 +14,7 @@ from conv_layers import face_plan  # noqa: E402
 
 def main(path, B=64):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-    plan = face_plan(B, fused=False, block=False, chain=False, ssh_fused=True)
+    plan = face_plan(B, fused=True, block=False, chain=False, ssh_fused=True, dual=(0,))
     # the face stream: the stream with the most conv launches (73 per step vs the plate net's 60);
     # its last len(plan) conv launches are the last step's layers
     per = {}

@@ -33,7 +33,7 @@ def last_step(d, counter, n):
 
 
 def main(fd, wd, B=64):
-    plan = face_plan(B, fused=False, block=False, chain=False, ssh_fused=True)
+    plan = face_plan(B, fused=True, block=False, chain=False, ssh_fused=True, dual=(0,))
     f = last_step(fd, "FETCH_SIZE", len(plan))
     w = last_step(wd, "WRITE_SIZE", len(plan))
     print(f"{'layer':12s} {'us':>7s} {'read MB':>9s} {'in MB':>8s} {'reread':>6s} {'write MB':>9s} {'out MB':>8s}")
