@@ -114,21 +114,40 @@ void reciprocal(int divisor, uint16_t* recip, uint16_t* corr, uint8_t* shift) {
 struct BitOut {   // jchuff.c emit_bits / flush_bits with 0xFF stuffing
     uint8_t* p;
     uint8_t* end;
-    uint64_t acc = 0;
-    int n = 0;
+    uint64_t acc = 0;   // the low n bits are pending, oldest first
+    int n = 0;          // < 32 between calls
     bool overflow = false;
-    inline void put(unsigned code, int size) {
+    inline void byte(uint8_t b) {
+        *p++ = b;
+        if (b == 0xFF) *p++ = 0;
+    }
+    inline void put(unsigned code, int size) {   // size <= 27
         acc = (acc << size) | (code & ((1u << size) - 1));
         n += size;
-        while (n >= 8) {
-            n -= 8;
-            const uint8_t byte = (uint8_t)(acc >> n);
-            if (p + 2 > end) { overflow = true; return; }
-            *p++ = byte;
-            if (byte == 0xFF) *p++ = 0;
+        if (n < 32) return;
+        n -= 32;
+        const uint32_t w = (uint32_t)(acc >> n);
+        if (p + 8 > end) { overflow = true; p = end - 8; }
+        const uint32_t x = ~w;                   // a 0xFF byte of w is a zero byte of x
+        if (!((x - 0x01010101u) & ~x & 0x80808080u)) {   // common case: 4 bytes, no stuffing
+            const uint32_t be = __builtin_bswap32(w);
+            memcpy(p, &be, 4);
+            p += 4;
+        } else {
+            byte((uint8_t)(w >> 24)); byte((uint8_t)(w >> 16)); byte((uint8_t)(w >> 8)); byte((uint8_t)w);
         }
     }
-    void flush() { put(0x7F, 7); acc = 0; n = 0; }
+    void flush() {      // seven 1-bits fill the partial byte; whole bytes out, the rest dropped
+        acc = (acc << 7) | 0x7F;
+        n += 7;
+        while (n >= 8) {
+            n -= 8;
+            if (p + 2 > end) { overflow = true; return; }
+            byte((uint8_t)(acc >> n));
+        }
+        acc = 0;
+        n = 0;
+    }
 };
 
 inline int nbits(int v) { return v ? 32 - __builtin_clz((unsigned)(v < 0 ? -v : v)) : 0; }
@@ -138,8 +157,8 @@ inline void encode_block(BitOut& o, const int16_t* blk, int& last_dc, const Huff
     int diff = blk[0] - last_dc;
     last_dc = blk[0];
     int nb = nbits(diff);
-    o.put(dc.code[nb], dc.size[nb]);
-    if (nb) o.put((unsigned)(diff < 0 ? diff - 1 : diff), nb);
+    // code and extra bits in one put (<= 16 + 11 bits)
+    o.put(((unsigned)dc.code[nb] << nb) | ((unsigned)(diff < 0 ? diff - 1 : diff) & ((1u << nb) - 1)), dc.size[nb] + nb);
     int r = 0;
     for (int k = 1; k < 64; ++k) {
         const int v = blk[kZigzag[k]];
@@ -147,8 +166,7 @@ inline void encode_block(BitOut& o, const int16_t* blk, int& last_dc, const Huff
         while (r > 15) { o.put(ac.code[0xF0], ac.size[0xF0]); r -= 16; }
         nb = nbits(v);
         const int sym = (r << 4) + nb;
-        o.put(ac.code[sym], ac.size[sym]);
-        o.put((unsigned)(v < 0 ? v - 1 : v), nb);
+        o.put(((unsigned)ac.code[sym] << nb) | ((unsigned)(v < 0 ? v - 1 : v) & ((1u << nb) - 1)), ac.size[sym] + nb);
         r = 0;
     }
     if (r) o.put(ac.code[0], ac.size[0]);

@@ -32,10 +32,17 @@ const int kZigzag[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11,
                          41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
                          30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 
+constexpr int kLook = 11;                 // lookahead bits
+
 struct Huff {
-    // 9-bit lookahead: len 0 = longer code (slow path)
-    uint8_t look_len[512];
-    uint8_t look_sym[512];
+    // kLook-bit lookahead: len 0 = longer code (slow path)
+    uint8_t look_len[1 << kLook];
+    uint8_t look_sym[1 << kLook];
+    // AC fast path (libjpeg-turbo style): code AND its extra bits inside the window
+    // -> total bits, coefficient run and value; len 0 = not decodable in one look
+    uint8_t fa_len[1 << kLook];
+    uint8_t fa_run[1 << kLook];              // k advance: r (value), 16 (ZRL), 64 (EOB)
+    int16_t fa_val[1 << kLook];
     int32_t maxcode[18];      // largest code of length l (-1 if none), maxcode[17] sentinel
     int32_t valoff[17];       // symbol index of the first code of length l minus that code
     uint8_t vals[256];
@@ -58,15 +65,27 @@ int build_huff(Huff& hf, const uint8_t* counts, const uint8_t* syms, int nsym) {
     if (nsym > 256) return -1;
     memcpy(hf.vals, syms, nsym);
     memset(hf.look_len, 0, sizeof hf.look_len);
+    memset(hf.fa_len, 0, sizeof hf.fa_len);
     int code = 0, k = 0;
     for (int l = 1; l <= 16; ++l) {
         hf.valoff[l] = k - code;
         for (int i = 0; i < counts[l - 1]; ++i, ++k, ++code) {
-            if (l <= 9) {   // fill every 9-bit prefix extension
-                const int base = code << (9 - l);
-                for (int e = 0; e < (1 << (9 - l)); ++e) {
+            if (l <= kLook) {   // fill every kLook-bit prefix extension
+                const int base = code << (kLook - l);
+                const int rs = syms[k], r = rs >> 4, sz = rs & 15;
+                for (int e = 0; e < (1 << (kLook - l)); ++e) {
                     hf.look_len[base + e] = (uint8_t)l;
                     hf.look_sym[base + e] = syms[k];
+                    if (sz == 0) {                       // EOB / ZRL (AC tables)
+                        hf.fa_len[base + e] = (uint8_t)l;
+                        hf.fa_run[base + e] = r == 15 ? 16 : 64;
+                        hf.fa_val[base + e] = 0;
+                    } else if (l + sz <= kLook) {
+                        const int extra = (e >> (kLook - l - sz)) & ((1 << sz) - 1);
+                        hf.fa_len[base + e] = (uint8_t)(l + sz);
+                        hf.fa_run[base + e] = (uint8_t)r;
+                        hf.fa_val[base + e] = (int16_t)(extra < (1 << (sz - 1)) ? extra - (1 << sz) + 1 : extra);
+                    }
                 }
             }
         }
@@ -193,6 +212,16 @@ struct Bits {
     int nb = 0;
     bool marker = false;
     void fill() {
+        // fast path: 4 bytes at once while none of them is 0xFF (no stuffing, no marker)
+        while (nb <= 32 && !marker && p + 4 <= n) {
+            uint32_t w;
+            memcpy(&w, d + p, 4);
+            if (((~w) - 0x01010101u) & w & 0x80808080u) break;   // a 0xFF byte among them (~w has a zero byte)
+            w = __builtin_bswap32(w);
+            acc |= (uint64_t)w << (32 - nb);
+            nb += 32;
+            p += 4;
+        }
         while (nb <= 56) {
             uint32_t v = 0;
             if (!marker && p < n) {
@@ -227,7 +256,7 @@ struct Bits {
 };
 
 inline int decode_sym(Bits& b, const Huff& h) {
-    const uint32_t look = b.peek(9);
+    const uint32_t look = b.peek(kLook);
     const int l = h.look_len[look];
     if (l) {
         b.skip(l);
@@ -282,6 +311,18 @@ int entropy(const Info& j, std::vector<uint32_t>& entries, std::vector<uint32_t>
                         pred[ci] += extend(b.get(s), s);
                         if (pred[ci]) ent_mcu.push_back((uint32_t)(0u << 16) | (uint16_t)(int16_t)pred[ci]);
                         for (int k = 1; k < 64;) {
+                            const uint32_t look = b.peek(kLook);
+                            if (const int fl = ac.fa_len[look]) {   // code + extra bits in one look
+                                b.skip(fl);
+                                const int run = ac.fa_run[look];
+                                if (run == 64) break;              // EOB
+                                if (run == 16) { k += 16; continue; }   // ZRL
+                                k += run;
+                                if (k > 63) return vd_set_error(VD_ERR_ARG, "jpeg: AC run past the block");
+                                ent_mcu.push_back(((uint32_t)kZigzag[k] << 16) | (uint16_t)ac.fa_val[look]);
+                                ++k;
+                                continue;
+                            }
                             const int rs = decode_sym(b, ac);
                             if (rs < 0) return vd_set_error(VD_ERR_ARG, "jpeg: bad AC code");
                             const int r = rs >> 4, sz = rs & 15;
