@@ -332,3 +332,21 @@ def test_heads_fp32_dual_downsample_bit_identical(gpu):
             ctx.close()
     for a, b in zip(out[1], out[0]):
         np.testing.assert_array_equal(a, b)
+
+
+def test_heads_fp32_exact_canvas_stem_bit_identical(gpu):
+    """The face letterbox canvas is integer-valued, exact in fp16: the fp16-pair stem
+    then runs with one activation plane and two products (option x6_exact, default
+    on). The dropped lo terms are exactly zero, so the heads are bit-identical."""
+    import vdmi
+    fr = _frames(2, 720, 1280, seed=19)
+    out = {}
+    for ex in (1, 0):
+        ctx = vdmi.Context(precision="fp32", max_batch=2, options={"x6_exact": ex})
+        try:
+            ctx.load_weights(0, face_weights("default"))
+            out[ex] = ctx.forward_heads(fr)
+        finally:
+            ctx.close()
+    for a, b in zip(out[1], out[0]):
+        np.testing.assert_array_equal(a, b)

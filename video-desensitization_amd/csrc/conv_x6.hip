@@ -45,11 +45,14 @@ constexpr int kAmaxFrames = 1024;               // LDS reserved for per-frame ma
 // for the compute-heavy layers, and the small tile (128 x BN, 4 waves, ONE stage,
 // three workgroups per CU) for small-K / small-M layers, where a workgroup's
 // load -> compute -> epilogue phases are short and neighbours on the CU overlap them.
+// TERMS: 3 = bf16 triples (A and B), 2 = fp16 pairs (A and B), 1 = fp16 pair weights
+// with activations exact in fp16 (one A plane: the integer-valued face canvas)
 template <int BM_, int BN, int NT_, int NST, int TERMS> struct X6Shape {
+    static constexpr int TA = TERMS == 1 ? 1 : TERMS, TB = TERMS == 1 ? 2 : TERMS;   // A / B planes
     static constexpr int BM = BM_, NT = NT_, WAVES = NT / 64;
     static constexpr int PL_A = BM * 64;                       // bytes per A plane
     static constexpr int PL_B = BN * 64;                       // bytes per B plane
-    static constexpr int STAGE = TERMS * (PL_A + PL_B);        // 256 x 128: 73 728 B (3 terms), 49 152 B (2)
+    static constexpr int STAGE = TA * PL_A + TB * PL_B;        // 256 x 128: 73 728 B (3 terms), 49 152 B (2)
     static constexpr int EPR = NST == 2 ? 128 : 64;            // epilogue rows per pass
     static constexpr int EPLD = BN + 4;                        // f32 epilogue row stride
     static constexpr int LDS = NST * STAGE > EPR * EPLD * 4 ? NST * STAGE : EPR * EPLD * 4;
@@ -57,7 +60,7 @@ template <int BM_, int BN, int NT_, int NST, int TERMS> struct X6Shape {
     static constexpr int WAVES_M = WAVES / WAVES_N;
     static constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
     static constexpr int TM = WTM / 16, TN = WTN / 16;
-    static constexpr int NDMA = TERMS * BN / 16;               // 1-KB DMA instructions per K tile
+    static constexpr int NDMA = TB * BN / 16;                  // 1-KB DMA instructions per K tile
     static constexpr int AROWS = NT / 4;                       // A rows per staging pass (2 passes)
     static_assert(BM == 2 * AROWS, "two A items per thread");
 };
@@ -129,6 +132,15 @@ __device__ __forceinline__ f32x4_t mfma_terms<3>(const u32x4 (&a)[3], const u32x
 }
 
 template <>
+__device__ __forceinline__ f32x4_t mfma_terms<1>(const u32x4 (&a)[3], const u32x4 (&b)[3], f32x4_t acc) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, a[0]), __builtin_bit_cast(f16x8_t, b[1]),
+                                                 acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, a[0]), __builtin_bit_cast(f16x8_t, b[0]),
+                                                 acc, 0, 0, 0);
+    return acc;
+}
+
+template <>
 __device__ __forceinline__ f32x4_t mfma_terms<2>(const u32x4 (&a)[3], const u32x4 (&b)[3], f32x4_t acc) {
 #define VDH_MFMA(pa, pb)                                                                                 \
     acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, a[pa]),                    \
@@ -147,10 +159,12 @@ __device__ __forceinline__ void split_pack(const float (&e)[8], float sa, u32x4 
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         if constexpr (TERMS == 3) split3(e[j], hv[j], mv[j], lv[j]);
-        else { split2h(e[j], sa, hv[j], mv[j]); lv[j] = 0; }
+        else if constexpr (TERMS == 2) { split2h(e[j], sa, hv[j], mv[j]); lv[j] = 0; }
+        else { hv[j] = __builtin_bit_cast(unsigned short, (_Float16)__builtin_fmaf(e[j], sa, 0.f)); mv[j] = lv[j] = 0; }
     }
     o[0] = u32x4{hv[0] | (hv[1] << 16), hv[2] | (hv[3] << 16), hv[4] | (hv[5] << 16), hv[6] | (hv[7] << 16)};
-    o[1] = u32x4{mv[0] | (mv[1] << 16), mv[2] | (mv[3] << 16), mv[4] | (mv[5] << 16), mv[6] | (mv[7] << 16)};
+    if constexpr (TERMS >= 2)
+        o[1] = u32x4{mv[0] | (mv[1] << 16), mv[2] | (mv[3] << 16), mv[4] | (mv[5] << 16), mv[6] | (mv[7] << 16)};
     if constexpr (TERMS == 3)
         o[2] = u32x4{lv[0] | (lv[1] << 16), lv[2] | (lv[3] << 16), lv[4] | (lv[5] << 16), lv[6] | (lv[7] << 16)};
 }
@@ -186,7 +200,7 @@ __global__ __launch_bounds__(NT, 2) void conv_x6_kernel(ConvArgs a) {
             iy0[i] = oy * a.stride - a.pad;
             ix0[i] = ox * a.stride - a.pad;
             pix0[i] = ((b * a.xh + iy0[i]) * a.xw + ix0[i]) * a.ldx + a.xcoff;
-            if constexpr (TERMS == 2) sa[i] = __builtin_ldexpf(1.f, act_scale_exp(a, b));
+            if constexpr (TERMS != 3) sa[i] = __builtin_ldexpf(1.f, act_scale_exp(a, b));
         } else {
             iy0[i] = -(1 << 28); ix0[i] = 0; pix0[i] = 0;
         }
@@ -254,7 +268,7 @@ __global__ __launch_bounds__(NT, 2) void conv_x6_kernel(ConvArgs a) {
         split_pack<TERMS>(e, sa[i], o);
         const int off = swz(arow + AROWS * i, apair);
 #pragma unroll
-        for (int p = 0; p < TERMS; ++p) *(u32x4*)(A + p * PL_A + off) = o[p];
+        for (int p = 0; p < S::TA; ++p) *(u32x4*)(A + p * PL_A + off) = o[p];
     };
 
     // ---- B: LDS-DMA, one instruction = 1 KB = 16 rows of one plane; NDMA per tile,
@@ -264,7 +278,7 @@ __global__ __launch_bounds__(NT, 2) void conv_x6_kernel(ConvArgs a) {
     const int my_dma = NDMA / WAVES + (wid < NDMA % WAVES ? 1 : 0);
     const __amdgpu_buffer_rsrc_t rsrc_w = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7fffffff, 0x00020000);
     auto dma_b = [&](int kt, int st) {
-        char* Bs = smem + st * STAGE + TERMS * PL_A;
+        char* Bs = smem + st * STAGE + S::TA * PL_A;
 #pragma unroll
         for (int q = 0; q < (NDMA + WAVES - 1) / WAVES; ++q) {
             const int j = wid + WAVES * q;
@@ -272,7 +286,7 @@ __global__ __launch_bounds__(NT, 2) void conv_x6_kernel(ConvArgs a) {
                 const int p = j / RB, r0 = (j % RB) * 16;
                 const int row = r0 + (lane >> 2), slot = lane & 3;
                 const int chunk = slot ^ (((row >> 3) & 1) * 3);
-                const unsigned off = (unsigned)((((long)(n0 + row) * nk + kt) * TERMS + p) * 64 + chunk * 16);
+                const unsigned off = (unsigned)((((long)(n0 + row) * nk + kt) * S::TB + p) * 64 + chunk * 16);
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_w, (lds_void_t*)(Bs + p * PL_B + r0 * 64), 16, off, 0,
                                                          0, 0);
             }
@@ -291,20 +305,20 @@ __global__ __launch_bounds__(NT, 2) void conv_x6_kernel(ConvArgs a) {
     // interleaved with the MFMA rows (VALU work beside the matrix cores)
     auto compute = [&](int st, bool split_next, int st_next, const u32x4 (&rn)[2][2]) {
         const char* A = smem + st * STAGE;
-        const char* Bs = A + TERMS * PL_A;
+        const char* Bs = A + S::TA * PL_A;
         const int ch = lane >> 4;
         if constexpr (TN > TM) {   // wide wave tile: all A fragments resident, B fragments streamed
             u32x4 af[TM][3];
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
-                for (int p = 0; p < TERMS; ++p)
+                for (int p = 0; p < S::TA; ++p)
                     af[i][p] = *(const u32x4*)(A + p * PL_A + swz(wm * S::WTM + i * 16 + (lane & 15), ch));
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
                 u32x4 bf[3];
 #pragma unroll
-                for (int p = 0; p < TERMS; ++p)
+                for (int p = 0; p < S::TB; ++p)
                     bf[p] = *(const u32x4*)(Bs + p * PL_B + swz(wn * S::WTN + j * 16 + (lane & 15), ch));
 #pragma unroll
                 for (int i = 0; i < TM; ++i) acc[i][j] = mfma_terms<TERMS>(af[i], bf, acc[i][j]);
@@ -316,13 +330,13 @@ __global__ __launch_bounds__(NT, 2) void conv_x6_kernel(ConvArgs a) {
 #pragma unroll
             for (int j = 0; j < TN; ++j)
 #pragma unroll
-                for (int p = 0; p < TERMS; ++p)
+                for (int p = 0; p < S::TB; ++p)
                     bf[j][p] = *(const u32x4*)(Bs + p * PL_B + swz(wn * S::WTN + j * 16 + (lane & 15), ch));
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
                 u32x4 af[3];
 #pragma unroll
-                for (int p = 0; p < TERMS; ++p)
+                for (int p = 0; p < S::TA; ++p)
                     af[p] = *(const u32x4*)(A + p * PL_A + swz(wm * S::WTM + i * 16 + (lane & 15), ch));
 #pragma unroll
                 for (int j = 0; j < TN; ++j) acc[i][j] = mfma_terms<TERMS>(af, bf[j], acc[i][j]);
@@ -426,7 +440,7 @@ __global__ __launch_bounds__(NT, 2) void conv_x6_kernel(ConvArgs a) {
             if (valid) {
             const float* er = ep + rr * EPLD + cg * 8;
             const size_t yo = (size_t)m * a.ldy + a.ycoff + nb;
-            const float inv_sa = TERMS == 2 ? __builtin_ldexpf(1.f, -act_scale_exp(a, fb)) : 1.f;
+            const float inv_sa = TERMS != 3 ? __builtin_ldexpf(1.f, -act_scale_exp(a, fb)) : 1.f;
             size_t roff = 0;
             if (a.res_mode != VD_RES_NONE) {
                 if (a.res_up) {
@@ -912,6 +926,9 @@ static hipError_t launch_terms(const ConvArgs& a0, hipStream_t s) {
                                                     big_tiles < small_tiles));
     if (small) {
         if (bn == 32) return launch_x6<128, 32, 256, 1, TERMS>(a, s);
+        if constexpr (TERMS == 2) {   // the integer-valued face canvas: one A plane, two products (stem)
+            if (bn == 64 && a.x_exact) return launch_x6<128, 64, 256, 1, 1>(a, s);
+        }
         if (bn == 64) return launch_x6<128, 64, 256, 1, TERMS>(a, s);
         return launch_x6<128, 128, 256, 1, TERMS>(a, s);
     }

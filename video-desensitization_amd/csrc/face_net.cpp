@@ -126,6 +126,7 @@ int vd_build_face(Ctx& c, const WMap& W) {
     if (rc) return rc;
     F.input.amax = nullptr;            // letterboxed canvas: |pixel - mean| <= 255
     F.input.bound = 255.f;
+    F.input.exact16 = true;            // integers (pixel, means 104/117/123, pad 128)
 
     Act feats[3];
     if (F.mnet) {

@@ -27,6 +27,7 @@ struct Act {          // NHWC activation buffer sized for cfg.max_batch frames
     // for the letterboxed canvas (amax NULL)
     unsigned* amax = nullptr;
     float bound = 0.f;
+    bool exact16 = false;      // every value an integer of |x| <= 2048 (the face letterbox canvas)
 };
 
 struct Conv {

@@ -448,6 +448,7 @@ int Ctx::run_conv_op(const Op& op, int f0, int n, int fam) {
     a.f32_split = cv.split;
     a.xmax = op.x.amax ? op.x.amax + f0 : nullptr;
     a.xbound = op.x.bound;
+    a.x_exact = (op.x.exact16 && cv.split == 2 && tune.x6_exact) ? 1 : 0;
     a.ymax = op.y.amax ? op.y.amax + f0 : nullptr;
     if (cv.split == 2 && !a.xmax && !(a.xbound > 0.f))
         return vd_set_error(VD_ERR_ARG, "internal: conv input without a range (fp16-pair plan)");
@@ -896,6 +897,7 @@ int vd_set_option(vd_ctx* h, const char* name, int value) {
         {"plate_s2d", &VdTune::plate_s2d}, {"f32_split", &VdTune::f32_split},
         {"x6_small_k", &VdTune::x6_small_k}, {"x6_small_tiles", &VdTune::x6_small_tiles},
         {"x6_stream", &VdTune::x6_stream}, {"x6_small_k2", &VdTune::x6_small_k2}, {"x6_bn256", &VdTune::x6_bn256},
+        {"x6_exact", &VdTune::x6_exact},
     };
     for (const Opt& o : opts)
         if (strcmp(o.n, name) == 0) {

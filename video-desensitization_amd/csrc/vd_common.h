@@ -40,6 +40,7 @@ struct VdTune {
     int x6_small_tiles = 512; //   ... and big-tile grids smaller than this (0 / 0: big tile always)
     int x6_small_k2 = 1 << 20;//   fp16 pairs: K at or below which N <= 64 layers take the small tile
     int x6_bn256 = 1;         // fp16 pairs: 256 x 256 tile for Cout % 256 == 0
+    int x6_exact = 1;         // fp16 pairs: one A plane for inputs exact in fp16 (the face stem)
     int f32_split = 2;        // plan (fp32, at weight load): 2 = operands scaled by powers of two
                               //   and split into fp16 pairs, 3 products on the f16 matrix cores;
                               //   1 = exact 3-term bf16 split, 6 products (conv_x6.hip);
@@ -79,6 +80,7 @@ struct ConvArgs {
     // fp16 pairs, fused downsample (x2): its split weights, rescaled BN scale, input range
     const void* wx3_2; const float* scale2_x;
     const unsigned* x2max; float x2bound;
+    int x_exact;                                 // fp16 pairs: input values exact in fp16 (integer canvas)
 };
 
 // One fused layer1 bottleneck (block.hip): x [B][H][W][cin] -> y [B][H][W][256],
