@@ -87,7 +87,7 @@ def test_c2_bf16_720p_heads_and_boxes(gpu, face_ctx_factory):
     fr = _frames720(3, seed=31)
     loc, conf, _ = ctx.forward_heads(fr)
     eloc, econf = _oracle_heads(fr)
-    assert _rel(loc, eloc) < 6e-2 and _rel(conf, econf) < 6e-2
+    assert _rel(loc, eloc) < 2e-2 and _rel(conf, econf) < 2e-2      # observed <= 0.0116 (~1.5x)
     got = ctx.detect(fr)
     pri = oanchors.get_anchors((640, 640))
     matched = total = 0

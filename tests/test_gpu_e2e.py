@@ -1,12 +1,13 @@
 """End-to-end parity: letterbox -> RetinaFace forward -> decode/NMS -> correction ->
 int() -> mosaic, GPU (C-ABI) vs the CPU oracle on identical synthetic frames.
 
-* fp32 (exact-f32 MFMA) mode: head outputs within 1e-4 of the torch-CPU oracle
+* fp32 mode (each plan: fp16 pairs, bf16 triples, exact-f32 MFMA): heads within 1e-4 of the torch-CPU oracle
   (relative to each tensor's max |value|); kept anchor indices identical except
   for candidates whose decision is within 1e-4 of a threshold (score vs 0.5,
   IoU vs 0.4), which the test excludes and counts; mosaic pixels bit-exact given
   the boxes.
-* bf16 mode: heads within 6e-2 relative; >= 90 % of oracle boxes matched by a
+* bf16 mode: heads within 2e-2 (R50) / 4.5e-2 (MobileNet) relative, ~1.5x the observed
+  error; >= 90 % of oracle boxes matched by a
   GPU box at IoU >= 0.9 (bf16 rounding moves near-threshold decisions, so box
   parity is claimed for fp32 mode only).
 """
@@ -49,6 +50,13 @@ def _rel(a, b):
     return np.abs(a - b).max() / (np.abs(b).max() + 1e-12)
 
 
+# 16-bit heads vs the f32 oracle: ~1.5x the largest error observed over 1080p / 720p /
+# 4K frames and two seeds (tools/observed_tolerances.py on the GPU box: bf16 R50
+# <= 0.0116 loc/conf, MobileNet-0.25 <= 0.0273; fp16 R50 <= 0.0018, MobileNet <= 0.0042)
+BF16_TOL = {"default": 2e-2, "mnet": 4.5e-2}
+FP16_TOL = {"default": 3e-3, "mnet": 6.5e-3}
+
+
 # fp32 plans: 1 = 3-term bf16 split (6 products), 2 = scaled fp16 pairs (3 products), 0 = exact-f32 MFMA
 SPLITS = [1, 2, 0]
 
@@ -70,7 +78,8 @@ def test_heads_bf16_close(gpu, face_ctx_factory, wkind):
     fr = _frames(2, 1080, 1920)
     loc, conf, _ = ctx.forward_heads(fr)
     eloc, econf, _ = _oracle_heads(fr, wkind)
-    assert _rel(loc, eloc) < 6e-2 and _rel(conf, econf) < 6e-2
+    tol = BF16_TOL[wkind]
+    assert _rel(loc, eloc) < tol and _rel(conf, econf) < tol
 
 
 @pytest.mark.parametrize("h,w,wkind", [(1080, 1920, "default"), (2160, 3840, "default"), (1080, 1920, "mnet")])
@@ -83,7 +92,8 @@ def test_heads_fp16_close(gpu, face_ctx_factory, h, w, wkind):
     fr = _frames(2, h, w, seed=17)
     loc, conf, ldm = ctx.forward_heads(fr)
     eloc, econf, eldm = _oracle_heads(fr, wkind)
-    assert _rel(loc, eloc) < 1e-2 and _rel(conf, econf) < 1e-2 and _rel(ldm, eldm) < 1e-2
+    tol = FP16_TOL[wkind]
+    assert _rel(loc, eloc) < tol and _rel(conf, econf) < tol and _rel(ldm, eldm) < tol
 
 
 def test_detect_fp16_agrees_4k(gpu, face_ctx_factory):

@@ -60,7 +60,7 @@ def test_plate_raw_fp16_close(gpu):
     fr = synth.frames(2, 1080, 1920, seed=5)
     got = _ctx("fp16").plate_raw(fr)
     exp, _, _ = _oracle_raw(fr)
-    assert _rel(got[:, 64:], exp[:, 64:]) < 1e-2
+    assert _rel(got[:, 64:], exp[:, 64:]) < 3e-3      # observed 0.0020 (~1.5x)
 
 
 def test_plate_raw_bf16_close(gpu):
@@ -68,7 +68,7 @@ def test_plate_raw_bf16_close(gpu):
     fr = synth.frames(2, 1080, 1920, seed=5)
     got = _ctx("bf16").plate_raw(fr)
     exp, _, _ = _oracle_raw(fr)
-    assert _rel(got[:, 64:], exp[:, 64:]) < 8e-2
+    assert _rel(got[:, 64:], exp[:, 64:]) < 5.5e-2    # observed 0.036 (~1.5x)
 
 
 @pytest.mark.parametrize("prec", ["fp32", "fp32-x6", "bf16"])
