@@ -255,7 +255,7 @@ def main():
         if not a.no_timing:
             res.update(instrumented(mode, precision))
         res["faces_per_frame"] = round(float(mode.faces.count.float().mean().item()), 2)
-        lists = frame_lists(mode.ctx, batches[-1][1]) if batches else []
+        lists = frame_lists(mode.ctx, batches[-1][1]) if batches and a.faces else []
         if world == 1 and precision == a.precision and a.host_pipeline:
             res["host_pipeline"] = host_pipeline(mode)
             res["jpeg_pipeline"] = jpeg_pipeline(mode)

@@ -176,3 +176,31 @@ def test_process_paired_letterbox_matches_separate(gpu, h, w):
     for b in range(2):
         np.testing.assert_array_equal(res["1"][1][b], res["0"][1][b])
         np.testing.assert_array_equal(res["1"][2][b], res["0"][2][b])
+
+
+@pytest.mark.parametrize("stage", [0, 1, 5])
+def test_process_plate_release_point(gpu, stage):
+    """Option plate_stage holds the plate branch back until face stage N has been
+    issued (default 3: its HBM-bound convs then overlap the MFMA-bound late face
+    layers). Scheduling only: the fp32 boxes and mosaicked frames equal the default's."""
+    import vdmi
+    from vdmi import _lib, synth, weights
+    fr = synth.frames(3, 1080, 1920, seed=22)
+    flags = _lib.VD_PROC_FACES | _lib.VD_PROC_PLATES | _lib.VD_PROC_MOSAIC | _lib.VD_PROC_MOSAIC_PLATES
+    res = {}
+    for st in (stage, 3):
+        c = vdmi.Context(precision="fp32", max_batch=3, options={"plate_stage": st})
+        try:
+            c.load_weights(0, weights.retinaface_state_dict(0))
+            c.load_weights(1, weights.yolov8n_state_dict(0))
+            for _ in range(2):                                     # a second call reuses the event
+                out, faces, plates = c.process(fr, flags=flags)
+            res[st] = (out.copy(), [faces.frame(b)[0].copy() for b in range(3)],
+                       [plates.frame(b)[0].copy() for b in range(3)])
+        finally:
+            c.close()
+    np.testing.assert_array_equal(res[stage][0], res[3][0])
+    assert sum(len(x) for x in res[3][1] + res[3][2]) > 0
+    for b in range(3):
+        np.testing.assert_array_equal(res[stage][1][b], res[3][1][b])
+        np.testing.assert_array_equal(res[stage][2][b], res[3][2][b])

@@ -163,6 +163,7 @@ struct Ctx {
     hipStream_t stream = nullptr, own_stream = nullptr;
     hipStream_t stream2 = nullptr;               // plate branch runs beside the face branch
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    int fork_at = -1;                                // run_ops records ev_fork after this many face ops
     std::mutex mu;
     std::vector<void*> allocs;
     std::vector<Conv> convs;

@@ -576,6 +576,7 @@ int Ctx::run_ops(const Net& net, int b, int e, int f0, int n) {
             if (er != hipSuccess) rc = vd_set_error(VD_ERR_HIP, "upsample: %s", hipGetErrorString(er));
         }
         if (rc) return rc;
+        if (&net == &face.net && i + 1 == fork_at) VD_CHECK_HIP(hipEventRecord(ev_fork, stream));
     }
     return VD_OK;
 }
@@ -897,7 +898,7 @@ int vd_set_option(vd_ctx* h, const char* name, int value) {
         {"plate_s2d", &VdTune::plate_s2d}, {"f32_split", &VdTune::f32_split},
         {"x6_small_k", &VdTune::x6_small_k}, {"x6_small_tiles", &VdTune::x6_small_tiles},
         {"x6_stream", &VdTune::x6_stream}, {"x6_small_k2", &VdTune::x6_small_k2}, {"x6_bn256", &VdTune::x6_bn256},
-        {"x6_exact", &VdTune::x6_exact},
+        {"x6_exact", &VdTune::x6_exact}, {"plate_stage", &VdTune::plate_stage},
     };
     for (const Opt& o : opts)
         if (strcmp(o.n, name) == 0) {
@@ -1054,13 +1055,25 @@ int vd_process(vd_ctx* h, const uint8_t* in, uint8_t* out, int n, int fh, int fw
             paired = true;
         }
     }
-    if (fork) {
+    // The plate branch may be held back until face stage `plate_stage` has been issued
+    // (its HBM-bound convs then overlap the MFMA-bound late face layers).
+    const int ps = ctx->tune.plate_stage;
+    ctx->fork_at = -1;
+    if (fork && ps > 0) {
+        ctx->fork_at = ps >= 5 ? (int)ctx->face.net.ops.size() : ctx->face.net.stage_end[std::min(ps, 4)];
+        if (ctx->fork_at <= 0) ctx->fork_at = -1;
+    }
+    if (fork && ctx->fork_at < 0) {
         VD_CHECK_HIP(hipEventRecord(ctx->ev_fork, ctx->stream));
         VD_CHECK_HIP(hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
     }
     if (do_faces) {
         if (!paired && (rc = ctx->face_letterbox(d, n, fh, fw, pitch))) return rc;
         if ((rc = ctx->face_forward(n))) return rc;
+        if (ctx->fork_at > 0) {
+            ctx->fork_at = -1;
+            VD_CHECK_HIP(hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
+        }
         if ((rc = ctx->face_post(n, fh, fw, tf))) return rc;
     }
     if (do_plates) {

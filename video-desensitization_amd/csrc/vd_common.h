@@ -35,6 +35,9 @@ struct VdTune {
     int stem_pool = 1;        // plan: stem conv + maxpool (stem.hip)
     int ssh_fuse = 1;         // plan: SSH conv3X3 + conv5X5_1 as one conv
     int plate_s2d = 1;        // plan: YOLO space-to-depth stem input
+    int plate_stage = 3;      // plate branch starts after face stage N (0: with the stem; 1-4: after
+                              //   layerN; 5: after the whole face net). After layer3 its HBM-bound
+                              //   convs overlap the MFMA-bound late face layers: 30.8 -> 30.0 ms/step
     int x6_stream = 1;        // fp32 split: streaming 1x1 kernel for K in {64, 128, 256}
     int x6_small_k = 256;     // fp32 split: K at or below which the small single-stage tile runs
     int x6_small_tiles = 512; //   ... and big-tile grids smaller than this (0 / 0: big tile always)
