@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP event timing")
+    ap.add_argument("--microbatch", type=int, default=0, help="frames per depth-first backbone micro-batch (0: off)")
+    ap.add_argument("--microbatch-stage", type=int, default=2, help="micro-batch the backbone through layer<N>")
     ap.add_argument("--faces", type=int, default=1, help="0: plates only, no mosaic (profiling the plate net)")
     ap.add_argument("--host-pipeline", type=int, default=1, help="1: also time the host-frame pipeline (PCIe incl.)")
     return ap.parse_args()
@@ -157,7 +159,8 @@ class Mode:
         if precision == "fp32_x6":        # fp32 plan on the exact 3-term bf16 split (6 products)
             opts["f32_split"] = 1
         self.ctx = vdmi.Context(device=dev.index or 0, precision=precision.split("_")[0],
-                                max_batch=a.batch, options=opts)
+                                max_batch=a.batch, options=opts, microbatch=a.microbatch,
+                                microbatch_stage=a.microbatch_stage)
         self.ctx.load_weights(_lib.VD_NET_RETINAFACE, sd)
         if plates:
             self.ctx.load_weights(_lib.VD_NET_YOLOV8N, weights.yolov8n_state_dict(0))
