@@ -305,22 +305,37 @@ def main():
         d_out = torch.empty_like(frames[:B])
         steps = max(1, min(a.steps, 5))
 
+        stage = {"decode": 0.0, "process": 0.0, "encode": 0.0}
+
         def one():
+            t = time.perf_counter()
             ctx.jpeg_decode(jp, out=d_in)
+            torch.cuda.synchronize(dev)
+            t1 = time.perf_counter()
             mode.process(d_in, d_out)
-            return ctx.jpeg_encode(d_out, quality=95, subsampling=2)
+            torch.cuda.synchronize(dev)
+            t2 = time.perf_counter()
+            r = ctx.jpeg_encode(d_out, quality=95, subsampling=2)
+            t3 = time.perf_counter()
+            stage["decode"] += t1 - t
+            stage["process"] += t2 - t1
+            stage["encode"] += t3 - t2
+            return r
         one()
         torch.cuda.synchronize(dev)
+        for k in stage:
+            stage[k] = 0.0
         t0 = time.perf_counter()
         for _ in range(steps):
             outj = one()
         d = time.perf_counter() - t0
         return {"value": round(B * steps / d, 2), "unit": "frames/s", "ms_per_step": round(d / steps * 1e3, 3),
+                "stage_ms_per_step": {k: round(v / steps * 1e3, 2) for k, v in stage.items()},
                 "steps": steps, "jpeg_bytes_in_per_frame": int(np.mean([len(j) for j in jp])),
                 "jpeg_bytes_out_per_frame": int(np.mean([len(j) for j in outj])),
                 "huffman_threads": 16,
-                "what": "in-memory q95 4:2:0 JPEG frames -> GPU decode -> vd_process -> GPU encode -> JPEG "
-                        "bytes (entropy coding on host threads)"}
+                "what": "in-memory q95 4:2:0 JPEG frames -> GPU decode (host Huffman threads + HIP IDCT) -> "
+                        "vd_process -> GPU encode (HIP FDCT + device Huffman coding) -> JPEG bytes"}
 
     def instrumented(mode, precision):
         """Per-kernel-family durations: the same K steps again, each launch bracketed

@@ -107,3 +107,35 @@ def test_encode_1080p_from_device_frames_after_process(jctx):
         assert g == pillow_jpeg(img, 95, 2)
     back = jctx.jpeg_decode(got)
     np.testing.assert_array_equal(back, np.stack([pillow_rgb(g) for g in got]))
+
+
+@pytest.fixture(scope="module")
+def hctx(gpu):
+    import vdmi
+    ctx = vdmi.Context(precision="fp32", max_batch=8, options={"jenc_gpu": 0})
+    yield ctx
+    ctx.close()
+
+
+@pytest.mark.parametrize("case", ENC_CASES + [(1080, 1920, 95, 2), (1080, 1920, 100, 0), (37, 1001, 75, 1)])
+@pytest.mark.parametrize("noise", [False, True])
+def test_encode_device_entropy_equals_host_threads(jctx, hctx, case, noise):
+    """Huffman coding on the device (default, option jenc_gpu; jpeg_enc.hip: per-unit
+    code lengths, a per-frame scan, atomic-OR word writes at neighbour boundaries, a
+    stuffing pass) writes the same bytes as the host threads' sequential coder
+    (jpeg_enc.cpp, pinned to Pillow) -- dummy blocks, long zero runs (ZRL), 0xFF
+    stuffing and noise frames of several MB included."""
+    h, w, q, sub = case
+    if noise:
+        rng = np.random.default_rng(h * w + q)
+        imgs = rng.integers(0, 256, (2, h, w, 3), dtype=np.uint8)
+    else:
+        imgs = np.stack([enc_frame(h, w, seed=s) for s in range(2)])
+    dev = jctx.jpeg_encode(imgs, quality=q, subsampling=sub)
+    host = hctx.jpeg_encode(imgs, quality=q, subsampling=sub)
+    assert [len(d) for d in dev] == [len(x) for x in host]
+    for d, x in zip(dev, host):
+        assert d == x
+    if h * w <= 64 * 64:
+        for img, d in zip(imgs, dev):
+            assert d == pillow_jpeg(img, q, sub)

@@ -190,10 +190,8 @@ struct Geo {
     long cblk[3], bpf;
 };
 
-// one frame: headers + entropy-coded segment + EOI; returns bytes or 0 on overflow
-size_t encode_frame(const Geo& g, const int16_t* coef, const uint16_t* ql, const uint16_t* qc, uint8_t* out,
-                    size_t cap) {
-    if (cap < 1024) return 0;
+// JFIF / DQT / SOF0 / DHT / SOS headers as libjpeg writes them; returns their length
+size_t write_headers(const Geo& g, const uint16_t* ql, const uint16_t* qc, uint8_t* out) {
     uint8_t* p = out;
     static const uint8_t head[] = {0xFF, 0xD8, 0xFF, 0xE0, 0x00, 0x10, 'J', 'F', 'I', 'F', 0x00,
                                    0x01, 0x01, 0x00, 0x00, 0x01, 0x00, 0x01, 0x00, 0x00};
@@ -212,6 +210,14 @@ size_t encode_frame(const Geo& g, const int16_t* coef, const uint16_t* ql, const
     put_dht(p, 1, 1, kAcChromaBits, kAcChromaVals);
     static const uint8_t sos[] = {0xFF, 0xDA, 0x00, 0x0C, 0x03, 0x01, 0x00, 0x02, 0x11, 0x03, 0x11, 0x00, 0x3F, 0x00};
     memcpy(p, sos, sizeof(sos)); p += sizeof(sos);
+    return (size_t)(p - out);
+}
+
+// one frame: headers + entropy-coded segment + EOI; returns bytes or 0 on overflow
+size_t encode_frame(const Geo& g, const int16_t* coef, const uint16_t* ql, const uint16_t* qc, uint8_t* out,
+                    size_t cap) {
+    if (cap < 1024) return 0;
+    uint8_t* p = out + write_headers(g, ql, qc, out);
     const Tables& T = tables();
     BitOut o{p, out + cap - 2};
     int last[3] = {0, 0, 0};
@@ -277,7 +283,10 @@ extern "C" int vd_jpeg_encode(vd_ctx* hctx, const uint8_t* frames, int n, int h,
     const size_t coef_bytes = (size_t)n * g.bpf * 128;
     int rc;
     if ((rc = ctx->ensure_staging(&ctx->jenc_dev, &ctx->jenc_dev_bytes, coef_bytes + tab_bytes + 64))) return rc;
-    if ((rc = ctx->ensure_pinned(&ctx->jenc_host, &ctx->jenc_host_bytes, coef_bytes + tab_bytes + 64))) return rc;
+    // pinned: the coefficients (host Huffman path), the quantiser tables, the device
+    // path's code tables and its per-frame segment lengths
+    const size_t pin_extra = 4 * 256 * 3 + (size_t)n * 4 + (size_t)(n + 1) * 8 + 64;
+    if ((rc = ctx->ensure_pinned(&ctx->jenc_host, &ctx->jenc_host_bytes, coef_bytes + tab_bytes + pin_extra))) return rc;
     VD_CHECK_HIP(hipEventSynchronize(ctx->jpeg_ev));   // a previous H2D out of the pinned buffers is done
     uint8_t* hp = (uint8_t*)ctx->jenc_host + coef_bytes;
     uint16_t* hrecip = (uint16_t*)hp;
@@ -307,6 +316,96 @@ extern "C" int vd_jpeg_encode(vd_ctx* hctx, const uint8_t* frames, int n, int h,
     hipError_t e = vd_launch_jpeg_fdct(a, ctx->stream);
     ctx->t_end();
     if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "jpeg fdct: %s", hipGetErrorString(e));
+    if (ctx->tune.jenc_gpu) {
+        // Huffman stage on the device (jpeg_enc.hip): segments land in device slots,
+        // one D2H per frame of its stuffed length behind the host-written headers
+        uint8_t hdr[1024];
+        const size_t hl = write_headers(g, ql, qc, hdr);
+        if (cap < hl + 2 + 16) return vd_set_error(VD_ERR_CAPACITY, "jpeg cap %zu below the headers", cap);
+        const int mcux = (w + 8 * g.hl - 1) / (8 * g.hl), mcuy = (h + 8 * g.vl - 1) / (8 * g.vl);
+        JpegHuffArgs ha{};
+        ha.coef = a.coef; ha.blocks_per_frame = g.bpf; ha.n = n; ha.hl = g.hl; ha.vl = g.vl;
+        for (int c = 0; c < 3; ++c) { ha.bw[c] = g.bw[c]; ha.bh[c] = g.bh[c]; ha.cblk[c] = g.cblk[c]; }
+        ha.mcux = mcux;
+        const long units = (long)mcux * mcuy * (g.hl * g.vl + 2);
+        if (units > (1L << 26)) return vd_set_error(VD_ERR_ARG, "vd_jpeg_encode: frame too large");
+        ha.units = (int)units;
+        ha.wcap = units * 54;                              // >= 1728 bits per unit: any block's codes fit
+        ha.segcap = (long)(cap - hl - 2);
+        const long nchunk_max = (ha.wcap * 4 + 4095) / 4096;
+        const size_t huf_tab = 4 * 256 * 2 + 4 * 256;
+        const size_t sz_bits = (size_t)n * units * 4, sz_words = (size_t)n * ha.wcap * 4, sz_seg = (size_t)n * ha.segcap;
+        const size_t sz_ff = (size_t)n * nchunk_max * 4;
+        const size_t need = huf_tab + sz_bits + (size_t)n * 8 + (size_t)(n + 1) * 8 + sz_ff + sz_words + sz_seg + 8 * 64;
+        if ((rc = ctx->ensure_staging(&ctx->jhuf_dev, &ctx->jhuf_dev_bytes, need))) return rc;
+        uint8_t* q = (uint8_t*)ctx->jhuf_dev;
+        auto carve = [&](size_t bytes) { uint8_t* r = q; q += (bytes + 63) / 64 * 64; return r; };
+        uint16_t* dcode = (uint16_t*)carve(huf_tab);
+        ha.code = dcode; ha.size = (const uint8_t*)(dcode + 4 * 256);
+        ha.bits = (unsigned*)carve(sz_bits);
+        ha.total = (unsigned*)carve((size_t)n * 4);
+        ha.segsize = (unsigned*)carve((size_t)n * 4);
+        ha.segbase = (unsigned long long*)carve((size_t)(n + 1) * 8);
+        ha.ffcnt = (unsigned*)carve(sz_ff);
+        ha.words = (unsigned*)carve(sz_words);
+        ha.seg = carve(sz_seg);
+        // code / size tables [dc0, dc1, ac0, ac1] through the pinned buffer's tail
+        const Tables& T = tables();
+        uint16_t* htab = (uint16_t*)(hp + tab_bytes);
+        const HuffEnc* order[4] = {&T.dc[0], &T.dc[1], &T.ac[0], &T.ac[1]};
+        for (int k = 0; k < 4; ++k) {
+            memcpy(htab + k * 256, order[k]->code, 512);
+            memcpy((uint8_t*)(htab + 4 * 256) + k * 256, order[k]->size, 256);
+        }
+        VD_CHECK_HIP(hipMemcpyAsync(dcode, htab, huf_tab, hipMemcpyHostToDevice, ctx->stream));
+        ctx->t_begin(4, 0);
+        e = vd_launch_jpeg_huff(ha, ctx->stream);
+        ctx->t_end();
+        if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "jpeg huffman: %s", hipGetErrorString(e));
+        // bit totals -> the chunk grid of the stuffing pass
+        unsigned* htot = (unsigned*)(hp + tab_bytes + huf_tab);
+        VD_CHECK_HIP(hipMemcpyAsync(htot, ha.total, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream));
+        VD_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+        unsigned maxbits = 0;
+        for (int i = 0; i < n; ++i) maxbits = std::max(maxbits, htot[i]);
+        ha.nchunk = (int)std::max<long>(1, ((long)maxbits / 8 + 1 + 4095) / 4096);
+        if (ha.nchunk > nchunk_max) return vd_set_error(VD_ERR_HIP, "jpeg huffman: bit count past the buffer");
+        ctx->t_begin(4, 0);
+        e = vd_launch_jpeg_stuff(ha, ctx->stream);
+        ctx->t_end();
+        if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "jpeg stuffing: %s", hipGetErrorString(e));
+        unsigned* hsz = htot;
+        unsigned long long* hbase = (unsigned long long*)(hp + tab_bytes + huf_tab + (size_t)n * 4 + 8);
+        hbase = (unsigned long long*)(((uintptr_t)hbase + 7) & ~(uintptr_t)7);
+        VD_CHECK_HIP(hipMemcpyAsync(hsz, ha.segsize, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream));
+        VD_CHECK_HIP(hipMemcpyAsync(hbase, ha.segbase, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
+        VD_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+        for (int i = 0; i < n; ++i)
+            if (hsz[i] == 0xFFFFFFFFu) return vd_set_error(VD_ERR_CAPACITY, "jpeg frame %d does not fit %zu bytes", i, cap);
+        const size_t packed = (size_t)hbase[n];
+        if ((rc = ctx->ensure_pinned(&ctx->jseg_host, &ctx->jseg_host_bytes, packed + 64))) return rc;
+        VD_CHECK_HIP(hipMemcpyAsync(ctx->jseg_host, ha.seg, packed, hipMemcpyDeviceToHost, ctx->stream));
+        VD_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+        // headers + segment + EOI into the caller's slots, host threads over frames
+        const uint8_t* segs = (const uint8_t*)ctx->jseg_host;
+        std::atomic<int> nx{0};
+        auto copier = [&]() {
+            for (int i; (i = nx.fetch_add(1)) < n;) {
+                uint8_t* o = out + (size_t)i * cap;
+                memcpy(o, hdr, hl);
+                memcpy(o + hl, segs + hbase[i], hsz[i]);
+                o[hl + hsz[i]] = 0xFF;
+                o[hl + hsz[i] + 1] = 0xD9;
+                sizes[i] = hl + hsz[i] + 2;
+            }
+        };
+        const int nth = std::max(1, std::min(n, ctx->jpeg_threads));
+        std::vector<std::thread> cp;
+        for (int t = 1; t < nth; ++t) cp.emplace_back(copier);
+        copier();
+        for (auto& t : cp) t.join();
+        return VD_OK;
+    }
     VD_CHECK_HIP(hipMemcpyAsync(ctx->jenc_host, dp, coef_bytes, hipMemcpyDeviceToHost, ctx->stream));
     VD_CHECK_HIP(hipStreamSynchronize(ctx->stream));
     // Huffman stage, one frame per host thread

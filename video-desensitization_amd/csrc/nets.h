@@ -183,6 +183,8 @@ struct Ctx {
     hipEvent_t jpeg_ev = nullptr;                 // last H2D out of jpeg_host / jenc_host
     // JPEG frame encode (jpeg_enc.cpp): device coefficients + tables, pinned host copy
     void* jenc_dev = nullptr; size_t jenc_dev_bytes = 0;
+    void* jhuf_dev = nullptr; size_t jhuf_dev_bytes = 0;   // device entropy stage buffers
+    void* jseg_host = nullptr; size_t jseg_host_bytes = 0; // pinned: packed entropy-coded segments
     void* jenc_host = nullptr; size_t jenc_host_bytes = 0;
     int jpeg_threads = 16;                        // host entropy-decode threads
     // fp16-pair plan: per-frame activation max slots, one region per network (face 0,

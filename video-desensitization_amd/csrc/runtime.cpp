@@ -852,6 +852,8 @@ int vd_destroy(vd_ctx* h) {
     if (ctx->jpeg_planes) hipFree(ctx->jpeg_planes);
     if (ctx->jpeg_host) hipHostFree(ctx->jpeg_host);
     if (ctx->jenc_dev) hipFree(ctx->jenc_dev);
+    if (ctx->jhuf_dev) hipFree(ctx->jhuf_dev);
+    if (ctx->jseg_host) hipHostFree(ctx->jseg_host);
     if (ctx->jenc_host) hipHostFree(ctx->jenc_host);
     if (ctx->jpeg_ev) hipEventDestroy(ctx->jpeg_ev);
     for (auto& t : ctx->ev_pool) { hipEventDestroy(t.a); hipEventDestroy(t.b); }
@@ -899,6 +901,7 @@ int vd_set_option(vd_ctx* h, const char* name, int value) {
         {"x6_small_k", &VdTune::x6_small_k}, {"x6_small_tiles", &VdTune::x6_small_tiles},
         {"x6_stream", &VdTune::x6_stream}, {"x6_small_k2", &VdTune::x6_small_k2}, {"x6_bn256", &VdTune::x6_bn256},
         {"x6_exact", &VdTune::x6_exact}, {"plate_stage", &VdTune::plate_stage},
+        {"jenc_gpu", &VdTune::jenc_gpu},
     };
     for (const Opt& o : opts)
         if (strcmp(o.n, name) == 0) {

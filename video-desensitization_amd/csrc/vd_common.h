@@ -35,6 +35,7 @@ struct VdTune {
     int stem_pool = 1;        // plan: stem conv + maxpool (stem.hip)
     int ssh_fuse = 1;         // plan: SSH conv3X3 + conv5X5_1 as one conv
     int plate_s2d = 1;        // plan: YOLO space-to-depth stem input
+    int jenc_gpu = 1;         // vd_jpeg_encode: Huffman coding on the device (0: host threads)
     int plate_stage = 3;      // plate branch starts after face stage N (0: with the stem; 1-4: after
                               //   layerN; 5: after the whole face net). After layer3 its HBM-bound
                               //   convs overlap the MFMA-bound late face layers: 30.8 -> 30.0 ms/step
@@ -286,8 +287,27 @@ struct JpegEncArgs {
     int16_t* coef;                              // [n][blocks_per_frame][64] natural order
 };
 
+// Device entropy stage (jpeg_enc.hip, after jpeg_fdct_kernel): one thread per
+// scan unit (a block in MCU order, dummy blocks included) sizes, then writes, its
+// Huffman code; a per-frame scan gives the bit offsets; a stuffing pass emits the
+// entropy-coded segment with 0xFF 0x00 and the 1-bit padding.
+struct JpegHuffArgs {
+    const int16_t* coef; long blocks_per_frame; int n;
+    int hl, vl, bw[3], bh[3]; long cblk[3];
+    int mcux, units;                            // MCUs per row; scan units per frame
+    const uint16_t* code; const uint8_t* size;  // [4][256]: DC luma, DC chroma, AC luma, AC chroma
+    unsigned* bits;                             // [n][units] code length, then exclusive bit offset
+    unsigned* total;                            // [n] bits per frame
+    unsigned* words; long wcap;                 // [n][wcap] MSB-first bit buffer (zeroed)
+    uint8_t* seg; long segcap; unsigned* segsize;   // stuffed segments packed frame after frame; lengths
+    unsigned* ffcnt; int nchunk;                // [n][nchunk] 0xFF bytes per 4-KB chunk, then output offsets
+    unsigned long long* segbase;                // [n + 1] frame offsets in seg (exclusive scan; [n] = total)
+};
+
 // ---- kernel launchers (one translation unit each) ----
 hipError_t vd_launch_jpeg_fdct(const JpegEncArgs& a, hipStream_t s);
+hipError_t vd_launch_jpeg_huff(const JpegHuffArgs& a, hipStream_t s);          // codes -> words, bit totals
+hipError_t vd_launch_jpeg_stuff(const JpegHuffArgs& a, hipStream_t s);         // words -> packed segments
 hipError_t vd_launch_amax_merge(unsigned* dst, const unsigned* src, int n, hipStream_t s);
 bool vd_conv1x1_stream_ok(const ConvArgs& a);
 bool vd_conv_big_ok(const ConvArgs& a);
