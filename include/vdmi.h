@@ -135,7 +135,7 @@ int   vd_set_stream(vd_ctx* ctx, void* hip_stream);   /* NULL -> library-owned s
  * rest to the next launch. Names: conv_stream conv_stream512 conv_dual conv_taps
  * conv_n192 conv_small conv_big conv_big_kmin stream_ntt lb_pair mosaic_map
  * block_fuse chain stem_pool ssh_fuse plate_s2d f32_split x6_small_k x6_small_tiles x6_stream
- * x6_small_k2 x6_bn256 x6_exact plate_stage.
+ * x6_small_k2 x6_bn256 x6_exact plate_stage jenc_gpu.
  * VD_ERR_ARG for unknown names. */
 int   vd_set_option(vd_ctx* ctx, const char* name, int value);
 void* vd_get_stream(vd_ctx* ctx);
@@ -167,8 +167,9 @@ int vd_jpeg_info(const uint8_t* data, size_t size, int* h, int* w, int* comps);
  * quality 95, 4:2:0), libjpeg-turbo's compressor with its defaults bit-identical
  * (Pillow Image.save(..., quality, subsampling) bytes). frames: n frames h x w x 3
  * RGB at `where`; subsampling 0 = 4:4:4, 1 = 4:2:2, 2 = 4:2:0. Colour conversion,
- * downsampling, ISLOW FDCT and quantisation in a HIP kernel, Huffman coding on host
- * threads. Frame i goes to out + i * cap, its length to sizes[i]; VD_ERR_CAPACITY
+ * downsampling, ISLOW FDCT and quantisation in a HIP kernel; Huffman coding and 0xFF
+ * stuffing in HIP kernels (option jenc_gpu=0: on host threads, same bytes); frames
+ * up to 2,000,000 scan blocks (8K). Frame i goes to out + i * cap, its length to sizes[i]; VD_ERR_CAPACITY
  * if a frame needs more than cap bytes. Returns when every frame is written. */
 int vd_jpeg_encode(vd_ctx* ctx, const uint8_t* frames, int n, int h, int w, size_t pitch, int where,
                    int quality, int subsampling, uint8_t* out, size_t cap, size_t* sizes);

@@ -328,7 +328,8 @@ extern "C" int vd_jpeg_encode(vd_ctx* hctx, const uint8_t* frames, int n, int h,
         for (int c = 0; c < 3; ++c) { ha.bw[c] = g.bw[c]; ha.bh[c] = g.bh[c]; ha.cblk[c] = g.cblk[c]; }
         ha.mcux = mcux;
         const long units = (long)mcux * mcuy * (g.hl * g.vl + 2);
-        if (units > (1L << 26)) return vd_set_error(VD_ERR_ARG, "vd_jpeg_encode: frame too large");
+        // 32-bit bit offsets: units x 1728 bits (the per-unit bound the word buffer is sized by) < 2^32
+        if (units > 2000000) return vd_set_error(VD_ERR_ARG, "vd_jpeg_encode: frame too large for the device coder");
         ha.units = (int)units;
         ha.wcap = units * 54;                              // >= 1728 bits per unit: any block's codes fit
         ha.segcap = (long)(cap - hl - 2);
