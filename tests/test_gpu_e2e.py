@@ -347,16 +347,43 @@ def test_heads_fp32_dual_downsample_bit_identical(gpu):
 def test_heads_fp32_exact_canvas_stem_bit_identical(gpu):
     """The face letterbox canvas is integer-valued, exact in fp16: the fp16-pair stem
     then runs with one activation plane and two products (option x6_exact, default
-    on). The dropped lo terms are exactly zero, so the heads are bit-identical."""
+    on). The dropped lo terms are exactly zero, so the heads are bit-identical. (The
+    unfused stem: option stem_pool=0; the default fuses stem and pool, below.)"""
     import vdmi
     fr = _frames(2, 720, 1280, seed=19)
     out = {}
     for ex in (1, 0):
-        ctx = vdmi.Context(precision="fp32", max_batch=2, options={"x6_exact": ex})
+        ctx = vdmi.Context(precision="fp32", max_batch=2, options={"x6_exact": ex, "stem_pool": 0})
         try:
             ctx.load_weights(0, face_weights("default"))
             out[ex] = ctx.forward_heads(fr)
         finally:
             ctx.close()
     for a, b in zip(out[1], out[0]):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_heads_fp32_fused_stem_pool_matches_unfused(gpu):
+    """fp32 plan, default: conv1 + bn1 + relu + maxpool in one kernel (stem.hip
+    stem_pool32_kernel) over an fp16 space-to-depth canvas, the pair weights'
+    two products per MAC, f32 stem tile in LDS, f32 pooled map with its per-frame
+    max. Against the unfused stem (option stem_pool=0: 7x7 conv on the f32 canvas,
+    then maxpool): the same products summed in another order -- heads within f32
+    rounding, identical keep lists and boxes."""
+    import vdmi
+    fr = _frames(3, 1080, 1920, seed=23)
+    heads, boxes = {}, {}
+    for sp in (1, 0):
+        ctx = vdmi.Context(precision="fp32", max_batch=3, options={"stem_pool": sp})
+        try:
+            ctx.load_weights(0, face_weights("default"))
+            heads[sp] = ctx.forward_heads(fr)
+            r = ctx.detect(fr)
+            boxes[sp] = [r.frame(b)[0].copy() for b in range(3)]
+        finally:
+            ctx.close()
+    for a, b in zip(heads[1], heads[0]):
+        assert np.abs(a - b).max() <= 2e-5 * (np.abs(b).max() + 1e-6)
+    assert sum(len(x) for x in boxes[0]) > 0
+    for a, b in zip(boxes[1], boxes[0]):
         np.testing.assert_array_equal(a, b)

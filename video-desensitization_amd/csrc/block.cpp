@@ -128,15 +128,30 @@ int Ctx::add_block(Net& net, int bi, const Act& x, Act& y) {
 // stem conv (space-to-depth 4x4, 16 -> 64) + maxpool 3x3/2 (stem.hip)
 int Ctx::add_stem_pool(Net& net, int ci, const Act& x, Act& y) {
     const Conv& cv = convs[ci];
-    if (f32 || f16 || x.f32 || y.f32 || cv.cin != 16 || cv.cin_pad != 16 || cv.cout != 64 || cv.kh != 4 || cv.kw != 4 ||
+    const bool pair = f32 && cv.split == 2;             // fp32 plan: fp16 pair weights, f32 pooled map
+    if ((f32 && !pair) || f16 || x.f32 || y.f32 != pair || (pair && !cv.wx3) || cv.cin != 16 || cv.cin_pad != 16 || cv.cout != 64 || cv.kh != 4 || cv.kw != 4 ||
         cv.stride != 1 || cv.pad != 1 || cv.act != VD_ACT_RELU || cv.kpad != 256 || x.c != 16 || y.c != 64 ||
         !vd_stem_pool_ok(x.h, x.w, y.h, y.w))
         return vd_set_error(VD_ERR_ARG, "fused stem plan shape mismatch");
-    std::vector<uint16_t> w;
-    std::vector<float> sc, sh;
-    int rc = fetch(cv, w, sc, sh);
-    if (rc) return rc;
-    std::vector<uint16_t> f = frags(w, cv.kpad, 4, 8, perm32);
+    std::vector<uint16_t> f;
+    int rc;
+    if (pair) {   // planes of the packed pair [npad][kpad / 32][2][32] -> fragments, hi then lo
+        const int nk = cv.kpad / 32;
+        std::vector<uint16_t> wx((size_t)cv.npad * cv.kpad * 2), pl((size_t)cv.npad * cv.kpad);
+        VD_CHECK_HIP(hipMemcpy(wx.data(), cv.wx3, wx.size() * 2, hipMemcpyDeviceToHost));
+        for (int p = 0; p < 2; ++p) {
+            for (int n = 0; n < cv.npad; ++n)
+                for (int k = 0; k < cv.kpad; ++k)
+                    pl[(size_t)n * cv.kpad + k] = wx[(((size_t)n * nk + k / 32) * 2 + p) * 32 + k % 32];
+            std::vector<uint16_t> fp = frags(pl, cv.kpad, 4, 8, perm32);
+            f.insert(f.end(), fp.begin(), fp.end());
+        }
+    } else {
+        std::vector<uint16_t> w;
+        std::vector<float> sc, sh;
+        if ((rc = fetch(cv, w, sc, sh))) return rc;
+        f = frags(w, cv.kpad, 4, 8, perm32);
+    }
     Op op{};
     op.kind = OP_STEMPOOL;
     op.conv = ci;
@@ -174,10 +189,15 @@ int Ctx::run_stem_pool_op(const Op& op, int f0, int n, int fam) {
     const Conv& cv = convs[op.conv];
     StemPoolArgs a{};
     a.x = foff_b(op.x, f0); a.B = n; a.xh = op.x.h; a.xw = op.x.w;
-    a.y = (void*)foff_b(op.y, f0); a.ph = op.y.h; a.pw = op.y.w;
+    a.y = (void*)((char*)op.y.p + (size_t)f0 * op.y.h * op.y.w * op.y.c * (op.y.f32 ? 4 : 2)); a.ph = op.y.h; a.pw = op.y.w;
     a.wf = op.wf; a.scale = cv.scale; a.shift = cv.shift;
+    const bool pair = op.y.f32;
+    if (pair) {
+        a.scale = cv.scale_x;                           // BN scale with the weights' power-of-two folded in
+        a.ymax = op.y.amax ? op.y.amax + f0 : nullptr;
+    }
     t_begin(fam, cv.flops_per_px * n * (double)(op.x.h - 1) * (op.x.w - 1));
-    hipError_t e = vd_launch_stem_pool(a, stream);
+    hipError_t e = pair ? vd_launch_stem_pool32(a, stream) : vd_launch_stem_pool(a, stream);
     t_end();
     if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "fused stem launch: %s", hipGetErrorString(e));
     return VD_OK;

@@ -119,9 +119,12 @@ int vd_build_face(Ctx& c, const WMap& W) {
     const int cpad = c.f32 ? 4 : 8;
     int rc;
     F.mnet = find_t(W, "body.stage1.0.0.weight") != nullptr;   // cfg_mnet (face.py:35, retinaface.py:60)
-    F.s2d = !c.f32 && !c.f16 && !F.mnet && H % 2 == 0 && Wd % 2 == 0;
+    // fp32 plan (fp16 pairs): the fused stem + pool on an fp16 space-to-depth canvas
+    const bool s2d32 = c.f32 && c.tune.f32_split == 2 && c.tune.stem_pool &&
+                       vd_stem_pool_ok(H / 2 + 1, Wd / 2 + 1, H / 4, Wd / 4);
+    F.s2d = ((!c.f32 && !c.f16) || s2d32) && !F.mnet && H % 2 == 0 && Wd % 2 == 0;
     c.amax_begin(0);
-    if (F.s2d) rc = c.act(F.input, H / 2 + 1, Wd / 2 + 1, 16);
+    if (F.s2d) rc = c.act(F.input, H / 2 + 1, Wd / 2 + 1, 16, false, c.f32);
     else rc = c.act(F.input, H, Wd, cpad);
     if (rc) return rc;
     F.input.amax = nullptr;            // letterboxed canvas: |pixel - mean| <= 255

@@ -201,7 +201,7 @@ struct Ctx {
     size_t ev_used = 0;
 
     int dalloc(void** p, size_t bytes);
-    int act(Act& a, int h, int w, int c, bool f32out = false);
+    int act(Act& a, int h, int w, int c, bool f32out = false, bool half = false);   // half: 2-byte elements
     int ensure_staging(void** p, size_t* have, size_t need);
     int ensure_pinned(void** p, size_t* have, size_t need);
     int upload_conv(Conv& cv, const std::vector<float>& w_oihw, const std::vector<float>& scale,

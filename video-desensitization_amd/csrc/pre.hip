@@ -76,6 +76,26 @@ __device__ __forceinline__ void canvas_px(const LetterboxArgs& a, const uint8_t*
     }
 }
 
+// one 2x2 block's 16 values (4 sub-pixels x [3 channels, 0]): bf16, or fp16 (a.out_f16:
+// the fp32 plan's fused stem canvas, integer values, exact)
+__device__ __forceinline__ void store_s2d(const LetterboxArgs& a, size_t idx, const float (&v)[16]) {
+    uint4 u[2];
+    if (a.out_f16) {
+        _Float16 t[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) t[i] = (_Float16)v[i];
+        u[0] = *(const uint4*)t; u[1] = *(const uint4*)(t + 8);
+    } else {
+        __bf16 t[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) t[i] = (__bf16)v[i];
+        u[0] = *(const uint4*)t; u[1] = *(const uint4*)(t + 8);
+    }
+    uint4* out = (uint4*)((uint16_t*)a.out + idx * 16);
+    out[0] = u[0];
+    out[1] = u[1];
+}
+
 // Space-to-depth form (a.s2d): one thread per 2x2 canvas block, 32 B out.
 __global__ __launch_bounds__(256) void letterbox_s2d_kernel(LetterboxArgs a) {
     const int X = blockIdx.x * 256 + threadIdx.x;
@@ -84,18 +104,16 @@ __global__ __launch_bounds__(256) void letterbox_s2d_kernel(LetterboxArgs a) {
     const int OW = a.ow / 2 + 1, OH = a.oh / 2 + 1;
     if (X >= OW) return;
     const uint8_t* img = a.src + (size_t)f * a.ih * a.pitch;
-    __bf16 t[16];
+    float t[16];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         const int y = 2 * Y + (s >> 1) - 1, x = 2 * X + (s & 1) - 1;
         float v[3] = {0.f, 0.f, 0.f};   // conv zero padding outside the canvas
         if ((unsigned)y < (unsigned)a.oh && (unsigned)x < (unsigned)a.ow) canvas_px(a, img, y, x, v);
-        t[4 * s + 0] = (__bf16)v[0]; t[4 * s + 1] = (__bf16)v[1]; t[4 * s + 2] = (__bf16)v[2];
-        t[4 * s + 3] = (__bf16)0.f;
+        t[4 * s + 0] = v[0]; t[4 * s + 1] = v[1]; t[4 * s + 2] = v[2];
+        t[4 * s + 3] = 0.f;
     }
-    __bf16* out = (__bf16*)a.out + (((size_t)f * OH + Y) * OW + X) * 16;
-    *(uint4*)out = *(const uint4*)t;
-    *(uint4*)(out + 8) = *(const uint4*)(t + 8);
+    store_s2d(a, ((size_t)f * OH + Y) * OW + X, t);
 }
 
 // Space-to-depth form with the source rows staged in LDS: one workgroup per
@@ -177,7 +195,7 @@ __global__ __launch_bounds__(256) void letterbox_s2d_lds_kernel(LetterboxArgs a)
     }
     __syncthreads();
     for (int X = threadIdx.x; X < OW; X += 256) {
-        __bf16 t[16];
+        float t[16];
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             const int h = s >> 1;
@@ -186,12 +204,10 @@ __global__ __launch_bounds__(256) void letterbox_s2d_lds_kernel(LetterboxArgs a)
             const int y = 2 * Y + h - 1;
             if ((unsigned)y < (unsigned)a.oh && (unsigned)x < (unsigned)a.ow)
                 lb_px_lds(a, lrow + (2 * h) * RS, lrow + (2 * h + 1) * RS, ty[h], x, rin[h], v);
-            t[4 * s + 0] = (__bf16)v[0]; t[4 * s + 1] = (__bf16)v[1]; t[4 * s + 2] = (__bf16)v[2];
-            t[4 * s + 3] = (__bf16)0.f;
+            t[4 * s + 0] = v[0]; t[4 * s + 1] = v[1]; t[4 * s + 2] = v[2];
+            t[4 * s + 3] = 0.f;
         }
-        __bf16* out = (__bf16*)a.out + (((size_t)f * OH + Y) * OW + X) * 16;
-        *(uint4*)out = *(const uint4*)t;
-        *(uint4*)(out + 8) = *(const uint4*)(t + 8);
+        store_s2d(a, ((size_t)f * OH + Y) * OW + X, t);
     }
 }
 

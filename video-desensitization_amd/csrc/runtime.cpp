@@ -85,9 +85,9 @@ int Ctx::dalloc(void** p, size_t bytes) {
     return VD_OK;
 }
 
-int Ctx::act(Act& a, int h, int w, int c, bool f32out) {
+int Ctx::act(Act& a, int h, int w, int c, bool f32out, bool half) {
     a.h = h; a.w = w; a.c = c;
-    a.f32 = f32out || f32;
+    a.f32 = !half && (f32out || f32);
     size_t bytes = (size_t)cfg.max_batch * h * w * c * (a.f32 ? 4 : 2);
     int rc = dalloc(&a.p, bytes);
     if (rc) return rc;
@@ -698,7 +698,9 @@ void Ctx::face_letterbox_args(const uint8_t* dframes, int n, int h, int w, size_
     a.mean[0] = 104.f; a.mean[1] = 117.f; a.mean[2] = 123.f;
     a.div = 1.f;
     a.flip = 0;
-    a.out = face.input.p; a.cpad = face.input.c; a.out_f32 = f32 ? 1 : 0; a.out_f16 = f16 ? 1 : 0;
+    // fp32 plan with the fused stem: an fp16 space-to-depth canvas (integer values, exact)
+    a.out = face.input.p; a.cpad = face.input.c; a.out_f32 = face.input.f32 ? 1 : 0;
+    a.out_f16 = (f16 || (f32 && !face.input.f32)) ? 1 : 0;
     a.s2d = face.s2d ? 1 : 0;
     *out = a;
 }
@@ -1194,7 +1196,7 @@ int vdt_letterbox(vd_ctx* h, const uint8_t* frames, int n, int fh, int fw, size_
     std::vector<uint16_t> hb;
     std::vector<float> hf;
     VD_CHECK_HIP(hipStreamSynchronize(ctx->stream));
-    if (ctx->f32) {
+    if (in.f32) {
         hf.resize(px * in.c);
         VD_CHECK_HIP(hipMemcpy(hf.data(), in.p, hf.size() * 4, hipMemcpyDeviceToHost));
     } else {
@@ -1211,8 +1213,12 @@ int vdt_letterbox(vd_ctx* h, const uint8_t* frames, int n, int fh, int fw, size_
                         if (c < 3) {
                             const int Y = (y + 1) >> 1, X = (x + 1) >> 1, s = ((y + 1) & 1) * 2 + ((x + 1) & 1);
                             const size_t i = (((size_t)f * in.h + Y) * in.w + X) * in.c + s * 4 + c;
-                            uint32_t u = (uint32_t)hb[i] << 16;
-                            memcpy(&v, &u, 4);
+                            if (ctx->f32) {                 // fused fp32 stem: fp16 canvas
+                                v = from_half(true, hb[i]);
+                            } else {
+                                uint32_t u = (uint32_t)hb[i] << 16;
+                                memcpy(&v, &u, 4);
+                            }
                         }
                         out[(((size_t)f * H + y) * W + x) * cpad + c] = v;
                     }
@@ -1222,7 +1228,7 @@ int vdt_letterbox(vd_ctx* h, const uint8_t* frames, int n, int fh, int fw, size_
         for (int c = 0; c < cpad; ++c) {
             float v = 0.f;
             if (c < in.c) {
-                if (ctx->f32) v = hf[i * in.c + c];
+                if (in.f32) v = hf[i * in.c + c];
                 else v = from_half(ctx->f16, hb[i * in.c + c]);
             }
             out[i * cpad + c] = v;

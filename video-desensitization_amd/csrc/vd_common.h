@@ -132,7 +132,9 @@ struct StemPoolArgs {
     const void* x; int B, xh, xw;
     void* y; int ph, pw;
     const void* wf;              // MFMA fragments [4 groups of 16 ch, pairs permuted][8 k-steps][64 lanes][8]
+                                 //   (fp32 plan: [2 planes: hi, lo] of that, fp16; x = X' in fp16, exact)
     const float* scale; const float* shift;
+    unsigned* ymax;              // fp32 plan: per-frame max |y| slots of the pooled map
 };
 
 // Device buffers + parameters for one frame batch's detection post-processing.
@@ -326,6 +328,7 @@ bool vd_block_ok(int cin, bool ds, int h, int w);
 bool vd_stem_pool_ok(int xh, int xw, int ph, int pw);
 hipError_t vd_launch_dwconv(const DwConvArgs& a, bool f32, bool f16, hipStream_t s);
 hipError_t vd_launch_stem_pool(const StemPoolArgs& a, hipStream_t s);
+hipError_t vd_launch_stem_pool32(const StemPoolArgs& a, hipStream_t s);   // fp16-pair plan, f32 pooled map
 hipError_t vd_launch_block(const BlockArgs& a, hipStream_t s);
 bool vd_chain_ok(int cmid, int cout, int kpad3, int kpad1, int ld_t2, int ld_res, int ld_y, int ld_y2, long M);
 hipError_t vd_launch_chain(const ChainArgs& a, hipStream_t s);
