@@ -19,7 +19,7 @@ def main(path, B=64):
     # its last len(plan) conv launches are the last step's layers
     per = {}
     for r in rows:
-        if "conv" in r["Kernel_Name"]:
+        if "conv" in r["Kernel_Name"] or "stem_pool" in r["Kernel_Name"]:
             per.setdefault(r["Stream_Id"], []).append(r)
     convs = max(per.values(), key=len)[-len(plan):]
     tot = fl_tot = 0

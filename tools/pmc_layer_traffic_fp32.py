@@ -25,7 +25,7 @@ def last_step(d, counter, n):
             vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
     per = {}
     for r in trace:
-        if "conv" in r["Kernel_Name"]:
+        if "conv" in r["Kernel_Name"] or "stem_pool" in r["Kernel_Name"]:
             per.setdefault(r["Stream_Id"], []).append(r)
     rows = max(per.values(), key=len)[-n:]          # the face stream: most conv launches
     return [(vals.get(r["Dispatch_Id"], 0.0) * 1024.0, (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3)
