@@ -236,8 +236,9 @@ class Context:
         if n == 0:
             raise ValueError("no frames")
         h, w, _ = jpeg_info(jpegs[0])
-        bufs = [ctypes.create_string_buffer(j, len(j)) for j in jpegs]
-        ptrs = (ctypes.c_void_p * n)(*[ctypes.addressof(b) for b in bufs])
+        # the bytes objects' own buffers (immutable; the library only reads them): no copy
+        bufs = [ctypes.c_char_p(j) for j in jpegs]
+        ptrs = (ctypes.c_void_p * n)(*[ctypes.cast(b, ctypes.c_void_p).value for b in bufs])
         sizes = (ctypes.c_size_t * n)(*[len(j) for j in jpegs])
         if out is None:
             out = np.empty((n, h, w, 3), np.uint8)

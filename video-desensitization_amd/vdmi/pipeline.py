@@ -341,15 +341,18 @@ def _write_bytes(data, path):
 
 def _gpu_codec_batches(batches, output_dir, face_detector, plate_detector, batch_size, mosaic_plates, io, logger,
                        quality):
-    """Frame I/O on the GPU: file bytes (reader threads, next batch prefetched) ->
-    vd_jpeg_decode into device frames -> one vd_process (faces | plates | mosaic) ->
-    vd_jpeg_encode from device memory -> writer threads. A frame the GPU decoder
-    does not take (progressive, other layout) is decoded by the host loader; a
-    batch whose inference fails is dropped (combine_detect.py:226-228)."""
+    """Frame I/O on the GPU: file bytes (reader threads) -> vd_jpeg_decode into
+    device frames -> one vd_process (faces | plates | mosaic) -> vd_jpeg_encode from
+    device memory -> writer threads. Batch i+1 is read and decoded (its host Huffman
+    threads and IDCT kernels, on a second weight-less context and stream) while
+    batch i is processed and encoded. A frame the GPU decoder does not take
+    (progressive, other layout) is decoded by the host loader; a batch whose
+    inference fails is dropped (combine_detect.py:226-228)."""
     import torch
-    from .context import DeviceBoxes, jpeg_info
+    from .context import Context, DeviceBoxes, jpeg_info
     ctx = fused_context(face_detector, plate_detector, batch_size)
     dev = torch.device(f"cuda:{ctx.device}")
+    dctx = Context(device=ctx.device, precision="fp32", max_batch=max(int(batch_size), 1))
     flags = _lib.VD_PROC_FACES | _lib.VD_PROC_MOSAIC | _lib.VD_PROC_PLATES
     if mosaic_plates:
         flags |= _lib.VD_PROC_MOSAIC_PLATES
@@ -357,17 +360,10 @@ def _gpu_codec_batches(batches, output_dir, face_detector, plate_detector, batch
     plates = DeviceBoxes(batch_size, 256, dev)
     totals = [0, 0, 0]
     save_futs = []
-    read = lambda files: list(io.map(_read_bytes, files))
-    fut = io.submit(read, batches[0]) if batches else None
-    for bi, files in enumerate(batches):
-        try:
-            blobs = fut.result()
-        except Exception as e:
-            logger.error(f"loading failed: {e}")
-            blobs = None
-        fut = io.submit(read, batches[bi + 1]) if bi + 1 < len(batches) else None
-        if blobs is None:
-            continue
+
+    def load(files):
+        """files -> [(items, device frames)] per frame size, decoded and synchronised"""
+        blobs = list(io.map(_read_bytes, files))
         groups = {}
         for f, b in zip(files, blobs):
             try:
@@ -375,27 +371,48 @@ def _gpu_codec_batches(batches, output_dir, face_detector, plate_detector, batch
             except Exception:
                 key = load_image_rgb(f).shape[:2]
             groups.setdefault(key, []).append((f, b))
+        out = []
         for (h, w), items in groups.items():
+            d_in = torch.empty((len(items), h, w, 3), dtype=torch.uint8, device=dev)
             try:
-                d_in = torch.empty((len(items), h, w, 3), dtype=torch.uint8, device=dev)
-                try:
-                    ctx.jpeg_decode([b for _, b in items], out=d_in)
-                except Exception:            # not a layout the GPU decoder takes: host decode
-                    d_in.copy_(torch.from_numpy(np.stack([load_image_rgb(f) for f, _ in items])))
-                    torch.cuda.synchronize(dev)  # the copy ran on torch's stream, not the context's
-                out, fc, pc = ctx.process(d_in, faces=faces, plates=plates, flags=flags)
-                jpgs = ctx.jpeg_encode(out, quality=quality, subsampling=2)
-            except Exception as e:           # combine_detect.py:226-228: the batch is dropped
-                logger.error(f"parallel inference failed: {e}")
+                dctx.jpeg_decode([b for _, b in items], out=d_in)
+                dctx.sync()
+            except Exception:                # not a layout the GPU decoder takes: host decode
+                d_in.copy_(torch.from_numpy(np.stack([load_image_rgb(f) for f, _ in items])))
+                torch.cuda.synchronize(dev)  # the copy ran on torch's stream, not a context's
+            out.append((items, d_in))
+        return out
+
+    ahead = ThreadPoolExecutor(1)
+    try:
+        fut = ahead.submit(load, batches[0]) if batches else None
+        for bi in range(len(batches)):
+            try:
+                decoded = fut.result()
+            except Exception as e:
+                logger.error(f"loading failed: {e}")
+                decoded = None
+            fut = ahead.submit(load, batches[bi + 1]) if bi + 1 < len(batches) else None
+            if decoded is None:
                 continue
-            n = len(items)
-            for (path, _), data in zip(items, jpgs):
-                save_futs.append(io.submit(_write_bytes, data,
-                                           os.path.join(output_dir, f"processed_{os.path.basename(path)}")))
-            totals[0] += n
-            totals[1] += int(fc.count[:n].sum().item())
-            if mosaic_plates:
-                totals[2] += int(pc.count[:n].sum().item())
+            for items, d_in in decoded:
+                try:
+                    out, fc, pc = ctx.process(d_in, faces=faces, plates=plates, flags=flags)
+                    jpgs = ctx.jpeg_encode(out, quality=quality, subsampling=2)
+                except Exception as e:       # combine_detect.py:226-228: the batch is dropped
+                    logger.error(f"parallel inference failed: {e}")
+                    continue
+                n = len(items)
+                for (path, _), data in zip(items, jpgs):
+                    save_futs.append(io.submit(_write_bytes, data,
+                                               os.path.join(output_dir, f"processed_{os.path.basename(path)}")))
+                totals[0] += n
+                totals[1] += int(fc.count[:n].sum().item())
+                if mosaic_plates:
+                    totals[2] += int(pc.count[:n].sum().item())
+    finally:
+        ahead.shutdown()
+        dctx.close()
     _save_all(save_futs, logger)
     return tuple(totals)
 
