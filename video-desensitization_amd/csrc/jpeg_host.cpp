@@ -24,6 +24,7 @@
 #include <atomic>
 #include <cstring>
 #include <thread>
+#include <memory>
 #include <vector>
 
 namespace {
@@ -285,8 +286,10 @@ int entropy(const Info& j, std::vector<uint32_t>& entries, std::vector<uint32_t>
     entries.clear();
     entries.reserve(nblk * 8);
     // blocks are produced in MCU order, stored grouped by block index: collect per block first
-    std::vector<uint32_t> ent_mcu;
-    ent_mcu.reserve(nblk * 8);
+    // at most 64 entries per block: written through a raw cursor (no per-entry capacity checks)
+    std::unique_ptr<uint32_t[]> ent_buf(new uint32_t[nblk * 64 + 64]);   // uninitialised
+    uint32_t* const ent0 = ent_buf.get();
+    uint32_t* wp = ent0;
     std::vector<uint32_t> where(nblk * 2);               // [start, count] into ent_mcu
     Bits b{j.scan, j.scan_len};
     int pred[3] = {0, 0, 0};
@@ -305,11 +308,11 @@ int entropy(const Info& j, std::vector<uint32_t>& entries, std::vector<uint32_t>
                 for (int by = 0; by < c.vs; ++by)
                     for (int bx = 0; bx < c.hs; ++bx) {
                         const size_t blk = cbase[ci] + (size_t)(my * c.vs + by) * c.bw + (mx * c.hs + bx);
-                        where[2 * blk] = (uint32_t)ent_mcu.size();
+                        where[2 * blk] = (uint32_t)(wp - ent0);
                         const int s = decode_sym(b, dc);
                         if (s < 0 || s > 11) return vd_set_error(VD_ERR_ARG, "jpeg: bad DC code");
                         pred[ci] += extend(b.get(s), s);
-                        if (pred[ci]) ent_mcu.push_back((uint32_t)(0u << 16) | (uint16_t)(int16_t)pred[ci]);
+                        if (pred[ci]) *wp++ = (uint32_t)(0u << 16) | (uint16_t)(int16_t)pred[ci];
                         for (int k = 1; k < 64;) {
                             const uint32_t look = b.peek(kLook);
                             if (const int fl = ac.fa_len[look]) {   // code + extra bits in one look
@@ -319,7 +322,7 @@ int entropy(const Info& j, std::vector<uint32_t>& entries, std::vector<uint32_t>
                                 if (run == 16) { k += 16; continue; }   // ZRL
                                 k += run;
                                 if (k > 63) return vd_set_error(VD_ERR_ARG, "jpeg: AC run past the block");
-                                ent_mcu.push_back(((uint32_t)kZigzag[k] << 16) | (uint16_t)ac.fa_val[look]);
+                                *wp++ = ((uint32_t)kZigzag[k] << 16) | (uint16_t)ac.fa_val[look];
                                 ++k;
                                 continue;
                             }
@@ -334,19 +337,19 @@ int entropy(const Info& j, std::vector<uint32_t>& entries, std::vector<uint32_t>
                             k += r;
                             if (k > 63) return vd_set_error(VD_ERR_ARG, "jpeg: AC run past the block");
                             const int v = extend(b.get(sz), sz);
-                            ent_mcu.push_back(((uint32_t)kZigzag[k] << 16) | (uint16_t)(int16_t)v);
+                            *wp++ = ((uint32_t)kZigzag[k] << 16) | (uint16_t)(int16_t)v;
                             ++k;
                         }
-                        where[2 * blk + 1] = (uint32_t)ent_mcu.size() - where[2 * blk];
+                        where[2 * blk + 1] = (uint32_t)(wp - ent0) - where[2 * blk];
                     }
             }
         }
     // regroup into block order
-    entries.resize(ent_mcu.size());
+    entries.resize((size_t)(wp - ent0));
     size_t o = 0;
     for (size_t blk = 0; blk < nblk; ++blk) {
         const uint32_t st = where[2 * blk], cn = where[2 * blk + 1];
-        memcpy(entries.data() + o, ent_mcu.data() + st, cn * 4);
+        memcpy(entries.data() + o, ent0 + st, cn * 4);
         counts[blk] = cn;
         o += cn;
     }
@@ -455,13 +458,24 @@ extern "C" int vd_jpeg_decode(vd_ctx* hctx, const uint8_t* const* data, const si
     uint32_t* hoff = (uint32_t*)hp;
     uint16_t* hq = (uint16_t*)(hp + off_bytes);
     uint32_t* hent = (uint32_t*)(hp + off_bytes + q_bytes);
-    size_t o = 0, b = 0;
-    for (int i = 0; i < n; ++i) {
-        for (size_t k = 0; k < cnt[i].size(); ++k, ++b) { hoff[b] = (uint32_t)o; o += cnt[i][k]; }
-        memcpy(hent + (o - ent[i].size()), ent[i].data(), ent[i].size() * 4);
-        for (int c = 0; c < j0.nc; ++c) memcpy(hq + ((size_t)i * 3 + c) * 64, info[i].q[info[i].c[c].tq], 128);
-    }
-    hoff[nblk] = (uint32_t)o;
+    // per-image entry bases, then the packing itself on the same host threads (a
+    // noise 1080p frame carries ~11 MB of entries: a serial copy would rival the decode)
+    std::vector<size_t> ebase(n + 1, 0);
+    for (int i = 0; i < n; ++i) ebase[i + 1] = ebase[i] + ent[i].size();
+    next = 0;
+    auto packer = [&]() {
+        for (int i; (i = next.fetch_add(1)) < n;) {
+            size_t o = ebase[i], b = (size_t)i * nblk_img;
+            for (size_t k = 0; k < cnt[i].size(); ++k, ++b) { hoff[b] = (uint32_t)o; o += cnt[i][k]; }
+            memcpy(hent + ebase[i], ent[i].data(), ent[i].size() * 4);
+            for (int c = 0; c < j0.nc; ++c) memcpy(hq + ((size_t)i * 3 + c) * 64, info[i].q[info[i].c[c].tq], 128);
+        }
+    };
+    pool.clear();
+    for (int t = 1; t < nthreads; ++t) pool.emplace_back(packer);
+    packer();
+    for (auto& t : pool) t.join();
+    hoff[nblk] = (uint32_t)ebase[n];
     VD_CHECK_HIP(hipMemcpyAsync(ctx->jpeg_dev, ctx->jpeg_host, off_bytes + q_bytes + tot_ent * 4,
                                 hipMemcpyHostToDevice, ctx->stream));
     VD_CHECK_HIP(hipEventRecord(ctx->jpeg_ev, ctx->stream));
