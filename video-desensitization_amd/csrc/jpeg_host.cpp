@@ -276,21 +276,25 @@ inline int decode_sym(Bits& b, const Huff& h) {
 
 inline int extend(int v, int s) { return (s && v < (1 << (s - 1))) ? v - (1 << s) + 1 : v; }
 
-// Entropy decode one image into per-block entry lists, block order (component,
-// block row, block col). blk_count[b] = entries of block b.
-int entropy(const Info& j, std::vector<uint32_t>& entries, std::vector<uint32_t>& counts) {
+// Entropy decode one image: entries (coefficient index << 16 | value) in MCU order
+// into `ent` (at most 64 per block, written through a raw cursor into an
+// uninitialised buffer), and per block, in block order (component, block row,
+// block col), where[2 b] = its first entry, where[2 b + 1] = its entry count.
+struct Entries {
+    std::unique_ptr<uint32_t[]> ent;
+    size_t n = 0;
+    std::vector<uint32_t> where;
+};
+
+int entropy(const Info& j, Entries& out) {
     size_t nblk = 0;
     size_t cbase[3];
     for (int i = 0; i < j.nc; ++i) { cbase[i] = nblk; nblk += (size_t)j.c[i].bw * j.c[i].bh; }
-    counts.assign(nblk, 0);
-    entries.clear();
-    entries.reserve(nblk * 8);
-    // blocks are produced in MCU order, stored grouped by block index: collect per block first
-    // at most 64 entries per block: written through a raw cursor (no per-entry capacity checks)
-    std::unique_ptr<uint32_t[]> ent_buf(new uint32_t[nblk * 64 + 64]);   // uninitialised
-    uint32_t* const ent0 = ent_buf.get();
+    out.ent.reset(new uint32_t[nblk * 64 + 64]);
+    uint32_t* const ent0 = out.ent.get();
     uint32_t* wp = ent0;
-    std::vector<uint32_t> where(nblk * 2);               // [start, count] into ent_mcu
+    std::vector<uint32_t>& where = out.where;
+    where.assign(nblk * 2, 0u);
     Bits b{j.scan, j.scan_len};
     int pred[3] = {0, 0, 0};
     int mcu_n = 0;
@@ -344,15 +348,7 @@ int entropy(const Info& j, std::vector<uint32_t>& entries, std::vector<uint32_t>
                     }
             }
         }
-    // regroup into block order
-    entries.resize((size_t)(wp - ent0));
-    size_t o = 0;
-    for (size_t blk = 0; blk < nblk; ++blk) {
-        const uint32_t st = where[2 * blk], cn = where[2 * blk + 1];
-        memcpy(entries.data() + o, ent0 + st, cn * 4);
-        counts[blk] = cn;
-        o += cn;
-    }
+    out.n = (size_t)(wp - ent0);
     return VD_OK;
 }
 
@@ -382,17 +378,20 @@ extern "C" int vdt_jpeg_coefficients(const uint8_t* data, size_t size, int16_t* 
                                      int* nblocks) {
     if (!data) return vd_set_error(VD_ERR_ARG, "null data");
     Info j;
-    std::vector<uint32_t> ent, cnt;
+    Entries en;
     int rc = parse(data, size, j);
-    if (!rc) rc = entropy(j, ent, cnt);
+    if (!rc) rc = entropy(j, en);
     if (rc) return rc;
-    if (nblocks) *nblocks = (int)cnt.size();
+    const size_t nb = en.where.size() / 2;
+    if (nblocks) *nblocks = (int)nb;
     if (!out) return VD_OK;
-    if (cap_blocks < cnt.size()) return vd_set_error(VD_ERR_ARG, "need %zu blocks", cnt.size());
-    memset(out, 0, cnt.size() * 64 * 2);
-    size_t o = 0;
-    for (size_t b = 0; b < cnt.size(); ++b)
-        for (uint32_t e = 0; e < cnt[b]; ++e, ++o) out[b * 64 + (ent[o] >> 16)] = (int16_t)(ent[o] & 0xFFFF);
+    if (cap_blocks < nb) return vd_set_error(VD_ERR_ARG, "need %zu blocks", nb);
+    memset(out, 0, nb * 64 * 2);
+    for (size_t b = 0; b < nb; ++b)
+        for (uint32_t e = 0; e < en.where[2 * b + 1]; ++e) {
+            const uint32_t v = en.ent[en.where[2 * b] + e];
+            out[b * 64 + (v >> 16)] = (int16_t)(v & 0xFFFF);
+        }
     return VD_OK;
 }
 
@@ -406,7 +405,7 @@ extern "C" int vd_jpeg_decode(vd_ctx* hctx, const uint8_t* const* data, const si
         return vd_set_error(VD_ERR_ARG, "vd_jpeg_decode: bad arguments");
     // 1) parse + entropy decode, one image per host thread
     std::vector<Info> info(n);
-    std::vector<std::vector<uint32_t>> ent(n), cnt(n);
+    std::vector<Entries> ent(n);
     std::vector<int> rcs(n, VD_OK);
     std::vector<std::string> errs(n);
     std::atomic<int> next{0};
@@ -415,7 +414,7 @@ extern "C" int vd_jpeg_decode(vd_ctx* hctx, const uint8_t* const* data, const si
             int rc = parse(data[i], sizes[i], info[i]);
             if (!rc && (info[i].h != fh || info[i].w != fw))
                 rc = vd_set_error(VD_ERR_ARG, "jpeg %d is %dx%d, expected %dx%d", i, info[i].w, info[i].h, fw, fh);
-            if (!rc) rc = entropy(info[i], ent[i], cnt[i]);
+            if (!rc) rc = entropy(info[i], ent[i]);
             rcs[i] = rc;
             if (rc) errs[i] = vd_last_error();
         }
@@ -443,7 +442,7 @@ extern "C" int vd_jpeg_decode(vd_ctx* hctx, const uint8_t* const* data, const si
     }
     a.blocks_per_image = (int)nblk_img;
     size_t tot_ent = 0;
-    for (int i = 0; i < n; ++i) tot_ent += ent[i].size();
+    for (int i = 0; i < n; ++i) tot_ent += ent[i].n;
     const size_t nblk = nblk_img * n;
     const size_t off_bytes = (nblk + 1) * 4, q_bytes = (size_t)n * 3 * 64 * 2, ent_bytes = std::max<size_t>(tot_ent, 1) * 4;
     const size_t need = off_bytes + q_bytes + ent_bytes + 64;
@@ -461,13 +460,19 @@ extern "C" int vd_jpeg_decode(vd_ctx* hctx, const uint8_t* const* data, const si
     // per-image entry bases, then the packing itself on the same host threads (a
     // noise 1080p frame carries ~11 MB of entries: a serial copy would rival the decode)
     std::vector<size_t> ebase(n + 1, 0);
-    for (int i = 0; i < n; ++i) ebase[i + 1] = ebase[i] + ent[i].size();
+    for (int i = 0; i < n; ++i) ebase[i + 1] = ebase[i] + ent[i].n;
     next = 0;
     auto packer = [&]() {
         for (int i; (i = next.fetch_add(1)) < n;) {
+            // regroup MCU order -> block order straight into the pinned buffer
             size_t o = ebase[i], b = (size_t)i * nblk_img;
-            for (size_t k = 0; k < cnt[i].size(); ++k, ++b) { hoff[b] = (uint32_t)o; o += cnt[i][k]; }
-            memcpy(hent + ebase[i], ent[i].data(), ent[i].size() * 4);
+            const std::vector<uint32_t>& wh = ent[i].where;
+            for (size_t k = 0; k < nblk_img; ++k, ++b) {
+                const uint32_t st = wh[2 * k], cn = wh[2 * k + 1];
+                hoff[b] = (uint32_t)o;
+                memcpy(hent + o, ent[i].ent.get() + st, (size_t)cn * 4);
+                o += cn;
+            }
             for (int c = 0; c < j0.nc; ++c) memcpy(hq + ((size_t)i * 3 + c) * 64, info[i].q[info[i].c[c].tq], 128);
         }
     };
