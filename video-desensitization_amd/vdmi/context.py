@@ -264,7 +264,10 @@ class Context:
         # typical frames need < 3 B/pixel; the retry bound covers any baseline block
         # (63 AC codes of 26 bits + DC, every byte stuffed) at 1.5-3 samples/pixel
         for cap in (h * w * 3 + 65536, h * w * 20 + 65536):
-            out = np.empty(n * cap, np.uint8)
+            # one staging buffer per context, reused (fresh pages would fault in on every call)
+            out = getattr(self, "_jenc_buf", None)
+            if out is None or out.size < n * cap:
+                out = self._jenc_buf = np.empty(n * cap, np.uint8)
             rc = self._lib.vd_jpeg_encode(self._h, p, n, h, w, pitch, where, int(quality), int(subsampling),
                                           ptr(out), cap, sizes)
             if rc != _lib.VD_ERR_CAPACITY:
