@@ -135,7 +135,7 @@ int   vd_set_stream(vd_ctx* ctx, void* hip_stream);   /* NULL -> library-owned s
  * rest to the next launch. Names: conv_stream conv_stream512 conv_dual conv_taps
  * conv_n192 conv_small conv_big conv_big_kmin stream_ntt lb_pair mosaic_map
  * block_fuse chain stem_pool ssh_fuse plate_s2d f32_split x6_small_k x6_small_tiles x6_stream
- * x6_small_k2 x6_bn256 x6_exact plate_stage jenc_gpu.
+ * x6_small_k2 x6_bn256 x6_exact x6_stream256 plate_stage jenc_gpu.
  * VD_ERR_ARG for unknown names. */
 int   vd_set_option(vd_ctx* ctx, const char* name, int value);
 void* vd_get_stream(vd_ctx* ctx);

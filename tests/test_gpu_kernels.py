@@ -196,7 +196,8 @@ CONV_CASES = [
 
 
 @pytest.mark.parametrize("prec", ["fp32", "fp32-big", "fp32-small", "fp32-exact", "fp32-x6", "fp32-x6-big",
-                                  "fp32-x6-small", "bf16", "fp16", "bf16-gemm64", "bf16-gemm128"])
+                                  "fp32-x6-small", "fp32-s128", "fp32-s256", "bf16", "fp16", "bf16-gemm64",
+                                  "bf16-gemm128"])
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv_matches_torch(gpu, face_ctx_factory, prec, case, options=None):
     """fp32: the default fp32 plan (conv_x6.hip, scaled fp16 pairs on the f16 matrix
@@ -208,6 +209,9 @@ def test_conv_matches_torch(gpu, face_ctx_factory, prec, case, options=None):
     (streaming 1x1 / streaming taps / phased / GEMM); bf16-gemm64 / -gemm128: the
     implicit GEMM with 64- and 128-row tiles forced through vd_set_option."""
     options = dict(options or {})
+    if prec in ("fp32-s128", "fp32-s256"):     # streaming 1x1 slices of 128 / 256 (default) channels, K 64 / 128
+        options.update(x6_stream256=0 if prec == "fp32-s128" else 2)
+        prec = "fp32"
     if prec.startswith("fp32-x6"):
         options.update(f32_split=1)
         prec = prec.replace("-x6", "")

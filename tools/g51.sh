@@ -1,0 +1,11 @@
+# 256-channel streaming slices (x6_stream256): conv parity, faces-only A/B
+set -u
+cd "${GRAFT_REPO_ROOT}"
+mkdir -p gpurun_out/g51
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_kernels.py -k "conv_matches_torch and fp32" -p no:cacheprovider > gpurun_out/g51/tests.log 2>&1; rc=$?
+tail -3 gpurun_out/g51/tests.log
+[ $rc -eq 0 ] || exit $rc
+for i in 1 2; do for v in 0 1 2; do
+timeout -k 10 200 python bench.py --compare "" --no-cpu-baseline --host-pipeline 0 --no-timing --steps 30 --plates 0 --option x6_stream256=$v > gpurun_out/g51/f$v.$i.json 2>gpurun_out/g51/err.txt || exit $?
+python -c "import json;d=json.load(open('gpurun_out/g51/f$v.$i.json'));print('faces s256=$v',d['value'],d['ms_per_step'])"
+done; done

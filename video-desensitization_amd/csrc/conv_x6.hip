@@ -910,6 +910,12 @@ static hipError_t launch_terms(const ConvArgs& a0, hipStream_t s) {
     ConvArgs a = a0;
     if (TERMS == 2) a.scale = a.scale_x;              // the fp16 pair's per-channel rescaled BN scale
     if (const int nch = stream_x6_nch(a, TERMS)) {
+        if constexpr (TERMS == 2) {   // 256-channel slices: each pixel read by half as many workgroups
+            if (a.tune && a.tune->x6_stream256 && a.cout % 256 == 0) {
+                if (a.cin_pad == 64) return stream_mode_x6<2, 16, TERMS>(a, s);
+                if (a.cin_pad == 128 && a.tune->x6_stream256 > 1) return stream_mode_x6<4, 16, TERMS>(a, s);   // 128 KB LDS
+            }
+        }
         if (a.cin_pad == 64) return nch == 128 ? stream_mode_x6<2, 8, TERMS>(a, s) : stream_mode_x6<2, 4, TERMS>(a, s);
         if (a.cin_pad == 128) return nch == 128 ? stream_mode_x6<4, 8, TERMS>(a, s) : stream_mode_x6<4, 4, TERMS>(a, s);
         if constexpr (TERMS == 2) return stream_mode_x6<8, 8, TERMS>(a, s);
