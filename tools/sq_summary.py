@@ -1,6 +1,6 @@
 """Per-kernel SQ counter summary of two rocprofv3 --pmc passes (tools/g54.sh):
 per kernel name, launches and the mean of each counter per launch, plus derived
-ratios (MFMA-busy and wait fractions of the wave / busy cycles).
+ratios (waits / active issue per wave cycle; VALU and LDS instructions per MFMA).
 
     python tools/sq_summary.py gpurun_out/g54/sq gpurun_out/g54/sq2 [out.txt]
 """
@@ -31,8 +31,9 @@ def main(a, b, out=None):
                 continue
             c = {name: v / max(len(n[k]), 1) for name, v in per[k].items()}
             extra = ""
-            if "SQ_BUSY_CYCLES" in c and c["SQ_BUSY_CYCLES"]:
-                extra = " mfma_busy/busy=%.3f" % (c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / c["SQ_BUSY_CYCLES"])
+            if "SQ_INSTS_MFMA" in c and c["SQ_INSTS_MFMA"]:
+                extra = " valu/mfma=%.2f lds/mfma=%.2f" % (c.get("SQ_INSTS_VALU", 0) / c["SQ_INSTS_MFMA"],
+                                                         c.get("SQ_INSTS_LDS", 0) / c["SQ_INSTS_MFMA"])
             if "SQ_WAVE_CYCLES" in c and c["SQ_WAVE_CYCLES"]:
                 extra += " wait_any/wave=%.3f active/wave=%.3f" % (c.get("SQ_WAIT_ANY", 0) / c["SQ_WAVE_CYCLES"],
                                                                    c.get("SQ_ACTIVE_INST_ANY", 0) / c["SQ_WAVE_CYCLES"])
