@@ -250,8 +250,11 @@ constexpr int XBUF3 = NDMA3 * 1024;
 constexpr int STB3 = NG3 * 16 * 256;       // 176 rows x 64 channels f32
 constexpr int VMCNT4 = 0x0F74;             // s_waitcnt vmcnt(4)
 
-__device__ __forceinline__ int st_off3(int row, int chunk) {   // chunk: 16 B = 4 channels, 0..15
-    return row * 256 + ((chunk ^ (row & 15)) << 4);
+// chunk: 16 B = 4 channels, 0..15. Key x ^ bit1(x) of x = row & 15: 16 consecutive
+// rows (stage A's 16 lanes) get 16 distinct keys, and rows r, r + 2 (stage B's two
+// pool pixels per 16 lanes) keys of opposite parity, so their even chunks don't collide
+__device__ __forceinline__ int st_off3(int row, int chunk) {
+    return row * 256 + ((chunk ^ (row & 15) ^ ((row >> 1) & 1)) << 4);
 }
 
 __device__ __forceinline__ f32x4_t mfma16(const u32x4& a, const u32x4& b, const f32x4_t& c) {
