@@ -56,6 +56,11 @@ def parse():
                     help="extra precisions measured on the same frames at N=1 (',' separated; '' = none)")
     ap.add_argument("--plates", type=int, default=1, help="1: run YOLOv8n beside RetinaFace (BASELINE config 3)")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    ap.add_argument("--backend", default=os.environ.get("VD_DIST_BACKEND", "nccl"), choices=["nccl", "gloo"],
+                    help="torch.distributed backend for N>1 (nccl = RCCL over xGMI; gloo for tests)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="every rank on cuda:0 (rehearsing the multi-rank path on a one-GPU box)")
+    ap.add_argument("--records-out", default="", help="rank 0 saves the gathered box records of the last step (.npy)")
     ap.add_argument("--frames", type=int, default=0, help="strong scaling: total frames per step (default 64*8)")
     ap.add_argument("--option", action="append", default=[], help="name=value kernel-selection switch (vd_set_option)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
@@ -188,8 +193,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.same_device:
+        local = 0
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group("gloo")
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
 
@@ -211,6 +221,7 @@ def main():
     out = torch.empty_like(frames)
     stream = torch.cuda.current_stream(dev)
     rec_cap = 64                      # box record: frame, count, 64 x (box, score, anchor)
+    gathered = {}
 
     def run(mode, timed_steps, sync=True):
         for _ in range(timed_steps):
@@ -218,7 +229,7 @@ def main():
             for s, n in batches:
                 fr, o = (frames, out) if n == B else (frames[:n], out[:n])
                 mode.process(fr, o)
-                if world > 1:
+                if world > 1 or a.records_out:
                     recs.append(pack_records(mode.faces.count[:n], mode.faces.xyxy[:n], rec_cap,
                                              mode.faces.score[:n], mode.faces.label[:n],
                                              torch.arange(f0 + s, f0 + s + n, dtype=torch.int32, device=dev)))
@@ -228,7 +239,11 @@ def main():
                     pad = torch.zeros((per_rank - rec.shape[0], rec.shape[1]), dtype=torch.int32, device=dev)
                     pad[:, 0] = -1
                     rec = torch.cat([rec, pad])
-                all_gather_records(rec)
+                got = all_gather_records(rec)
+                if mode.precision == a.precision:
+                    gathered["rec"] = got
+            elif recs and mode.precision == a.precision:
+                gathered["rec"] = torch.cat(recs)
 
     def timed(mode):
         torch.cuda.synchronize(dev)
@@ -460,6 +475,8 @@ def main():
         parity["definition"] = ("fraction of bench frames whose complete keep lists (anchor indices in NMS "
                                 "order) / keep lists and int boxes are identical")
         res["parity"] = parity
+    if rank == 0 and a.records_out and "rec" in gathered:
+        np.save(a.records_out, gathered["rec"].cpu().numpy())
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

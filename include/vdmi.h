@@ -170,7 +170,9 @@ int vd_jpeg_info(const uint8_t* data, size_t size, int* h, int* w, int* comps);
  * downsampling, ISLOW FDCT and quantisation in a HIP kernel; Huffman coding and 0xFF
  * stuffing in HIP kernels (option jenc_gpu=0: on host threads, same bytes); frames
  * up to 2,000,000 scan blocks (8K). Frame i goes to out + i * cap, its length to sizes[i]; VD_ERR_CAPACITY
- * if a frame needs more than cap bytes. Returns when every frame is written. */
+ * if a frame needs more than cap bytes -- with the device coder sizes[i] then holds an
+ * upper bound of frame i's length (re-size and call again), with host threads 0.
+ * Returns when every frame is written. */
 int vd_jpeg_encode(vd_ctx* ctx, const uint8_t* frames, int n, int h, int w, size_t pitch, int where,
                    int quality, int subsampling, uint8_t* out, size_t cap, size_t* sizes);
 /* The complete keep lists of the last vd_detect / vd_detect_plates / vd_process

@@ -15,6 +15,12 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libvdmi.so on cuda:0)")
     config.addinivalue_line("markers", "slow: long-running CPU test")
+    config.addinivalue_line("markers", "parity: oracle box-parity test (ordered first in the session)")
+
+
+def pytest_collection_modifyitems(session, config, items):
+    """Oracle parity tests run first, so a later -x stop cannot hide them."""
+    items.sort(key=lambda it: 0 if it.get_closest_marker("parity") else 1)
 
 
 def _have_gpu():

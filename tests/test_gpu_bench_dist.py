@@ -1,0 +1,48 @@
+"""bench.py's multi-rank branch (BASELINE config 4) exercised before the
+driver's 8-GPU scaling run: two ranks launched by torch.distributed.run on the one
+GPU of the test box (--same-device, gloo for the record all-gather), strong scaling
+over one list of frames. The all-gathered per-frame box records must equal a
+single-rank run over the same list (fp32: per-frame results do not depend on the
+batch a frame lands in)."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+COMMON = ["--scaling", "strong", "--frames", "6", "--batch", "6", "--steps", "1", "--warmup", "0", "--no-timing",
+          "--compare", "", "--host-pipeline", "0", "--no-cpu-baseline"]
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(cmd, out):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run(cmd + ["--records-out", out], cwd=ROOT, env=env, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    return r.stdout
+
+
+def test_bench_two_ranks_strong_equals_single_rank(gpu, tmp_path):
+    from vdmi.dist import unpack_records
+    one = str(tmp_path / "one.npy")
+    two = str(tmp_path / "two.npy")
+    _run([sys.executable, "bench.py"] + COMMON, one)
+    out = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
+                "--backend", "gloo", "--same-device"] + COMMON, two)
+    assert '"n_gpus": 2' in out
+    r1, r2 = unpack_records(np.load(one)), unpack_records(np.load(two))
+    assert list(r1) == list(range(6)) and list(r2) == list(range(6))
+    assert sum(v[3] for v in r1.values()) > 0
+    assert r2 == r1

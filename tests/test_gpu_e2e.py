@@ -1,11 +1,9 @@
 """End-to-end parity: letterbox -> RetinaFace forward -> decode/NMS -> correction ->
 int() -> mosaic, GPU (C-ABI) vs the CPU oracle on identical synthetic frames.
 
-* fp32 mode (each plan: fp16 pairs, bf16 triples, exact-f32 MFMA): heads within 1e-4 of the torch-CPU oracle
-  (relative to each tensor's max |value|); kept anchor indices identical except
-  for candidates whose decision is within 1e-4 of a threshold (score vs 0.5,
-  IoU vs 0.4), which the test excludes and counts; mosaic pixels bit-exact given
-  the boxes.
+* fp32 mode: heads and every frame's boxes against the oracle at every config size
+  live in tests/test_gpu_parity_fp32.py (run first); here: mosaic pixels bit-exact
+  given the boxes, the drop-in surface, and fused-vs-unfused A/B checks.
 * bf16 mode: heads within 2e-2 (R50) / 4.5e-2 (MobileNet) relative, ~1.5x the observed
   error; >= 90 % of oracle boxes matched by a
   GPU box at IoU >= 0.9 (bf16 rounding moves near-threshold decisions, so box
@@ -55,21 +53,6 @@ def _rel(a, b):
 # <= 0.0116 loc/conf, MobileNet-0.25 <= 0.0273; fp16 R50 <= 0.0018, MobileNet <= 0.0042)
 BF16_TOL = {"default": 2e-2, "mnet": 4.5e-2}
 FP16_TOL = {"default": 3e-3, "mnet": 6.5e-3}
-
-
-# fp32 plans: 1 = 3-term bf16 split (6 products), 2 = scaled fp16 pairs (3 products), 0 = exact-f32 MFMA
-SPLITS = [1, 2, 0]
-
-
-@pytest.mark.parametrize("split", SPLITS)
-@pytest.mark.parametrize("h,w,wkind", [(1080, 1920, "default"), (720, 1280, "default"), (1080, 1920, "mnet"),
-                                        (720, 1280, "mnet")])
-def test_heads_fp32_match_oracle(gpu, face_ctx_factory, h, w, wkind, split):
-    ctx = face_ctx_factory("fp32", 8, wkind, options=(("f32_split", split),))
-    fr = _frames(2, h, w)
-    loc, conf, ldm = ctx.forward_heads(fr)
-    eloc, econf, eldm = _oracle_heads(fr, wkind)
-    assert _rel(loc, eloc) < 1e-4 and _rel(conf, econf) < 1e-4 and _rel(ldm, eldm) < 1e-4
 
 
 @pytest.mark.parametrize("wkind", ["default", "mnet"])
@@ -177,46 +160,6 @@ def test_heads_bf16_fused_stem_pool_matches_unfused(gpu):
             ctx.close()
     for a, b in zip(out["1"], out["0"]):
         np.testing.assert_array_equal(a, b)
-
-
-def _near_decision(conf_b, boxes_norm, thr=0.5, iou=0.4, eps=1e-4):
-    """Anchors whose score is within eps of thr, or whose IoU with another candidate
-    is within eps of the NMS threshold: decisions there are ulp-sensitive."""
-    score = obbox.softmax2(conf_b)[:, 1]
-    near = np.abs(score - thr) < eps
-    cand = np.nonzero(score >= thr)[0]
-    b = boxes_norm[cand]
-    if len(cand) > 1:
-        x1 = np.maximum(b[:, None, 0], b[None, :, 0]); y1 = np.maximum(b[:, None, 1], b[None, :, 1])
-        x2 = np.minimum(b[:, None, 2], b[None, :, 2]); y2 = np.minimum(b[:, None, 3], b[None, :, 3])
-        inter = np.clip(x2 - x1, 0, None) * np.clip(y2 - y1, 0, None)
-        ar = (b[:, 2] - b[:, 0]) * (b[:, 3] - b[:, 1])
-        iou_m = inter / (ar[:, None] + ar[None, :] - inter + 1e-30)
-        np.fill_diagonal(iou_m, 0)
-        near[cand[(np.abs(iou_m - iou) < eps).any(1)]] = True
-    return near
-
-
-@pytest.mark.parametrize("split", SPLITS)
-@pytest.mark.parametrize("wkind", ["default", "mnet"])
-def test_detect_fp32_matches_oracle(gpu, face_ctx_factory, wkind, split):
-    ctx = face_ctx_factory("fp32", 8, wkind, options=(("f32_split", split),))
-    fr = _frames(3, 1080, 1920, seed=2)
-    got = ctx.detect(fr)
-    eloc, econf, _ = _oracle_heads(fr, wkind)
-    pri = oanchors.get_anchors((640, 640))
-    exact = 0
-    for b in range(3):
-        idx, boxes, _ = obbox.postprocess_frame(eloc[b], econf[b], pri, 0.5, 0.4)
-        xi, xf, sc, lab = got.frame(b)
-        near = _near_decision(econf[b], obbox.decode(eloc[b], pri))
-        if near[idx].any() or near[lab].any():
-            continue                      # ulp-sensitive frame: excluded (counted below)
-        exact += 1
-        np.testing.assert_array_equal(lab, idx)
-        fb = obbox.correct_and_scale(boxes, 1080, 1920)
-        np.testing.assert_allclose(xf, fb, rtol=0, atol=0.05)     # pixels; forward differs in ulps
-    assert exact >= 2, "too many near-threshold frames to judge parity"
 
 
 def test_process_mosaic_exact_given_boxes(gpu, face_ctx_factory):

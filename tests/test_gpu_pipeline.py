@@ -151,3 +151,60 @@ def test_batch_process_images_gpu_jpeg_codec(gpu, tmp_path):
         Image.fromarray(exp).save(b, "JPEG", quality=95, subsampling=2)
         assert (out_dir / f"processed_{name}").read_bytes() == b.getvalue(), name
     assert nf == total and total > 0
+
+
+def test_batch_process_images_two_frame_sizes(gpu, tmp_path):
+    """Frames of two sizes in one folder: the fused path opens one FramePipeline per
+    size on ONE shared context, each submission re-binds the context to its own
+    compute stream (the one that waited on that slot's upload). Every saved frame
+    equals the oracle mosaic of the drop-in detector's boxes (none is left
+    unmosaicked by a stream race)."""
+    import vdmi
+    from vdmi import synth, weights
+    from vdmi.pipeline import batch_process_images
+    frames = {}
+    for i in range(8):
+        h, w = (720, 1280) if i % 2 else (1080, 1920)
+        frames[f"m{i:02d}.png"] = np.repeat(np.repeat(synth.frame(h // 2, w // 2, i, seed=12), 2, 0), 2, 1)
+    for name in frames:
+        (tmp_path / name).write_bytes(b"")
+    saved = {}
+    face = vdmi.Retinaface(input_shape=[640, 640, 3], nms_iou=0.4, max_batch=4,
+                           weights=weights.retinaface_state_dict(0))
+    plate = vdmi.YOLO(weights="random", max_batch=4)
+    n, nf, _ = batch_process_images(str(tmp_path), str(tmp_path / "out"), face, plate, batch_size=4,
+                                    loader=lambda p: frames[os.path.basename(p)],
+                                    saver=lambda img, p: saved.__setitem__(os.path.basename(p), img))
+    assert n == 8 and len(saved) == 8
+    total = 0
+    for name, img in frames.items():
+        boxes = face.detect_images([img])[0][1]
+        total += len(boxes)
+        exp = omosaic.mosaic_frame(img, [tuple(int(v) for v in b) for b in boxes], 8)
+        np.testing.assert_array_equal(saved[f"processed_{name}"], exp, err_msg=name)
+    assert nf == total and total > 0
+
+
+def test_batch_process_images_load_failure_aborts(gpu, tmp_path):
+    """combine_detect.py:209-211: the loader runs outside the inference try, so an
+    unreadable frame aborts the call; the batches submitted before it are still
+    finished and saved."""
+    import vdmi
+    from vdmi import synth, weights
+    from vdmi.pipeline import batch_process_images
+    for i in range(6):
+        (tmp_path / f"x{i}.png").write_bytes(b"")
+    saved = {}
+
+    def loader(p):
+        if os.path.basename(p) == "x5.png":
+            raise ValueError(f"cannot read image: {p}")
+        return synth.frame(360, 640, 1, seed=2)
+
+    face = vdmi.Retinaface(input_shape=[640, 640, 3], max_batch=1, weights=weights.retinaface_state_dict(0))
+    plate = vdmi.YOLO(weights="random", max_batch=1)
+    with pytest.raises(ValueError, match="cannot read"):
+        batch_process_images(str(tmp_path), str(tmp_path / "o"), face, plate, batch_size=1, loader=loader,
+                             saver=lambda img, p: saved.__setitem__(os.path.basename(p), img))
+    listed = [f for f in os.listdir(tmp_path) if f.endswith(".png")]
+    assert len(saved) == listed.index("x5.png")      # every batch listed before the bad frame

@@ -92,3 +92,79 @@ def test_library_entropy_decode_matches_oracle(case):
     j = ojpeg.parse(d)
     exp = np.concatenate([c.reshape(-1, 64) for c in ojpeg.coefficients(j)])
     np.testing.assert_array_equal(_lib_coefficients(d).astype(np.int64), exp)
+
+
+# --------------------------------------------------------------- malformed input
+def _segments(d):
+    """[(marker, offset of the FF byte, segment length)] up to SOS."""
+    out, o = [], 2
+    while o + 4 <= len(d):
+        m, ln = d[o + 1], (d[o + 2] << 8) | d[o + 3]
+        out.append((m, o, ln))
+        if m == 0xDA:
+            break
+        o += 2 + ln
+    return out
+
+
+def _seg(d, marker):
+    return next((o, ln) for m, o, ln in _segments(d) if m == marker)
+
+
+def _oversubscribed_dht(d):
+    """Move three codes of some length to length 1: 3 one-bit codes cannot exist."""
+    b = bytearray(d)
+    o, _ = _seg(d, 0xC4)
+    counts = o + 5                       # FF C4 Lh Ll Tc/Th counts[16]
+    src = next(l for l in range(1, 16) if b[counts + l] >= 3)
+    b[counts + src] -= 3
+    b[counts] += 3
+    return bytes(b)
+
+
+def _truncated_sos(d):
+    b = bytearray(d)
+    o, _ = _seg(d, 0xDA)
+    b[o + 2], b[o + 3] = 0, 3            # Ls = 3: room for Ns only
+    return bytes(b)
+
+
+def _duplicate_component(d):
+    b = bytearray(d)
+    o, _ = _seg(d, 0xC0)
+    b[o + 10 + 3] = b[o + 10]            # component 2 id = component 1 id
+    return bytes(b)
+
+
+def _second_sof(d):
+    o, ln = _seg(d, 0xC0)
+    sof = d[o:o + 2 + ln]
+    s, _ = _seg(d, 0xDA)
+    return d[:s] + sof + d[s:]
+
+
+@pytest.mark.parametrize("mutate,msg", [(_oversubscribed_dht, "Huffman"), (_truncated_sos, "SOS"),
+                                        (_duplicate_component, "duplicate"), (_second_sof, "more than one")])
+def test_library_rejects_malformed_jpeg(mutate, msg):
+    """The host parser (jpeg_host.cpp) refuses headers that would otherwise index
+    past its tables: an over-subscribed DHT (fills past the 2048-entry lookahead),
+    a short SOS, duplicate component ids (unassigned table indices), two SOFs."""
+    import vdmi
+    d = mutate(make_jpeg(48, 64, 95, 2))
+    with pytest.raises(vdmi.VdError, match=msg):
+        vdmi.jpeg_info(d)
+    with pytest.raises(vdmi.VdError):
+        _lib_coefficients(d)
+
+
+def test_library_rejects_truncated_scan_without_crash():
+    """Entropy data cut short: the bit reader feeds zeros past the end (as libjpeg
+    does) -- the call returns (an error or zero-padded coefficients), never reads past."""
+    import vdmi
+    d = make_jpeg(64, 96, 95, 2)
+    o, ln = _seg(d, 0xDA)
+    cut = d[:o + 2 + ln + 40]
+    try:
+        _lib_coefficients(cut)
+    except vdmi.VdError:
+        pass

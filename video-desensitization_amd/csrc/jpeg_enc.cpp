@@ -368,6 +368,7 @@ extern "C" int vd_jpeg_encode(vd_ctx* hctx, const uint8_t* frames, int n, int h,
         VD_CHECK_HIP(hipMemcpyAsync(htot, ha.total, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream));
         VD_CHECK_HIP(hipStreamSynchronize(ctx->stream));
         unsigned maxbits = 0;
+        std::vector<unsigned> htot_bits(htot, htot + n);
         for (int i = 0; i < n; ++i) maxbits = std::max(maxbits, htot[i]);
         ha.nchunk = (int)std::max<long>(1, ((long)maxbits / 8 + 1 + 4095) / 4096);
         if (ha.nchunk > nchunk_max) return vd_set_error(VD_ERR_HIP, "jpeg huffman: bit count past the buffer");
@@ -381,8 +382,14 @@ extern "C" int vd_jpeg_encode(vd_ctx* hctx, const uint8_t* frames, int n, int h,
         VD_CHECK_HIP(hipMemcpyAsync(hsz, ha.segsize, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream));
         VD_CHECK_HIP(hipMemcpyAsync(hbase, ha.segbase, (size_t)(n + 1) * 8, hipMemcpyDeviceToHost, ctx->stream));
         VD_CHECK_HIP(hipStreamSynchronize(ctx->stream));
-        for (int i = 0; i < n; ++i)
-            if (hsz[i] == 0xFFFFFFFFu) return vd_set_error(VD_ERR_CAPACITY, "jpeg frame %d does not fit %zu bytes", i, cap);
+        bool fits = true;
+        for (int i = 0; i < n; ++i) fits = fits && hsz[i] != 0xFFFFFFFFu;
+        if (!fits) {
+            // sizes[] <- an upper bound of each frame's file (every coded byte stuffed):
+            // the caller re-sizes its slots from it instead of guessing
+            for (int i = 0; i < n; ++i) sizes[i] = hl + 2 + 2 * ((size_t)htot_bits[i] / 8 + 1) + 16;
+            return vd_set_error(VD_ERR_CAPACITY, "jpeg frames do not fit %zu bytes (sizes[] holds the bound)", cap);
+        }
         const size_t packed = (size_t)hbase[n];
         if ((rc = ctx->ensure_pinned(&ctx->jseg_host, &ctx->jseg_host_bytes, packed + 64))) return rc;
         VD_CHECK_HIP(hipMemcpyAsync(ctx->jseg_host, ha.seg, packed, hipMemcpyDeviceToHost, ctx->stream));

@@ -50,7 +50,7 @@ struct Huff {
     bool present = false;
 };
 
-struct Comp { int id, hs, vs, tq, td, ta, bw, bh; };
+struct Comp { int id = -1, hs = 0, vs = 0, tq = 0, td = 0, ta = 0, bw = 0, bh = 0; bool scanned = false; };
 
 struct Info {
     int h = 0, w = 0, nc = 0, hmax = 1, vmax = 1, mcux = 0, mcuy = 0, restart = 0;
@@ -71,6 +71,9 @@ int build_huff(Huff& hf, const uint8_t* counts, const uint8_t* syms, int nsym) {
     for (int l = 1; l <= 16; ++l) {
         hf.valoff[l] = k - code;
         for (int i = 0; i < counts[l - 1]; ++i, ++k, ++code) {
+            // an over-subscribed table would index past the lookahead arrays below:
+            // reject it before any fill (code must fit in l bits)
+            if (code >= (1 << l)) return -1;
             if (l <= kLook) {   // fill every kLook-bit prefix extension
                 const int base = code << (kLook - l);
                 const int rs = syms[k], r = rs >> 4, sz = rs & 15;
@@ -91,7 +94,6 @@ int build_huff(Huff& hf, const uint8_t* counts, const uint8_t* syms, int nsym) {
             }
         }
         hf.maxcode[l] = counts[l - 1] ? code - 1 : -1;
-        if (code > (1 << l)) return -1;   // over-subscribed table
         code <<= 1;
     }
     hf.maxcode[17] = 0x7fffffff;
@@ -142,6 +144,7 @@ int parse(const uint8_t* d, size_t n, Info& j) {
                 p += 17 + ns;
             }
         } else if (m == 0xC0 || m == 0xC1) {               // SOF0 / SOF1
+            if (sof) return vd_set_error(VD_ERR_ARG, "jpeg: more than one frame header");
             if (sl < 6 || s[0] != 8) return vd_set_error(VD_ERR_ARG, "jpeg: only 8-bit samples are supported");
             j.h = u16be(s + 1);
             j.w = u16be(s + 3);
@@ -156,6 +159,8 @@ int parse(const uint8_t* d, size_t n, Info& j) {
                 c.tq = s[8 + 3 * i] & 3;
                 if (c.hs < 1 || c.hs > 2 || c.vs < 1 || c.vs > 2)
                     return vd_set_error(VD_ERR_ARG, "jpeg: sampling %dx%d not supported", c.hs, c.vs);
+                for (int k = 0; k < i; ++k)
+                    if (j.c[k].id == c.id) return vd_set_error(VD_ERR_ARG, "jpeg: duplicate component id %d", c.id);
             }
             sof = true;
         } else if ((m >= 0xC2 && m <= 0xCF) && m != 0xC4 && m != 0xC8 && m != 0xCC) {
@@ -165,13 +170,18 @@ int parse(const uint8_t* d, size_t n, Info& j) {
             j.restart = u16be(s);
         } else if (m == 0xDA) {                            // SOS
             if (!sof) return vd_set_error(VD_ERR_ARG, "jpeg: SOS before SOF");
+            if (j.scan) return vd_set_error(VD_ERR_ARG, "jpeg: more than one scan (not baseline)");
+            if (sl < 1) return vd_set_error(VD_ERR_ARG, "jpeg: bad SOS");
             const int ns = s[0];
             if (ns != j.nc) return vd_set_error(VD_ERR_ARG, "jpeg: non-interleaved scans not supported");
+            if (sl < 1 + 2 * ns + 3) return vd_set_error(VD_ERR_ARG, "jpeg: truncated SOS");
             for (int i = 0; i < ns; ++i) {
                 const int id = s[1 + 2 * i];
                 int ci = -1;
                 for (int k = 0; k < j.nc; ++k) if (j.c[k].id == id) ci = k;
                 if (ci < 0) return vd_set_error(VD_ERR_ARG, "jpeg: scan names an unknown component");
+                if (j.c[ci].scanned) return vd_set_error(VD_ERR_ARG, "jpeg: scan names component %d twice", id);
+                j.c[ci].scanned = true;
                 j.c[ci].td = s[2 + 2 * i] >> 4;
                 j.c[ci].ta = s[2 + 2 * i] & 15;
                 if (j.c[ci].td > 3 || j.c[ci].ta > 3) return vd_set_error(VD_ERR_ARG, "jpeg: bad table index");
@@ -199,6 +209,7 @@ int parse(const uint8_t* d, size_t n, Info& j) {
         Comp& c = j.c[i];
         c.bw = j.mcux * c.hs;
         c.bh = j.mcuy * c.vs;
+        if (!c.scanned) return vd_set_error(VD_ERR_ARG, "jpeg: component %d is not in the scan", i);
         if (!j.qpresent[c.tq] || !j.dc[c.td].present || !j.ac[c.ta].present)
             return vd_set_error(VD_ERR_ARG, "jpeg: component %d references a missing table", i);
     }

@@ -261,9 +261,12 @@ class Context:
         the reference's frame write, combine_detect.py:174-180)."""
         p, n, h, w, pitch, where, keep = _frames_arg(frames)
         sizes = (ctypes.c_size_t * n)()
-        # typical frames need < 3 B/pixel; the retry bound covers any baseline block
-        # (63 AC codes of 26 bits + DC, every byte stuffed) at 1.5-3 samples/pixel
-        for cap in (h * w * 3 + 65536, h * w * 20 + 65536):
+        # typical frames need < 3 B/pixel; on VD_ERR_CAPACITY the device coder reports
+        # each frame's bound in sizes[] (the host coder 0: then the bound of any
+        # baseline block, 63 AC codes of 26 bits + DC, every byte stuffed)
+        caps = [h * w * 3 + 65536]
+        while len(caps) < 3:
+            cap = caps[-1]
             # one staging buffer per context, reused (fresh pages would fault in on every call)
             out = getattr(self, "_jenc_buf", None)
             if out is None or out.size < n * cap:
@@ -272,6 +275,8 @@ class Context:
                                           ptr(out), cap, sizes)
             if rc != _lib.VD_ERR_CAPACITY:
                 break
+            need = max(sizes[i] for i in range(n))
+            caps.append(need + 64 if need > cap else h * w * 20 + 65536)
         check(rc)
         del keep
         return [out[i * cap:i * cap + sizes[i]].tobytes() for i in range(n)]

@@ -77,6 +77,9 @@ def all_gather_records(rec, group=None):
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
+    if rec.device.type == "cuda" and dist.get_backend(group) == "gloo":
+        # gloo (CPU tests, bench --backend gloo): gather through host memory
+        return all_gather_records(rec.cpu(), group).to(rec.device)
     out = torch.empty((world * rec.shape[0], rec.shape[1]), dtype=rec.dtype, device=rec.device)
     if rec.device.type == "cuda":
         dist.all_gather_into_tensor(out, rec.contiguous(), group=group)

@@ -16,10 +16,12 @@ Differences, all deliberate:
   ``weights="random"`` (tests, benchmarks).
 * The returned image is the caller's array itself, not a copy (face.py:129 copies;
   the driver never reads it, combine_detect.py:237).
-* Extra keywords: ``precision`` ("fp32" default = the reference's arithmetic,
-  exact-f32 MFMA; "bf16" / "fp16" trade box parity for 4-6x throughput, see
+* Extra keywords: ``precision`` ("fp32" default: f32 activations and weights, each
+  conv on scaled fp16 pairs -- three f16 MFMA products, f32 accumulation, heads
+  within 6e-6 of the torch-CPU fp32 forward; option ``f32_split=0`` runs exact-f32
+  MFMA instead; "bf16" / "fp16" trade box parity for 2-3x throughput, see
   INTEGRATION.md), ``max_batch``, ``device_index``, ``seed``, ``weights``
-  (a state_dict, or "random").
+  (a state_dict, or "random"), ``options`` (kernel-selection switches).
 """
 import os
 

@@ -7,7 +7,9 @@ plates, take face boxes from ``face_results[j][1]`` and plate boxes from
 -- Results objects yield [], so plate boxes are discarded exactly as in the
 reference unless ``mosaic_plates=True``), int() them (:243-244), mosaic every box
 in order (:246-249), save, count, and drop a batch whose inference raises
-(:226-228).
+(:226-228). A frame that fails to load aborts the call, as in the reference (its
+loader runs outside the try, :209-211), after the batches already submitted have
+been finished and saved.
 
 When both detectors are the vdmi drop-ins, the batch body is ONE ``vd_process``
 on one context (letterbox, both forwards, NMS, mosaic of every kept box) driven
@@ -151,6 +153,9 @@ class FramePipeline:
             self.s_comp.wait_event(self.ev_down[k])
         faces = self.d_faces[k]
         plates = self.d_plates[k] if self.plates else None
+        # several pipelines (one per frame size) may share the context: the compute
+        # stream that waited on this slot's upload is the one the library must run on
+        self.ctx.set_stream(self.s_comp.cuda_stream)
         self.ctx.process(self.d_in[k, :n], self.d_out[k, :n], faces=faces, plates=plates, flags=self.flags)
         self.ev_comp[k].record(self.s_comp)
         with torch.cuda.stream(self.s_down):
@@ -235,6 +240,8 @@ def batch_process_images(input_dir, output_dir, face_detector, plate_detector, b
     PCIe; the bytes written equal libjpeg-turbo's encode of the processed frames."""
     logger = logging.getLogger("VideoProcessor.batch_process_images")
     custom_io = loader is not None or saver is not None
+    if gpu_codec is True and custom_io:
+        raise ValueError("gpu_codec=True reads and writes JPEG bytes itself: it cannot use a custom loader/saver")
     loader = loader or load_image_rgb
     saver = saver or save_output_image
     image_paths = [os.path.join(input_dir, f) for f in os.listdir(input_dir) if f.lower().endswith(IMAGE_EXT)]
@@ -272,7 +279,8 @@ def _fused_batches(batches, output_dir, face_detector, plate_detector, batch_siz
     """The vdmi path, streaming: decode batch b+1 (threads) while batch b is on the
     GPU (FramePipeline: one vd_process per batch), collect batch b-1 and hand its
     frames to the encoder threads. Frames of another size get their own pipeline;
-    a batch whose load or inference fails is dropped (combine_detect.py:226-228)."""
+    a batch whose inference fails is dropped (combine_detect.py:226-228), a load
+    failure aborts the call (:209-211)."""
     totals = [0, 0, 0]
     save_futs = []
     ctx = fused_context(face_detector, plate_detector, batch_size)
@@ -296,37 +304,42 @@ def _fused_batches(batches, output_dir, face_detector, plate_detector, batch_siz
 
     pending = None
     fut = io.submit(load, batches[0]) if batches else None
-    for bi, files in enumerate(batches):
-        try:
-            imgs = fut.result()
-        except Exception as e:
-            logger.error(f"loading failed: {e}")
-            imgs = None
-        fut = io.submit(load, batches[bi + 1]) if bi + 1 < len(batches) else None
-        if imgs is None:
-            continue
-        groups = {}
-        for f, im in zip(files, imgs):
-            groups.setdefault(im.shape, []).append((f, im))
-        for shape, items in groups.items():
-            if shape not in pipes:
-                pipes[shape] = FramePipeline(ctx, shape[0], shape[1], max_batch=batch_size, plates=True,
-                                             mosaic_plates=mosaic_plates)
-            try:
-                cur = (pipes[shape], pipes[shape].submit(np.stack([im for _, im in items])),
-                       [f for f, _ in items])
-            except Exception as e:       # combine_detect.py:226-228: the batch is dropped
-                logger.error(f"parallel inference failed: {e}")
-                cur = None
-            if pending is not None:
-                finish(pending)
-            pending = cur
-    if pending is not None:
-        finish(pending)
-    for pipe in pipes.values():
-        pipe.close()
-    _save_all(save_futs, logger)
+    try:
+        for bi, files in enumerate(batches):
+            imgs = fut.result()          # a load failure propagates (combine_detect.py:209-211)
+            fut = io.submit(load, batches[bi + 1]) if bi + 1 < len(batches) else None
+            pending = _submit_groups(files, imgs, pipes, ctx, batch_size, mosaic_plates, pending, finish, logger)
+    finally:
+        if fut is not None:
+            fut.cancel()
+        if pending is not None:
+            finish(pending)
+        for pipe in pipes.values():
+            pipe.close()
+        _save_all(save_futs, logger)
     return tuple(totals)
+
+
+def _submit_groups(files, imgs, pipes, ctx, batch_size, mosaic_plates, pending, finish, logger):
+    """Submit one loaded batch (one pipeline per frame size), finishing the previous
+    submission behind it; returns the new pending submission."""
+    groups = {}
+    for f, im in zip(files, imgs):
+        groups.setdefault(im.shape, []).append((f, im))
+    for shape, items in groups.items():
+        if shape not in pipes:
+            pipes[shape] = FramePipeline(ctx, shape[0], shape[1], max_batch=batch_size, plates=True,
+                                         mosaic_plates=mosaic_plates)
+        try:
+            cur = (pipes[shape], pipes[shape].submit(np.stack([im for _, im in items])),
+                   [f for f, _ in items])
+        except Exception as e:       # combine_detect.py:226-228: the batch is dropped
+            logger.error(f"parallel inference failed: {e}")
+            cur = None
+        if pending is not None:
+            finish(pending)
+        pending = cur
+    return pending
 
 
 def _read_bytes(path):
@@ -387,14 +400,8 @@ def _gpu_codec_batches(batches, output_dir, face_detector, plate_detector, batch
     try:
         fut = ahead.submit(load, batches[0]) if batches else None
         for bi in range(len(batches)):
-            try:
-                decoded = fut.result()
-            except Exception as e:
-                logger.error(f"loading failed: {e}")
-                decoded = None
+            decoded = fut.result()       # a load failure propagates (combine_detect.py:209-211)
             fut = ahead.submit(load, batches[bi + 1]) if bi + 1 < len(batches) else None
-            if decoded is None:
-                continue
             for items, d_in in decoded:
                 try:
                     out, fc, pc = ctx.process(d_in, faces=faces, plates=plates, flags=flags)
@@ -413,7 +420,7 @@ def _gpu_codec_batches(batches, output_dir, face_detector, plate_detector, batch
     finally:
         ahead.shutdown()
         dctx.close()
-    _save_all(save_futs, logger)
+        _save_all(save_futs, logger)
     return tuple(totals)
 
 
@@ -424,11 +431,7 @@ def _threaded_batches(batches, output_dir, face_detector, plate_detector, loader
     total = faces = plates = 0
     save_futs = []
     for files in batches:
-        try:
-            batch_images = list(io.map(loader, files))
-        except Exception as e:
-            logger.error(f"loading failed: {e}")
-            continue
+        batch_images = list(io.map(loader, files))      # raises, as combine_detect.py:209-211
         with ThreadPoolExecutor(max_workers=2) as infer:   # face || plate, as the reference does
             ff = infer.submit(face_detector.detect_images, batch_images.copy())
             fp = infer.submit(plate_detector, batch_images.copy(), verbose=False, conf=0.5)
