@@ -51,6 +51,10 @@ def parse():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--frames-src", default="noise", choices=["noise", "up2"],
+                    help="noise: counter-hash frames at full size; up2: hash frames at half size, 2x nearest "
+                         "upsampled (the ratio-2 / ratio-6 letterboxes of 720p / 4K then see structure and the "
+                         "seeded weights detect faces; raw noise at those ratios averages out to none)")
     ap.add_argument("--precision", default="fp32", choices=["bf16", "fp16", "fp32", "fp32_x6", "fp32_exact"])
     ap.add_argument("--compare", default="fp32_x6,fp32_exact,bf16,fp16",
                     help="extra precisions measured on the same frames at N=1 (',' separated; '' = none)")
@@ -84,17 +88,23 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
-def cpu_baseline(frames, sd, seconds):
-    """The CPU oracle (torch-CPU fp32 convs + numpy decode/NMS/mosaic) on a bounded
-    sample of the same synthetic frames, on this host's cores. Returns the timing
-    record and the oracle's per-frame (keep list, int boxes) for the parity block."""
+def cpu_baseline(frames, sd, seconds, plates=True):
+    """The CPU oracle on a bounded sample of the same synthetic frames, on this host's
+    cores, doing what the headline step does per frame: torch-CPU fp32 RetinaFace +
+    numpy decode/NMS/correction, the YOLOv8n plate forward + NMS beside it (when the
+    headline runs plates; the reference discards plate boxes, combine_detect.py:239),
+    and the sequential mosaic. Returns the timing record and the oracle's per-frame
+    (keep list, int boxes) for the parity block."""
     import torch
     from oracle import anchors, bbox, letterbox, mosaic
     from oracle.retinaface import build_oracle_model
+    from oracle.yolov8 import build_oracle_yolo, postprocess as yolo_post, raw_heads
+    from vdmi import weights
     # the GPU box shares its host: use the per-GPU CPU share (OMP_NUM_THREADS, 16 there)
     cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
     torch.set_num_threads(cores)
     m = build_oracle_model(sd)
+    ym = build_oracle_yolo(weights.yolov8n_state_dict(0)) if plates else None
     pri = anchors.get_anchors((640, 640))
     done = 0
     ref = []
@@ -106,6 +116,11 @@ def cpu_baseline(frames, sd, seconds):
             loc, cls, _ = m.forward_raw(torch.from_numpy(x))
         idx, boxes, _ = bbox.postprocess_frame(loc[0].numpy(), cls[0].numpy(), pri, 0.5, 0.4)
         ib = bbox.truncate_boxes(bbox.correct_and_scale(boxes, img.shape[0], img.shape[1]))
+        if ym is not None:       # plate forward + NMS (boxes discarded like the reference)
+            yx = letterbox.yolo_preprocess([img])
+            with torch.no_grad():
+                lv = ym(torch.from_numpy(yx))
+            yolo_post(raw_heads(lv), [tuple(t.shape[2:]) for t in lv], yx.shape[2:], img.shape[:2])
         mosaic.mosaic_frame(img, [tuple(int(v) for v in r) for r in ib], 8)
         ref.append((np.asarray(idx, np.int64), np.asarray(ib, np.int64).reshape(-1, 4)))
         done += 1
@@ -114,7 +129,8 @@ def cpu_baseline(frames, sd, seconds):
     dt = time.perf_counter() - t0
     rec = {"value": done / dt, "unit": "frames/s", "cores": cores, "kind": "port", "cpu_model": cpu_model(),
            "sample": f"{done} x {frames.shape[2]}x{frames.shape[1]} synthetic frames through the oracle "
-                     f"(torch-CPU fp32 RetinaFace-R50 + numpy decode/NMS/mosaic; faces only), {dt:.1f} s"}
+                     f"(torch-CPU fp32 RetinaFace-R50 + numpy decode/NMS/mosaic"
+                     f"{' + YOLOv8n plate forward/NMS' if plates else ''}; one frame at a time), {dt:.1f} s"}
     return rec, ref
 
 
@@ -216,7 +232,11 @@ def main():
         total = world * B
         f0, nloc, per_rank = rank * B, B, B
     batches = [(s, min(B, nloc - s)) for s in range(0, nloc, B)]
-    host = synth.frames(min(B, max(nloc, 1)), H, W, seed=0, start=f0)   # one batch of distinct frames, reused
+    nhost = min(B, max(nloc, 1))                          # one batch of distinct frames, reused
+    if a.frames_src == "up2":
+        host = np.repeat(np.repeat(synth.frames(nhost, H // 2, W // 2, seed=0, start=f0), 2, axis=1), 2, axis=2)
+    else:
+        host = synth.frames(nhost, H, W, seed=0, start=f0)
     frames = torch.from_numpy(host).to(dev)
     out = torch.empty_like(frames)
     stream = torch.cuda.current_stream(dev)
@@ -431,11 +451,12 @@ def main():
 
     head, head_lists = measure(a.precision)
     res = {
-        "metric": "end-to-end detect+blur FPS on 1920x1080 frames",
+        "metric": f"end-to-end detect+blur FPS on {W}x{H} frames",
         "value": head["value"], "unit": "frames/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": head["ms_per_step"], "higher_is_better": True, "scaling": a.scaling,
         "vs_baseline": None, "dtype": "fp32" if a.precision.startswith("fp32") else a.precision,
-        "data": "synthetic (counter-hash frames, seeded random weights)",
+        "data": "synthetic (counter-hash frames" + (", 2x nearest-upsampled" if a.frames_src == "up2" else "") +
+                ", seeded random weights)",
         "config": {"workload": f"RetinaFace-R50+FPN+SSH{' + YOLOv8n plates' if plates else ''} detect + mosaic "
                                f"write-back, {total} frames of {W}x{H} per step over {world} GPU(s) "
                                f"(batches of {B} per GPU)",
@@ -465,7 +486,7 @@ def main():
         if modes:
             res["modes"] = modes
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        base, ref = cpu_baseline(host[:64], sd, a.cpu_baseline_seconds)
+        base, ref = cpu_baseline(host[:64], sd, a.cpu_baseline_seconds, plates=plates)
         res["cpu_baseline"] = base
         for p, lists in [(a.precision, head_lists)] + list(mode_lists.items()):
             if p.startswith("fp32"):

@@ -153,25 +153,31 @@ def _agree(a, b):
     return sum(np.array_equal(x[0], y[0]) and np.array_equal(x[1], y[1]) for x, y in zip(a, b)) / len(a)
 
 
-# Floors: measured fractions of 64 frames with keep lists + int boxes identical to
-# the fp32 path (bench.py `parity`, BENCH_r02) minus a margin for box-to-box variation.
-PARITY_FLOOR = {"bf16": 0.0, "fp16": 0.0}
+# Floors, measured on the B=64 bench frames (r03 GPU run, printed by the test) minus a
+# margin for box-to-box variation: the fraction of fp32 face boxes that a 16-bit box
+# matches at IoU >= 0.9. (Identical keep lists are rare in 16 bits -- ~30 faces per
+# frame with seeded weights, so one moved near-threshold box flips a frame -- and
+# that fraction is printed, not asserted: box-index parity is an fp32-plan claim.)
+# r03: bf16 1895/1964 = 0.965, fp16 1944/1964 = 0.990 (0/64 frames identical in either)
+IOU09_FLOOR = {"bf16": 0.94, "fp16": 0.975}
 
 
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
 def test_c3_b64_keep_list_agreement_with_fp32(c3_runs, prec):
-    """Measured, not assumed: the fraction of B=64 frames whose complete face keep
-    lists and int boxes equal the fp32 path's; boxes that differ still overlap."""
+    """Measured, not assumed: the fraction of fp32 boxes over B=64 frames that the
+    16-bit path reproduces at IoU >= 0.9, against a floor; plus the fraction of frames
+    whose complete keep lists and int boxes are identical (reported)."""
     _, runs = c3_runs
     f32, other = runs["fp32"][1], runs[prec][1]
     frac = _agree(other, f32)
-    print(f"{prec} vs fp32: {frac:.3f} of 64 frames identical")
-    assert frac >= PARITY_FLOOR[prec]
     total = matched = 0
     for x, y in zip(f32, other):
         total += len(x[1])
-        matched += _iou_match(x[1].astype(np.float64), y[1].astype(np.float64), 0.8)
-    assert total > 0 and matched / total >= 0.9, (matched, total)
+        matched += _iou_match(x[1].astype(np.float64), y[1].astype(np.float64), 0.9)
+    m09 = matched / max(total, 1)
+    print(f"{prec} vs fp32: {frac:.3f} of 64 frames identical; {matched}/{total} = {m09:.4f} of fp32 boxes "
+          f"matched at IoU >= 0.9")
+    assert total > 0 and m09 >= IOU09_FLOOR[prec], (matched, total)
 
 
 # ------------------------------------------------------------------ C5 (one GPU)

@@ -195,7 +195,7 @@ CONV_CASES = [
 ]
 
 
-@pytest.mark.parametrize("prec", ["fp32", "fp32-big", "fp32-small", "fp32-exact", "fp32-x6", "fp32-x6-big",
+@pytest.mark.parametrize("prec", ["fp32", "fp32-big", "fp32-mf32", "fp32-small", "fp32-exact", "fp32-x6", "fp32-x6-big",
                                   "fp32-x6-small", "fp32-s128", "fp32-s256", "bf16", "fp16", "bf16-gemm64",
                                   "bf16-gemm128"])
 @pytest.mark.parametrize("case", CONV_CASES)
@@ -218,6 +218,9 @@ def test_conv_matches_torch(gpu, face_ctx_factory, prec, case, options=None):
     if prec == "fp32-exact":
         options.update(f32_split=0)
         prec = "fp32"
+    if prec == "fp32-mf32":                   # the big tile on v_mfma_f32_32x32x16_f16 (option x6_mf32)
+        options.update(x6_mf32=1)
+        prec = "fp32-big"
     if prec in ("fp32-big", "fp32-small"):    # force one x6 tile form (conv_x6.hip)
         options.update(x6_small_k=0, x6_small_k2=0, x6_small_tiles=0, x6_stream=0) if prec == "fp32-big" else \
             options.update(x6_small_k=1 << 30, x6_stream=0)

@@ -50,9 +50,10 @@ pytestmark = [pytest.mark.gpu, pytest.mark.parity]
 # bound is ~65 ulps at 1920 px (observed: 2.1e-4 px at x = 273).
 F32_BOUND = {"score": 2e-5, "order": 2e-5, "iou": 2e-5, "trunc": 2e-3}
 # heads: max |gpu - oracle| / max |oracle| per tensor, ~1.5x the largest observed
-# over the cases (r03, R50: pairs 3.9e-6, exact 3.2e-6, bf16 triples 4.4e-6)
+# over the cases (r03, R50: pairs 3.9e-6, exact 3.2e-6, bf16 triples 4.4e-6; MobileNet-0.25:
+# pairs 2.6e-6, exact 2.3e-6)
 HEAD_TOL = {("pairs", "default"): 6e-6, ("exact", "default"): 5e-6, ("bf16x3", "default"): 7e-6,
-            ("pairs", "mnet"): 1e-4, ("exact", "mnet"): 1e-4}
+            ("pairs", "mnet"): 4e-6, ("exact", "mnet"): 3.5e-6}
 
 
 def _synth(n, h, w, seed, start=0):

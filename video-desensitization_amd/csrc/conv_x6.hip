@@ -30,6 +30,7 @@
 //     ds_read_b128 fragment reads for the 16-row MFMA operand pattern.
 #include "vd_common.h"
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 #include <cstring>
 
@@ -47,7 +48,7 @@ constexpr int kAmaxFrames = 1024;               // LDS reserved for per-frame ma
 // load -> compute -> epilogue phases are short and neighbours on the CU overlap them.
 // TERMS: 3 = bf16 triples (A and B), 2 = fp16 pairs (A and B), 1 = fp16 pair weights
 // with activations exact in fp16 (one A plane: the integer-valued face canvas)
-template <int BM_, int BN, int NT_, int NST, int TERMS> struct X6Shape {
+template <int BM_, int BN, int NT_, int NST, int TERMS, int MF = 16> struct X6Shape {
     static constexpr int TA = TERMS == 1 ? 1 : TERMS, TB = TERMS == 1 ? 2 : TERMS;   // A / B planes
     static constexpr int BM = BM_, NT = NT_, WAVES = NT / 64;
     static constexpr int PL_A = BM * 64;                       // bytes per A plane
@@ -59,7 +60,7 @@ template <int BM_, int BN, int NT_, int NST, int TERMS> struct X6Shape {
     static constexpr int WAVES_N = BN >= 64 ? 2 : 1;
     static constexpr int WAVES_M = WAVES / WAVES_N;
     static constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
-    static constexpr int TM = WTM / 16, TN = WTN / 16;
+    static constexpr int TM = WTM / MF, TN = WTN / MF;            // MFMA blocks per wave tile
     static constexpr int NDMA = TB * BN / 16;                  // 1-KB DMA instructions per K tile
     static constexpr int AROWS = NT / 4;                       // A rows per staging pass (2 passes)
     static_assert(BM == 2 * AROWS, "two A items per thread");
@@ -152,6 +153,22 @@ __device__ __forceinline__ f32x4_t mfma_terms<2>(const u32x4 (&a)[3], const u32x
     return acc;
 }
 
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+
+// fp16 pair on the 32x32x16 matrix-core form: the same three products per K step of
+// 16, half the MFMA instructions of the 16x16x32 form for the same work, and 24 of
+// every 32 issue cycles free for the A split / address VALU (16x16x32: 8 of 16)
+__device__ __forceinline__ f32x16_t mfma_pair32(const u32x4 (&a)[3], const u32x4 (&b)[3], f32x16_t acc) {
+#define VDH_MFMA32(pa, pb)                                                                               \
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8_t, a[pa]),                    \
+                                                 __builtin_bit_cast(f16x8_t, b[pb]), acc, 0, 0, 0)
+    VDH_MFMA32(1, 0);
+    VDH_MFMA32(0, 1);
+    VDH_MFMA32(0, 0);
+#undef VDH_MFMA32
+    return acc;
+}
+
 // 8 f32 -> TERMS packed 16-B planes (bf16 truncation split, or scaled fp16 pair)
 template <int TERMS>
 __device__ __forceinline__ void split_pack(const float (&e)[8], float sa, u32x4 (&o)[3]) {
@@ -169,9 +186,10 @@ __device__ __forceinline__ void split_pack(const float (&e)[8], float sa, u32x4 
         o[2] = u32x4{lv[0] | (lv[1] << 16), lv[2] | (lv[3] << 16), lv[4] | (lv[5] << 16), lv[6] | (lv[7] << 16)};
 }
 
-template <int BM, int BN, int NT, int NST, int TERMS>
+template <int BM, int BN, int NT, int NST, int TERMS, int MF>
 __global__ __launch_bounds__(NT, 2) void conv_x6_kernel(ConvArgs a) {
-    using S = X6Shape<BM, BN, NT, NST, TERMS>;
+    static_assert(MF == 16 || (MF == 32 && TERMS == 2), "32x32x16 form: fp16 pairs only");
+    using S = X6Shape<BM, BN, NT, NST, TERMS, MF>;
     constexpr int STAGE = S::STAGE, PL_A = S::PL_A, PL_B = S::PL_B, TM = S::TM, TN = S::TN, WAVES = S::WAVES;
     constexpr int AROWS = S::AROWS;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -293,11 +311,12 @@ __global__ __launch_bounds__(NT, 2) void conv_x6_kernel(ConvArgs a) {
         }
     };
 
-    f32x4_t acc[TM][TN];
+    using AccT = typename std::conditional<MF == 32, f32x16_t, f32x4_t>::type;
+    AccT acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < TN; ++j) acc[i][j] = AccT{};
     if (a.ymax)   // beyond the stages / epilogue image; ordered before use by the main loop's barriers
         for (int f = tid; f < a.B; f += NT) ((unsigned*)(smem + S::LDS))[f] = 0u;
 
@@ -307,7 +326,29 @@ __global__ __launch_bounds__(NT, 2) void conv_x6_kernel(ConvArgs a) {
         const char* A = smem + st * STAGE;
         const char* Bs = A + S::TA * PL_A;
         const int ch = lane >> 4;
-        if constexpr (TN > TM) {   // wide wave tile: all A fragments resident, B fragments streamed
+        if constexpr (MF == 32) {   // two K steps of 16: lane l reads row l % 32, 16-B chunk 2 s + l / 32
+            const int r32 = lane & 31, c32 = lane >> 5;
+#pragma unroll
+            for (int sk = 0; sk < 2; ++sk) {
+                u32x4 af[TM][3];
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int p = 0; p < 2; ++p)
+                        af[i][p] = *(const u32x4*)(A + p * PL_A + swz(wm * S::WTM + i * 32 + r32, 2 * sk + c32));
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    u32x4 bf[3];
+#pragma unroll
+                    for (int p = 0; p < 2; ++p)
+                        bf[p] = *(const u32x4*)(Bs + p * PL_B + swz(wn * S::WTN + j * 32 + r32, 2 * sk + c32));
+#pragma unroll
+                    for (int i = 0; i < TM; ++i) acc[i][j] = mfma_pair32(af[i], bf, acc[i][j]);
+                    if (split_next && sk == 0 && j == 0) store_item(st_next, rn, 0);
+                    if (split_next && sk == 1 && j == 0) store_item(st_next, rn, 1);
+                }
+            }
+        } else if constexpr (TN > TM) {   // wide wave tile: all A fragments resident, B fragments streamed
             u32x4 af[TM][3];
 #pragma unroll
             for (int i = 0; i < TM; ++i)
@@ -418,14 +459,25 @@ __global__ __launch_bounds__(NT, 2) void conv_x6_kernel(ConvArgs a) {
         if (h) __syncthreads();
         const int wrow = wm * S::WTM - h * EPR;        // this wave's first row within the pass
         if (wrow >= 0 && wrow < EPR) {
+            if constexpr (MF == 32) {   // 32x32 C layout: row 8 (r / 4) + 4 (l / 32) + r % 4, column l % 32
 #pragma unroll
-            for (int i = 0; i < TM; ++i)
+                for (int i = 0; i < TM; ++i)
 #pragma unroll
-                for (int j = 0; j < TN; ++j)
+                    for (int j = 0; j < TN; ++j)
 #pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        ep[(wrow + i * 16 + (lane >> 4) * 4 + r) * EPLD + wn * S::WTN + j * 16 + (lane & 15)] =
-                            acc[i][j][r];
+                        for (int r = 0; r < 16; ++r)
+                            ep[(wrow + i * 32 + 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3)) * EPLD + wn * S::WTN +
+                               j * 32 + (lane & 31)] = acc[i][j][r];
+            } else {
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            ep[(wrow + i * 16 + (lane >> 4) * 4 + r) * EPLD + wn * S::WTN + j * 16 + (lane & 15)] =
+                                acc[i][j][r];
+            }
         }
         __syncthreads();
 #pragma unroll
@@ -866,11 +918,11 @@ bool vd_conv_x6_ok(const ConvArgs& a) {
            xbytes < 2147483647.0;
 }
 
-template <int BM, int BN, int NT, int NST, int TERMS>
+template <int BM, int BN, int NT, int NST, int TERMS, int MF = 16>
 static hipError_t launch_x6(const ConvArgs& a0, hipStream_t s) {
-    using S = X6Shape<BM, BN, NT, NST, TERMS>;
+    using S = X6Shape<BM, BN, NT, NST, TERMS, MF>;
     static const bool attr = [] {
-        (void)hipFuncSetAttribute((const void*)conv_x6_kernel<BM, BN, NT, NST, TERMS>,
+        (void)hipFuncSetAttribute((const void*)conv_x6_kernel<BM, BN, NT, NST, TERMS, MF>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS + 4 * kAmaxFrames);
         return true;
     }();
@@ -880,7 +932,7 @@ static hipError_t launch_x6(const ConvArgs& a0, hipStream_t s) {
     a.ntiles_n = (a.cout + BN - 1) / BN;
     const int mt = (a.M + BM - 1) / BM;
     const int lds = S::LDS + (a.ymax ? 4 * a.B : 0);
-    hipLaunchKernelGGL((conv_x6_kernel<BM, BN, NT, NST, TERMS>), dim3(mt * a.ntiles_n), dim3(NT), lds, s, a);
+    hipLaunchKernelGGL((conv_x6_kernel<BM, BN, NT, NST, TERMS, MF>), dim3(mt * a.ntiles_n), dim3(NT), lds, s, a);
     return hipGetLastError();
 }
 
@@ -944,13 +996,16 @@ static hipError_t launch_terms(const ConvArgs& a0, hipStream_t s) {
         // (layer3/4 and FPN 12-20 % faster than 256 x 128; not below ~200 tiles: FPN output3,
         // 100 tiles, 137 -> 199 us)
         const long t256 = (long)((a.M + 255) / 256) * (a.cout / 256);
-        if (a.tune && a.tune->x6_bn256 && a.cout % 256 == 0 && t256 >= 192)
+        if (a.tune && a.tune->x6_bn256 && a.cout % 256 == 0 && t256 >= 192) {
+            if (a.tune->x6_mf32) return launch_x6<256, 256, 512, 2, TERMS, 32>(a, s);
             return launch_x6<256, 256, 512, 2, TERMS>(a, s);
+        }
         // Cout 192 (the fused SSH conv5X5_1 + conv3X3): one 192-wide N tile instead of two
         // 128-wide ones with a quarter of the MFMAs on padding rows (level 0 1716 -> 1264 us,
         // level 1 526 -> 396; not for level 2's 100 tiles: 137 -> 178)
         if (a.tune && a.tune->x6_bn256 && a.cout == 192 && (a.M + 255) / 256 >= 192)
             return launch_x6<256, 192, 512, 2, TERMS>(a, s);
+        if (a.tune && a.tune->x6_mf32) return launch_x6<256, 128, 512, 2, TERMS, 32>(a, s);
     }
     return launch_x6<256, 128, 512, 2, TERMS>(a, s);
 }

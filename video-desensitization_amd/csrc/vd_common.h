@@ -47,6 +47,7 @@ struct VdTune {
     int x6_small_k2 = 1 << 20;//   fp16 pairs: K at or below which N <= 64 layers take the small tile
     int x6_bn256 = 1;         // fp16 pairs: 256 x 256 tile for Cout % 256 == 0
     int x6_exact = 1;         // fp16 pairs: one A plane for inputs exact in fp16 (the face stem)
+    int x6_mf32 = 0;          // fp16 pairs: 256 x {256,128} tiles on v_mfma_f32_32x32x16_f16 (else 16x16x32)
     int f32_split = 2;        // plan (fp32, at weight load): 2 = operands scaled by powers of two
                               //   and split into fp16 pairs, 3 products on the f16 matrix cores;
                               //   1 = exact 3-term bf16 split, 6 products (conv_x6.hip);
