@@ -330,3 +330,27 @@ def test_heads_fp32_fused_stem_pool_matches_unfused(gpu):
     assert sum(len(x) for x in boxes[0]) > 0
     for a, b in zip(boxes[1], boxes[0]):
         np.testing.assert_array_equal(a, b)
+
+
+def test_heads_fp32_fused_layer1_matches_unfused(gpu):
+    """fp32 plan, default: each layer1 bottleneck as one kernel (block32.hip: t1 / t2 in
+    LDS as per-tile-scaled fp16 pairs); option block_fuse32=0 keeps the conv-by-conv
+    chain (per-frame scales). The same products rounded at different points: heads
+    within f32 rounding of each other (the oracle bound), identical boxes."""
+    import vdmi
+    fr = _frames(3, 1080, 1920, seed=29)
+    heads, boxes = {}, {}
+    for fz in (1, 0):
+        ctx = vdmi.Context(precision="fp32", max_batch=3, options={"block_fuse32": fz})
+        try:
+            ctx.load_weights(0, face_weights("default"))
+            heads[fz] = ctx.forward_heads(fr)
+            r = ctx.detect(fr)
+            boxes[fz] = [r.frame(b)[0].copy() for b in range(3)]
+        finally:
+            ctx.close()
+    for a, b in zip(heads[1], heads[0]):
+        assert np.abs(a - b).max() <= 6e-6 * (np.abs(b).max() + 1e-6), np.abs(a - b).max() / np.abs(b).max()
+    assert sum(len(x) for x in boxes[0]) > 0
+    for a, b in zip(boxes[1], boxes[0]):
+        np.testing.assert_array_equal(a, b)

@@ -195,7 +195,7 @@ CONV_CASES = [
 ]
 
 
-@pytest.mark.parametrize("prec", ["fp32", "fp32-big", "fp32-mf32", "fp32-small", "fp32-exact", "fp32-x6", "fp32-x6-big",
+@pytest.mark.parametrize("prec", ["fp32", "fp32-big", "fp32-mf32", "fp32-mid", "fp32-small", "fp32-exact", "fp32-x6", "fp32-x6-big",
                                   "fp32-x6-small", "fp32-s128", "fp32-s256", "bf16", "fp16", "bf16-gemm64",
                                   "bf16-gemm128"])
 @pytest.mark.parametrize("case", CONV_CASES)
@@ -217,6 +217,9 @@ def test_conv_matches_torch(gpu, face_ctx_factory, prec, case, options=None):
         prec = prec.replace("-x6", "")
     if prec == "fp32-exact":
         options.update(f32_split=0)
+        prec = "fp32"
+    if prec == "fp32-mid":                    # 1x1 convs on the 128 x 128 two-stage tile (option x6_mid)
+        options.update(x6_mid=1 << 20, x6_stream=0)
         prec = "fp32"
     if prec == "fp32-mf32":                   # the big tile on v_mfma_f32_32x32x16_f16 (option x6_mf32)
         options.update(x6_mf32=1)
@@ -343,6 +346,40 @@ def test_bottleneck_fused_matches_torch_and_chain(gpu, face_ctx_factory, case):
     assert np.abs(got - ref).max() / scale < 2e-2
     assert np.abs(got - chain).max() / scale < 1e-2
     assert np.mean(got == chain) > 0.95        # mostly bit-identical after bf16 rounding
+
+
+@pytest.mark.parametrize("case", BLOCK_CASES)
+def test_bottleneck_fp32_fused_matches_float64(gpu, face_ctx_factory, case):
+    """block32.hip (the fp32 plan's one-kernel layer1 bottleneck: fp16 pairs, t1 / t2
+    scaled per tile in LDS) against a float64 torch bottleneck on the same f32 inputs,
+    beside the conv-by-conv fp32 chain of the same library (per-frame scales): both sit
+    at f32 rounding (< 2e-6 of the output range), the fused error within 2x the chain's."""
+    n, h, w, cin, ds = case
+    ctx = face_ctx_factory("fp32", 8)
+    rng = np.random.default_rng(h * 100 + w + cin + 7)
+    he = lambda co, ci, k: (rng.standard_normal((co, ci, k, k)) * np.sqrt(2.0 / (ci * k * k))).astype(F32)
+    x = np.maximum(rng.standard_normal((n, h, w, cin)), 0).astype(F32)      # a ReLU output, as in the net
+    w1, w2, w3 = he(64, cin, 1), he(64, 64, 3), he(256, 64, 1)
+    b1, b2, b3 = _bn(rng, 64), _bn(rng, 64), _bn(rng, 256)
+    wd, bd = (he(256, cin, 1), _bn(rng, 256)) if ds else (None, None)
+    got = ctx.bottleneck(x, w1, b1, w2, b2, w3, b3, wd, bd, fused=True)
+    chain = ctx.bottleneck(x, w1, b1, w2, b2, w3, b3, wd, bd, fused=False)
+
+    T = lambda a: torch.from_numpy(np.asarray(a, np.float64))
+    conv = lambda v, wt, p: torch.nn.functional.conv2d(v, T(wt), padding=p)
+    aff = lambda v, b, c: v * T(b[:c]).view(1, c, 1, 1) + T(b[c:]).view(1, c, 1, 1)
+    xt = T(x).permute(0, 3, 1, 2)
+    t1 = torch.relu(aff(conv(xt, w1, 0), b1, 64))
+    t2 = torch.relu(aff(conv(t1, w2, 1), b2, 64))
+    idt = aff(conv(xt, wd, 0), bd, 256) if ds else xt
+    ref = torch.relu(aff(conv(t2, w3, 0), b3, 256) + idt).permute(0, 2, 3, 1).numpy()
+    scale = np.abs(ref).max()
+    e_fused = np.abs(got - ref).max() / scale
+    e_chain = np.abs(chain - ref).max() / scale
+    print(f"fp32 bottleneck {case}: fused {e_fused:.2e}, chain {e_chain:.2e}")
+    assert got.shape == ref.shape
+    assert e_fused < 2e-6 and e_chain < 2e-6
+    assert e_fused <= 2 * e_chain + 1e-7
 
 
 # ------------------------------------------------------------------ post-processing

@@ -12,14 +12,15 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from conv_layers import face_plan  # noqa: E402
 
 
-def main(path, B=64):
+def main(path, B=64, block=True):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-    plan = face_plan(B, fused=True, block=False, chain=False, ssh_fused=True, dual=(0,))
+    # fp32 plan: layer1 bottlenecks fused (block32.hip) unless option block_fuse32=0
+    plan = face_plan(B, fused=True, block=block, chain=False, ssh_fused=True, dual=(0,))
     # the face stream: the stream with the most conv launches (73 per step vs the plate net's 60);
     # its last len(plan) conv launches are the last step's layers
     per = {}
     for r in rows:
-        if "conv" in r["Kernel_Name"] or "stem_pool" in r["Kernel_Name"]:
+        if "conv" in r["Kernel_Name"] or "stem_pool" in r["Kernel_Name"] or "bottleneck" in r["Kernel_Name"]:
             per.setdefault(r["Stream_Id"], []).append(r)
     convs = max(per.values(), key=len)[-len(plan):]
     tot = fl_tot = 0
@@ -35,4 +36,4 @@ def main(path, B=64):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 64)
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 64, (sys.argv[3] != "0") if len(sys.argv) > 3 else True)

@@ -992,6 +992,13 @@ static hipError_t launch_terms(const ConvArgs& a0, hipStream_t s) {
     }
     if (bn == 32) return launch_x6<256, 32, 512, 2, TERMS>(a, s);
     if (bn == 64) return launch_x6<256, 64, 512, 2, TERMS>(a, s);
+    if constexpr (TERMS == 2) {
+        // short-K 1x1 layers (HBM-bound f32 tensors): a 128 x 128 two-stage tile at two
+        // workgroups per CU, so one workgroup's epilogue / prologue overlaps the other's
+        // main loop, and 4x the tiles of the 256 x 256 form balance the last round
+        if (a.tune && a.tune->x6_mid && a.kh == 1 && a.kw == 1 && a.kpad <= a.tune->x6_mid && a.cout % 128 == 0)
+            return launch_x6<128, 128, 256, 2, TERMS>(a, s);
+    }
     if constexpr (TERMS == 2) {   // 64 x 128 wave tiles: 2/3 of the LDS fragment reads per MFMA
         // (layer3/4 and FPN 12-20 % faster than 256 x 128; not below ~200 tiles: FPN output3,
         // 100 tiles, 137 -> 199 us)

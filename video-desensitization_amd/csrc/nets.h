@@ -46,6 +46,7 @@ struct Conv {
 // of conv1/conv2/conv3(/downsample) repacked for the fused kernel.
 struct Block {
     int cin = 0, ds = 0;
+    bool f32 = false;                         // fp32 plan (block32.hip): fp16-pair planes / fragments
     int c1 = -1, c2 = -1, c3 = -1, cd = -1;   // the per-conv plans (flops, unfused fallback)
     void* w1 = nullptr;
     void* w2 = nullptr;

@@ -31,6 +31,7 @@ struct VdTune {
     int lb_pair = 1;          // one letterbox launch for both canvases when geometry allows
     int mosaic_map = 1;       // mosaic output pass: per-band vector maps (0: generic path)
     int block_fuse = 1;       // plan: fused layer1 bottlenecks (block.hip)
+    int block_fuse32 = 1;     // plan, fp32 (fp16 pairs): fused layer1 bottlenecks (block32.hip)
     int chain = 1;            // plan: layer2 conv3 + next conv1 (chain.hip)
     int stem_pool = 1;        // plan: stem conv + maxpool (stem.hip)
     int ssh_fuse = 1;         // plan: SSH conv3X3 + conv5X5_1 as one conv
@@ -47,6 +48,7 @@ struct VdTune {
     int x6_small_k2 = 1 << 20;//   fp16 pairs: K at or below which N <= 64 layers take the small tile
     int x6_bn256 = 1;         // fp16 pairs: 256 x 256 tile for Cout % 256 == 0
     int x6_exact = 1;         // fp16 pairs: one A plane for inputs exact in fp16 (the face stem)
+    int x6_mid = 0;           // fp16 pairs: 1x1 convs with K <= this on the 128 x 128 two-stage tile (0: off)
     int x6_mf32 = 0;          // fp16 pairs: 256 x {256,128} tiles on v_mfma_f32_32x32x16_f16 (else 16x16x32)
     int f32_split = 2;        // plan (fp32, at weight load): 2 = operands scaled by powers of two
                               //   and split into fp16 pairs, 3 products on the f16 matrix cores;
@@ -103,6 +105,22 @@ struct BlockArgs {
     const float* bn;             // s1 t1 s2 t2 (64 each) s3 t3 sd td (256 each)
     unsigned long long* diag;    // optional: per-stage cycle sums of workgroup 0, wave 0 (tools/convbench)
     int mode;                    // experiments (tools/convbench VD_BLOCK_MODE); 0 in production
+};
+
+// One fused layer1 bottleneck in the fp32 plan (block32.hip): x f32 [B][H][W][cin]
+// -> y f32 [B][H][W][256]; weights as fp16 hi / lo planes of the per-conv pair
+// packing (row scales folded into the BN scales), per-frame range slots of x / y.
+struct Block32Args {
+    const void* x; void* y;
+    int B, H, W, cin, ds;
+    int tiles_x, tiles_y;        // 16-wide x 8-high output tiles
+    const void* w1;              // conv1 planes [2][cin/32][64 rows][32] fp16 (LDS image source)
+    const void* w2;              // conv2 fragments [4 jn][2 hf][9 taps][2 planes][64 lanes][8] fp16
+    const void* w3;              // conv3 fragments [8 waves][2 tiles][2 k-steps][2 planes][64][8] (rows permuted)
+    const void* wd;              // downsample fragments, same layout (ds)
+    const float* bn;             // s1 h1 s2 h2 (64 each), s3 h3 (256 each), sd hd (256 each, ds)
+    const unsigned* xmax;        // x's per-frame max |x| slots (frame 0 of this call)
+    unsigned* ymax;              // y's slots (atomic max)
 };
 
 // A bottleneck's conv3 (+ identity, ReLU) and the next bottleneck's conv1 in one
@@ -328,6 +346,8 @@ hipError_t vd_launch_conv_x6(const ConvArgs& a, hipStream_t s);
 void vd_pack_x6(const float* w, int npad, int kpad, uint16_t* out);   // host: f32 [npad][kpad] -> split planes
 void vd_pack_x3h(const float* w, int npad, int kpad, uint16_t* out, float* row_inv);   // ... fp16 pairs
 bool vd_block_ok(int cin, bool ds, int h, int w);
+bool vd_block32_ok(int cin, bool ds, int h, int w);
+hipError_t vd_launch_block32(const Block32Args& a, hipStream_t s);
 bool vd_stem_pool_ok(int xh, int xw, int ph, int pw);
 hipError_t vd_launch_dwconv(const DwConvArgs& a, bool f32, bool f16, hipStream_t s);
 hipError_t vd_launch_stem_pool(const StemPoolArgs& a, hipStream_t s);

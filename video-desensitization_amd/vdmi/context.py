@@ -329,9 +329,9 @@ class Context:
         return out
 
     def bottleneck(self, x, w1, bn1, w2, bn2, w3, bn3, wd=None, bnd=None, fused=True):
-        """One ResNet layer1 bottleneck (bf16 context): x f32 NHWC [n,h,w,cin] -> f32 NHWC
-        [n,h,w,256]; bnK = concat(scale, shift). fused: the one-kernel block, else the
-        conv-by-conv chain."""
+        """One ResNet layer1 bottleneck (bf16 or fp32 context): x f32 NHWC [n,h,w,cin] -> f32
+        NHWC [n,h,w,256]; bnK = concat(scale, shift). fused: the one-kernel block
+        (block.hip / block32.hip), else the conv-by-conv chain."""
         f = lambda a: None if a is None else np.ascontiguousarray(a, np.float32)
         x = f(x)
         n, h, wd_, cin = x.shape
