@@ -32,6 +32,77 @@ def test_decode_matches_pillow(jctx, case):
     np.testing.assert_array_equal(got[1], exp)
 
 
+@pytest.fixture(scope="module")
+def jctx_host_dec(gpu):
+    """Entropy decode on host threads (option jdec_gpu=0): the pre-device path, pinned
+    to Pillow by the tests above in earlier rounds."""
+    import vdmi
+    ctx = vdmi.Context(precision="fp32", max_batch=8, options={"jdec_gpu": 0})
+    yield ctx
+    ctx.close()
+
+
+@pytest.mark.parametrize("chunk", [16, 48, 256])
+@pytest.mark.parametrize("case", CASES)
+def test_device_entropy_small_chunks_matches_pillow(gpu, case, chunk):
+    """jpeg_dec.hip with tiny chunks (option jdec_chunk): every frame is cut into many
+    speculatively decoded chunks, so block boundaries, the block-in-MCU phase and DC
+    predictors must all be recovered by the synchronisation passes; the result is
+    still libjpeg-turbo's decode bit for bit."""
+    import vdmi
+    h, w, q, sub = case[:4]
+    ctx = vdmi.Context(precision="fp32", max_batch=4, options={"jdec_chunk": chunk})
+    try:
+        ds = [make_jpeg(h, w, q, sub, seed=s) for s in range(3)]
+        got = ctx.jpeg_decode(ds)
+        for g, d in zip(got, ds):
+            np.testing.assert_array_equal(g, pillow_rgb(d))
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("noise", [False, True])
+def test_device_entropy_1080p_equals_host_threads(jctx, jctx_host_dec, noise):
+    """1080p q95 4:2:0 frames (ffmpeg-split shape), structured and noise (2.4 MB of
+    entropy data per frame, ~1200 chunks): device and host entropy stages give the
+    same frames, equal to Pillow's decode."""
+    from vdmi import synth
+    fr = synth.frames(3, 1080, 1920, seed=21)
+    if not noise:
+        fr = np.repeat(np.repeat(fr[:, ::4, ::4], 4, 1), 4, 2)
+    jp = []
+    for f in fr:
+        b = io.BytesIO()
+        Image.fromarray(f).save(b, "JPEG", quality=95)
+        jp.append(b.getvalue())
+    dev = jctx.jpeg_decode(jp)
+    host = jctx_host_dec.jpeg_decode(jp)
+    np.testing.assert_array_equal(dev, host)
+    np.testing.assert_array_equal(dev[0], pillow_rgb(jp[0]))
+
+
+def test_device_entropy_damaged_stream_same_as_host(jctx, jctx_host_dec):
+    """Damaged entropy data (bytes overwritten mid-scan, a truncated scan): the device
+    stage flags the stream and the host stage decides, so the result (or the error) is
+    the host decoder's."""
+    import vdmi
+    d = bytearray(make_jpeg(64, 96, 95, 2, seed=3))
+    sos = d.index(b"\xff\xda")
+    for k in range(sos + 40, sos + 60):
+        d[k] = (d[k] * 37 + 11) & 0xFF
+        if d[k] == 0xFF:
+            d[k] = 0xFE
+    cut = bytes(d[:sos + 100])
+    for blob in (bytes(d), cut):
+        try:
+            h = jctx_host_dec.jpeg_decode([blob])
+        except vdmi.VdError as e:
+            with pytest.raises(vdmi.VdError):
+                jctx.jpeg_decode([blob])
+            continue
+        np.testing.assert_array_equal(jctx.jpeg_decode([blob]), h)
+
+
 def _video_frames(n, h=1080, w=1920, q=95):
     """ffmpeg-like frames: synthetic 1080p RGB encoded by libjpeg (Pillow) at q95, 4:2:0."""
     from vdmi import synth

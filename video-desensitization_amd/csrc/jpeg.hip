@@ -77,10 +77,15 @@ __global__ __launch_bounds__(256) void jpeg_idct_kernel(JpegArgs a) {
         lb = (int)(gb - (long)img * a.blocks_per_image);
         c = (a.nc > 2 && lb >= a.cblk[2]) ? 2 : ((a.nc > 1 && lb >= a.cblk[1]) ? 1 : 0);
         const uint16_t* q = a.quant + ((size_t)img * 3 + c) * 64;
-        for (uint32_t e = a.blk_off[gb] + t; e < a.blk_off[gb + 1]; e += 8) {
-            const uint32_t v = a.entries[e];
-            const int k = (int)(v >> 16) & 63;
-            coef[g][k] = (int)(int16_t)(v & 0xFFFFu) * (int)q[k];
+        if (a.dense) {
+#pragma unroll
+            for (int k = t * 8; k < t * 8 + 8; ++k) coef[g][k] = (int)a.dense[gb * 64 + k] * (int)q[k];
+        } else {
+            for (uint32_t e = a.blk_off[gb] + t; e < a.blk_off[gb + 1]; e += 8) {
+                const uint32_t v = a.entries[e];
+                const int k = (int)(v >> 16) & 63;
+                coef[g][k] = (int)(int16_t)(v & 0xFFFFu) * (int)q[k];
+            }
         }
     }
     __syncthreads();

@@ -1,0 +1,406 @@
+// jpeg_dec.hip — baseline JPEG entropy decoding on the device (self-synchronising
+// parallel Huffman decode), feeding jpeg.hip's IDCT / colour kernels.
+//
+// Replaces the host entropy stage of the frame read (jpeg_host.cpp: cv2.imread of
+// the ffmpeg-split frames, combine_detect.py:167-172; libjpeg-turbo's jdhuff.c
+// [ext] decode restated). A frame's entropy-coded segment is one sequential bit
+// stream (the ffmpeg-split frames carry no restart markers), so it is cut into
+// fixed-size chunks of raw bytes, one thread each, and decoded speculatively:
+//
+//   jdec_prep_kernel   per frame: stuffed 0x00 bytes per chunk, exclusive scan ->
+//                      D[i], the data-bit position of chunk i's first byte
+//                      (positions count data bits, stuffed bytes excluded).
+//   jdec_sync_kernel   chunk i decodes whole blocks (MCU order) from a start state
+//                      (data-bit position, block-in-MCU u; a state is always a
+//                      block boundary) until the first block boundary at or past
+//                      chunk i+1's start: its exit state E[i], blocks started and
+//                      the sum of DC differences per component. Pass 0 starts every
+//                      chunk at its first data bit with u = 0 (exact for chunk 0);
+//                      pass p > 0 restarts chunk i from E[i-1] of pass p-1 where that
+//                      differs from the state it last started from. Huffman codes
+//                      resynchronise within a few codewords, and the block-in-MCU
+//                      phase within a few MCUs (luma and chroma tables differ), so a
+//                      wrong start converges onto the true block boundaries and E[i]
+//                      stops changing; the host launches passes until no exit state
+//                      changes. In speculative passes an invalid code or a run past
+//                      the block ends the block (a wrong start must keep going).
+//   jdec_scan_kernel   per frame: exclusive scans of the block counts and DC sums
+//                      -> each chunk's first block index and DC predictors.
+//   jdec_write_kernel  each chunk decodes its blocks once more from its final start
+//                      state, DC = predictor + difference, coefficients dequantised
+//                      later by jpeg_idct_kernel; blocks go dense (int16 natural
+//                      order, component-plane block order) through a per-thread LDS
+//                      block; an invalid code or a run past a block here is a
+//                      corrupt stream (the frame is rejected, as the host decoder).
+// Tables (jpeg_host.cpp build_huff, per distinct DHT set of the batch): an 11-bit
+// lookahead for every table, libjpeg-turbo's AC fast path (code + extra bits in one
+// lookup), and the canonical maxcode / valoff / vals slow path for longer codes.
+#include "vd_common.h"
+
+namespace {
+
+constexpr int kLook = 11;
+constexpr int WG = 256;
+
+__constant__ int kZig[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48,
+                             41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
+                             30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+
+// data-bit reader over raw scan bytes: 0xFF 0x00 -> 0xFF, a marker or the end of the
+// segment feeds zeros (jdhuff.c fill_bit_buffer), 16-B windows of global memory
+struct Reader {
+    const uint8_t* d;
+    uint32_t n;                // raw bytes of the segment
+    uint32_t p;                // next raw byte to fetch
+    uint64_t acc;              // left-aligned bit buffer
+    int nb;
+    bool end;
+    uint32_t wbase;
+    uint4 wv;
+    uint32_t pos;              // data-bit position of acc's top bit
+
+    __device__ __forceinline__ uint32_t byte_at(uint32_t i) {
+        if (i >= n) return 0x100u;                              // past the segment
+        const uint32_t b = i & ~15u;
+        if (b != wbase) {
+            wbase = b;
+            wv = *(const uint4*)(d + b);
+        }
+        const uint32_t q = (i >> 2) & 3u;
+        const uint32_t w = q == 0 ? wv.x : (q == 1 ? wv.y : (q == 2 ? wv.z : wv.w));
+        return (w >> ((i & 3u) * 8u)) & 0xFFu;
+    }
+    __device__ __forceinline__ void fill() {
+        while (nb <= 56) {
+            uint32_t v = 0;
+            if (!end) {
+                const uint32_t c = byte_at(p);
+                if (c > 0xFFu) {
+                    end = true;
+                } else if (c == 0xFFu) {
+                    if (byte_at(p + 1) == 0u) { v = 0xFFu; p += 2; }
+                    else end = true;                            // a marker: zeros from here
+                } else {
+                    v = c;
+                    ++p;
+                }
+            }
+            acc |= (uint64_t)v << (56 - nb);
+            nb += 8;
+        }
+    }
+    // start at raw byte r (whose first data bit is data position dpos), then skip to `to`
+    __device__ void seek(const uint8_t* data, uint32_t nbytes, uint32_t r, uint32_t dpos, uint32_t to) {
+        d = data; n = nbytes; p = r; acc = 0; nb = 0; end = false; wbase = 0xFFFFFFFFu; pos = dpos;
+        if (p > 0 && p < n && byte_at(p) == 0u && byte_at(p - 1) == 0xFFu) ++p;   // a stuffed byte: no data
+        uint32_t k = to - dpos;
+        while (k) {
+            const int s = k > 32 ? 32 : (int)k;
+            if (nb < s) fill();
+            acc <<= s; nb -= s; pos += s; k -= s;
+        }
+    }
+    __device__ __forceinline__ uint32_t peek(int k) { if (nb < k) fill(); return (uint32_t)(acc >> (64 - k)); }
+    __device__ __forceinline__ void skip(int k) { acc <<= k; nb -= k; pos += k; }
+    __device__ __forceinline__ int get(int k) {
+        if (k == 0) return 0;
+        const uint32_t v = peek(k);
+        skip(k);
+        return (int)v;
+    }
+};
+
+__device__ __forceinline__ int extend(int v, int s) { return (s && v < (1 << (s - 1))) ? v - (1 << s) + 1 : v; }
+
+__device__ __forceinline__ int decode_sym(Reader& b, const JLds& T, int t) {
+    const uint32_t look = b.peek(kLook);
+    const uint32_t e = T.look[t][look];
+    if (e >> 8) {
+        b.skip((int)(e >> 8));
+        return (int)(e & 0xFFu);
+    }
+    const uint32_t code = b.peek(16);
+    for (int len = kLook - 1; len <= 16; ++len) {
+        const int c = (int)(code >> (16 - len));
+        if (T.maxcode[t][len] >= 0 && c <= T.maxcode[t][len]) {
+            b.skip(len);
+            return T.vals[t][(T.valoff[t][len] + c) & 255];
+        }
+    }
+    return -1;
+}
+
+// per batch
+struct JdecArgs {
+    const uint8_t* bytes;          // raw scan segments, frame f at bytes + seg_off[f] (16-B aligned)
+    const uint32_t* seg_off;       // [n]
+    const uint32_t* seg_len;       // [n] raw bytes
+    const uint32_t* chunk0;        // [n + 1] first global chunk of each frame
+    const uint8_t* tab_of;         // [n] table set per frame
+    const JLds* tabs;              // [sets]
+    int n, chunk_bytes;
+    int bpm;                       // blocks per MCU
+    int ucomp[6], udc[6], uac[6];  // per block-in-MCU: component, DC / AC table (0..1 of the set)
+    int ubx[6], uby[6];            // its block offset within the MCU's component area
+    int mcux, total_blocks;        // per frame
+    int cblk[3], bw[3], hs[3], vs[3];
+    int blocks_per_image;
+    // per chunk
+    uint32_t* D;                   // [chunks + frames] data-bit start (frame end at chunk0[f+1] + f)
+    uint32_t* stuffed;             // scratch [chunks]
+    uint32_t* S;                   // start state: pos
+    uint8_t* Su;                   //   block-in-MCU
+    uint32_t* Epos[2]; uint8_t* Eu[2];   // exit state, ping-pong per pass
+    uint32_t* nblk;                // blocks started
+    int* dcs;                      // [chunks][3] DC difference sums
+    uint32_t* base;                // first block index (scan)
+    int* dcoff;                    // [chunks][3] DC predictors at the chunk start
+    int16_t* dense;                // [n][blocks_per_image][64]
+    int* flags;                    // [0] exit states changed, [1] corrupt stream
+};
+
+// one frame per workgroup: stuffed bytes per chunk -> data-bit positions
+__global__ __launch_bounds__(WG) void jdec_prep_kernel(JdecArgs a) {
+    const int f = blockIdx.x, t = threadIdx.x;
+    const uint8_t* d = a.bytes + a.seg_off[f];
+    const uint32_t nbytes = a.seg_len[f];
+    const uint32_t c0 = a.chunk0[f], nch = a.chunk0[f + 1] - c0;
+    __shared__ uint32_t s[WG];
+    uint32_t carry = 0;
+    for (uint32_t g0 = 0; g0 < nch; g0 += WG) {
+        const uint32_t i = g0 + t;
+        uint32_t cnt = 0;
+        if (i < nch) {
+            const uint32_t r0 = i * a.chunk_bytes, r1 = min(nbytes, r0 + a.chunk_bytes);
+            uint32_t prev = r0 > 0 ? d[r0 - 1] : 0u;
+            for (uint32_t r = r0; r < r1; ++r) {
+                const uint32_t c = d[r];
+                cnt += (c == 0u && prev == 0xFFu) ? 1u : 0u;
+                prev = (c == 0u && prev == 0xFFu) ? 0u : c;   // 0xFF 0x00 0x00: the second 00 is data
+            }
+        }
+        s[t] = cnt;
+        __syncthreads();
+        for (int o = 1; o < WG; o <<= 1) {                 // inclusive Hillis-Steele scan
+            const uint32_t v = t >= o ? s[t - o] : 0u;
+            __syncthreads();
+            s[t] += v;
+            __syncthreads();
+        }
+        if (i < nch) a.D[c0 + f + i] = 8u * (i * (uint32_t)a.chunk_bytes - (carry + s[t] - cnt));
+        carry += s[WG - 1];
+        __syncthreads();
+    }
+    if (t == 0) a.D[c0 + f + nch] = 8u * (nbytes - carry);   // the frame's data bits (chunk end of the last)
+}
+
+// decode whole blocks from (pos, u) until the first block boundary at or past `stop`;
+// MODE 0: counting (speculative: errors end the block), MODE 1: writing (errors flag)
+template <int MODE>
+__device__ __forceinline__ void decode_blocks(const JdecArgs& a, const JLds& T, Reader& b, int& u, uint32_t stop,
+                                              uint32_t& nblk, int (&dcs)[3], uint32_t blk0, int (&pred)[3],
+                                              int16_t* lblk, int16_t* dense, bool& bad) {
+    while (b.pos < stop) {
+        if constexpr (MODE == 1) {
+            if (blk0 + nblk >= (uint32_t)a.total_blocks) return;      // past the frame's last block
+#pragma unroll
+            for (int k = 0; k < 64; k += 8) *(uint4*)(lblk + k) = make_uint4(0, 0, 0, 0);
+        }
+        const int c = a.ucomp[u];
+        int s = decode_sym(b, T, a.udc[u]);
+        int diff = 0;
+        if (s < 0 || s > 11) {
+            if constexpr (MODE == 1) { bad = true; return; }
+            if (s < 0) b.skip(1);                                      // keep moving: a wrong start resyncs
+            s = 0;
+        } else {
+            diff = extend(b.get(s), s);
+        }
+        dcs[c] += diff;
+        if constexpr (MODE == 1) {
+            pred[c] += diff;
+            lblk[0] = (int16_t)pred[c];
+        }
+        const int at = 2 + a.uac[u];
+        for (int k = 1; k < 64;) {
+            const uint32_t look = b.peek(kLook);
+            const uint32_t f = T.fast[at - 2][look];
+            if (f & 0xFFu) {
+                b.skip((int)(f & 0xFFu));
+                const int run = (int)((f >> 8) & 0xFFu);
+                if (run == 64) break;                                  // EOB
+                if (run == 16) { k += 16; continue; }                  // ZRL
+                k += run;
+                if (k > 63) { if constexpr (MODE == 1) { bad = true; return; } break; }
+                if constexpr (MODE == 1) lblk[kZig[k]] = (int16_t)(f >> 16);
+                ++k;
+                continue;
+            }
+            const int rs = decode_sym(b, T, at);
+            if (rs < 0) {
+                if constexpr (MODE == 1) { bad = true; return; }
+                b.skip(1);
+                break;
+            }
+            const int r = rs >> 4, sz = rs & 15;
+            if (sz == 0) {
+                if (r != 15) break;
+                k += 16;
+                continue;
+            }
+            k += r;
+            if (k > 63) { if constexpr (MODE == 1) { bad = true; return; } break; }
+            const int v = extend(b.get(sz), sz);
+            if constexpr (MODE == 1) lblk[kZig[k]] = (int16_t)v;
+            ++k;
+        }
+        if constexpr (MODE == 1) {   // the finished block -> its component plane
+            const uint32_t g = blk0 + nblk;
+            const uint32_t m = g / a.bpm;
+            const int mx = (int)(m % a.mcux), my = (int)(m / a.mcux);
+            const size_t pb = (size_t)a.cblk[c] + (size_t)(my * a.vs[c] + a.uby[u]) * a.bw[c] + mx * a.hs[c] + a.ubx[u];
+            int16_t* dst = dense + pb * 64;
+#pragma unroll
+            for (int k = 0; k < 64; k += 8) *(uint4*)(dst + k) = *(const uint4*)(lblk + k);
+        }
+        ++nblk;
+        u = u + 1 == a.bpm ? 0 : u + 1;
+    }
+}
+
+__device__ __forceinline__ void load_tables(const JdecArgs& a, int f, JLds* T) {
+    const uint32_t* src = (const uint32_t*)(a.tabs + a.tab_of[f]);
+    uint32_t* dst = (uint32_t*)T;
+    for (int i = threadIdx.x; i < (int)(sizeof(JLds) / 4); i += WG) dst[i] = src[i];
+    __syncthreads();
+}
+
+// pass 0 (first = 1) or a resynchronisation pass over every chunk of the batch;
+// workgroups never straddle frames (wg_frame / wg_chunk0 from the host)
+__global__ __launch_bounds__(WG) void jdec_sync_kernel(JdecArgs a, const int* wg_frame, const uint32_t* wg_chunk,
+                                                        int pass) {
+    __shared__ JLds T;
+    const int f = wg_frame[blockIdx.x];
+    load_tables(a, f, &T);
+    const uint32_t c0 = a.chunk0[f], nch = a.chunk0[f + 1] - c0;
+    const uint32_t i = wg_chunk[blockIdx.x] + threadIdx.x;        // chunk within the frame
+    if (i >= nch) return;
+    const uint32_t g = c0 + i;
+    const int pi = (pass + 1) & 1, po = pass & 1;                  // pass p reads E[(p-1)&1], writes E[p&1]
+    uint32_t spos;
+    int su;
+    if (pass == 0) {
+        spos = a.D[c0 + f + i];
+        su = 0;
+    } else {
+        if (i == 0) {                                             // exact since pass 0
+            a.Epos[po][g] = a.Epos[pi][g];
+            a.Eu[po][g] = a.Eu[pi][g];
+            return;
+        }
+        spos = a.Epos[pi][g - 1];
+        su = a.Eu[pi][g - 1];
+        if (spos == a.S[g] && su == a.Su[g]) {                    // same start: same decode
+            a.Epos[po][g] = a.Epos[pi][g];
+            a.Eu[po][g] = a.Eu[pi][g];
+            return;
+        }
+    }
+    Reader b;
+    b.seek(a.bytes + a.seg_off[f], a.seg_len[f], i * (uint32_t)a.chunk_bytes, a.D[c0 + f + i], spos);
+    int u = su;
+    uint32_t nb = 0;
+    int dcs[3] = {0, 0, 0}, pred[3] = {0, 0, 0};
+    bool bad = false;
+    decode_blocks<0>(a, T, b, u, a.D[c0 + f + i + 1], nb, dcs, 0, pred, nullptr, nullptr, bad);
+    a.S[g] = spos;
+    a.Su[g] = (uint8_t)su;
+    a.nblk[g] = nb;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) a.dcs[(size_t)g * 3 + c] = dcs[c];
+    if (pass > 0 && (b.pos != a.Epos[pi][g] || (uint8_t)u != a.Eu[pi][g])) atomicOr(a.flags, 1);
+    a.Epos[po][g] = b.pos;
+    a.Eu[po][g] = (uint8_t)u;
+}
+
+// per frame: exclusive scans of block counts and DC sums over its chunks
+__global__ __launch_bounds__(WG) void jdec_scan_kernel(JdecArgs a) {
+    const int f = blockIdx.x, t = threadIdx.x;
+    const uint32_t c0 = a.chunk0[f], nch = a.chunk0[f + 1] - c0;
+    __shared__ int s[4][WG];
+    int carry[4] = {0, 0, 0, 0};
+    for (uint32_t g0 = 0; g0 < nch; g0 += WG) {
+        const uint32_t i = g0 + t;
+        int v[4] = {0, 0, 0, 0};
+        if (i < nch) {
+            v[0] = (int)a.nblk[c0 + i];
+            for (int c = 0; c < 3; ++c) v[1 + c] = a.dcs[(size_t)(c0 + i) * 3 + c];
+        }
+        for (int q = 0; q < 4; ++q) s[q][t] = v[q];
+        __syncthreads();
+        for (int o = 1; o < WG; o <<= 1) {
+            int x[4];
+            for (int q = 0; q < 4; ++q) x[q] = t >= o ? s[q][t - o] : 0;
+            __syncthreads();
+            for (int q = 0; q < 4; ++q) s[q][t] += x[q];
+            __syncthreads();
+        }
+        if (i < nch) {
+            a.base[c0 + i] = (uint32_t)(carry[0] + s[0][t] - v[0]);
+            for (int c = 0; c < 3; ++c) a.dcoff[(size_t)(c0 + i) * 3 + c] = carry[1 + c] + s[1 + c][t] - v[1 + c];
+        }
+        for (int q = 0; q < 4; ++q) carry[q] += s[q][WG - 1];
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(WG) void jdec_write_kernel(JdecArgs a, const int* wg_frame, const uint32_t* wg_chunk) {
+    __shared__ JLds T;
+    __shared__ __attribute__((aligned(16))) int16_t lb[WG][64];
+    const int f = wg_frame[blockIdx.x];
+    load_tables(a, f, &T);
+    const uint32_t c0 = a.chunk0[f], nch = a.chunk0[f + 1] - c0;
+    const uint32_t i = wg_chunk[blockIdx.x] + threadIdx.x;
+    if (i >= nch) return;
+    const uint32_t g = c0 + i;
+    Reader b;
+    b.seek(a.bytes + a.seg_off[f], a.seg_len[f], i * (uint32_t)a.chunk_bytes, a.D[c0 + f + i], a.S[g]);
+    int u = a.Su[g];
+    uint32_t nb = 0;
+    int dcs[3] = {0, 0, 0};
+    int pred[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) pred[c] = a.dcoff[(size_t)g * 3 + c];
+    bool bad = false;
+    decode_blocks<1>(a, T, b, u, a.D[c0 + f + i + 1], nb, dcs, a.base[g], pred, lb[threadIdx.x],
+                     a.dense + (size_t)f * a.blocks_per_image * 64, bad);
+    if (bad) atomicOr(a.flags + 1, 1);
+    if (i + 1 == nch && a.base[g] + nb < (uint32_t)a.total_blocks) atomicOr(a.flags + 1, 2);   // too few blocks
+}
+
+}  // namespace
+
+// one stage of the device entropy decode (jpeg_host.cpp drives the sequence)
+hipError_t vd_launch_jdec(const JdecLaunch& L, hipStream_t s) {
+    JdecArgs a{};
+    a.bytes = L.bytes; a.seg_off = L.seg_off; a.seg_len = L.seg_len; a.chunk0 = L.chunk0; a.tab_of = L.tab_of;
+    a.tabs = (const JLds*)L.tabs; a.n = L.n; a.chunk_bytes = L.chunk_bytes; a.bpm = L.bpm;
+    for (int k = 0; k < 6; ++k) { a.ucomp[k] = L.ucomp[k]; a.udc[k] = L.udc[k]; a.uac[k] = L.uac[k]; a.ubx[k] = L.ubx[k]; a.uby[k] = L.uby[k]; }
+    a.mcux = L.mcux; a.total_blocks = L.total_blocks;
+    for (int c = 0; c < 3; ++c) { a.cblk[c] = L.cblk[c]; a.bw[c] = L.bw[c]; a.hs[c] = L.hs[c]; a.vs[c] = L.vs[c]; }
+    a.blocks_per_image = L.blocks_per_image;
+    a.D = L.D; a.stuffed = nullptr; a.S = L.S; a.Su = L.Su;
+    a.Epos[0] = L.Epos[0]; a.Epos[1] = L.Epos[1]; a.Eu[0] = L.Eu[0]; a.Eu[1] = L.Eu[1];
+    a.nblk = L.nblk; a.dcs = L.dcs; a.base = L.base; a.dcoff = L.dcoff; a.dense = L.dense; a.flags = L.flags;
+    if (L.stage == 0) {
+        hipLaunchKernelGGL(jdec_prep_kernel, dim3(a.n), dim3(WG), 0, s, a);
+    } else if (L.stage == 1) {
+        hipLaunchKernelGGL(jdec_sync_kernel, dim3(L.nwg), dim3(WG), 0, s, a, L.wg_frame, L.wg_chunk, L.pass);
+    } else if (L.stage == 2) {
+        hipLaunchKernelGGL(jdec_scan_kernel, dim3(a.n), dim3(WG), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(jdec_write_kernel, dim3(L.nwg), dim3(WG), 0, s, a, L.wg_frame, L.wg_chunk);
+    }
+    return hipGetLastError();
+}

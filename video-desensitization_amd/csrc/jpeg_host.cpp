@@ -370,6 +370,185 @@ bool same_layout(const Info& a, const Info& b) {
     return true;
 }
 
+// ---- device entropy decode (jpeg_dec.hip) ------------------------------------
+// Host part: table sets (deduplicated over the batch), scan segments copied 16-B
+// aligned into one pinned buffer with the metadata, one H2D, then prep -> sync
+// passes (until no chunk's exit state changes) -> scan -> write. Returns with
+// *used = false (and nothing launched that matters) when the batch is not eligible
+// (restart markers, table ids > 1, > 6 blocks per MCU) or the device flags a
+// corrupt stream / no convergence: the caller then runs the host entropy stage,
+// whose results and error messages are the reference behaviour.
+void fill_tables(const Info& j, JLds& t) {
+    memset(&t, 0, sizeof t);
+    const Huff* hs[4] = {&j.dc[0], &j.dc[1], &j.ac[0], &j.ac[1]};
+    for (int q = 0; q < 4; ++q) {
+        const Huff& h = *hs[q];
+        if (!h.present) continue;
+        for (int i = 0; i < (1 << kLook); ++i) t.look[q][i] = (uint16_t)((h.look_len[i] << 8) | h.look_sym[i]);
+        if (q >= 2)
+            for (int i = 0; i < (1 << kLook); ++i)
+                t.fast[q - 2][i] = (uint32_t)h.fa_len[i] | ((uint32_t)h.fa_run[i] << 8) | ((uint32_t)(uint16_t)h.fa_val[i] << 16);
+        for (int l = 0; l < 18; ++l) t.maxcode[q][l] = h.maxcode[l];
+        for (int l = 0; l < 17; ++l) t.valoff[q][l] = h.valoff[l];
+        memcpy(t.vals[q], h.vals, 256);
+    }
+}
+
+int device_entropy(Ctx* ctx, const std::vector<Info>& info, int n, JpegArgs& a, size_t nblk_img, int nthreads,
+                   bool* used) {
+    *used = false;
+    const Info& j0 = info[0];
+    if (!ctx->tune.jdec_gpu) return VD_OK;
+    int bpm = 0;
+    for (int c = 0; c < j0.nc; ++c) bpm += j0.c[c].hs * j0.c[c].vs;
+    if (bpm > 6) return VD_OK;
+    for (int f = 0; f < n; ++f) {
+        if (info[f].restart) return VD_OK;
+        for (int c = 0; c < j0.nc; ++c)
+            if (info[f].c[c].td > 1 || info[f].c[c].ta > 1 || !info[f].dc[info[f].c[c].td].present ||
+                !info[f].ac[info[f].c[c].ta].present)
+                return VD_OK;
+        if (info[f].scan_len >= (1u << 28)) return VD_OK;
+    }
+    JdecLaunch L{};
+    L.n = n; L.bpm = bpm;
+    {
+        int u = 0;
+        for (int c = 0; c < j0.nc; ++c)
+            for (int by = 0; by < j0.c[c].vs; ++by)
+                for (int bx = 0; bx < j0.c[c].hs; ++bx, ++u) {
+                    L.ucomp[u] = c; L.udc[u] = j0.c[c].td; L.uac[u] = j0.c[c].ta; L.ubx[u] = bx; L.uby[u] = by;
+                }
+    }
+    L.mcux = j0.mcux;
+    L.total_blocks = j0.mcux * j0.mcuy * bpm;
+    for (int c = 0; c < 3; ++c) { L.cblk[c] = a.cblk[c]; L.bw[c] = a.bw[c]; L.hs[c] = a.hs[c]; L.vs[c] = a.vs[c]; }
+    L.blocks_per_image = (int)nblk_img;
+    // per-frame table sets (the component -> table ids are the batch's: same layout)
+    for (int f = 1; f < n; ++f)
+        for (int c = 0; c < j0.nc; ++c)
+            if (info[f].c[c].td != j0.c[c].td || info[f].c[c].ta != j0.c[c].ta) return VD_OK;
+    std::vector<JLds> sets;
+    std::vector<uint8_t> tab_of(n);
+    JLds tmp;
+    for (int f = 0; f < n; ++f) {
+        fill_tables(info[f], tmp);
+        size_t k = 0;
+        while (k < sets.size() && memcmp(&sets[k], &tmp, sizeof tmp)) ++k;
+        if (k == sets.size()) {
+            if (sets.size() >= 255) return VD_OK;
+            sets.push_back(tmp);
+        }
+        tab_of[f] = (uint8_t)k;
+    }
+    const int C = std::max(16, ctx->tune.jdec_chunk / 16 * 16);
+    L.chunk_bytes = C;
+    std::vector<uint32_t> seg_off(n), seg_len(n), chunk0(n + 1);
+    std::vector<int> wg_frame;
+    std::vector<uint32_t> wg_chunk;
+    size_t bytes_total = 0;
+    uint32_t nc_total = 0;
+    for (int f = 0; f < n; ++f) {
+        seg_off[f] = (uint32_t)bytes_total;
+        seg_len[f] = (uint32_t)info[f].scan_len;
+        bytes_total += (info[f].scan_len + 16 + 15) / 16 * 16;             // 16-B windows read past the end
+        chunk0[f] = nc_total;
+        const uint32_t nch = std::max<uint32_t>(1, (uint32_t)((info[f].scan_len + C - 1) / C));
+        for (uint32_t c = 0; c < nch; c += 256) { wg_frame.push_back(f); wg_chunk.push_back(c); }
+        nc_total += nch;
+    }
+    chunk0[n] = nc_total;
+    if (bytes_total >= (1ull << 32)) return VD_OK;
+    const int nwg = (int)wg_frame.size();
+    // pinned image: metadata | quant | tables | segments
+    auto al = [](size_t x) { return (x + 255) / 256 * 256; };
+    const size_t o_soff = 0, o_slen = al(o_soff + n * 4), o_c0 = al(o_slen + n * 4), o_tab = al(o_c0 + (n + 1) * 4);
+    const size_t o_wgf = al(o_tab + n), o_wgc = al(o_wgf + nwg * 4), o_q = al(o_wgc + nwg * 4);
+    const size_t o_tabs = al(o_q + (size_t)n * 3 * 64 * 2), o_bytes = al(o_tabs + sets.size() * sizeof(JLds));
+    const size_t himg = o_bytes + bytes_total;
+    int rc;
+    VD_CHECK_HIP(hipEventSynchronize(ctx->jpeg_ev));                     // the previous H2D from it is done
+    if ((rc = ctx->ensure_pinned(&ctx->jdec_host, &ctx->jdec_host_bytes, himg))) return rc;
+    if ((rc = ctx->ensure_staging(&ctx->jdec_dev, &ctx->jdec_dev_bytes, himg))) return rc;
+    char* hp = (char*)ctx->jdec_host;
+    memcpy(hp + o_soff, seg_off.data(), n * 4);
+    memcpy(hp + o_slen, seg_len.data(), n * 4);
+    memcpy(hp + o_c0, chunk0.data(), (n + 1) * 4);
+    memcpy(hp + o_tab, tab_of.data(), n);
+    memcpy(hp + o_wgf, wg_frame.data(), nwg * 4);
+    memcpy(hp + o_wgc, wg_chunk.data(), nwg * 4);
+    memcpy(hp + o_tabs, sets.data(), sets.size() * sizeof(JLds));
+    uint16_t* hq = (uint16_t*)(hp + o_q);
+    std::atomic<int> next{0};
+    auto copier = [&]() {
+        for (int f; (f = next.fetch_add(1)) < n;) {
+            char* dst = hp + o_bytes + seg_off[f];
+            memcpy(dst, info[f].scan, info[f].scan_len);
+            memset(dst + info[f].scan_len, 0, (info[f].scan_len + 31) / 16 * 16 - info[f].scan_len);
+            for (int c = 0; c < j0.nc; ++c) memcpy(hq + ((size_t)f * 3 + c) * 64, info[f].q[info[f].c[c].tq], 128);
+        }
+    };
+    {
+        std::vector<std::thread> pool;
+        for (int t = 1; t < nthreads; ++t) pool.emplace_back(copier);
+        copier();
+        for (auto& t : pool) t.join();
+    }
+    VD_CHECK_HIP(hipMemcpyAsync(ctx->jdec_dev, hp, himg, hipMemcpyHostToDevice, ctx->stream));
+    VD_CHECK_HIP(hipEventRecord(ctx->jpeg_ev, ctx->stream));
+    // device work area: per chunk state + the dense blocks
+    const size_t NC = nc_total;
+    const size_t w_D = 0, w_S = al(w_D + (NC + n) * 4), w_Su = al(w_S + NC * 4), w_E0 = al(w_Su + NC);
+    const size_t w_E1 = al(w_E0 + NC * 4), w_U0 = al(w_E1 + NC * 4), w_U1 = al(w_U0 + NC), w_nb = al(w_U1 + NC);
+    const size_t w_dcs = al(w_nb + NC * 4), w_base = al(w_dcs + NC * 12), w_dco = al(w_base + NC * 4);
+    const size_t w_fl = al(w_dco + NC * 12), w_dense = al(w_fl + 16);
+    const size_t wbytes = w_dense + (size_t)n * nblk_img * 128;
+    if ((rc = ctx->ensure_staging(&ctx->jdec_work, &ctx->jdec_work_bytes, wbytes))) return rc;
+    char* dp = (char*)ctx->jdec_dev;
+    char* wp = (char*)ctx->jdec_work;
+    L.seg_off = (const uint32_t*)(dp + o_soff); L.seg_len = (const uint32_t*)(dp + o_slen);
+    L.chunk0 = (const uint32_t*)(dp + o_c0); L.tab_of = (const uint8_t*)(dp + o_tab);
+    L.wg_frame = (const int*)(dp + o_wgf); L.wg_chunk = (const uint32_t*)(dp + o_wgc);
+    L.tabs = (const JLds*)(dp + o_tabs); L.bytes = (const uint8_t*)(dp + o_bytes);
+    L.D = (uint32_t*)(wp + w_D); L.S = (uint32_t*)(wp + w_S); L.Su = (uint8_t*)(wp + w_Su);
+    L.Epos[0] = (uint32_t*)(wp + w_E0); L.Epos[1] = (uint32_t*)(wp + w_E1);
+    L.Eu[0] = (uint8_t*)(wp + w_U0); L.Eu[1] = (uint8_t*)(wp + w_U1);
+    L.nblk = (uint32_t*)(wp + w_nb); L.dcs = (int*)(wp + w_dcs); L.base = (uint32_t*)(wp + w_base);
+    L.dcoff = (int*)(wp + w_dco); L.flags = (int*)(wp + w_fl); L.dense = (int16_t*)(wp + w_dense);
+    L.nwg = nwg;
+    hipError_t e;
+    L.stage = 0;
+    if ((e = vd_launch_jdec(L, ctx->stream)) != hipSuccess) return vd_set_error(VD_ERR_HIP, "jdec prep: %s", hipGetErrorString(e));
+    VD_CHECK_HIP(hipMemsetAsync(L.flags, 0, 16, ctx->stream));
+    L.stage = 1; L.pass = 0;
+    if ((e = vd_launch_jdec(L, ctx->stream)) != hipSuccess) return vd_set_error(VD_ERR_HIP, "jdec pass: %s", hipGetErrorString(e));
+    int flag[4] = {1, 0, 0, 0};
+    int pass = 1;
+    for (; pass <= 64; ++pass) {
+        VD_CHECK_HIP(hipMemsetAsync(L.flags, 0, 4, ctx->stream));
+        L.pass = pass;
+        if ((e = vd_launch_jdec(L, ctx->stream)) != hipSuccess) return vd_set_error(VD_ERR_HIP, "jdec pass: %s", hipGetErrorString(e));
+        VD_CHECK_HIP(hipMemcpyAsync(flag, L.flags, 4, hipMemcpyDeviceToHost, ctx->stream));
+        VD_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+        if (flag[0] == 0) break;
+    }
+    ctx->jdec_passes = pass;
+    if (flag[0] != 0) return VD_OK;                                    // no convergence: host decode
+    L.stage = 2;
+    if ((e = vd_launch_jdec(L, ctx->stream)) != hipSuccess) return vd_set_error(VD_ERR_HIP, "jdec scan: %s", hipGetErrorString(e));
+    L.stage = 3;
+    if ((e = vd_launch_jdec(L, ctx->stream)) != hipSuccess) return vd_set_error(VD_ERR_HIP, "jdec write: %s", hipGetErrorString(e));
+    VD_CHECK_HIP(hipMemcpyAsync(flag, L.flags, 8, hipMemcpyDeviceToHost, ctx->stream));
+    VD_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    if (flag[1] != 0) return VD_OK;                                    // corrupt: the host decoder reports it
+    a.dense = L.dense;
+    a.quant = (const uint16_t*)(dp + o_q);
+    a.blk_off = nullptr;
+    a.entries = nullptr;
+    *used = true;
+    return VD_OK;
+}
+
 }  // namespace
 
 extern "C" int vd_jpeg_info(const uint8_t* data, size_t size, int* h, int* w, int* comps) {
@@ -406,6 +585,8 @@ extern "C" int vdt_jpeg_coefficients(const uint8_t* data, size_t size, int16_t* 
     return VD_OK;
 }
 
+static int launch_idct_color(Ctx* ctx, JpegArgs& a, uint8_t* out, int fh, size_t pitch, int where, int n);
+
 extern "C" int vd_jpeg_decode(vd_ctx* hctx, const uint8_t* const* data, const size_t* sizes, int n, uint8_t* out,
                               int fh, int fw, size_t pitch, int where) {
     Ctx* ctx = (Ctx*)hctx;
@@ -414,33 +595,34 @@ extern "C" int vd_jpeg_decode(vd_ctx* hctx, const uint8_t* const* data, const si
     if (hipSetDevice(ctx->device) != hipSuccess) return vd_set_error(VD_ERR_HIP, "hipSetDevice(%d) failed", ctx->device);
     if (!data || !sizes || !out || n <= 0 || n > ctx->cfg.max_batch || fh <= 0 || fw <= 0 || pitch < (size_t)fw * 3)
         return vd_set_error(VD_ERR_ARG, "vd_jpeg_decode: bad arguments");
-    // 1) parse + entropy decode, one image per host thread
+    // 1) parse every frame's headers (and find its entropy-coded segment), host threads
     std::vector<Info> info(n);
     std::vector<Entries> ent(n);
     std::vector<int> rcs(n, VD_OK);
     std::vector<std::string> errs(n);
     std::atomic<int> next{0};
-    auto worker = [&]() {
+    const int nthreads = std::max(1, std::min(n, ctx->jpeg_threads));
+    auto run_threads = [&](auto&& fn) {
+        next = 0;
+        std::vector<std::thread> pool;
+        for (int t = 1; t < nthreads; ++t) pool.emplace_back(fn);
+        fn();
+        for (auto& t : pool) t.join();
+    };
+    run_threads([&]() {
         for (int i; (i = next.fetch_add(1)) < n;) {
             int rc = parse(data[i], sizes[i], info[i]);
             if (!rc && (info[i].h != fh || info[i].w != fw))
                 rc = vd_set_error(VD_ERR_ARG, "jpeg %d is %dx%d, expected %dx%d", i, info[i].w, info[i].h, fw, fh);
-            if (!rc) rc = entropy(info[i], ent[i]);
             rcs[i] = rc;
             if (rc) errs[i] = vd_last_error();
         }
-    };
-    const int nthreads = std::max(1, std::min(n, ctx->jpeg_threads));
-    std::vector<std::thread> pool;
-    for (int t = 1; t < nthreads; ++t) pool.emplace_back(worker);
-    worker();
-    for (auto& t : pool) t.join();
+    });
     for (int i = 0; i < n; ++i)
         if (rcs[i]) return vd_set_error(rcs[i], "jpeg %d: %s", i, errs[i].c_str());
     for (int i = 1; i < n; ++i)
         if (!same_layout(info[0], info[i]))
             return vd_set_error(VD_ERR_ARG, "jpeg %d: component layout differs from jpeg 0 (one call decodes one stream)", i);
-    // 2) pack: per image [blocks] offsets (global), entries, quant tables
     const Info& j0 = info[0];
     JpegArgs a{};
     a.n = n; a.h = fh; a.w = fw; a.nc = j0.nc; a.hmax = j0.hmax; a.vmax = j0.vmax;
@@ -452,12 +634,31 @@ extern "C" int vd_jpeg_decode(vd_ctx* hctx, const uint8_t* const* data, const si
         nblk_img += (size_t)a.bw[c] * a.bh[c];
     }
     a.blocks_per_image = (int)nblk_img;
+    int rc;
+    // 2a) entropy decode on the device (jpeg_dec.hip) when the batch allows it
+    bool dev_done = false;
+    if ((rc = device_entropy(ctx, info, n, a, nblk_img, nthreads, &dev_done))) return rc;
+    if (dev_done) {
+        if ((rc = ctx->ensure_staging(&ctx->jpeg_planes, &ctx->jpeg_planes_bytes, nblk_img * n * 64 + 64))) return rc;
+        a.planes = (uint8_t*)ctx->jpeg_planes;
+        return launch_idct_color(ctx, a, out, fh, pitch, where, n);
+    }
+    // 2b) entropy decode on host threads into sparse coefficient lists
+    run_threads([&]() {
+        for (int i; (i = next.fetch_add(1)) < n;) {
+            const int rc = entropy(info[i], ent[i]);
+            rcs[i] = rc;
+            if (rc) errs[i] = vd_last_error();
+        }
+    });
+    for (int i = 0; i < n; ++i)
+        if (rcs[i]) return vd_set_error(rcs[i], "jpeg %d: %s", i, errs[i].c_str());
+    // pack: per image [blocks] offsets (global), entries, quant tables
     size_t tot_ent = 0;
     for (int i = 0; i < n; ++i) tot_ent += ent[i].n;
     const size_t nblk = nblk_img * n;
     const size_t off_bytes = (nblk + 1) * 4, q_bytes = (size_t)n * 3 * 64 * 2, ent_bytes = std::max<size_t>(tot_ent, 1) * 4;
     const size_t need = off_bytes + q_bytes + ent_bytes + 64;
-    int rc;
     if ((rc = ctx->ensure_pinned(&ctx->jpeg_host, &ctx->jpeg_host_bytes, need))) return rc;
     if ((rc = ctx->ensure_staging(&ctx->jpeg_dev, &ctx->jpeg_dev_bytes, need))) return rc;
     const size_t plane_bytes = nblk * 64;
@@ -473,6 +674,7 @@ extern "C" int vd_jpeg_decode(vd_ctx* hctx, const uint8_t* const* data, const si
     std::vector<size_t> ebase(n + 1, 0);
     for (int i = 0; i < n; ++i) ebase[i + 1] = ebase[i] + ent[i].n;
     next = 0;
+    std::vector<std::thread> pool;
     auto packer = [&]() {
         for (int i; (i = next.fetch_add(1)) < n;) {
             // regroup MCU order -> block order straight into the pinned buffer
@@ -500,7 +702,12 @@ extern "C" int vd_jpeg_decode(vd_ctx* hctx, const uint8_t* const* data, const si
     a.quant = (const uint16_t*)(dp + off_bytes);
     a.entries = (const uint32_t*)(dp + off_bytes + q_bytes);
     a.planes = (uint8_t*)ctx->jpeg_planes;
-    // 3) device: IDCT into planes, then upsample + color into the frames
+    return launch_idct_color(ctx, a, out, fh, pitch, where, n);
+}
+
+// 3) device: IDCT into planes, then upsample + color into the frames
+static int launch_idct_color(Ctx* ctx, JpegArgs& a, uint8_t* out, int fh, size_t pitch, int where, int n) {
+    int rc;
     uint8_t* dout = out;
     if (where == VD_HOST) {
         if ((rc = ctx->ensure_staging(&ctx->stage_in, &ctx->stage_in_bytes, (size_t)n * fh * pitch))) return rc;

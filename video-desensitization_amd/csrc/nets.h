@@ -182,6 +182,11 @@ struct Ctx {
     void* jpeg_dev = nullptr; size_t jpeg_dev_bytes = 0;
     void* jpeg_planes = nullptr; size_t jpeg_planes_bytes = 0;
     hipEvent_t jpeg_ev = nullptr;                 // last H2D out of jpeg_host / jenc_host
+    // device entropy decode (jpeg_dec.hip): pinned segments + tables + metadata, device copy, dense blocks
+    void* jdec_host = nullptr; size_t jdec_host_bytes = 0;
+    void* jdec_dev = nullptr; size_t jdec_dev_bytes = 0;
+    void* jdec_work = nullptr; size_t jdec_work_bytes = 0;
+    int jdec_passes = 0;                          // sync passes of the last device decode (test hook)
     // JPEG frame encode (jpeg_enc.cpp): device coefficients + tables, pinned host copy
     void* jenc_dev = nullptr; size_t jenc_dev_bytes = 0;
     void* jhuf_dev = nullptr; size_t jhuf_dev_bytes = 0;   // device entropy stage buffers

@@ -853,6 +853,9 @@ int vd_destroy(vd_ctx* h) {
     if (ctx->jpeg_dev) hipFree(ctx->jpeg_dev);
     if (ctx->jpeg_planes) hipFree(ctx->jpeg_planes);
     if (ctx->jpeg_host) hipHostFree(ctx->jpeg_host);
+    if (ctx->jdec_host) hipHostFree(ctx->jdec_host);
+    if (ctx->jdec_dev) hipFree(ctx->jdec_dev);
+    if (ctx->jdec_work) hipFree(ctx->jdec_work);
     if (ctx->jenc_dev) hipFree(ctx->jenc_dev);
     if (ctx->jhuf_dev) hipFree(ctx->jhuf_dev);
     if (ctx->jseg_host) hipHostFree(ctx->jseg_host);
@@ -903,7 +906,7 @@ int vd_set_option(vd_ctx* h, const char* name, int value) {
         {"x6_small_k", &VdTune::x6_small_k}, {"x6_small_tiles", &VdTune::x6_small_tiles},
         {"x6_stream", &VdTune::x6_stream}, {"x6_small_k2", &VdTune::x6_small_k2}, {"x6_bn256", &VdTune::x6_bn256},
         {"x6_exact", &VdTune::x6_exact}, {"x6_mid", &VdTune::x6_mid}, {"block_fuse32", &VdTune::block_fuse32}, {"x6_mf32", &VdTune::x6_mf32}, {"x6_stream256", &VdTune::x6_stream256}, {"plate_stage", &VdTune::plate_stage},
-        {"jenc_gpu", &VdTune::jenc_gpu},
+        {"jenc_gpu", &VdTune::jenc_gpu}, {"jdec_gpu", &VdTune::jdec_gpu}, {"jdec_chunk", &VdTune::jdec_chunk},
     };
     for (const Opt& o : opts)
         if (strcmp(o.n, name) == 0) {

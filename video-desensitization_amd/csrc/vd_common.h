@@ -37,6 +37,8 @@ struct VdTune {
     int ssh_fuse = 1;         // plan: SSH conv3X3 + conv5X5_1 as one conv
     int plate_s2d = 1;        // plan: YOLO space-to-depth stem input
     int jenc_gpu = 1;         // vd_jpeg_encode: Huffman coding on the device (0: host threads)
+    int jdec_gpu = 1;         // vd_jpeg_decode: entropy decode on the device (0: host threads)
+    int jdec_chunk = 2048;    //   raw scan bytes per decoding thread (tests force small chunks)
     int plate_stage = 3;      // plate branch starts after face stage N (0: with the stem; 1-4: after
                               //   layerN; 5: after the whole face net). After layer3 its HBM-bound
                               //   convs overlap the MFMA-bound late face layers: 30.8 -> 30.0 ms/step
@@ -232,6 +234,8 @@ struct JpegArgs {
     const uint16_t* quant;                      // [n][3][64] natural order
     const uint32_t* entries;                    // natural index << 16 | int16 quantized value
     uint8_t* planes;                            // [n * blocks_per_image][64] decoded samples
+    const int16_t* dense;                       // or (device entropy decode) dense quantized blocks
+                                                // [n * blocks_per_image][64] natural order; entries unused
     uint8_t* out; size_t pitch;                 // RGB frames [n][h][pitch]
 };
 
@@ -299,6 +303,36 @@ __device__ __forceinline__ void amax_lds_flush(const unsigned* s, unsigned* g, i
     for (int f = threadIdx.x; f < nframes; f += blockDim.x)
         if (s[f]) atomicMax(g + f, s[f]);
 }
+
+// Device entropy decode (jpeg_dec.hip). JLds: one Huffman table set as the kernels
+// hold it in LDS (jpeg_host.cpp build_huff tables): 11-bit lookahead (len << 8 | sym)
+// for dc0 dc1 ac0 ac1, the AC fast path (len | run << 8 | (u16)value << 16; run 64 =
+// EOB, 16 = ZRL), and the canonical slow path.
+struct JLds {
+    uint16_t look[4][2048];
+    uint32_t fast[2][2048];
+    int32_t maxcode[4][18];
+    int32_t valoff[4][17];
+    uint8_t vals[4][256];
+};
+struct JdecLaunch {
+    int stage;                     // 0 prep, 1 sync pass, 2 scan, 3 write
+    int pass, nwg;
+    const int* wg_frame; const uint32_t* wg_chunk;   // workgroup -> (frame, first chunk)
+    const uint8_t* bytes; const uint32_t* seg_off; const uint32_t* seg_len; const uint32_t* chunk0;
+    const uint8_t* tab_of; const JLds* tabs;
+    int n, chunk_bytes, bpm;
+    int ucomp[6], udc[6], uac[6], ubx[6], uby[6];
+    int mcux, total_blocks;
+    int cblk[3], bw[3], hs[3], vs[3];
+    int blocks_per_image;
+    uint32_t* D; uint32_t* S; uint8_t* Su;
+    uint32_t* Epos[2]; uint8_t* Eu[2];
+    uint32_t* nblk; int* dcs; uint32_t* base; int* dcoff;
+    int16_t* dense;
+    int* flags;
+};
+hipError_t vd_launch_jdec(const JdecLaunch& L, hipStream_t s);
 
 // One batch of RGB frames -> quantized coefficient blocks (jpeg_enc.hip -> jpeg_enc.cpp).
 struct JpegEncArgs {
