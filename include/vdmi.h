@@ -230,6 +230,9 @@ int vdt_bottleneck(vd_ctx* ctx, const float* x, int n, int h, int w, int cin,
 int vdt_jpeg_coefficients(const uint8_t* data, size_t size, int16_t* out, size_t cap_blocks, int* nblocks);
 int vdt_plate_raw(vd_ctx* ctx, const uint8_t* frames, int n, int h, int w, size_t pitch,
                   int where, float* out, int* anchors);
+/* The last vd_jpeg_decode's device entropy stage: synchronisation passes run (pass 0
+ * included; 0 when the host entropy stage ran). */
+int vdt_jdec_stats(vd_ctx* ctx, int* passes);
 
 #ifdef __cplusplus
 }

@@ -354,3 +354,23 @@ def test_heads_fp32_fused_layer1_matches_unfused(gpu):
     assert sum(len(x) for x in boxes[0]) > 0
     for a, b in zip(boxes[1], boxes[0]):
         np.testing.assert_array_equal(a, b)
+
+
+def test_heads_fp32_tail_split_bit_identical(gpu):
+    """fp32 plan: the big-tile layers' last partial round runs as a second launch of a
+    narrower tile (conv_x6.hip launch_x6_big, option x6_tail). The split is along N
+    only, so every output keeps its K order and MFMA form: heads bit-identical to the
+    unsplit launches. x6_slots=8 makes every big-tile layer of a 3-frame batch split."""
+    import vdmi
+    fr = _frames(3, 1080, 1920, seed=31)
+    heads = {}
+    for tail in (0, 1, 2):
+        ctx = vdmi.Context(precision="fp32", max_batch=3, options={"x6_tail": tail, "x6_slots": 8})
+        try:
+            ctx.load_weights(0, face_weights("default"))
+            heads[tail] = ctx.forward_heads(fr)
+        finally:
+            ctx.close()
+    for t in (1, 2):
+        for a, b in zip(heads[t], heads[0]):
+            np.testing.assert_array_equal(a, b)

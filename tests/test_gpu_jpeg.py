@@ -42,16 +42,19 @@ def jctx_host_dec(gpu):
     ctx.close()
 
 
+@pytest.mark.parametrize("sync", [128, 0, 2])
 @pytest.mark.parametrize("chunk", [16, 48, 256])
 @pytest.mark.parametrize("case", CASES)
-def test_device_entropy_small_chunks_matches_pillow(gpu, case, chunk):
+def test_device_entropy_small_chunks_matches_pillow(gpu, case, chunk, sync):
     """jpeg_dec.hip with tiny chunks (option jdec_chunk): every frame is cut into many
     speculatively decoded chunks, so block boundaries, the block-in-MCU phase and DC
-    predictors must all be recovered by the synchronisation passes; the result is
-    still libjpeg-turbo's decode bit for bit."""
+    predictors must all be recovered by the resynchronisation passes -- with the early
+    stop at the previous trajectory (jdec_sync states recorded per chunk; 2: lists
+    shorter than most chunks) or without it (0); the result is still libjpeg-turbo's
+    decode bit for bit."""
     import vdmi
     h, w, q, sub = case[:4]
-    ctx = vdmi.Context(precision="fp32", max_batch=4, options={"jdec_chunk": chunk})
+    ctx = vdmi.Context(precision="fp32", max_batch=4, options={"jdec_chunk": chunk, "jdec_sync": sync})
     try:
         ds = [make_jpeg(h, w, q, sub, seed=s) for s in range(3)]
         got = ctx.jpeg_decode(ds)
@@ -76,6 +79,7 @@ def test_device_entropy_1080p_equals_host_threads(jctx, jctx_host_dec, noise):
         Image.fromarray(f).save(b, "JPEG", quality=95)
         jp.append(b.getvalue())
     dev = jctx.jpeg_decode(jp)
+    assert jctx.jdec_passes() >= 2, "the device entropy stage ran"
     host = jctx_host_dec.jpeg_decode(jp)
     np.testing.assert_array_equal(dev, host)
     np.testing.assert_array_equal(dev[0], pillow_rgb(jp[0]))

@@ -201,7 +201,7 @@ __global__ __launch_bounds__(NT, 2) void conv_x6_kernel(ConvArgs a) {
     const int q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
     const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
     const int tn = wg % a.ntiles_n, tm = wg / a.ntiles_n;
-    const int m0 = tm * BM, n0 = tn * BN;
+    const int m0 = a.mbase + tm * BM, n0 = tn * BN;
 
     // ---- A staging: thread = (row, k-pair) items; item i: row = (tid >> 2) + AROWS i, pair = tid & 3 (k 8p..8p+7)
     const int apair = tid & 3, arow = tid >> 2;
@@ -918,8 +918,9 @@ bool vd_conv_x6_ok(const ConvArgs& a) {
            xbytes < 2147483647.0;
 }
 
+// rows [mbase, M) of the conv (mbase a multiple of the caller's tile rows)
 template <int BM, int BN, int NT, int NST, int TERMS, int MF = 16>
-static hipError_t launch_x6(const ConvArgs& a0, hipStream_t s) {
+static hipError_t launch_x6(const ConvArgs& a0, hipStream_t s, int mbase = 0, int mtiles = -1) {
     using S = X6Shape<BM, BN, NT, NST, TERMS, MF>;
     static const bool attr = [] {
         (void)hipFuncSetAttribute((const void*)conv_x6_kernel<BM, BN, NT, NST, TERMS, MF>,
@@ -930,10 +931,47 @@ static hipError_t launch_x6(const ConvArgs& a0, hipStream_t s) {
     ConvArgs a = a0;
     a.w = a.wx3;                                   // the kernel reads the split planes
     a.ntiles_n = (a.cout + BN - 1) / BN;
-    const int mt = (a.M + BM - 1) / BM;
+    a.mbase = mbase;
+    const int mt = mtiles >= 0 ? mtiles : (a.M - mbase + BM - 1) / BM;
     const int lds = S::LDS + (a.ymax ? 4 * a.B : 0);
     hipLaunchKernelGGL((conv_x6_kernel<BM, BN, NT, NST, TERMS, MF>), dim3(mt * a.ntiles_n), dim3(NT), lds, s, a);
     return hipGetLastError();
+}
+
+static int device_cus() {
+    static const int cus = [] {
+        int dev = 0, n = 256;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        return std::max(1, n);
+    }();
+    return cus;
+}
+
+// The 256 x BN two-stage tile runs one workgroup per CU, so a grid of R full rounds
+// plus a partial one leaves most CUs idle during the last round (400 tiles of layer3:
+// 1.56 rounds on 256 CUs take 2). Tail split: the whole rounds as usual, then the
+// remaining rows in one more launch of a narrower tile (BN / 2 or BN / 4 columns),
+// 2-4x as many workgroups, each a fraction of the time. Splitting N (never K) leaves
+// every output's sum in the same K order on the same MFMA form, so the result is
+// bit-identical to the unsplit launch.
+template <int BN, int TERMS, int MF = 16>
+static hipError_t launch_x6_big(const ConvArgs& a, hipStream_t s) {
+    const int tail = a.tune ? a.tune->x6_tail : 0;
+    const int nt = (a.cout + BN - 1) / BN, mt = (a.M + 255) / 256;
+    const int slots = a.tune && a.tune->x6_slots > 0 ? a.tune->x6_slots : device_cus();
+    const long total = (long)mt * nt;
+    if (TERMS != 2 || MF != 16 || !tail || total <= slots || total % slots == 0 || slots % nt) {
+        return launch_x6<256, BN, 512, 2, TERMS, MF>(a, s);
+    }
+    const int mt_main = (int)(total / slots) * (slots / nt);
+    if (mt_main <= 0 || mt_main >= mt) return launch_x6<256, BN, 512, 2, TERMS, MF>(a, s);
+    hipError_t e = launch_x6<256, BN, 512, 2, TERMS, MF>(a, s, 0, mt_main);
+    if (e != hipSuccess) return e;
+    const int mb = mt_main * 256;
+    constexpr int BN1 = BN == 192 ? 64 : BN / 2, BN2 = BN == 192 ? 64 : BN / 4;
+    if (tail == 1 || BN2 < 32) return launch_x6<256, BN1, 512, 2, TERMS, MF>(a, s, mb);
+    return launch_x6<256, BN2, 512, 2, TERMS, MF>(a, s, mb);
 }
 
 // N tile follows Cout (weights are packed with Npad a multiple of 128, so every
@@ -1005,16 +1043,16 @@ static hipError_t launch_terms(const ConvArgs& a0, hipStream_t s) {
         const long t256 = (long)((a.M + 255) / 256) * (a.cout / 256);
         if (a.tune && a.tune->x6_bn256 && a.cout % 256 == 0 && t256 >= 192) {
             if (a.tune->x6_mf32) return launch_x6<256, 256, 512, 2, TERMS, 32>(a, s);
-            return launch_x6<256, 256, 512, 2, TERMS>(a, s);
+            return launch_x6_big<256, TERMS>(a, s);
         }
         // Cout 192 (the fused SSH conv5X5_1 + conv3X3): one 192-wide N tile instead of two
         // 128-wide ones with a quarter of the MFMAs on padding rows (level 0 1716 -> 1264 us,
         // level 1 526 -> 396; not for level 2's 100 tiles: 137 -> 178)
         if (a.tune && a.tune->x6_bn256 && a.cout == 192 && (a.M + 255) / 256 >= 192)
-            return launch_x6<256, 192, 512, 2, TERMS>(a, s);
+            return launch_x6_big<192, TERMS>(a, s);
         if (a.tune && a.tune->x6_mf32) return launch_x6<256, 128, 512, 2, TERMS, 32>(a, s);
     }
-    return launch_x6<256, 128, 512, 2, TERMS>(a, s);
+    return launch_x6_big<128, TERMS>(a, s);
 }
 
 // fp16 pairs: bottleneck conv3 (1x1, K 64 / 128, ReLU) + downsample (1x1, K 64 / 256,

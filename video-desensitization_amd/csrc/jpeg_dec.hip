@@ -32,6 +32,15 @@
 //                      order, component-plane block order) through a per-thread LDS
 //                      block; an invalid code or a run past a block here is a
 //                      corrupt stream (the frame is rejected, as the host decoder).
+// Early stop (option jdec_sync = R > 0): every decode records the first R block-
+// boundary states of its trajectory (position, phase, DC sums so far), and a pass-p
+// decode that reaches a state of the chunk's previous trajectory stops there: a state
+// determines everything after it, so the rest of the decode, its exit state, block
+// count and DC sums are the previous ones (counts and sums adjusted by the recorded
+// prefix), and the new trajectory's list is the new prefix plus the old suffix. A
+// resynchronisation pass then costs the distance to the meeting point rather than a
+// whole chunk (noise frames at q95 need 50-200 blocks, 1-5 chunks, to converge from a
+// wrong start, so several passes run; real frames a few blocks).
 // Tables (jpeg_host.cpp build_huff, per distinct DHT set of the batch): an 11-bit
 // lookahead for every table, libjpeg-turbo's AC fast path (code + extra bits in one
 // lookup), and the canonical maxcode / valoff / vals slow path for longer codes.
@@ -48,7 +57,16 @@ __constant__ int kZig[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18,
 
 
 // data-bit reader over raw scan bytes: 0xFF 0x00 -> 0xFF, a marker or the end of the
-// segment feeds zeros (jdhuff.c fill_bit_buffer), 16-B windows of global memory
+// segment feeds zeros (jdhuff.c fill_bit_buffer). Each lane holds 64 raw bytes of
+// its stream in registers ([wb, wb + 64), wb 16-B aligned). Refills are wave-wide:
+// refill() runs at the start of every symbol on all active lanes, and when any of
+// them has fewer than kLow bytes left, all of them reload 64 bytes from their read
+// position -- one memory latency per refill for the whole wave instead of one per
+// lane and window (lanes cross their windows at unrelated times, and a wave waits
+// for every load any lane issues). A symbol consumes at most one fill: 8 data bytes,
+// 16 raw bytes with stuffing, so kLow = 24 keeps every read inside the buffer.
+constexpr uint32_t kLow = 24;
+
 struct Reader {
     const uint8_t* d;
     uint32_t n;                // raw bytes of the segment
@@ -56,23 +74,53 @@ struct Reader {
     uint64_t acc;              // left-aligned bit buffer
     int nb;
     bool end;
-    uint32_t wbase;
-    uint4 wv;
     uint32_t pos;              // data-bit position of acc's top bit
+    uint32_t wb;               // raw byte of w[0]
+    uint32_t w[16];
 
-    __device__ __forceinline__ uint32_t byte_at(uint32_t i) {
-        if (i >= n) return 0x100u;                              // past the segment
-        const uint32_t b = i & ~15u;
-        if (b != wbase) {
-            wbase = b;
-            wv = *(const uint4*)(d + b);
-        }
-        const uint32_t q = (i >> 2) & 3u;
-        const uint32_t w = q == 0 ? wv.x : (q == 1 ? wv.y : (q == 2 ? wv.z : wv.w));
-        return (w >> ((i & 3u) * 8u)) & 0xFFu;
+    __device__ __forceinline__ void load(uint32_t base) {
+        wb = base;
+        const uint4* src = (const uint4*)(d + base);
+        const uint4 a0 = src[0], a1 = src[1], a2 = src[2], a3 = src[3];
+        w[0] = a0.x; w[1] = a0.y; w[2] = a0.z; w[3] = a0.w;
+        w[4] = a1.x; w[5] = a1.y; w[6] = a1.z; w[7] = a1.w;
+        w[8] = a2.x; w[9] = a2.y; w[10] = a2.z; w[11] = a2.w;
+        w[12] = a3.x; w[13] = a3.y; w[14] = a3.z; w[15] = a3.w;
     }
-    __device__ __forceinline__ void fill() {
-        while (nb <= 56) {
+    // wave-uniform point: every active lane calls it
+    __device__ __forceinline__ void refill() {
+        const bool low = wb + 64u - p < kLow;
+        if (__builtin_amdgcn_ballot_w64(low)) load(p & ~15u);
+    }
+    __device__ __forceinline__ uint32_t word(uint32_t q) const {   // w[q], q in [0, 16), no dynamic indexing
+        const uint32_t b0 = q & 1u, b1 = q & 2u, b2 = q & 4u, b3 = q & 8u;
+        const uint32_t l0 = b0 ? w[1] : w[0], l1 = b0 ? w[3] : w[2], l2 = b0 ? w[5] : w[4], l3 = b0 ? w[7] : w[6];
+        const uint32_t l4 = b0 ? w[9] : w[8], l5 = b0 ? w[11] : w[10], l6 = b0 ? w[13] : w[12], l7 = b0 ? w[15] : w[14];
+        const uint32_t m0 = b1 ? l1 : l0, m1 = b1 ? l3 : l2, m2 = b1 ? l5 : l4, m3 = b1 ? l7 : l6;
+        const uint32_t n0 = b2 ? m1 : m0, n1 = b2 ? m3 : m2;
+        return b3 ? n1 : n0;
+    }
+    __device__ __forceinline__ uint32_t byte_at(uint32_t i) const {
+        if (i >= n) return 0x100u;                              // past the segment
+        const uint32_t o = i - wb;
+        return (word(o >> 2) >> ((o & 3u) * 8u)) & 0xFFu;
+    }
+    // make nb >= 32: four data bytes at once when none is 0xFF (the common case), else
+    // byte by byte with the stuffing / marker rules
+    __device__ __forceinline__ void topup() {
+        if (!end && p + 4u <= n) {
+            const uint32_t o = p - wb;
+            const uint32_t v = __builtin_amdgcn_alignbyte(word((o >> 2) + 1u), word(o >> 2), o & 3u);
+            const uint32_t x = ~v;
+            if (((x - 0x01010101u) & ~x & 0x80808080u) == 0u) {   // no 0xFF byte
+                const uint32_t be = __builtin_bswap32(v);
+                acc |= (uint64_t)be << (32 - nb);
+                nb += 32;
+                p += 4;
+                return;
+            }
+        }
+        while (nb < 32) {
             uint32_t v = 0;
             if (!end) {
                 const uint32_t c = byte_at(p);
@@ -90,18 +138,27 @@ struct Reader {
             nb += 8;
         }
     }
+    // start of a symbol (wave-uniform point): buffer reload if any lane runs low, then
+    // at least 32 bits in acc -- one symbol with its extra bits needs at most 27
+    __device__ __forceinline__ void step() {
+        refill();
+        if (nb < 32) topup();
+    }
     // start at raw byte r (whose first data bit is data position dpos), then skip to `to`
+    // (wave-uniform: every active lane calls it)
     __device__ void seek(const uint8_t* data, uint32_t nbytes, uint32_t r, uint32_t dpos, uint32_t to) {
-        d = data; n = nbytes; p = r; acc = 0; nb = 0; end = false; wbase = 0xFFFFFFFFu; pos = dpos;
-        if (p > 0 && p < n && byte_at(p) == 0u && byte_at(p - 1) == 0xFFu) ++p;   // a stuffed byte: no data
+        d = data; n = nbytes; p = r; acc = 0; nb = 0; end = false; pos = dpos;
+        load(p & ~15u);
+        if (p > 0 && p < n && byte_at(p) == 0u && (p - 1 >= wb ? byte_at(p - 1) : (uint32_t)d[p - 1]) == 0xFFu)
+            ++p;                                                // a stuffed byte: no data
         uint32_t k = to - dpos;
         while (k) {
+            step();
             const int s = k > 32 ? 32 : (int)k;
-            if (nb < s) fill();
             acc <<= s; nb -= s; pos += s; k -= s;
         }
     }
-    __device__ __forceinline__ uint32_t peek(int k) { if (nb < k) fill(); return (uint32_t)(acc >> (64 - k)); }
+    __device__ __forceinline__ uint32_t peek(int k) const { return (uint32_t)(acc >> (64 - k)); }   // after step()
     __device__ __forceinline__ void skip(int k) { acc <<= k; nb -= k; pos += k; }
     __device__ __forceinline__ int get(int k) {
         if (k == 0) return 0;
@@ -157,7 +214,14 @@ struct JdecArgs {
     uint32_t* base;                // first block index (scan)
     int* dcoff;                    // [chunks][3] DC predictors at the chunk start
     int16_t* dense;                // [n][blocks_per_image][64]
-    int* flags;                    // [0] exit states changed, [1] corrupt stream
+    int* flags;                    // [0] exit states changed, [1] corrupt stream, [2] fast sync failed
+    // early stop: the first R states of each chunk's current trajectory, two list buffers
+    int R;                         // states recorded per chunk (0: off)
+    uint32_t* Lpos[2]; uint8_t* Lu[2];   // [chunks][R]
+    int* Ldc[2];                   // [chunks][R][3] DC difference sums before the state
+    uint8_t* Lcnt[2];              // [chunks] states in the list
+    uint8_t* Lsel;                 // [chunks] buffer holding the chunk's current list
+    uint32_t* own;                 // [chunks] blocks the write decodes
 };
 
 // one frame per workgroup: stuffed bytes per chunk -> data-bit positions
@@ -195,19 +259,30 @@ __global__ __launch_bounds__(WG) void jdec_prep_kernel(JdecArgs a) {
     if (t == 0) a.D[c0 + f + nch] = 8u * (nbytes - carry);   // the frame's data bits (chunk end of the last)
 }
 
-// decode whole blocks from (pos, u) until the first block boundary at or past `stop`;
-// MODE 0: counting (speculative: errors end the block), MODE 1: writing (errors flag)
+// decode whole blocks from (pos, u) until the first block boundary at or past `stop`
+// (MODE 0: counting, speculative: errors end the block; MODE 2: the same, recording
+// the first K states at L), or exactly `limit` blocks (MODE 1: writing, errors flag)
 template <int MODE>
 __device__ __forceinline__ void decode_blocks(const JdecArgs& a, const JLds& T, Reader& b, int& u, uint32_t stop,
                                               uint32_t& nblk, int (&dcs)[3], uint32_t blk0, int (&pred)[3],
-                                              int16_t* lblk, int16_t* dense, bool& bad) {
-    while (b.pos < stop) {
+                                              int16_t* lblk, int16_t* dense, bool& bad, uint32_t limit = 0,
+                                              size_t L0 = 0, const uint8_t* zig = nullptr) {
+    while (MODE == 1 ? nblk < limit : b.pos < stop) {
         if constexpr (MODE == 1) {
             if (blk0 + nblk >= (uint32_t)a.total_blocks) return;      // past the frame's last block
 #pragma unroll
             for (int k = 0; k < 64; k += 8) *(uint4*)(lblk + k) = make_uint4(0, 0, 0, 0);
         }
+        if constexpr (MODE == 2) {
+            if (nblk < (uint32_t)a.R) {
+                a.Lpos[0][L0 + nblk] = b.pos;
+                a.Lu[0][L0 + nblk] = (uint8_t)u;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) a.Ldc[0][(L0 + nblk) * 3 + c] = dcs[c];
+            }
+        }
         const int c = a.ucomp[u];
+        b.step();
         int s = decode_sym(b, T, a.udc[u]);
         int diff = 0;
         if (s < 0 || s > 11) {
@@ -224,6 +299,7 @@ __device__ __forceinline__ void decode_blocks(const JdecArgs& a, const JLds& T, 
         }
         const int at = 2 + a.uac[u];
         for (int k = 1; k < 64;) {
+            b.step();
             const uint32_t look = b.peek(kLook);
             const uint32_t f = T.fast[at - 2][look];
             if (f & 0xFFu) {
@@ -233,7 +309,7 @@ __device__ __forceinline__ void decode_blocks(const JdecArgs& a, const JLds& T, 
                 if (run == 16) { k += 16; continue; }                  // ZRL
                 k += run;
                 if (k > 63) { if constexpr (MODE == 1) { bad = true; return; } break; }
-                if constexpr (MODE == 1) lblk[kZig[k]] = (int16_t)(f >> 16);
+                if constexpr (MODE == 1) lblk[zig[k]] = (int16_t)(f >> 16);
                 ++k;
                 continue;
             }
@@ -252,7 +328,7 @@ __device__ __forceinline__ void decode_blocks(const JdecArgs& a, const JLds& T, 
             k += r;
             if (k > 63) { if constexpr (MODE == 1) { bad = true; return; } break; }
             const int v = extend(b.get(sz), sz);
-            if constexpr (MODE == 1) lblk[kZig[k]] = (int16_t)v;
+            if constexpr (MODE == 1) lblk[zig[k]] = (int16_t)v;
             ++k;
         }
         if constexpr (MODE == 1) {   // the finished block -> its component plane
@@ -313,7 +389,62 @@ __global__ __launch_bounds__(WG) void jdec_sync_kernel(JdecArgs a, const int* wg
     uint32_t nb = 0;
     int dcs[3] = {0, 0, 0}, pred[3] = {0, 0, 0};
     bool bad = false;
-    decode_blocks<0>(a, T, b, u, a.D[c0 + f + i + 1], nb, dcs, 0, pred, nullptr, nullptr, bad);
+    const uint32_t stop = a.D[c0 + f + i + 1];
+    const size_t L0 = (size_t)g * a.R;
+    if (a.R == 0) {
+        decode_blocks<0>(a, T, b, u, stop, nb, dcs, 0, pred, nullptr, nullptr, bad);
+    } else if (pass == 0) {
+        decode_blocks<2>(a, T, b, u, stop, nb, dcs, 0, pred, nullptr, nullptr, bad, 0, L0);
+        a.Lcnt[0][g] = (uint8_t)min(nb, (uint32_t)a.R);
+        a.Lsel[g] = 0;
+    } else {
+        // decode until the chunk's end or a state of its previous trajectory
+        const int cur = a.Lsel[g], nxt = cur ^ 1;
+        const uint32_t cnt = a.Lcnt[cur][g];
+        const uint32_t* op = a.Lpos[cur] + L0;
+        const uint8_t* ou = a.Lu[cur] + L0;
+        uint32_t j = 0;
+        bool met = false;
+        while (b.pos < stop) {
+            while (j < cnt && op[j] < b.pos) ++j;
+            if (j < cnt && op[j] == b.pos && ou[j] == (uint8_t)u) { met = true; break; }
+            if (nb < (uint32_t)a.R) {
+                a.Lpos[nxt][L0 + nb] = b.pos;
+                a.Lu[nxt][L0 + nb] = (uint8_t)u;
+#pragma unroll
+                for (int c = 0; c < 3; ++c) a.Ldc[nxt][(L0 + nb) * 3 + c] = dcs[c];
+            }
+            decode_blocks<0>(a, T, b, u, b.pos + 1, nb, dcs, 0, pred, nullptr, nullptr, bad);   // one block
+        }
+        uint32_t ncnt = min(nb, (uint32_t)a.R);
+        if (met) {   // the rest is the previous decode: its suffix, exit state and sums
+            const int* od = a.Ldc[cur] + L0 * 3;
+            int dm[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) dm[c] = od[j * 3 + c];
+            for (uint32_t t = j; t < cnt && nb + (t - j) < (uint32_t)a.R; ++t) {
+                const uint32_t q = nb + (t - j);
+                a.Lpos[nxt][L0 + q] = op[t];
+                a.Lu[nxt][L0 + q] = ou[t];
+#pragma unroll
+                for (int c = 0; c < 3; ++c) a.Ldc[nxt][(L0 + q) * 3 + c] = dcs[c] + od[t * 3 + c] - dm[c];
+                ncnt = q + 1;
+            }
+            const uint32_t nb_old = a.nblk[g];
+            a.nblk[g] = nb + (nb_old - j);
+#pragma unroll
+            for (int c = 0; c < 3; ++c) a.dcs[(size_t)g * 3 + c] = dcs[c] + a.dcs[(size_t)g * 3 + c] - dm[c];
+            a.Lcnt[nxt][g] = (uint8_t)ncnt;
+            a.Lsel[g] = (uint8_t)nxt;
+            a.S[g] = spos;
+            a.Su[g] = (uint8_t)su;
+            a.Epos[po][g] = a.Epos[pi][g];
+            a.Eu[po][g] = a.Eu[pi][g];
+            return;
+        }
+        a.Lcnt[nxt][g] = (uint8_t)ncnt;
+        a.Lsel[g] = (uint8_t)nxt;
+    }
     a.S[g] = spos;
     a.Su[g] = (uint8_t)su;
     a.nblk[g] = nb;
@@ -334,8 +465,10 @@ __global__ __launch_bounds__(WG) void jdec_scan_kernel(JdecArgs a) {
         const uint32_t i = g0 + t;
         int v[4] = {0, 0, 0, 0};
         if (i < nch) {
-            v[0] = (int)a.nblk[c0 + i];
-            for (int c = 0; c < 3; ++c) v[1 + c] = a.dcs[(size_t)(c0 + i) * 3 + c];
+            const uint32_t g = c0 + i;
+            v[0] = (int)a.nblk[g];
+            for (int c = 0; c < 3; ++c) v[1 + c] = a.dcs[(size_t)g * 3 + c];
+            a.own[g] = (uint32_t)v[0];
         }
         for (int q = 0; q < 4; ++q) s[q][t] = v[q];
         __syncthreads();
@@ -358,6 +491,8 @@ __global__ __launch_bounds__(WG) void jdec_scan_kernel(JdecArgs a) {
 __global__ __launch_bounds__(WG) void jdec_write_kernel(JdecArgs a, const int* wg_frame, const uint32_t* wg_chunk) {
     __shared__ JLds T;
     __shared__ __attribute__((aligned(16))) int16_t lb[WG][64];
+    __shared__ uint8_t zig[64];                                    // zigzag -> natural (LDS: a per-lane index)
+    if (threadIdx.x < 64) zig[threadIdx.x] = (uint8_t)kZig[threadIdx.x];
     const int f = wg_frame[blockIdx.x];
     load_tables(a, f, &T);
     const uint32_t c0 = a.chunk0[f], nch = a.chunk0[f + 1] - c0;
@@ -373,8 +508,8 @@ __global__ __launch_bounds__(WG) void jdec_write_kernel(JdecArgs a, const int* w
 #pragma unroll
     for (int c = 0; c < 3; ++c) pred[c] = a.dcoff[(size_t)g * 3 + c];
     bool bad = false;
-    decode_blocks<1>(a, T, b, u, a.D[c0 + f + i + 1], nb, dcs, a.base[g], pred, lb[threadIdx.x],
-                     a.dense + (size_t)f * a.blocks_per_image * 64, bad);
+    decode_blocks<1>(a, T, b, u, 0, nb, dcs, a.base[g], pred, lb[threadIdx.x],
+                     a.dense + (size_t)f * a.blocks_per_image * 64, bad, a.own[g], 0, zig);
     if (bad) atomicOr(a.flags + 1, 1);
     if (i + 1 == nch && a.base[g] + nb < (uint32_t)a.total_blocks) atomicOr(a.flags + 1, 2);   // too few blocks
 }
@@ -393,6 +528,8 @@ hipError_t vd_launch_jdec(const JdecLaunch& L, hipStream_t s) {
     a.D = L.D; a.stuffed = nullptr; a.S = L.S; a.Su = L.Su;
     a.Epos[0] = L.Epos[0]; a.Epos[1] = L.Epos[1]; a.Eu[0] = L.Eu[0]; a.Eu[1] = L.Eu[1];
     a.nblk = L.nblk; a.dcs = L.dcs; a.base = L.base; a.dcoff = L.dcoff; a.dense = L.dense; a.flags = L.flags;
+    a.R = L.R; a.Lsel = L.Lsel; a.own = L.own;
+    for (int k = 0; k < 2; ++k) { a.Lpos[k] = L.Lpos[k]; a.Lu[k] = L.Lu[k]; a.Ldc[k] = L.Ldc[k]; a.Lcnt[k] = L.Lcnt[k]; }
     if (L.stage == 0) {
         hipLaunchKernelGGL(jdec_prep_kernel, dim3(a.n), dim3(WG), 0, s, a);
     } else if (L.stage == 1) {

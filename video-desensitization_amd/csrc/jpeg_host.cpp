@@ -451,7 +451,7 @@ int device_entropy(Ctx* ctx, const std::vector<Info>& info, int n, JpegArgs& a, 
     for (int f = 0; f < n; ++f) {
         seg_off[f] = (uint32_t)bytes_total;
         seg_len[f] = (uint32_t)info[f].scan_len;
-        bytes_total += (info[f].scan_len + 16 + 15) / 16 * 16;             // 16-B windows read past the end
+        bytes_total += (info[f].scan_len + 80 + 15) / 16 * 16;             // 64-B reader buffers read past the end
         chunk0[f] = nc_total;
         const uint32_t nch = std::max<uint32_t>(1, (uint32_t)((info[f].scan_len + C - 1) / C));
         for (uint32_t c = 0; c < nch; c += 256) { wg_frame.push_back(f); wg_chunk.push_back(c); }
@@ -484,7 +484,7 @@ int device_entropy(Ctx* ctx, const std::vector<Info>& info, int n, JpegArgs& a, 
         for (int f; (f = next.fetch_add(1)) < n;) {
             char* dst = hp + o_bytes + seg_off[f];
             memcpy(dst, info[f].scan, info[f].scan_len);
-            memset(dst + info[f].scan_len, 0, (info[f].scan_len + 31) / 16 * 16 - info[f].scan_len);
+            memset(dst + info[f].scan_len, 0, (info[f].scan_len + 95) / 16 * 16 - info[f].scan_len);
             for (int c = 0; c < j0.nc; ++c) memcpy(hq + ((size_t)f * 3 + c) * 64, info[f].q[info[f].c[c].tq], 128);
         }
     };
@@ -498,10 +498,17 @@ int device_entropy(Ctx* ctx, const std::vector<Info>& info, int n, JpegArgs& a, 
     VD_CHECK_HIP(hipEventRecord(ctx->jpeg_ev, ctx->stream));
     // device work area: per chunk state + the dense blocks
     const size_t NC = nc_total;
+    const int R = std::min(255, std::max(0, ctx->tune.jdec_sync));
     const size_t w_D = 0, w_S = al(w_D + (NC + n) * 4), w_Su = al(w_S + NC * 4), w_E0 = al(w_Su + NC);
     const size_t w_E1 = al(w_E0 + NC * 4), w_U0 = al(w_E1 + NC * 4), w_U1 = al(w_U0 + NC), w_nb = al(w_U1 + NC);
     const size_t w_dcs = al(w_nb + NC * 4), w_base = al(w_dcs + NC * 12), w_dco = al(w_base + NC * 4);
-    const size_t w_fl = al(w_dco + NC * 12), w_dense = al(w_fl + 16);
+    const size_t w_fl = al(w_dco + NC * 12), w_own = al(w_fl + 16), w_sel = al(w_own + NC * 4);
+    size_t w_L[2][4], o = al(w_sel + NC);
+    for (int k = 0; k < 2; ++k) {   // Lpos, Lu, Ldc, Lcnt
+        w_L[k][0] = o; w_L[k][1] = al(o + NC * R * 4); w_L[k][2] = al(w_L[k][1] + NC * R);
+        w_L[k][3] = al(w_L[k][2] + NC * R * 12); o = al(w_L[k][3] + NC);
+    }
+    const size_t w_dense = o;
     const size_t wbytes = w_dense + (size_t)n * nblk_img * 128;
     if ((rc = ctx->ensure_staging(&ctx->jdec_work, &ctx->jdec_work_bytes, wbytes))) return rc;
     char* dp = (char*)ctx->jdec_dev;
@@ -515,29 +522,35 @@ int device_entropy(Ctx* ctx, const std::vector<Info>& info, int n, JpegArgs& a, 
     L.Eu[0] = (uint8_t*)(wp + w_U0); L.Eu[1] = (uint8_t*)(wp + w_U1);
     L.nblk = (uint32_t*)(wp + w_nb); L.dcs = (int*)(wp + w_dcs); L.base = (uint32_t*)(wp + w_base);
     L.dcoff = (int*)(wp + w_dco); L.flags = (int*)(wp + w_fl); L.dense = (int16_t*)(wp + w_dense);
+    L.own = (uint32_t*)(wp + w_own); L.Lsel = (uint8_t*)(wp + w_sel); L.R = R;
+    for (int k = 0; k < 2; ++k) {
+        L.Lpos[k] = (uint32_t*)(wp + w_L[k][0]); L.Lu[k] = (uint8_t*)(wp + w_L[k][1]);
+        L.Ldc[k] = (int*)(wp + w_L[k][2]); L.Lcnt[k] = (uint8_t*)(wp + w_L[k][3]);
+    }
     L.nwg = nwg;
     hipError_t e;
-    L.stage = 0;
-    if ((e = vd_launch_jdec(L, ctx->stream)) != hipSuccess) return vd_set_error(VD_ERR_HIP, "jdec prep: %s", hipGetErrorString(e));
+    auto launch = [&](int stage, const char* what) -> int {
+        L.stage = stage;
+        if ((e = vd_launch_jdec(L, ctx->stream)) != hipSuccess) return vd_set_error(VD_ERR_HIP, "jdec %s: %s", what, hipGetErrorString(e));
+        return VD_OK;
+    };
+    if ((rc = launch(0, "prep"))) return rc;
     VD_CHECK_HIP(hipMemsetAsync(L.flags, 0, 16, ctx->stream));
-    L.stage = 1; L.pass = 0;
-    if ((e = vd_launch_jdec(L, ctx->stream)) != hipSuccess) return vd_set_error(VD_ERR_HIP, "jdec pass: %s", hipGetErrorString(e));
+    L.pass = 0;
+    if ((rc = launch(1, "pass"))) return rc;
     int flag[4] = {1, 0, 0, 0};
     int pass = 1;
     for (; pass <= 64; ++pass) {
         VD_CHECK_HIP(hipMemsetAsync(L.flags, 0, 4, ctx->stream));
         L.pass = pass;
-        if ((e = vd_launch_jdec(L, ctx->stream)) != hipSuccess) return vd_set_error(VD_ERR_HIP, "jdec pass: %s", hipGetErrorString(e));
+        if ((rc = launch(1, "pass"))) return rc;
         VD_CHECK_HIP(hipMemcpyAsync(flag, L.flags, 4, hipMemcpyDeviceToHost, ctx->stream));
         VD_CHECK_HIP(hipStreamSynchronize(ctx->stream));
         if (flag[0] == 0) break;
     }
-    ctx->jdec_passes = pass;
+    ctx->jdec_passes = pass + 1;
     if (flag[0] != 0) return VD_OK;                                    // no convergence: host decode
-    L.stage = 2;
-    if ((e = vd_launch_jdec(L, ctx->stream)) != hipSuccess) return vd_set_error(VD_ERR_HIP, "jdec scan: %s", hipGetErrorString(e));
-    L.stage = 3;
-    if ((e = vd_launch_jdec(L, ctx->stream)) != hipSuccess) return vd_set_error(VD_ERR_HIP, "jdec write: %s", hipGetErrorString(e));
+    if ((rc = launch(2, "scan")) || (rc = launch(3, "write"))) return rc;
     VD_CHECK_HIP(hipMemcpyAsync(flag, L.flags, 8, hipMemcpyDeviceToHost, ctx->stream));
     VD_CHECK_HIP(hipStreamSynchronize(ctx->stream));
     if (flag[1] != 0) return VD_OK;                                    // corrupt: the host decoder reports it
@@ -582,6 +595,14 @@ extern "C" int vdt_jpeg_coefficients(const uint8_t* data, size_t size, int16_t* 
             const uint32_t v = en.ent[en.where[2 * b] + e];
             out[b * 64 + (v >> 16)] = (int16_t)(v & 0xFFFF);
         }
+    return VD_OK;
+}
+
+extern "C" int vdt_jdec_stats(vd_ctx* hctx, int* passes) {
+    Ctx* ctx = (Ctx*)hctx;
+    if (!ctx) return vd_set_error(VD_ERR_ARG, "null context");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    if (passes) *passes = ctx->jdec_passes;
     return VD_OK;
 }
 

@@ -38,6 +38,7 @@ struct VdTune {
     int plate_s2d = 1;        // plan: YOLO space-to-depth stem input
     int jenc_gpu = 1;         // vd_jpeg_encode: Huffman coding on the device (0: host threads)
     int jdec_gpu = 1;         // vd_jpeg_decode: entropy decode on the device (0: host threads)
+    int jdec_sync = 128;      //   states recorded per chunk: passes stop at the previous trajectory (0: off)
     int jdec_chunk = 2048;    //   raw scan bytes per decoding thread (tests force small chunks)
     int plate_stage = 3;      // plate branch starts after face stage N (0: with the stem; 1-4: after
                               //   layerN; 5: after the whole face net). After layer3 its HBM-bound
@@ -52,6 +53,12 @@ struct VdTune {
     int x6_exact = 1;         // fp16 pairs: one A plane for inputs exact in fp16 (the face stem)
     int x6_mid = 0;           // fp16 pairs: 1x1 convs with K <= this on the 128 x 128 two-stage tile (0: off)
     int x6_mf32 = 0;          // fp16 pairs: 256 x {256,128} tiles on v_mfma_f32_32x32x16_f16 (else 16x16x32)
+    int x6_tail = 0;          // fp16 pairs, big tiles: rows past the last full round of 256-row tiles on
+                              //   narrower tiles (1: BN/2, 2: BN/4 columns, 0: off); N splits keep every
+                              //   output's K order, so results do not depend on the split. Measured
+                              //   slower (27.6 -> 28.5 / 28.9 ms per step for 1 / 2): the narrow tiles
+                              //   fetch more per FLOP, and a partial round's workgroups run faster alone
+    int x6_slots = 0;         //   workgroup slots of one round (0: the CU count; tests force small values)
     int f32_split = 2;        // plan (fp32, at weight load): 2 = operands scaled by powers of two
                               //   and split into fp16 pairs, 3 products on the f16 matrix cores;
                               //   1 = exact 3-term bf16 split, 6 products (conv_x6.hip);
@@ -92,6 +99,7 @@ struct ConvArgs {
     const void* wx3_2; const float* scale2_x;
     const unsigned* x2max; float x2bound;
     int x_exact;                                 // fp16 pairs: input values exact in fp16 (integer canvas)
+    int mbase;                                   // conv_x6 tiles: first output row of the launch (tail split)
 };
 
 // One fused layer1 bottleneck (block.hip): x [B][H][W][cin] -> y [B][H][W][256],
@@ -331,6 +339,7 @@ struct JdecLaunch {
     uint32_t* nblk; int* dcs; uint32_t* base; int* dcoff;
     int16_t* dense;
     int* flags;
+    int R; uint32_t* Lpos[2]; uint8_t* Lu[2]; int* Ldc[2]; uint8_t* Lcnt[2]; uint8_t* Lsel; uint32_t* own;
 };
 hipError_t vd_launch_jdec(const JdecLaunch& L, hipStream_t s);
 

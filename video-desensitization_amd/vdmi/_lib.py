@@ -90,6 +90,7 @@ SIGNATURES = [
     ("vdt_bottleneck", _I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
     ("vdt_plate_raw", _I, [_P, _P, _I, _I, _I, _SZ, _I, _P, ctypes.POINTER(_I)]),
     ("vdt_jpeg_coefficients", _I, [_P, _SZ, _P, _SZ, ctypes.POINTER(_I)]),
+    ("vdt_jdec_stats", _I, [_P, ctypes.POINTER(_I)]),
 ]
 
 _lib = None

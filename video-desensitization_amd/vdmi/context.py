@@ -253,12 +253,22 @@ class Context:
         check(self._lib.vd_jpeg_decode(self._h, ptrs, sizes, n, optr, h, w, w * 3, where))
         return out
 
-    def jpeg_encode(self, frames, quality=95, subsampling=2):
+    def jdec_passes(self):
+        """Synchronisation passes of the last jpeg_decode's device entropy stage (pass 0
+        included; 0 when the host entropy stage ran) -- test / bench hook."""
+        p = ctypes.c_int(0)
+        check(self._lib.vdt_jdec_stats(self._h, ctypes.byref(p)))
+        return p.value
+
+    def jpeg_encode(self, frames, quality=95, subsampling=2, copy=True):
         """RGB uint8 frames [n,h,w,3] (numpy, or a torch tensor on the GPU: encoded
         from device memory, no D2H of pixels) -> list of JFIF bytes, bit-identical to
         libjpeg-turbo's compressor (Pillow ``Image.save(..., quality=quality,
         subsampling=subsampling)``; cv2.imwrite's defaults are quality 95, 4:2:0 --
-        the reference's frame write, combine_detect.py:174-180)."""
+        the reference's frame write, combine_detect.py:174-180).
+        copy=False: read-only memoryviews into one buffer of this call (no per-frame
+        copy into bytes objects; the buffer lives as long as any view does).
+        """
         p, n, h, w, pitch, where, keep = _frames_arg(frames)
         sizes = (ctypes.c_size_t * n)()
         # typical frames need < 3 B/pixel; on VD_ERR_CAPACITY the device coder reports
@@ -267,10 +277,12 @@ class Context:
         caps = [h * w * 3 + 65536]
         while len(caps) < 3:
             cap = caps[-1]
-            # one staging buffer per context, reused (fresh pages would fault in on every call)
-            out = getattr(self, "_jenc_buf", None)
-            if out is None or out.size < n * cap:
-                out = self._jenc_buf = np.empty(n * cap, np.uint8)
+            if copy:   # one staging buffer per context, reused (fresh pages would fault in on every call)
+                out = getattr(self, "_jenc_buf", None)
+                if out is None or out.size < n * cap:
+                    out = self._jenc_buf = np.empty(n * cap, np.uint8)
+            else:      # this call's own buffer: the views stay valid (first touch on the copy threads)
+                out = np.empty(n * cap, np.uint8)
             rc = self._lib.vd_jpeg_encode(self._h, p, n, h, w, pitch, where, int(quality), int(subsampling),
                                           ptr(out), cap, sizes)
             if rc != _lib.VD_ERR_CAPACITY:
@@ -279,6 +291,9 @@ class Context:
             caps.append(need + 64 if need > cap else h * w * 20 + 65536)
         check(rc)
         del keep
+        if not copy:
+            mv = memoryview(out).toreadonly()
+            return [mv[i * cap:i * cap + sizes[i]] for i in range(n)]
         return [out[i * cap:i * cap + sizes[i]].tobytes() for i in range(n)]
 
     # -- instrumentation ------------------------------------------------------

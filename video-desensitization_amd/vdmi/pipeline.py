@@ -396,7 +396,25 @@ def _gpu_codec_batches(batches, output_dir, face_detector, plate_detector, batch
             out.append((items, d_in))
         return out
 
-    ahead = ThreadPoolExecutor(1)
+    # batch i+1 decoded (dctx), batch i processed (ctx), batch i-1 encoded (ectx): three
+    # contexts, each with its own stream and lock, so the three stages overlap
+    ectx = Context(device=ctx.device, precision="fp32", max_batch=max(int(batch_size), 1))
+
+    def encode(items, out):
+        jpgs = ectx.jpeg_encode(out, quality=quality, subsampling=2, copy=False)
+        return [io.submit(_write_bytes, data, os.path.join(output_dir, f"processed_{os.path.basename(path)}"))
+                for (path, _), data in zip(items, jpgs)]
+
+    def collect(fut):
+        try:
+            save_futs.extend(fut.result())
+        except Exception as e:           # combine_detect.py:226-228: the batch is dropped
+            logger.error(f"parallel inference failed: {e}")
+            return False
+        return True
+
+    ahead, behind = ThreadPoolExecutor(1), ThreadPoolExecutor(1)
+    enc = []                             # (future, counts) of batches being encoded
     try:
         fut = ahead.submit(load, batches[0]) if batches else None
         for bi in range(len(batches)):
@@ -405,21 +423,26 @@ def _gpu_codec_batches(batches, output_dir, face_detector, plate_detector, batch
             for items, d_in in decoded:
                 try:
                     out, fc, pc = ctx.process(d_in, faces=faces, plates=plates, flags=flags)
-                    jpgs = ctx.jpeg_encode(out, quality=quality, subsampling=2)
-                except Exception as e:       # combine_detect.py:226-228: the batch is dropped
+                    ctx.sync()           # the encode context reads `out` on its own stream
+                except Exception as e:   # combine_detect.py:226-228: the batch is dropped
                     logger.error(f"parallel inference failed: {e}")
                     continue
                 n = len(items)
-                for (path, _), data in zip(items, jpgs):
-                    save_futs.append(io.submit(_write_bytes, data,
-                                               os.path.join(output_dir, f"processed_{os.path.basename(path)}")))
-                totals[0] += n
-                totals[1] += int(fc.count[:n].sum().item())
-                if mosaic_plates:
-                    totals[2] += int(pc.count[:n].sum().item())
+                counts = (n, int(fc.count[:n].sum().item()), int(pc.count[:n].sum().item()) if mosaic_plates else 0)
+                enc.append((behind.submit(encode, items, out), counts))
+                while len(enc) > 1:      # at most one batch encoding behind the one just processed
+                    f0, c0 = enc.pop(0)
+                    if collect(f0):
+                        totals[0] += c0[0]; totals[1] += c0[1]; totals[2] += c0[2]
+        while enc:
+            f0, c0 = enc.pop(0)
+            if collect(f0):
+                totals[0] += c0[0]; totals[1] += c0[1]; totals[2] += c0[2]
     finally:
         ahead.shutdown()
+        behind.shutdown()
         dctx.close()
+        ectx.close()
         _save_all(save_futs, logger)
     return tuple(totals)
 
