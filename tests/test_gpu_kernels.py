@@ -47,6 +47,24 @@ def test_mosaic_matches_oracle(gpu, face_ctx_factory, h, w, k):
         np.testing.assert_array_equal(got[i], exp)
 
 
+@pytest.mark.parametrize("nt", [1, 3])
+def test_mosaic_nontemporal_matches_oracle(gpu, nt):
+    """Option mosaic_nt: the output pass's stores (1) and source loads (3) non-temporal
+    -- the same bytes."""
+    import vdmi
+    from vdmi import mosaic_frames, synth
+    ctx = vdmi.Context(precision="bf16", max_batch=4, options={"mosaic_nt": nt})
+    try:
+        rng = np.random.default_rng(5)
+        frames = synth.frames(3, 1080, 1920, seed=9)
+        boxes = _rand_boxes(rng, 3, 1080, 1920, 20)
+        got = mosaic_frames(frames, boxes, 8, ctx=ctx)
+        for i in range(3):
+            np.testing.assert_array_equal(got[i], omosaic.mosaic_frame(frames[i], boxes[i], 8))
+    finally:
+        ctx.close()
+
+
 def test_mosaic_nested_chain_and_levels(gpu, face_ctx_factory):
     """Deeply nested boxes force walks that leave a row band (global fallback)."""
     from vdmi import mosaic_frames, synth

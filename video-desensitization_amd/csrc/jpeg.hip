@@ -126,10 +126,10 @@ __device__ __forceinline__ int samp(const JpegArgs& a, int img, int c, int x, in
 
 // jdsample.c fancy upsampling of component c at output pixel (x, y)
 __device__ __forceinline__ int upsampled(const JpegArgs& a, int img, int c, int x, int y) {
-    const int fx = a.hmax / a.hs[c], fy = a.vmax / a.vs[c];
+    const int fx = a.fx[c], fy = a.fy[c];
     if (fx == 1 && fy == 1) return samp(a, img, c, x, y);
-    const int dw = (a.w * a.hs[c] + a.hmax - 1) / a.hmax;      // downsampled_width
-    const int dh = (a.h * a.vs[c] + a.vmax - 1) / a.vmax;      // downsampled_height
+    const int dw = a.dw[c];                                   // downsampled_width
+    const int dh = a.dh[c];                                   // downsampled_height
     const int i = x >> 1;
     if (fy == 1) {                                            // h2v1
         const int r = y, p = samp(a, img, c, i, r);
@@ -147,34 +147,75 @@ __device__ __forceinline__ int upsampled(const JpegArgs& a, int img, int c, int 
 
 __device__ __forceinline__ int clamp255(int v) { return v < 0 ? 0 : (v > 255 ? 255 : v); }
 
+__device__ __forceinline__ void pixel_rgb(const JpegArgs& a, int img, int x, int y, int& r, int& g, int& b) {
+    const int Y = upsampled(a, img, 0, x, y);
+    if (a.nc == 1) { r = g = b = Y; return; }
+    // jdcolor.c build_ycc_rgb_table: SCALEBITS 16, FIX(x) = x * 65536 + 0.5
+    const int cb = upsampled(a, img, 1, x, y) - 128, cr = upsampled(a, img, 2, x, y) - 128;
+    const int cr_r = (91881 * cr + 32768) >> 16;
+    const int cb_b = (116130 * cb + 32768) >> 16;
+    const int gg = ((-22554 * cb + 32768) + (-46802 * cr)) >> 16;
+    r = clamp255(Y + cr_r);
+    g = clamp255(Y + gg);
+    b = clamp255(Y + cb_b);
+}
+
+// one lane per output pixel (any width / pitch)
 __global__ __launch_bounds__(256) void jpeg_color_kernel(JpegArgs a) {
     const long p = (long)blockIdx.x * 256 + threadIdx.x;
     const int img = blockIdx.y;
     if (p >= (long)a.h * a.w) return;
     const int y = (int)(p / a.w), x = (int)(p - (long)y * a.w);
     uint8_t* dst = a.out + (size_t)img * a.h * a.pitch + (size_t)y * a.pitch + (size_t)x * 3;
-    const int Y = upsampled(a, img, 0, x, y);
-    if (a.nc == 1) {
-        dst[0] = dst[1] = dst[2] = (uint8_t)Y;
-        return;
+    int r, g, b;
+    pixel_rgb(a, img, x, y, r, g, b);
+    dst[0] = (uint8_t)r;
+    dst[1] = (uint8_t)g;
+    dst[2] = (uint8_t)b;
+}
+
+// one lane per 4 pixels of a row (w % 4 == 0, pitch % 4 == 0): 12 bytes as three
+// dword stores instead of 12 byte stores, neighbouring samples shared through L1
+__global__ __launch_bounds__(256) void jpeg_color4_kernel(JpegArgs a) {
+    const int q = blockIdx.x * 256 + threadIdx.x;            // 4-pixel group within the image
+    const int img = blockIdx.y;
+    const int gw = a.w >> 2;
+    if (q >= a.h * gw) return;
+    const int y = q / gw, x = (q - y * gw) * 4;
+    unsigned v[3] = {0u, 0u, 0u};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        int r, g, b;
+        pixel_rgb(a, img, x + k, y, r, g, b);
+        const int o = 3 * k;
+        v[o >> 2] |= (unsigned)r << (8 * (o & 3));
+        v[(o + 1) >> 2] |= (unsigned)g << (8 * ((o + 1) & 3));
+        v[(o + 2) >> 2] |= (unsigned)b << (8 * ((o + 2) & 3));
     }
-    // jdcolor.c build_ycc_rgb_table: SCALEBITS 16, FIX(x) = x * 65536 + 0.5
-    const int cb = upsampled(a, img, 1, x, y) - 128, cr = upsampled(a, img, 2, x, y) - 128;
-    const int cr_r = (91881 * cr + 32768) >> 16;
-    const int cb_b = (116130 * cb + 32768) >> 16;
-    const int g = ((-22554 * cb + 32768) + (-46802 * cr)) >> 16;
-    dst[0] = (uint8_t)clamp255(Y + cr_r);
-    dst[1] = (uint8_t)clamp255(Y + g);
-    dst[2] = (uint8_t)clamp255(Y + cb_b);
+    unsigned* dst = (unsigned*)(a.out + (size_t)img * a.h * a.pitch + (size_t)y * a.pitch + (size_t)x * 3);
+    dst[0] = v[0];
+    dst[1] = v[1];
+    dst[2] = v[2];
 }
 
 }  // namespace
 
-hipError_t vd_launch_jpeg(const JpegArgs& a, hipStream_t s) {
+hipError_t vd_launch_jpeg(const JpegArgs& a0, hipStream_t s) {
+    JpegArgs a = a0;
+    for (int c = 0; c < 3; ++c) {
+        const int hs = a.hs[c] > 0 ? a.hs[c] : 1, vs = a.vs[c] > 0 ? a.vs[c] : 1;
+        a.fx[c] = a.hmax / hs;
+        a.fy[c] = a.vmax / vs;
+        a.dw[c] = (a.w * hs + a.hmax - 1) / a.hmax;
+        a.dh[c] = (a.h * vs + a.vmax - 1) / a.vmax;
+    }
     const long total = (long)a.n * a.blocks_per_image;
     if (total <= 0) return hipSuccess;
     hipLaunchKernelGGL(jpeg_idct_kernel, dim3((unsigned)((total + BLK_PER_WG - 1) / BLK_PER_WG)), dim3(256), 0, s, a);
     const long px = (long)a.h * a.w;
-    hipLaunchKernelGGL(jpeg_color_kernel, dim3((unsigned)((px + 255) / 256), a.n), dim3(256), 0, s, a);
+    if ((a.w & 3) == 0 && (a.pitch & 3) == 0 && ((uintptr_t)a.out & 3) == 0 && px / 4 < (1L << 31))
+        hipLaunchKernelGGL(jpeg_color4_kernel, dim3((unsigned)((px / 4 + 255) / 256), a.n), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(jpeg_color_kernel, dim3((unsigned)((px + 255) / 256), a.n), dim3(256), 0, s, a);
     return hipGetLastError();
 }

@@ -214,7 +214,7 @@ struct JdecArgs {
     uint32_t* base;                // first block index (scan)
     int* dcoff;                    // [chunks][3] DC predictors at the chunk start
     int16_t* dense;                // [n][blocks_per_image][64]
-    int* flags;                    // [0] exit states changed, [1] corrupt stream, [2] fast sync failed
+    int* flags;                    // [1] corrupt stream; [4 + p] exit states changed in pass p (p <= 64)
     // early stop: the first R states of each chunk's current trajectory, two list buffers
     int R;                         // states recorded per chunk (0: off)
     uint32_t* Lpos[2]; uint8_t* Lu[2];   // [chunks][R]
@@ -235,13 +235,26 @@ __global__ __launch_bounds__(WG) void jdec_prep_kernel(JdecArgs a) {
     for (uint32_t g0 = 0; g0 < nch; g0 += WG) {
         const uint32_t i = g0 + t;
         uint32_t cnt = 0;
-        if (i < nch) {
+        if (i < nch) {   // 0xFF 0x00 pairs whose 0x00 lies in the chunk, 16 bytes at a time
             const uint32_t r0 = i * a.chunk_bytes, r1 = min(nbytes, r0 + a.chunk_bytes);
-            uint32_t prev = r0 > 0 ? d[r0 - 1] : 0u;
-            for (uint32_t r = r0; r < r1; ++r) {
-                const uint32_t c = d[r];
-                cnt += (c == 0u && prev == 0xFFu) ? 1u : 0u;
-                prev = (c == 0u && prev == 0xFFu) ? 0u : c;   // 0xFF 0x00 0x00: the second 00 is data
+            uint32_t prev_ff = r0 > 0 && d[r0 - 1] == 0xFFu ? 1u : 0u;   // previous byte is 0xFF
+            for (uint32_t r = r0; r < r1; r += 16) {
+                const uint4 v = *(const uint4*)(d + r);                  // 16-B aligned (chunk_bytes % 16 == 0)
+                const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+                const uint32_t valid = r1 - r;                          // bytes of this vector in the chunk
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t w = wv[k];
+                    // exact per-byte masks (0x80 in each byte that is 0x00 / 0xFF)
+                    const uint32_t z = ~(((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w | 0x7F7F7F7Fu);
+                    const uint32_t nw = ~w;
+                    const uint32_t ff = ~(((nw & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | nw | 0x7F7F7F7Fu);
+                    uint32_t pairs = ((ff << 8) | (prev_ff << 7)) & z;           // 0xFF then 0x00
+                    const uint32_t nvalid = valid > 4u * k ? min(valid - 4u * k, 4u) : 0u;
+                    pairs &= nvalid >= 4 ? 0xFFFFFFFFu : ((1u << (8 * nvalid)) - 1u);
+                    cnt += __builtin_popcount(pairs);
+                    prev_ff = ff >> 31;
+                }
             }
         }
         s[t] = cnt;
@@ -259,89 +272,152 @@ __global__ __launch_bounds__(WG) void jdec_prep_kernel(JdecArgs a) {
     if (t == 0) a.D[c0 + f + nch] = 8u * (nbytes - carry);   // the frame's data bits (chunk end of the last)
 }
 
-// decode whole blocks from (pos, u) until the first block boundary at or past `stop`
-// (MODE 0: counting, speculative: errors end the block; MODE 2: the same, recording
-// the first K states at L), or exactly `limit` blocks (MODE 1: writing, errors flag)
+// Per-lane symbol loop (one symbol of every lane per iteration: DC and AC symbols
+// share the table lookup, so lanes in different coefficient positions do not split
+// the wave into separate DC / AC paths). Block boundaries (k == 0) are where a decode
+// stops, records its state or meets an earlier trajectory.
+//   MODE 0: count until the first boundary at or past `stop` (speculative: an invalid
+//           code or a run past the block ends the block, a wrong start keeps going)
+//   MODE 2: MODE 0, recording the first R states into list 0
+//   MODE 3: MODE 0, recording into list `nxt` and stopping at a state of list `cur`
+//   MODE 1: write exactly `limit` blocks (the first at global block blk0) straight
+//           into the zeroed dense buffer; an invalid code or a run past the block is a
+//           corrupt stream (bad)
+struct Walk {
+    uint32_t stop, limit, blk0;
+    size_t L0;
+    int cur, nxt;                  // MODE 3 lists
+    uint32_t cnt, j;               // MODE 3: cur list length, merge index (in/out)
+    int16_t* dense;                // MODE 1: the frame's dense blocks
+    bool met, bad;
+};
+
+__device__ __forceinline__ void record(const JdecArgs& a, int buf, size_t at, uint32_t pos, int u, const int (&dcs)[3]) {
+    uint32_t* lp = buf ? a.Lpos[1] : a.Lpos[0];
+    uint8_t* lu = buf ? a.Lu[1] : a.Lu[0];
+    int* ld = buf ? a.Ldc[1] : a.Ldc[0];
+    lp[at] = pos;
+    lu[at] = (uint8_t)u;
+    ld[at * 3] = dcs[0];
+    ld[at * 3 + 1] = dcs[1];
+    ld[at * 3 + 2] = dcs[2];
+}
+
 template <int MODE>
-__device__ __forceinline__ void decode_blocks(const JdecArgs& a, const JLds& T, Reader& b, int& u, uint32_t stop,
-                                              uint32_t& nblk, int (&dcs)[3], uint32_t blk0, int (&pred)[3],
-                                              int16_t* lblk, int16_t* dense, bool& bad, uint32_t limit = 0,
-                                              size_t L0 = 0, const uint8_t* zig = nullptr) {
-    while (MODE == 1 ? nblk < limit : b.pos < stop) {
-        if constexpr (MODE == 1) {
-            if (blk0 + nblk >= (uint32_t)a.total_blocks) return;      // past the frame's last block
+__device__ __forceinline__ void decode_run(const JdecArgs& a, const JLds& T, Reader& b, int& u, uint32_t& nblk,
+                                           int (&dcs)[3], int (&pred)[3], Walk& w, const uint8_t* zig = nullptr) {
+    // per block-in-MCU tables / component as packed bit fields (no per-lane indexing of kernel arguments)
+    uint32_t pk_c = 0, pk_dc = 0, pk_ac = 0, pk_bx = 0, pk_by = 0;
 #pragma unroll
-            for (int k = 0; k < 64; k += 8) *(uint4*)(lblk + k) = make_uint4(0, 0, 0, 0);
-        }
-        if constexpr (MODE == 2) {
-            if (nblk < (uint32_t)a.R) {
-                a.Lpos[0][L0 + nblk] = b.pos;
-                a.Lu[0][L0 + nblk] = (uint8_t)u;
-#pragma unroll
-                for (int c = 0; c < 3; ++c) a.Ldc[0][(L0 + nblk) * 3 + c] = dcs[c];
+    for (int i = 0; i < 6; ++i) {
+        pk_c |= (uint32_t)a.ucomp[i] << (2 * i);
+        pk_dc |= (uint32_t)(a.udc[i] & 1) << i;
+        pk_ac |= (uint32_t)(a.uac[i] & 1) << i;
+        pk_bx |= (uint32_t)(a.ubx[i] & 1) << i;
+        pk_by |= (uint32_t)(a.uby[i] & 1) << i;
+    }
+    const uint32_t* dcop = MODE == 3 ? (w.cur ? a.Lpos[1] : a.Lpos[0]) + w.L0 : nullptr;
+    const uint8_t* dcou = MODE == 3 ? (w.cur ? a.Lu[1] : a.Lu[0]) + w.L0 : nullptr;
+    // MODE 3: entries j and j+1 of the previous trajectory in registers, the next one
+    // loaded a block ahead of its use (a dependent global load per boundary otherwise)
+    uint32_t p0 = 0xFFFFFFFFu, p1 = 0xFFFFFFFFu, u0 = 0, u1 = 0;
+    if constexpr (MODE == 3) {
+        if (w.j < w.cnt) { p0 = dcop[w.j]; u0 = dcou[w.j]; }
+        if (w.j + 1 < w.cnt) { p1 = dcop[w.j + 1]; u1 = dcou[w.j + 1]; }
+    }
+    int k = 0, c = 0, tdc = 0, tac = 0;
+    int16_t* dst = nullptr;
+    for (;;) {
+        if (k == 0) {                                           // block boundary
+            bool live = MODE == 1 ? (nblk < w.limit && w.blk0 + nblk < (uint32_t)a.total_blocks) : b.pos < w.stop;
+            if constexpr (MODE == 3) {
+                if (live) {
+                    while (w.j < w.cnt && p0 < b.pos) {             // advance: usually one step, prefetched
+                        ++w.j;
+                        p0 = p1; u0 = u1;
+                        if (w.j + 1 < w.cnt) { p1 = dcop[w.j + 1]; u1 = dcou[w.j + 1]; }
+                        else p1 = 0xFFFFFFFFu;
+                    }
+                    if (w.j < w.cnt && p0 == b.pos && u0 == (uint32_t)u) { w.met = true; live = false; }
+                }
+            }
+            if (!live) break;
+            if constexpr (MODE == 2 || MODE == 3) {
+                if (nblk < (uint32_t)a.R) record(a, MODE == 2 ? 0 : w.nxt, w.L0 + nblk, b.pos, u, dcs);
+            }
+            c = (int)((pk_c >> (2 * u)) & 3u);
+            tdc = (int)((pk_dc >> u) & 1u);
+            tac = (int)((pk_ac >> u) & 1u);
+            if constexpr (MODE == 1) {
+                const uint32_t g = w.blk0 + nblk;
+                const uint32_t m = g / a.bpm;
+                const int mx = (int)(m % a.mcux), my = (int)(m / a.mcux);
+                const int bx = (int)((pk_bx >> u) & 1u), by = (int)((pk_by >> u) & 1u);
+                const size_t pb = (size_t)a.cblk[c] + (size_t)(my * a.vs[c] + by) * a.bw[c] + mx * a.hs[c] + bx;
+                dst = w.dense + pb * 64;
             }
         }
-        const int c = a.ucomp[u];
         b.step();
-        int s = decode_sym(b, T, a.udc[u]);
-        int diff = 0;
-        if (s < 0 || s > 11) {
-            if constexpr (MODE == 1) { bad = true; return; }
-            if (s < 0) b.skip(1);                                      // keep moving: a wrong start resyncs
-            s = 0;
-        } else {
-            diff = extend(b.get(s), s);
-        }
-        dcs[c] += diff;
-        if constexpr (MODE == 1) {
-            pred[c] += diff;
-            lblk[0] = (int16_t)pred[c];
-        }
-        const int at = 2 + a.uac[u];
-        for (int k = 1; k < 64;) {
-            b.step();
-            const uint32_t look = b.peek(kLook);
-            const uint32_t f = T.fast[at - 2][look];
-            if (f & 0xFFu) {
-                b.skip((int)(f & 0xFFu));
-                const int run = (int)((f >> 8) & 0xFFu);
-                if (run == 64) break;                                  // EOB
-                if (run == 16) { k += 16; continue; }                  // ZRL
-                k += run;
-                if (k > 63) { if constexpr (MODE == 1) { bad = true; return; } break; }
-                if constexpr (MODE == 1) lblk[zig[k]] = (int16_t)(f >> 16);
-                ++k;
-                continue;
-            }
-            const int rs = decode_sym(b, T, at);
-            if (rs < 0) {
-                if constexpr (MODE == 1) { bad = true; return; }
+        const uint32_t look = b.peek(kLook);
+        const bool isdc = k == 0;
+        const uint32_t* tb = isdc ? T.fastdc[tdc] : T.fast[tac];
+        const uint32_t e = tb[look];
+        int run, val;
+        if (e & 0xFFu) {
+            b.skip((int)(e & 0xFFu));
+            run = (int)((e >> 8) & 0xFFu);
+            val = (int)(int16_t)(e >> 16);
+        } else {                                                // code + extra bits longer than the lookahead
+            int rs = decode_sym(b, T, isdc ? tdc : 2 + tac);
+            if (isdc) {
+                if (rs < 0 || rs > 11) {
+                    if constexpr (MODE == 1) { w.bad = true; return; }
+                    if (rs < 0) b.skip(1);                      // keep moving: a wrong start resyncs
+                    rs = 0;
+                }
+                run = 0;
+                val = extend(b.get(rs), rs);
+            } else if (rs < 0) {
+                if constexpr (MODE == 1) { w.bad = true; return; }
                 b.skip(1);
-                break;
+                run = 64;                                       // the block ends
+                val = 0;
+            } else {
+                const int r = rs >> 4, sz = rs & 15;
+                run = sz == 0 ? (r == 15 ? 16 : 64) : r;
+                val = sz == 0 ? 0 : extend(b.get(sz), sz);
             }
-            const int r = rs >> 4, sz = rs & 15;
-            if (sz == 0) {
-                if (r != 15) break;
-                k += 16;
-                continue;
+        }
+        if (isdc) {
+            dcs[0] += c == 0 ? val : 0;
+            dcs[1] += c == 1 ? val : 0;
+            dcs[2] += c == 2 ? val : 0;
+            if constexpr (MODE == 1) {
+                pred[0] += c == 0 ? val : 0;
+                pred[1] += c == 1 ? val : 0;
+                pred[2] += c == 2 ? val : 0;
+                dst[0] = (int16_t)(c == 0 ? pred[0] : (c == 1 ? pred[1] : pred[2]));
             }
-            k += r;
-            if (k > 63) { if constexpr (MODE == 1) { bad = true; return; } break; }
-            const int v = extend(b.get(sz), sz);
-            if constexpr (MODE == 1) lblk[zig[k]] = (int16_t)v;
-            ++k;
+            k = 1;
+        } else if (run == 64) {                                 // EOB
+            k = 64;
+        } else if (run == 16) {                                 // ZRL (a coefficient's run is <= 15)
+            k += 16;
+        } else {
+            k += run;
+            if (k > 63) {
+                if constexpr (MODE == 1) { w.bad = true; return; }
+                k = 64;
+            } else {
+                if constexpr (MODE == 1) dst[zig[k]] = (int16_t)val;
+                ++k;
+            }
         }
-        if constexpr (MODE == 1) {   // the finished block -> its component plane
-            const uint32_t g = blk0 + nblk;
-            const uint32_t m = g / a.bpm;
-            const int mx = (int)(m % a.mcux), my = (int)(m / a.mcux);
-            const size_t pb = (size_t)a.cblk[c] + (size_t)(my * a.vs[c] + a.uby[u]) * a.bw[c] + mx * a.hs[c] + a.ubx[u];
-            int16_t* dst = dense + pb * 64;
-#pragma unroll
-            for (int k = 0; k < 64; k += 8) *(uint4*)(dst + k) = *(const uint4*)(lblk + k);
+        if (k >= 64) {                                          // the block is done
+            ++nblk;
+            u = u + 1 == a.bpm ? 0 : u + 1;
+            k = 0;
         }
-        ++nblk;
-        u = u + 1 == a.bpm ? 0 : u + 1;
     }
 }
 
@@ -388,13 +464,14 @@ __global__ __launch_bounds__(WG) void jdec_sync_kernel(JdecArgs a, const int* wg
     int u = su;
     uint32_t nb = 0;
     int dcs[3] = {0, 0, 0}, pred[3] = {0, 0, 0};
-    bool bad = false;
-    const uint32_t stop = a.D[c0 + f + i + 1];
     const size_t L0 = (size_t)g * a.R;
+    Walk w{};
+    w.stop = a.D[c0 + f + i + 1];
+    w.L0 = L0;
     if (a.R == 0) {
-        decode_blocks<0>(a, T, b, u, stop, nb, dcs, 0, pred, nullptr, nullptr, bad);
+        decode_run<0>(a, T, b, u, nb, dcs, pred, w);
     } else if (pass == 0) {
-        decode_blocks<2>(a, T, b, u, stop, nb, dcs, 0, pred, nullptr, nullptr, bad, 0, L0);
+        decode_run<2>(a, T, b, u, nb, dcs, pred, w);
         a.Lcnt[0][g] = (uint8_t)min(nb, (uint32_t)a.R);
         a.Lsel[g] = 0;
     } else {
@@ -403,19 +480,10 @@ __global__ __launch_bounds__(WG) void jdec_sync_kernel(JdecArgs a, const int* wg
         const uint32_t cnt = a.Lcnt[cur][g];
         const uint32_t* op = a.Lpos[cur] + L0;
         const uint8_t* ou = a.Lu[cur] + L0;
-        uint32_t j = 0;
-        bool met = false;
-        while (b.pos < stop) {
-            while (j < cnt && op[j] < b.pos) ++j;
-            if (j < cnt && op[j] == b.pos && ou[j] == (uint8_t)u) { met = true; break; }
-            if (nb < (uint32_t)a.R) {
-                a.Lpos[nxt][L0 + nb] = b.pos;
-                a.Lu[nxt][L0 + nb] = (uint8_t)u;
-#pragma unroll
-                for (int c = 0; c < 3; ++c) a.Ldc[nxt][(L0 + nb) * 3 + c] = dcs[c];
-            }
-            decode_blocks<0>(a, T, b, u, b.pos + 1, nb, dcs, 0, pred, nullptr, nullptr, bad);   // one block
-        }
+        w.cur = cur; w.nxt = nxt; w.cnt = cnt; w.j = 0;
+        decode_run<3>(a, T, b, u, nb, dcs, pred, w);
+        const bool met = w.met;
+        const uint32_t j = w.j;
         uint32_t ncnt = min(nb, (uint32_t)a.R);
         if (met) {   // the rest is the previous decode: its suffix, exit state and sums
             const int* od = a.Ldc[cur] + L0 * 3;
@@ -450,7 +518,7 @@ __global__ __launch_bounds__(WG) void jdec_sync_kernel(JdecArgs a, const int* wg
     a.nblk[g] = nb;
 #pragma unroll
     for (int c = 0; c < 3; ++c) a.dcs[(size_t)g * 3 + c] = dcs[c];
-    if (pass > 0 && (b.pos != a.Epos[pi][g] || (uint8_t)u != a.Eu[pi][g])) atomicOr(a.flags, 1);
+    if (pass > 0 && (b.pos != a.Epos[pi][g] || (uint8_t)u != a.Eu[pi][g])) atomicOr(a.flags + 4 + pass, 1);
     a.Epos[po][g] = b.pos;
     a.Eu[po][g] = (uint8_t)u;
 }
@@ -490,7 +558,6 @@ __global__ __launch_bounds__(WG) void jdec_scan_kernel(JdecArgs a) {
 
 __global__ __launch_bounds__(WG) void jdec_write_kernel(JdecArgs a, const int* wg_frame, const uint32_t* wg_chunk) {
     __shared__ JLds T;
-    __shared__ __attribute__((aligned(16))) int16_t lb[WG][64];
     __shared__ uint8_t zig[64];                                    // zigzag -> natural (LDS: a per-lane index)
     if (threadIdx.x < 64) zig[threadIdx.x] = (uint8_t)kZig[threadIdx.x];
     const int f = wg_frame[blockIdx.x];
@@ -507,9 +574,12 @@ __global__ __launch_bounds__(WG) void jdec_write_kernel(JdecArgs a, const int* w
     int pred[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) pred[c] = a.dcoff[(size_t)g * 3 + c];
-    bool bad = false;
-    decode_blocks<1>(a, T, b, u, 0, nb, dcs, a.base[g], pred, lb[threadIdx.x],
-                     a.dense + (size_t)f * a.blocks_per_image * 64, bad, a.own[g], 0, zig);
+    Walk w{};
+    w.limit = a.own[g];
+    w.blk0 = a.base[g];
+    w.dense = a.dense + (size_t)f * a.blocks_per_image * 64;
+    decode_run<1>(a, T, b, u, nb, dcs, pred, w, zig);
+    const bool bad = w.bad;
     if (bad) atomicOr(a.flags + 1, 1);
     if (i + 1 == nch && a.base[g] + nb < (uint32_t)a.total_blocks) atomicOr(a.flags + 1, 2);   // too few blocks
 }

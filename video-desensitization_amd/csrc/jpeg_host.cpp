@@ -388,6 +388,14 @@ void fill_tables(const Info& j, JLds& t) {
         if (q >= 2)
             for (int i = 0; i < (1 << kLook); ++i)
                 t.fast[q - 2][i] = (uint32_t)h.fa_len[i] | ((uint32_t)h.fa_run[i] << 8) | ((uint32_t)(uint16_t)h.fa_val[i] << 16);
+        else   // DC: code + size bits within the lookahead, baseline sizes (<= 11) only
+            for (int i = 0; i < (1 << kLook); ++i) {
+                const int l = h.look_len[i], sz = h.look_sym[i];
+                if (l == 0 || sz > 11 || l + sz > kLook) continue;
+                const int extra = sz ? (i >> (kLook - l - sz)) & ((1 << sz) - 1) : 0;
+                const int v = sz && extra < (1 << (sz - 1)) ? extra - (1 << sz) + 1 : extra;
+                t.fastdc[q][i] = (uint32_t)(l + sz) | ((uint32_t)(uint16_t)v << 16);
+            }
         for (int l = 0; l < 18; ++l) t.maxcode[q][l] = h.maxcode[l];
         for (int l = 0; l < 17; ++l) t.valoff[q][l] = h.valoff[l];
         memcpy(t.vals[q], h.vals, 256);
@@ -502,7 +510,7 @@ int device_entropy(Ctx* ctx, const std::vector<Info>& info, int n, JpegArgs& a, 
     const size_t w_D = 0, w_S = al(w_D + (NC + n) * 4), w_Su = al(w_S + NC * 4), w_E0 = al(w_Su + NC);
     const size_t w_E1 = al(w_E0 + NC * 4), w_U0 = al(w_E1 + NC * 4), w_U1 = al(w_U0 + NC), w_nb = al(w_U1 + NC);
     const size_t w_dcs = al(w_nb + NC * 4), w_base = al(w_dcs + NC * 12), w_dco = al(w_base + NC * 4);
-    const size_t w_fl = al(w_dco + NC * 12), w_own = al(w_fl + 16), w_sel = al(w_own + NC * 4);
+    const size_t w_fl = al(w_dco + NC * 12), w_own = al(w_fl + 4 * (4 + 65)), w_sel = al(w_own + NC * 4);
     size_t w_L[2][4], o = al(w_sel + NC);
     for (int k = 0; k < 2; ++k) {   // Lpos, Lu, Ldc, Lcnt
         w_L[k][0] = o; w_L[k][1] = al(o + NC * R * 4); w_L[k][2] = al(w_L[k][1] + NC * R);
@@ -535,21 +543,31 @@ int device_entropy(Ctx* ctx, const std::vector<Info>& info, int n, JpegArgs& a, 
         return VD_OK;
     };
     if ((rc = launch(0, "prep"))) return rc;
-    VD_CHECK_HIP(hipMemsetAsync(L.flags, 0, 16, ctx->stream));
+    VD_CHECK_HIP(hipMemsetAsync(L.flags, 0, 4 * (4 + 65), ctx->stream));
     L.pass = 0;
     if ((rc = launch(1, "pass"))) return rc;
-    int flag[4] = {1, 0, 0, 0};
-    int pass = 1;
-    for (; pass <= 64; ++pass) {
-        VD_CHECK_HIP(hipMemsetAsync(L.flags, 0, 4, ctx->stream));
-        L.pass = pass;
-        if ((rc = launch(1, "pass"))) return rc;
-        VD_CHECK_HIP(hipMemcpyAsync(flag, L.flags, 4, hipMemcpyDeviceToHost, ctx->stream));
+    // resynchronisation passes in groups of jdec_group between host checks (a pass after
+    // convergence only copies exit states), until one changes no exit state
+    const int grp = std::max(1, ctx->tune.jdec_group);
+    int pf[65] = {0};
+    int pass = 1, conv = 0;
+    while (!conv && pass <= 64) {
+        const int last = std::min(64, pass + grp - 1);
+        for (int p = pass; p <= last; ++p) {
+            L.pass = p;
+            if ((rc = launch(1, "pass"))) return rc;
+        }
+        VD_CHECK_HIP(hipMemcpyAsync(pf + pass, L.flags + 4 + pass, 4 * (last - pass + 1), hipMemcpyDeviceToHost, ctx->stream));
         VD_CHECK_HIP(hipStreamSynchronize(ctx->stream));
-        if (flag[0] == 0) break;
+        for (int p = pass; p <= last && !conv; ++p)
+            if (pf[p] == 0) conv = p;
+        pass = last + 1;
     }
-    ctx->jdec_passes = pass + 1;
-    if (flag[0] != 0) return VD_OK;                                    // no convergence: host decode
+    ctx->jdec_passes = conv ? conv + 1 : 65;
+    if (!conv) return VD_OK;                                          // no convergence: host decode
+    int flag[4] = {0, 0, 0, 0};
+    // the write stores each coefficient straight into its dense block: zeros first
+    VD_CHECK_HIP(hipMemsetAsync(L.dense, 0, (size_t)n * nblk_img * 128, ctx->stream));
     if ((rc = launch(2, "scan")) || (rc = launch(3, "write"))) return rc;
     VD_CHECK_HIP(hipMemcpyAsync(flag, L.flags, 8, hipMemcpyDeviceToHost, ctx->stream));
     VD_CHECK_HIP(hipStreamSynchronize(ctx->stream));

@@ -55,8 +55,10 @@ struct MosaicArgs {
     MBox* table; int tcap;                           // [n][tcap] prepared boxes
     int* cpref;                                      // [n][BOX_FAST+1] prefix sums of box cells sw*sh
     uint32_t* cells;                                 // [n][CELL_CAP] walked colour per cell
-    int map_on;                                      // fast path on (option mosaic_map=0 forces the generic path)
+    int map_on;                                      // bit 0: fast path on (option mosaic_map=0 forces the generic
+                                                     // path); bit 1: non-temporal output stores, bit 2: loads
 };
+typedef unsigned mos_u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int frame_boxes(const MosaicArgs& a, int f, int& n0) {
     n0 = a.cnt0 ? min(max(a.cnt0[f], 0), a.cap0) : 0;
@@ -333,7 +335,7 @@ __global__ __launch_bounds__(256) void mosaic_out_kernel(MosaicArgs a) {
     const int row_bytes = a.w * 3;
     const uint32_t* cells = a.cells + (size_t)f * CELL_CAP;
 
-    bool fast = use_cells && !overflow && a.vec_ok && nt <= MAPBOX && a.map_on;
+    bool fast = use_cells && !overflow && a.vec_ok && nt <= MAPBOX && (a.map_on & 1);
     if (fast) {
         // wave 0, per band box t: the band's slice of its cell rows [uy_lo, uy_hi]
         // (exclusive prefix sum of their cell counts); sw must fit the map's 11 bits
@@ -648,11 +650,20 @@ __global__ __launch_bounds__(256) void mosaic_out_kernel(MosaicArgs a) {
         int r = tid / vpr, c = tid - (tid / vpr) * vpr;
         int j = tid;
         uint4 v0{}, v1{}, v2{}, v3{};
+        const bool nt_st = a.map_on & 2, nt_ld = a.map_on & 4;
+        auto ld = [&](int jj) -> uint4 {
+            if (nt_ld) return __builtin_bit_cast(uint4, __builtin_nontemporal_load((const mos_u32x4*)(s4 + jj)));
+            return s4[jj];
+        };
+        auto st = [&](int jj, const uint4& v) {
+            if (nt_st) __builtin_nontemporal_store(__builtin_bit_cast(mos_u32x4, v), (mos_u32x4*)(d4 + jj));
+            else d4[jj] = v;
+        };
         auto load4 = [&](int jj, uint4& x0, uint4& x1, uint4& x2, uint4& x3) {
-            if (jj < nvec) x0 = s4[jj];
-            if (jj + 256 < nvec) x1 = s4[jj + 256];
-            if (jj + 512 < nvec) x2 = s4[jj + 512];
-            if (jj + 768 < nvec) x3 = s4[jj + 768];
+            if (jj < nvec) x0 = ld(jj);
+            if (jj + 256 < nvec) x1 = ld(jj + 256);
+            if (jj + 512 < nvec) x2 = ld(jj + 512);
+            if (jj + 768 < nvec) x3 = ld(jj + 768);
         };
         load4(j, v0, v1, v2, v3);
         for (; j < nvec; j += 4 * 256) {
@@ -671,10 +682,10 @@ __global__ __launch_bounds__(256) void mosaic_out_kernel(MosaicArgs a) {
                 if (h2) process(v2, r2, c2, lds);
                 if (h3) process(v3, r3, c3, lds);
             }
-            d4[j] = v0;
-            if (h1) d4[j + 256] = v1;
-            if (h2) d4[j + 512] = v2;
-            if (h3) d4[j + 768] = v3;
+            st(j, v0);
+            if (h1) st(j + 256, v1);
+            if (h2) st(j + 512, v2);
+            if (h3) st(j + 768, v3);
             r = r3; c = c3;
             advance(r, c);
             v0 = n0; v1 = n1; v2 = n2; v3 = n3;

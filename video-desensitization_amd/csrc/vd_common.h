@@ -30,6 +30,7 @@ struct VdTune {
     int stream_ntt = 16;      // streaming 1x1: 256-channel slices where Cout allows (8: 128)
     int lb_pair = 1;          // one letterbox launch for both canvases when geometry allows
     int mosaic_map = 1;       // mosaic output pass: per-band vector maps (0: generic path)
+    int mosaic_nt = 0;        //   non-temporal output stores (1), and source loads (3)
     int block_fuse = 1;       // plan: fused layer1 bottlenecks (block.hip)
     int block_fuse32 = 1;     // plan, fp32 (fp16 pairs): fused layer1 bottlenecks (block32.hip)
     int chain = 1;            // plan: layer2 conv3 + next conv1 (chain.hip)
@@ -39,7 +40,8 @@ struct VdTune {
     int jenc_gpu = 1;         // vd_jpeg_encode: Huffman coding on the device (0: host threads)
     int jdec_gpu = 1;         // vd_jpeg_decode: entropy decode on the device (0: host threads)
     int jdec_sync = 128;      //   states recorded per chunk: passes stop at the previous trajectory (0: off)
-    int jdec_chunk = 2048;    //   raw scan bytes per decoding thread (tests force small chunks)
+    int jdec_chunk = 1024;    //   raw scan bytes per decoding thread (tests force small chunks)
+    int jdec_group = 4;       //   resynchronisation passes launched between host convergence checks
     int plate_stage = 3;      // plate branch starts after face stage N (0: with the stem; 1-4: after
                               //   layerN; 5: after the whole face net). After layer3 its HBM-bound
                               //   convs overlap the MFMA-bound late face layers: 30.8 -> 30.0 ms/step
@@ -245,6 +247,8 @@ struct JpegArgs {
     const int16_t* dense;                       // or (device entropy decode) dense quantized blocks
                                                 // [n * blocks_per_image][64] natural order; entries unused
     uint8_t* out; size_t pitch;                 // RGB frames [n][h][pitch]
+    int fx[3], fy[3], dw[3], dh[3];             // per component: upsampling factors, downsampled size
+                                                // (vd_launch_jpeg fills them)
 };
 
 // TERMS = 2 (fp16 pair): each frame's activations are scaled by a power of two so
@@ -319,6 +323,7 @@ __device__ __forceinline__ void amax_lds_flush(const unsigned* s, unsigned* g, i
 struct JLds {
     uint16_t look[4][2048];
     uint32_t fast[2][2048];
+    uint32_t fastdc[2][2048];                   // DC code + extra bits in one lookup (len | diff << 16)
     int32_t maxcode[4][18];
     int32_t valoff[4][17];
     uint8_t vals[4][256];
