@@ -230,6 +230,21 @@ int vdt_bottleneck(vd_ctx* ctx, const float* x, int n, int h, int w, int cin,
 int vdt_jpeg_coefficients(const uint8_t* data, size_t size, int16_t* out, size_t cap_blocks, int* nblocks);
 int vdt_plate_raw(vd_ctx* ctx, const uint8_t* frames, int n, int h, int w, size_t pitch,
                   int where, float* out, int* anchors);
+/* ---- .record container I/O (host; replaces foreign/recordDeal.so) ------------
+ * vd_record_extract_h265: every *.record* file of record_dir (sorted; CyberRT
+ * segments) -> <out_dir>/hevcs/<camera>.h265 per camera topic
+ * /drivers/camera/<camera>/compressed/image: the CompressedImage data of its
+ * messages from the first key frame on, concatenated (replaces
+ * recordDeal.read_record2h265_all, combine_detect.py:839).
+ * vd_record_repack_h265: the same records rewritten into out_dir with each
+ * extracted message's data replaced by the matching access unit of
+ * <videos_dir>/<camera>.h265 (or .hevc, processed_<camera>.h265); everything else
+ * carried over, positions and sizes recomputed (replaces
+ * recordDeal.write_allH265_record_all, combine_detect.py:958). Uncompressed
+ * records only. */
+int vd_record_extract_h265(const char* record_dir, const char* out_dir, int* topics_written);
+int vd_record_repack_h265(const char* record_dir, const char* videos_dir, const char* out_dir, int* records_written);
+
 /* The last vd_jpeg_decode's device entropy stage: synchronisation passes run (pass 0
  * included; 0 when the host entropy stage ran). */
 int vdt_jdec_stats(vd_ctx* ctx, int* passes);

@@ -1,0 +1,211 @@
+"""`.record` container I/O (csrc/record.cpp through the C-ABI; vdmi.record mirrors
+the reference's recordDeal.read_record2h265_all / write_allH265_record_all,
+combine_detect.py:839, :958) against the Python restatement of the CyberRT layout
+(oracle/record.py). No GPU.
+
+Parity unpinned with the reference module itself: recordDeal.so is a prebuilt binary
+(never run), cyber_record is absent and the reference ships no .record fixture; the
+records here are synthetic, written by the oracle as CyberRT's RecordFileWriter lays
+them out, with synthetic H.265 access units (Annex-B NAL units)."""
+import os
+import struct
+
+import numpy as np
+import pytest
+
+from oracle import record as orec
+
+CAMS = ["/drivers/camera/front_wide/compressed/image", "/drivers/camera/left_back/compressed/image",
+        "/drivers/camera/rear/compressed/image"]
+OTHER = "/apollo/sensor/gnss/best_pose"
+
+
+def nal(t, payload):
+    return b"\x00\x00\x00\x01" + bytes([t << 1, 1]) + payload
+
+
+def au(rng, key, n=None):
+    """one access unit: VPS/SPS/PPS + IDR slice (key) or a TRAIL_R slice, payload
+    bytes 1..255 (no start-code emulation), first_slice_segment_in_pic_flag set"""
+    n = int(rng.integers(20, 200)) if n is None else n
+    body = bytes([0x80]) + bytes(rng.integers(1, 256, n, dtype=np.uint8))
+    if key:
+        return (nal(32, bytes(rng.integers(1, 256, 8, dtype=np.uint8))) + nal(33, bytes([1, 2, 3])) +
+                nal(34, bytes([4, 5])) + nal(19, body))
+    return nal(1, body)
+
+
+def make_records(tmp, rng, segments=2, per_seg=12, lead=(2, 0, 3)):
+    """segments of a record: each camera topic leads with `lead[i]` non-key units
+    before its first key frame; a non-camera topic in between"""
+    chans = [(c, "apollo.drivers.CompressedImage") for c in CAMS] + [(OTHER, "apollo.localization.Pose")]
+    k = [0] * len(CAMS)
+    blobs, names = [], []
+    t = 1_000_000
+    for s in range(segments):
+        chunks = []
+        for c in range(3):
+            msgs = []
+            for _ in range(per_seg // 3):
+                for i, topic in enumerate(CAMS):
+                    key = k[i] == lead[i] or (k[i] > lead[i] and (k[i] - lead[i]) % 5 == 0)
+                    msgs.append((topic, t, orec.compressed_image(au(rng, key), frame_id=topic.split("/")[3])))
+                    k[i] += 1
+                    t += 1000
+                msgs.append((OTHER, t, bytes(rng.integers(0, 256, 40, dtype=np.uint8))))
+                t += 1000
+            chunks.append(msgs)
+        data = orec.write_record(chans, chunks)
+        name = f"test.record.{s:05d}"
+        with open(os.path.join(tmp, name), "wb") as f:
+            f.write(data)
+        blobs.append(data)
+        names.append(name)
+    return blobs, names
+
+
+@pytest.fixture
+def rec(tmp_path):
+    rng = np.random.default_rng(3)
+    src = tmp_path / "records"
+    src.mkdir()
+    blobs, names = make_records(str(src), rng)
+    return tmp_path, src, blobs, names
+
+
+def test_extract_matches_oracle(rec):
+    from vdmi import record
+    tmp, src, blobs, _ = rec
+    n = record.read_record2h265_all(str(src), str(tmp / "h265"))
+    exp = orec.extract(blobs, set(CAMS))
+    assert n == len(exp) == 3
+    for cam, data in exp.items():
+        got = (tmp / "h265" / "hevcs" / f"{cam}.h265").read_bytes()
+        assert got == data
+        assert orec.is_key_frame(got[:300])            # starts at the first key frame
+
+
+def test_repack_with_own_streams_is_byte_identical(rec):
+    from vdmi import record
+    tmp, src, blobs, names = rec
+    record.read_record2h265_all(str(src), str(tmp / "h265"))
+    n = record.write_allH265_record_all(str(src), str(tmp / "h265" / "hevcs"), str(tmp / "out"))
+    assert n == len(names)
+    for name, data in zip(names, blobs):
+        assert (tmp / "out" / name).read_bytes() == data
+        assert not (tmp / "out" / (name + ".tmp_record")).exists()
+
+
+def test_repack_replaces_camera_data_and_relayouts(rec):
+    """Desensitised streams with other access-unit sizes: exactly the extracted
+    messages change (in order), every other message is untouched, and the layout
+    (chunk raw sizes, index positions / caches, header size and index position)
+    describes the new file."""
+    from vdmi import record
+    tmp, src, blobs, names = rec
+    rng = np.random.default_rng(9)
+    vids = tmp / "videos"
+    vids.mkdir()
+    orig = orec.extract(blobs, set(CAMS))
+    new_aus = {}
+    for cam in orig:
+        # as many units as extracted messages, new payloads and lengths, same key pattern
+        units = []
+        for ch, _, content in [m for d in blobs for m in orec.messages(d)]:
+            if ch.split("/")[3] != cam:
+                continue
+            units.append(orec.get(orec.parse(content), 4))
+        first = next(i for i, u in enumerate(units) if orec.is_key_frame(u))
+        repl = [au(rng, orec.is_key_frame(u), n=int(rng.integers(5, 400))) for u in units[first:]]
+        new_aus[cam] = (first, repl)
+        (vids / f"{cam}.h265").write_bytes(b"".join(repl))
+    record.write_allH265_record_all(str(src), str(vids), str(tmp / "out"))
+    seen = {cam: 0 for cam in orig}
+    for name, data in zip(names, blobs):
+        out = (tmp / "out" / name).read_bytes()
+        hdr, secs = orec.read_sections(out)
+        assert orec.get(hdr, 12) == len(out)
+        idx_sec = [s for s in secs if s[0] == orec.INDEX]
+        assert len(idx_sec) == 1 and orec.get(hdr, 6) == idx_sec[0][1]
+        by_pos = {p: (t, b) for t, p, b in secs}
+        for e in orec.parse(idx_sec[0][2]):
+            f = orec.parse(e[2])
+            t, pos = orec.get(f, 1), orec.get(f, 2)
+            assert by_pos[pos][0] == t
+            if t == orec.CHUNK_HEADER:
+                raw = orec.get(orec.parse(orec.get(f, 102)), 4)
+                nxt = [s for s in secs if s[1] > pos][0]
+                assert nxt[0] == orec.CHUNK_BODY and raw == len(nxt[2])
+                assert orec.get(orec.parse(by_pos[pos][1]), 4) == len(nxt[2])
+        a, b = orec.messages(data), orec.messages(out)
+        assert [(c, t) for c, t, _ in a] == [(c, t) for c, t, _ in b]
+        for (ch, _, ca), (_, _, cb) in zip(a, b):
+            if ch not in CAMS:
+                assert ca == cb
+                continue
+            cam = ch.split("/")[3]
+            first, repl = new_aus[cam]
+            k = seen[cam]
+            seen[cam] += 1
+            fa, fb = orec.parse(ca), orec.parse(cb)
+            if k < first:
+                assert ca == cb
+            else:
+                assert orec.get(fb, 4) == repl[k - first]
+                assert [x for x in fa if x[0] != 4] == [x for x in fb if x[0] != 4]
+
+
+def test_repack_short_stream_keeps_the_rest(rec):
+    from vdmi import record
+    tmp, src, blobs, names = rec
+    vids = tmp / "videos"
+    vids.mkdir()
+    rng = np.random.default_rng(1)
+    cam = CAMS[0].split("/")[3]
+    repl = [au(rng, True, n=50), au(rng, False, n=60)]
+    (vids / f"{cam}.h265").write_bytes(b"".join(repl))
+    record.write_allH265_record_all(str(src), str(vids), str(tmp / "out"))
+    got = [orec.get(orec.parse(c), 4) for d in names for ch, _, c in orec.messages((tmp / "out" / d).read_bytes())
+           if ch == CAMS[0]]
+    exp = [orec.get(orec.parse(c), 4) for d in blobs for ch, _, c in orec.messages(d) if ch == CAMS[0]]
+    first = next(i for i, u in enumerate(exp) if orec.is_key_frame(u))
+    assert got[:first] == exp[:first]
+    assert got[first:first + 2] == repl
+    assert got[first + 2:] == exp[first + 2:]
+
+
+def test_record_errors(tmp_path):
+    import vdmi
+    from vdmi import record
+    with pytest.raises(vdmi.VdError):
+        record.read_record2h265_all(str(tmp_path / "missing"), str(tmp_path / "o"))
+    d = tmp_path / "bad"
+    d.mkdir()
+    (d / "x.record").write_bytes(b"not a record" * 10)
+    with pytest.raises(vdmi.VdError):
+        record.read_record2h265_all(str(d), str(tmp_path / "o"))
+    c = tmp_path / "comp"
+    c.mkdir()
+    chans = [(CAMS[0], "apollo.drivers.CompressedImage")]
+    rng = np.random.default_rng(0)
+    data = orec.write_record(chans, [[(CAMS[0], 1, orec.compressed_image(au(rng, True)))]], compress=2)
+    (c / "y.record").write_bytes(data)
+    with pytest.raises(vdmi.VdError, match="compressed"):
+        record.read_record2h265_all(str(c), str(tmp_path / "o"))
+    # a truncated section
+    (c / "y.record").write_bytes(orec.write_record(chans, [[(CAMS[0], 1, orec.compressed_image(au(rng, True)))]])[:-7])
+    with pytest.raises(vdmi.VdError):
+        record.read_record2h265_all(str(c), str(tmp_path / "o"))
+
+
+def test_oracle_layout_known_answer():
+    """The section header and the header region as RecordFileWriter writes them:
+    {int32 type, 4 zero bytes, int64 size}, the Header message, '0' then zeros to 2048."""
+    data = orec.write_record([("/a", "T")], [[("/a", 5, b"xy")]])
+    t, pad, n = struct.unpack_from("<iiq", data, 0)
+    assert (t, pad) == (orec.HEADER, 0) and n < orec.HEADER_LENGTH
+    assert data[16 + n:16 + n + 1] == b"0" and set(data[17 + n:16 + orec.HEADER_LENGTH]) == {0}
+    hdr, secs = orec.read_sections(data)
+    assert [s[0] for s in secs] == [orec.CHANNEL, orec.CHUNK_HEADER, orec.CHUNK_BODY, orec.INDEX]
+    assert orec.get(hdr, 12) == len(data) and orec.get(hdr, 6) == secs[-1][1]
+    assert orec.messages(data) == [("/a", 5, b"xy")]

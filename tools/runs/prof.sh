@@ -11,5 +11,5 @@ eval timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/$T -o run 
 S=$(find gpurun_out/$T -name 'run_kernel_stats.csv' | head -1)
 K=$(find gpurun_out/$T -name 'run_kernel_trace.csv' | head -1)
 python tools/prof_summary.py "$S" gpurun_out/$T/summary.md > /dev/null 2>&1 || true
-python tools/fp32_layers.py "$K" 64 ${PROF_BLOCK:-1} > gpurun_out/$T/layers.txt 2>&1 || true
+python tools/fp32_layers.py "$K" ${PROF_B:-64} ${PROF_BLOCK:-1} > gpurun_out/$T/layers.txt 2>&1 || true
 tail -3 gpurun_out/$T/layers.txt

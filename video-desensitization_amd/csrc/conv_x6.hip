@@ -62,15 +62,35 @@ template <int BM_, int BN, int NT_, int NST, int TERMS, int MF = 16> struct X6Sh
     static constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
     static constexpr int TM = WTM / MF, TN = WTN / MF;            // MFMA blocks per wave tile
     static constexpr int NDMA = TB * BN / 16;                  // 1-KB DMA instructions per K tile
-    static constexpr int AROWS = NT / 4;                       // A rows per staging pass (2 passes)
-    static_assert(BM == 2 * AROWS, "two A items per thread");
+    static constexpr int AROWS = NT / 4;                       // A rows per staging pass
+    static constexpr int AITEMS = BM / AROWS;                  // A items (row, 8 k) per thread: 2 (8 waves), 4 (4 waves)
+    static_assert(BM % AROWS == 0 && (AITEMS == 2 || AITEMS == 4), "A items per thread");
 };
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 64 + ((chunk ^ (((row >> 3) & 1) * 3)) << 4); }
 
-// s_waitcnt vmcnt(n) for n in [0, 7] (immediate operand)
+// s_waitcnt vmcnt(n) for n in [0, 23] (immediate operand)
 __device__ __forceinline__ void wait_vm(int n) {
     switch (n) {
+        case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); return;
+        case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); return;
+        case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); return;
+        case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); return;
+        case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); return;
+        case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); return;
+        case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); return;
+        case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); return;
+        case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); return;
+        case 17: asm volatile("s_waitcnt vmcnt(17)" ::: "memory"); return;
+        case 18: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); return;
+        case 19: asm volatile("s_waitcnt vmcnt(19)" ::: "memory"); return;
+        case 20: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); return;
+        case 21: asm volatile("s_waitcnt vmcnt(21)" ::: "memory"); return;
+        case 22: asm volatile("s_waitcnt vmcnt(22)" ::: "memory"); return;
+        case 23: asm volatile("s_waitcnt vmcnt(23)" ::: "memory"); return;
+        default: break;
+    }
+    switch (n < 8 ? n : 7) {
         case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
         case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
         case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
@@ -187,11 +207,14 @@ __device__ __forceinline__ void split_pack(const float (&e)[8], float sa, u32x4 
 }
 
 template <int BM, int BN, int NT, int NST, int TERMS, int MF>
-__global__ __launch_bounds__(NT, 2) void conv_x6_kernel(ConvArgs a) {
+// 8 waves: two workgroups' worth of waves per SIMD pair (256 VGPRs each); 4 waves (one
+// per SIMD, 128 x 128 wave tiles): the whole 512-register file per wave, the
+// accumulators in AGPRs
+__global__ __launch_bounds__(NT, NT == 256 && BM == 256 ? 1 : 2) void conv_x6_kernel(ConvArgs a) {
     static_assert(MF == 16 || (MF == 32 && TERMS == 2), "32x32x16 form: fp16 pairs only");
     using S = X6Shape<BM, BN, NT, NST, TERMS, MF>;
     constexpr int STAGE = S::STAGE, PL_A = S::PL_A, PL_B = S::PL_B, TM = S::TM, TN = S::TN, WAVES = S::WAVES;
-    constexpr int AROWS = S::AROWS;
+    constexpr int AROWS = S::AROWS, AIT = S::AITEMS;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid / S::WAVES_N, wn = wid % S::WAVES_N;
@@ -206,11 +229,12 @@ __global__ __launch_bounds__(NT, 2) void conv_x6_kernel(ConvArgs a) {
     // ---- A staging: thread = (row, k-pair) items; item i: row = (tid >> 2) + AROWS i, pair = tid & 3 (k 8p..8p+7)
     const int apair = tid & 3, arow = tid >> 2;
     const int ohw = a.yh * a.yw;
-    int pix0[2];                                    // element offsets (xbytes < 2^31: vd_conv_x6_ok)
-    int iy0[2], ix0[2];
-    float sa[2] = {1.f, 1.f};                       // fp16 pair: the row's frame scale 2^k
+    int pix0[AIT];                                  // element offsets (xbytes < 2^31: vd_conv_x6_ok)
+    int iy0[AIT], ix0[AIT];
+    float sa[AIT];                                  // fp16 pair: the row's frame scale 2^k
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < AIT; ++i) {
+        sa[i] = 1.f;
         const int m = m0 + arow + AROWS * i;
         if (m < a.M) {
             const int b = m / ohw, rem = m - b * ohw;
@@ -233,7 +257,7 @@ __global__ __launch_bounds__(NT, 2) void conv_x6_kernel(ConvArgs a) {
 
     // two register sets of A (8 f32 of each of 2 rows): tile t lives in set t & 1,
     // loaded two iterations before it is split into LDS
-    u32x4 ra[2][2][2];                              // [set][item][half]
+    u32x4 ra[2][AIT][2];                            // [set][item][half]
     // per half h: the (dy, dx, c) of this thread's 4-channel chunk kt*8 + 2*apair + h,
     // advanced by 32 channels per load_a call (tiles are loaded in order): no
     // divisions and no branches in the load path
@@ -246,7 +270,7 @@ __global__ __launch_bounds__(NT, 2) void conv_x6_kernel(ConvArgs a) {
         tdy[h] = t / a.kw;
         tdx[h] = t - tdy[h] * a.kw;
     }
-    auto load_a = [&](u32x4 (&r)[2][2]) {
+    auto load_a = [&](u32x4 (&r)[AIT][2]) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             // a chunk past the last tap (K padding) is pushed off the image rows, so
@@ -254,7 +278,7 @@ __global__ __launch_bounds__(NT, 2) void conv_x6_kernel(ConvArgs a) {
             const int dyk = tdy[h] < a.kh ? tdy[h] : (1 << 28);
             const int toff = tdy[h] * tap_dy + tdx[h] * a.ldx + tc[h];
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
+            for (int i = 0; i < AIT; ++i) {
                 const unsigned iy = (unsigned)(iy0[i] + dyk), ix = (unsigned)(ix0[i] + tdx[h]);
                 const bool ok = (iy < (unsigned)a.xh) & (ix < (unsigned)a.xw);
                 const unsigned off = ok ? (unsigned)(pix0[i] + toff) * 4u : 0x80000000u;
@@ -274,7 +298,7 @@ __global__ __launch_bounds__(NT, 2) void conv_x6_kernel(ConvArgs a) {
             }
         }
     };
-    auto store_item = [&](int st, const u32x4 (&r)[2][2], int i) {
+    auto store_item = [&](int st, const u32x4 (&r)[AIT][2], int i) {
         char* A = smem + st * STAGE;
         float e[8];
 #pragma unroll
@@ -322,7 +346,7 @@ __global__ __launch_bounds__(NT, 2) void conv_x6_kernel(ConvArgs a) {
 
     // one K tile from stage st; the split + LDS write of the next tile's A items are
     // interleaved with the MFMA rows (VALU work beside the matrix cores)
-    auto compute = [&](int st, bool split_next, int st_next, const u32x4 (&rn)[2][2]) {
+    auto compute = [&](int st, bool split_next, int st_next, const u32x4 (&rn)[AIT][2]) {
         const char* A = smem + st * STAGE;
         const char* Bs = A + S::TA * PL_A;
         const int ch = lane >> 4;
@@ -344,8 +368,9 @@ __global__ __launch_bounds__(NT, 2) void conv_x6_kernel(ConvArgs a) {
                         bf[p] = *(const u32x4*)(Bs + p * PL_B + swz(wn * S::WTN + j * 32 + r32, 2 * sk + c32));
 #pragma unroll
                     for (int i = 0; i < TM; ++i) acc[i][j] = mfma_pair32(af[i], bf, acc[i][j]);
-                    if (split_next && sk == 0 && j == 0) store_item(st_next, rn, 0);
-                    if (split_next && sk == 1 && j == 0) store_item(st_next, rn, 1);
+#pragma unroll
+                    for (int q = 0; q < AIT; ++q)
+                        if (split_next && sk == q * 2 / AIT && j == (q * 2 % AIT) * TN / AIT) store_item(st_next, rn, q);
                 }
             }
         } else if constexpr (TN > TM) {   // wide wave tile: all A fragments resident, B fragments streamed
@@ -363,8 +388,9 @@ __global__ __launch_bounds__(NT, 2) void conv_x6_kernel(ConvArgs a) {
                     bf[p] = *(const u32x4*)(Bs + p * PL_B + swz(wn * S::WTN + j * 16 + (lane & 15), ch));
 #pragma unroll
                 for (int i = 0; i < TM; ++i) acc[i][j] = mfma_terms<TERMS>(af[i], bf, acc[i][j]);
-                if (split_next && j == 0) store_item(st_next, rn, 0);
-                if (split_next && j == TN / 2) store_item(st_next, rn, 1);
+#pragma unroll
+                for (int q = 0; q < AIT; ++q)
+                    if (split_next && j == q * TN / AIT) store_item(st_next, rn, q);
             }
         } else {
             u32x4 bf[TN][3];
@@ -381,8 +407,14 @@ __global__ __launch_bounds__(NT, 2) void conv_x6_kernel(ConvArgs a) {
                     af[p] = *(const u32x4*)(A + p * PL_A + swz(wm * S::WTM + i * 16 + (lane & 15), ch));
 #pragma unroll
                 for (int j = 0; j < TN; ++j) acc[i][j] = mfma_terms<TERMS>(af, bf[j], acc[i][j]);
-                if (split_next && i == 0) store_item(st_next, rn, 0);
-                if (split_next && i == (TM > 2 ? 2 : 1)) store_item(st_next, rn, 1);
+                if constexpr (AIT == 2) {
+                    if (split_next && i == 0) store_item(st_next, rn, 0);
+                    if (split_next && i == (TM > 2 ? 2 : 1)) store_item(st_next, rn, 1);
+                } else {
+#pragma unroll
+                    for (int q = 0; q < AIT; ++q)
+                        if (split_next && i == q * TM / AIT) store_item(st_next, rn, q);
+                }
             }
         }
     };
@@ -393,16 +425,16 @@ __global__ __launch_bounds__(NT, 2) void conv_x6_kernel(ConvArgs a) {
     // are those of iteration t-1's end -- A(t+2), B(t+1) -- so B(t) and A(t+1) retire
     // at vmcnt(4 + my_dma) (fewer when the tail issued less).
     load_a(ra[0]);
-    store_item(0, ra[0], 0);
-    store_item(0, ra[0], 1);
+#pragma unroll
+    for (int q = 0; q < AIT; ++q) store_item(0, ra[0], q);
     dma_b(0, 0);
     if (nk > 1) load_a(ra[1]);
     if (nk > 1) dma_b(1, 1);
     if (nk > 2) load_a(ra[0]);
-    auto iter = [&](int kt, const u32x4 (&rnext)[2][2], u32x4 (&rfree)[2][2]) {
+    auto iter = [&](int kt, const u32x4 (&rnext)[AIT][2], u32x4 (&rfree)[AIT][2]) {
         // younger than B(kt) / A(kt+1): A(kt+2) loads (issued iff kt+2 < nk) and
         // B(kt+1) DMA (iff kt+1 < nk)
-        const int younger = (kt + 2 < nk ? 4 : 0) + (kt + 1 < nk ? my_dma : 0);
+        const int younger = (kt + 2 < nk ? 2 * AIT : 0) + (kt + 1 < nk ? my_dma : 0);
         wait_vm(younger);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this thread's A(kt) ds_writes
         __builtin_amdgcn_s_barrier();
@@ -424,12 +456,12 @@ __global__ __launch_bounds__(NT, 2) void conv_x6_kernel(ConvArgs a) {
     // ---- one LDS stage: per tile, B(kt) DMA and the split A(kt) write, then
     // compute; A(kt+1)'s loads run under it (registers), B waits for the stage
     load_a(ra[0]);
-    auto iter1 = [&](int kt, const u32x4 (&rcur)[2][2], u32x4 (&rnext)[2][2]) {
+    auto iter1 = [&](int kt, const u32x4 (&rcur)[AIT][2], u32x4 (&rnext)[AIT][2]) {
         dma_b(kt, 0);
-        store_item(0, rcur, 0);                               // compiler waits for A(kt)'s loads
-        store_item(0, rcur, 1);
+#pragma unroll
+        for (int q = 0; q < AIT; ++q) store_item(0, rcur, q);   // compiler waits for A(kt)'s loads
         if (kt + 1 < nk) load_a(rnext);
-        wait_vm(kt + 1 < nk ? 4 : 0);                         // B(kt) landed (older than A(kt+1))
+        wait_vm(kt + 1 < nk ? 2 * AIT : 0);                   // B(kt) landed (older than A(kt+1))
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
