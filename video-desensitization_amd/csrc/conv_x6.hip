@@ -1031,6 +1031,27 @@ template <int TERMS>
 static hipError_t launch_terms(const ConvArgs& a0, hipStream_t s) {
     ConvArgs a = a0;
     if (TERMS == 2) a.scale = a.scale_x;              // the fp16 pair's per-channel rescaled BN scale
+    if constexpr (TERMS == 2) {   // YOLO's SiLU 1x1 convs (C2f cv1 / cv2, SPPF cv1) on the streaming form
+        if (a.tune && a.tune->x6_stream_silu && a.act == VD_ACT_SILU && a.res_mode == VD_RES_NONE && a.kh == 1 &&
+            a.kw == 1 && a.pad == 0 && a.kpad == a.cin_pad && !((a.ldx | a.xcoff | a.ldy | a.ycoff) & 7)) {
+            const int k = a.cin_pad, co = a.cout;
+            const int nch = co % 128 == 0 ? 128 : (co % 64 == 0 ? 64 : (co % 32 == 0 ? 32 : 0));
+            if (nch) {
+#define VD_SILU(KS, NTT) return launch_stream_x6<KS, NTT, VD_ACT_SILU, VD_RES_NONE, 2>(a, s)
+                if (k == 32 && nch == 32) VD_SILU(1, 2);
+                if (k == 32 && nch == 64) VD_SILU(1, 4);
+                if (k == 64 && nch == 64) VD_SILU(2, 4);
+                if (k == 64 && nch == 128) VD_SILU(2, 8);
+                if (k == 96 && nch == 64) VD_SILU(3, 4);
+                if (k == 128 && nch == 64) VD_SILU(4, 4);
+                if (k == 128 && nch == 128) VD_SILU(4, 8);
+                if (k == 192 && nch == 64) VD_SILU(6, 4);
+                if (k == 192 && nch == 128) VD_SILU(6, 8);
+                if (k == 256 && nch == 128) VD_SILU(8, 8);
+#undef VD_SILU
+            }
+        }
+    }
     if (const int nch = stream_x6_nch(a, TERMS)) {
         if constexpr (TERMS == 2) {   // 256-channel slices: each pixel read by half as many workgroups
             if (a.tune && a.tune->x6_stream256 && a.cout % 256 == 0) {
