@@ -374,3 +374,36 @@ def test_heads_fp32_tail_split_bit_identical(gpu):
     for t in (1, 2):
         for a, b in zip(heads[t], heads[0]):
             np.testing.assert_array_equal(a, b)
+
+
+def test_heads_fp32_halo_conv(gpu):
+    """fp32 plan: the 3x3 stride-1 convs with W <= 126 (layer2-4 conv2, FPN merges, SSH
+    conv5X5_1 + conv3X3 at levels 0-2) run on conv_x6_halo_kernel (input split once per
+    32-channel chunk over the tile's halo; option x6_halo, 2 = three B stages). Same
+    products, K summed chunk-major instead of tap-major: heads within f32 rounding of
+    the tap-major kernel, identical boxes; the two- and three-stage forms bit-identical
+    (same K order); batch-invariant (a frame's heads do not depend on its batch mates,
+    so halos that straddle frames read only zero padding)."""
+    import vdmi
+    fr = _frames(3, 1080, 1920, seed=37)
+    heads, boxes = {}, {}
+    for h in (2, 1, 0):
+        ctx = vdmi.Context(precision="fp32", max_batch=3, options={"x6_halo": h})
+        try:
+            ctx.load_weights(0, face_weights("default"))
+            heads[h] = ctx.forward_heads(fr)
+            r = ctx.detect(fr)
+            boxes[h] = [r.frame(b)[0].copy() for b in range(3)]
+            if h:
+                one = ctx.forward_heads(fr[1:2])
+                for a, b in zip(one, heads[h]):
+                    np.testing.assert_array_equal(a[0], b[1])
+        finally:
+            ctx.close()
+    for a, b in zip(heads[2], heads[1]):
+        np.testing.assert_array_equal(a, b)
+    for a, b in zip(heads[1], heads[0]):
+        assert np.abs(a - b).max() <= 6e-6 * (np.abs(b).max() + 1e-6), np.abs(a - b).max() / np.abs(b).max()
+    assert sum(len(x) for x in boxes[0]) > 0
+    for a, b in zip(boxes[1], boxes[0]):
+        np.testing.assert_array_equal(a, b)

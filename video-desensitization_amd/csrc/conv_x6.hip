@@ -50,7 +50,7 @@ constexpr int kAmaxFrames = 1024;               // LDS reserved for per-frame ma
 // with activations exact in fp16 (one A plane: the integer-valued face canvas)
 template <int BM_, int BN, int NT_, int NST, int TERMS, int MF = 16> struct X6Shape {
     static constexpr int TA = TERMS == 1 ? 1 : TERMS, TB = TERMS == 1 ? 2 : TERMS;   // A / B planes
-    static constexpr int BM = BM_, NT = NT_, WAVES = NT / 64;
+    static constexpr int BM = BM_, BNV = BN, NT = NT_, WAVES = NT / 64, TERMSV = TERMS;
     static constexpr int PL_A = BM * 64;                       // bytes per A plane
     static constexpr int PL_B = BN * 64;                       // bytes per B plane
     static constexpr int STAGE = TA * PL_A + TB * PL_B;        // 256 x 128: 73 728 B (3 terms), 49 152 B (2)
@@ -204,6 +204,125 @@ __device__ __forceinline__ void split_pack(const float (&e)[8], float sa, u32x4 
         o[1] = u32x4{mv[0] | (mv[1] << 16), mv[2] | (mv[3] << 16), mv[4] | (mv[5] << 16), mv[6] | (mv[7] << 16)};
     if constexpr (TERMS == 3)
         o[2] = u32x4{lv[0] | (lv[1] << 16), lv[2] | (lv[3] << 16), lv[4] | (lv[5] << 16), lv[6] | (lv[7] << 16)};
+}
+
+// The fused epilogue of the 256 / 128-row tiles: BM / EPR passes of EPR accumulator
+// rows through LDS, then BN + residual (incl. the FPN nearest-2x source) +
+// activation + 16-B stores + the per-frame max |y| into the output's slots.
+template <class S, int MF, class AccT>
+__device__ __forceinline__ void x6_epilogue(const ConvArgs& a, AccT (&acc)[S::TM][S::TN], int m0, int n0, int wm,
+                                            int wn, int tid, int lane, char* smem, int amax_off) {
+    constexpr int BM = S::BM, BN = S::BNV, NT = S::NT, TM = S::TM, TN = S::TN, TERMS = S::TERMSV;
+    const int ohw = a.yh * a.yw;
+    // ---- fused epilogue: BM / EPR passes of EPR rows through LDS ([EPR][BN+4] f32)
+    constexpr int EPLD = S::EPLD, EPR = S::EPR, CG = BN / 8, ITEMS = EPR * CG / NT;
+    static_assert(ITEMS >= 1 && (EPR * CG) % NT == 0, "epilogue items");
+    float* ep = (float*)smem;
+    const bool vec_ok = ((a.cout & 7) == 0) && ((a.ldy & 7) == 0) && ((a.ycoff & 7) == 0) &&
+                        (a.res_mode == VD_RES_NONE || (((a.res_ld | a.res_coff) & 7) == 0));
+    unsigned* s_amax = (unsigned*)(smem + amax_off);   // per-frame max |y| of this tile (a.ymax)
+    int tfb = -1;                                      // this thread's first frame and its running max;
+    float tmax = 0.f;                                  // items of a later frame go to LDS directly (rare)
+#pragma unroll
+    for (int h = 0; h < BM / EPR; ++h) {
+        if (h) __syncthreads();
+        const int wrow = wm * S::WTM - h * EPR;        // this wave's first row within the pass
+        if (wrow >= 0 && wrow < EPR) {
+            if constexpr (MF == 32) {   // 32x32 C layout: row 8 (r / 4) + 4 (l / 32) + r % 4, column l % 32
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r)
+                            ep[(wrow + i * 32 + 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3)) * EPLD + wn * S::WTN +
+                               j * 32 + (lane & 31)] = acc[i][j][r];
+            } else {
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            ep[(wrow + i * 16 + (lane >> 4) * 4 + r) * EPLD + wn * S::WTN + j * 16 + (lane & 15)] =
+                                acc[i][j][r];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < ITEMS; ++q) {              // EPR rows x CG groups of 8 channels / NT threads
+            const int it = tid + NT * q;
+            const int rr = it / CG, cg = it % CG;
+            const int m = m0 + h * EPR + rr;
+            const int nb = n0 + cg * 8;
+            const bool valid = m < a.M && nb < a.cout;
+            const int fb = valid ? m / ohw : -1;
+            float vmax = 0.f;
+            if (valid) {
+            const float* er = ep + rr * EPLD + cg * 8;
+            const size_t yo = (size_t)m * a.ldy + a.ycoff + nb;
+            const float inv_sa = TERMS != 3 ? __builtin_ldexpf(1.f, -act_scale_exp(a, fb)) : 1.f;
+            size_t roff = 0;
+            if (a.res_mode != VD_RES_NONE) {
+                if (a.res_up) {
+                    const int b = m / ohw, rem = m - b * ohw;
+                    const int oy = rem / a.yw, ox = rem - oy * a.yw;
+                    roff = ((size_t)(b * a.rh + (oy >> 1)) * a.rw + (ox >> 1)) * a.res_ld + a.res_coff + nb;
+                } else {
+                    roff = (size_t)m * a.res_ld + a.res_coff + nb;
+                }
+            }
+            if (vec_ok) {
+                const float4 s0 = *(const float4*)(a.scale + nb), s1 = *(const float4*)(a.scale + nb + 4);
+                const float4 h0 = *(const float4*)(a.shift + nb), h1 = *(const float4*)(a.shift + nb + 4);
+                const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+                const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+                const float4 e0 = *(const float4*)er, e1 = *(const float4*)(er + 4);
+                const float ev[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+                float rv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+                if (a.res_mode != VD_RES_NONE) {
+                    const float4 r0 = *(const float4*)((const float*)a.res + roff);
+                    const float4 r1 = *(const float4*)((const float*)a.res + roff + 4);
+                    rv[0] = r0.x; rv[1] = r0.y; rv[2] = r0.z; rv[3] = r0.w;
+                    rv[4] = r1.x; rv[5] = r1.y; rv[6] = r1.z; rv[7] = r1.w;
+                }
+                float v[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    float t = (ev[e] * inv_sa) * sc[e] + sh[e];
+                    if (a.res_mode == VD_RES_PRE_ACT) t += rv[e];
+                    t = act_apply(t, a.act, a.slope);
+                    if (a.res_mode == VD_RES_POST_ACT) t += rv[e];
+                    v[e] = t;
+                    vmax = fmaxf(vmax, fabsf(t));
+                }
+                *(float4*)((float*)a.y + yo) = make_float4(v[0], v[1], v[2], v[3]);
+                *(float4*)((float*)a.y + yo + 4) = make_float4(v[4], v[5], v[6], v[7]);
+            } else {
+                for (int e = 0; e < 8 && nb + e < a.cout; ++e) {
+                    const int n = nb + e;
+                    float t = (er[e] * inv_sa) * a.scale[n] + a.shift[n];
+                    const float rv = a.res_mode != VD_RES_NONE ? ((const float*)a.res)[roff + e] : 0.f;
+                    if (a.res_mode == VD_RES_PRE_ACT) t += rv;
+                    t = act_apply(t, a.act, a.slope);
+                    if (a.res_mode == VD_RES_POST_ACT) t += rv;
+                    ((float*)a.y)[yo + e] = t;
+                    vmax = fmaxf(vmax, fabsf(t));
+                }
+            }
+            }   // valid
+            if (valid && a.ymax) {
+                if (tfb < 0) tfb = fb;
+                if (fb == tfb) tmax = fmaxf(tmax, vmax);
+                else if (vmax > 0.f) atomicMax(s_amax + fb, __float_as_uint(vmax));
+            }
+        }
+    }
+    if (a.ymax) {
+        amax_lds_add(s_amax, tfb, tmax);
+        __syncthreads();
+        amax_lds_flush(s_amax, a.ymax, a.B);
+    }
 }
 
 template <int BM, int BN, int NT, int NST, int TERMS, int MF>
@@ -477,115 +596,211 @@ __global__ __launch_bounds__(NT, NT == 256 && BM == 256 ? 1 : 2) void conv_x6_ke
     }
     __syncthreads();
 
-    // ---- fused epilogue: BM / EPR passes of EPR rows through LDS ([EPR][BN+4] f32)
-    constexpr int EPLD = S::EPLD, EPR = S::EPR, CG = BN / 8, ITEMS = EPR * CG / NT;
-    static_assert(ITEMS >= 1 && (EPR * CG) % NT == 0, "epilogue items");
-    float* ep = (float*)smem;
-    const bool vec_ok = ((a.cout & 7) == 0) && ((a.ldy & 7) == 0) && ((a.ycoff & 7) == 0) &&
-                        (a.res_mode == VD_RES_NONE || (((a.res_ld | a.res_coff) & 7) == 0));
-    unsigned* s_amax = (unsigned*)(smem + S::LDS);     // per-frame max |y| of this tile (a.ymax)
-    int tfb = -1;                                      // this thread's first frame and its running max;
-    float tmax = 0.f;                                  // items of a later frame go to LDS directly (rare)
+    x6_epilogue<S, MF>(a, acc, m0, n0, wm, wn, tid, lane, smem, S::LDS);
+}
+
+// ---------------------------------------------------------------------------
+// 3x3 / stride 1 / pad 1 convs on fp16 pairs with the input split ONCE per 32-channel
+// chunk (option x6_halo). The 256 output rows of a tile are 256 consecutive pixels
+// m0..m0+255 (any frames); tap (dy, dx) of row r reads input pixel m + dy W + dx, so
+// all nine taps of a chunk read inside the linear "halo" m0 - W - 1 .. m0 + 256 + W.
+// The K loop runs chunk-major (chunk c, then its nine taps): the halo's f32 rows of
+// chunk c are loaded once (registers, during chunk c-1's taps), split into fp16
+// hi / lo planes once and written to LDS; each tap's A fragments are then halo rows
+// shifted by dy W + dx, a padded tap (off the frame's rows or columns, or past M)
+// reads a zero row instead -- the per-lane row address carries the padding. The
+// conv_x6_kernel path splits every input element nine times (once per tap) and
+// loads it nine times; B (the pre-split weights of tap t, chunk c = K tile t CH + c)
+// arrives by LDS-DMA into NSB stages: with two, two barriers per K tile as there;
+// with three, the stage a DMA refills was last read two tiles ago, so one barrier per
+// K tile (plus one per chunk before the halo is rewritten). Same products, same f32
+// accumulation, K summed in another order (chunk-major instead of tap-major).
+template <int BN, int NSB>
+__global__ __launch_bounds__(512, 2) void conv_x6_halo_kernel(ConvArgs a) {
+    using S = X6Shape<256, BN, 512, 2, 2>;
+    constexpr int BM = 256, NT = 512, TM = S::TM, TN = S::TN, WAVES = S::WAVES, PL_B = S::PL_B;
+    constexpr int QI = 4;                           // halo items (row, 8 channels) per thread: HR <= 512
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid / S::WAVES_N, wn = wid % S::WAVES_N;
+    const int nwg = gridDim.x, bid = blockIdx.x;
+    const int q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
+    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    const int tn = wg % a.ntiles_n, tm = wg / a.ntiles_n;
+    const int m0 = a.mbase + tm * BM, n0 = tn * BN;
+    const int W = a.yw, H = a.yh, HW = H * W;
+    const int HR = BM + 2 * W + 2, HP = HR + 1;     // halo rows + one zero row (index HR)
+    const int PL_H = HP * 64;
+    char* Ah = smem + NSB * 2 * PL_B;               // after the B stages
+    const int CH = a.cin_pad / 32, nsteps = 9 * CH, nk = a.kpad / KT;
+
+    // ---- halo staging: item i = tid + NT q: row hr = i >> 2, 8 channels pr = i & 3
+    const long xbytes = (long)a.B * a.xh * a.xw * a.ldx * 4;
+    const __amdgpu_buffer_rsrc_t rsrc_x = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, (int)xbytes, 0x00020000);
+    int hoff[QI];                                    // element offset of the item's pixel + channels
+    float hsa[QI];
 #pragma unroll
-    for (int h = 0; h < BM / EPR; ++h) {
-        if (h) __syncthreads();
-        const int wrow = wm * S::WTM - h * EPR;        // this wave's first row within the pass
-        if (wrow >= 0 && wrow < EPR) {
-            if constexpr (MF == 32) {   // 32x32 C layout: row 8 (r / 4) + 4 (l / 32) + r % 4, column l % 32
+    for (int q = 0; q < QI; ++q) {
+        const int it = tid + NT * q, hr = it >> 2, pr = it & 3;
+        const int pix = m0 - W - 1 + hr;
+        const bool ok = hr < HR && pix >= 0 && pix < a.M;
+        hoff[q] = ok ? pix * a.ldx + a.xcoff + pr * 8 : -1;
+        hsa[q] = ok ? __builtin_ldexpf(1.f, act_scale_exp(a, pix / HW)) : 1.f;
+    }
+    u32x4 hx[QI][2];
+    auto load_halo = [&](int c) {
 #pragma unroll
-                for (int i = 0; i < TM; ++i)
+        for (int q = 0; q < QI; ++q) {
+            const unsigned off = hoff[q] >= 0 ? (unsigned)(hoff[q] + c * KT) * 4u : 0x80000000u;
+            hx[q][0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc_x, (int)off, 0, 0));
+            hx[q][1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc_x, (int)off, 16, 0));
+        }
+    };
+    auto store_halo = [&]() {
 #pragma unroll
-                    for (int j = 0; j < TN; ++j)
+        for (int q = 0; q < QI; ++q) {
+            const int it = tid + NT * q, hr = it >> 2, pr = it & 3;
+            if (hr < HR) {
+                float e[8];
 #pragma unroll
-                        for (int r = 0; r < 16; ++r)
-                            ep[(wrow + i * 32 + 8 * (r >> 2) + 4 * (lane >> 5) + (r & 3)) * EPLD + wn * S::WTN +
-                               j * 32 + (lane & 31)] = acc[i][j][r];
-            } else {
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int j = 0; j < TN; ++j)
-#pragma unroll
-                        for (int r = 0; r < 4; ++r)
-                            ep[(wrow + i * 16 + (lane >> 4) * 4 + r) * EPLD + wn * S::WTN + j * 16 + (lane & 15)] =
-                                acc[i][j][r];
+                for (int j = 0; j < 4; ++j) {
+                    e[j] = __uint_as_float(hx[q][0][j]);
+                    e[4 + j] = __uint_as_float(hx[q][1][j]);
+                }
+                u32x4 o[3];
+                split_pack<2>(e, hsa[q], o);
+                *(u32x4*)(Ah + swz(hr, pr)) = o[0];
+                *(u32x4*)(Ah + PL_H + swz(hr, pr)) = o[1];
             }
         }
-        __syncthreads();
+    };
+
+    // ---- B: LDS-DMA as conv_x6_kernel, K tile of step s = tap * CH + chunk
+    constexpr int RB = BN / 16, NDMA = S::NDMA;
+    const int my_dma = NDMA / WAVES + (wid < NDMA % WAVES ? 1 : 0);
+    const __amdgpu_buffer_rsrc_t rsrc_w = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7fffffff, 0x00020000);
+    auto dma_b = [&](int s, int st) {
+        const int c = s / 9, kt = (s - 9 * c) * CH + c;
+        char* Bs = smem + st * 2 * PL_B;
 #pragma unroll
-        for (int q = 0; q < ITEMS; ++q) {              // EPR rows x CG groups of 8 channels / NT threads
-            const int it = tid + NT * q;
-            const int rr = it / CG, cg = it % CG;
-            const int m = m0 + h * EPR + rr;
-            const int nb = n0 + cg * 8;
-            const bool valid = m < a.M && nb < a.cout;
-            const int fb = valid ? m / ohw : -1;
-            float vmax = 0.f;
-            if (valid) {
-            const float* er = ep + rr * EPLD + cg * 8;
-            const size_t yo = (size_t)m * a.ldy + a.ycoff + nb;
-            const float inv_sa = TERMS != 3 ? __builtin_ldexpf(1.f, -act_scale_exp(a, fb)) : 1.f;
-            size_t roff = 0;
-            if (a.res_mode != VD_RES_NONE) {
-                if (a.res_up) {
-                    const int b = m / ohw, rem = m - b * ohw;
-                    const int oy = rem / a.yw, ox = rem - oy * a.yw;
-                    roff = ((size_t)(b * a.rh + (oy >> 1)) * a.rw + (ox >> 1)) * a.res_ld + a.res_coff + nb;
-                } else {
-                    roff = (size_t)m * a.res_ld + a.res_coff + nb;
-                }
-            }
-            if (vec_ok) {
-                const float4 s0 = *(const float4*)(a.scale + nb), s1 = *(const float4*)(a.scale + nb + 4);
-                const float4 h0 = *(const float4*)(a.shift + nb), h1 = *(const float4*)(a.shift + nb + 4);
-                const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-                const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
-                const float4 e0 = *(const float4*)er, e1 = *(const float4*)(er + 4);
-                const float ev[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
-                float rv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-                if (a.res_mode != VD_RES_NONE) {
-                    const float4 r0 = *(const float4*)((const float*)a.res + roff);
-                    const float4 r1 = *(const float4*)((const float*)a.res + roff + 4);
-                    rv[0] = r0.x; rv[1] = r0.y; rv[2] = r0.z; rv[3] = r0.w;
-                    rv[4] = r1.x; rv[5] = r1.y; rv[6] = r1.z; rv[7] = r1.w;
-                }
-                float v[8];
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    float t = (ev[e] * inv_sa) * sc[e] + sh[e];
-                    if (a.res_mode == VD_RES_PRE_ACT) t += rv[e];
-                    t = act_apply(t, a.act, a.slope);
-                    if (a.res_mode == VD_RES_POST_ACT) t += rv[e];
-                    v[e] = t;
-                    vmax = fmaxf(vmax, fabsf(t));
-                }
-                *(float4*)((float*)a.y + yo) = make_float4(v[0], v[1], v[2], v[3]);
-                *(float4*)((float*)a.y + yo + 4) = make_float4(v[4], v[5], v[6], v[7]);
-            } else {
-                for (int e = 0; e < 8 && nb + e < a.cout; ++e) {
-                    const int n = nb + e;
-                    float t = (er[e] * inv_sa) * a.scale[n] + a.shift[n];
-                    const float rv = a.res_mode != VD_RES_NONE ? ((const float*)a.res)[roff + e] : 0.f;
-                    if (a.res_mode == VD_RES_PRE_ACT) t += rv;
-                    t = act_apply(t, a.act, a.slope);
-                    if (a.res_mode == VD_RES_POST_ACT) t += rv;
-                    ((float*)a.y)[yo + e] = t;
-                    vmax = fmaxf(vmax, fabsf(t));
-                }
-            }
-            }   // valid
-            if (valid && a.ymax) {
-                if (tfb < 0) tfb = fb;
-                if (fb == tfb) tmax = fmaxf(tmax, vmax);
-                else if (vmax > 0.f) atomicMax(s_amax + fb, __float_as_uint(vmax));
+        for (int q = 0; q < (NDMA + WAVES - 1) / WAVES; ++q) {
+            const int j = wid + WAVES * q;
+            if (j < NDMA) {
+                const int p = j / RB, r0 = (j % RB) * 16;
+                const int row = r0 + (lane >> 2), slot = lane & 3;
+                const int chunk = slot ^ (((row >> 3) & 1) * 3);
+                const unsigned off = (unsigned)((((long)(n0 + row) * nk + kt) * 2 + p) * 64 + chunk * 16);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_w, (lds_void_t*)(Bs + p * PL_B + r0 * 64), 16, off, 0,
+                                                         0, 0);
             }
         }
+    };
+
+    // ---- per-lane A rows: this lane's output row of each fragment i, its halo row for
+    // tap (0, 0) and which neighbours exist (bit 0 y-1, 1 y+1, 2 x-1, 3 x+1, 4 row < M)
+    int arow[TM], aflg[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int r = wm * S::WTM + i * 16 + (lane & 15), m = m0 + r;
+        const int rem = m % HW, y = rem / W, x = rem - y * W;
+        arow[i] = r + W + 1;
+        aflg[i] = (y > 0 ? 1 : 0) | (y < H - 1 ? 2 : 0) | (x > 0 ? 4 : 0) | (x < W - 1 ? 8 : 0) | (m < a.M ? 16 : 0);
     }
-    if (a.ymax) {
-        amax_lds_add(s_amax, tfb, tmax);
-        __syncthreads();
-        amax_lds_flush(s_amax, a.ymax, a.B);
+
+    using AccT = f32x4_t;
+    AccT acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = AccT{};
+    const int amax_off = std::max(NSB * 2 * PL_B + 2 * PL_H, S::EPR * S::EPLD * 4);
+    if (a.ymax)
+        for (int f = tid; f < a.B; f += NT) ((unsigned*)(smem + amax_off))[f] = 0u;
+
+    auto compute = [&](int st, int dy, int dx) {
+        const char* Bs = smem + st * 2 * PL_B;
+        const int ch = lane >> 4;
+        const int need = (dy < 0 ? 1 : 0) | (dy > 0 ? 2 : 0) | (dx < 0 ? 4 : 0) | (dx > 0 ? 8 : 0) | 16;
+        const int shift = dy * W + dx;
+        u32x4 af[TM][3];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int hr = (aflg[i] & need) == need ? arow[i] + shift : HR;
+            const int o = swz(hr, ch);
+            af[i][0] = *(const u32x4*)(Ah + o);
+            af[i][1] = *(const u32x4*)(Ah + PL_H + o);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            u32x4 bf[3];
+            bf[0] = *(const u32x4*)(Bs + swz(wn * S::WTN + j * 16 + (lane & 15), ch));
+            bf[1] = *(const u32x4*)(Bs + PL_B + swz(wn * S::WTN + j * 16 + (lane & 15), ch));
+#pragma unroll
+            for (int i = 0; i < TM; ++i) acc[i][j] = mfma_terms<2>(af[i], bf, acc[i][j]);
+        }
+    };
+
+    // ---- prologue: chunk 0's halo in LDS (+ the zero row), B of steps 0 and 1 in flight,
+    // chunk 1's halo loading into registers
+    load_halo(0);
+    store_halo();
+    if (tid < 8) *(u32x4*)(Ah + (tid >> 2) * PL_H + swz(HR, tid & 3)) = u32x4{0u, 0u, 0u, 0u};
+    dma_b(0, 0);
+    if (nsteps > 1) dma_b(1, 1);
+    if (CH > 1) load_halo(1);
+    // Per thread VMEM issue order: ... [halo loads of chunk c+2 at the end of step
+    // 9c+8], B(s+2) at the end of step s. At the top of step s, younger than B(s):
+    // B(s+1) (if issued) and the halo loads issued at the end of step s-1 or (s = 1)
+    // in the prologue after B(1).
+    if constexpr (NSB == 3) {
+        // VMEM issue order per step s: [top] B(s+2); [end, tap 8] halo loads of chunk
+        // c+2. Younger than B(s) (issued at the top of s-2): B(s+1) and the halo loads
+        // issued at the end of s-2 or s-1 (the prologue's chunk-1 loads count as "end
+        // of step -1").
+        auto halo_after = [&](int j) { return j == -1 ? CH > 1 : (j >= 0 && j % 9 == 8 && j / 9 + 2 < CH); };
+        for (int s = 0; s < nsteps; ++s) {
+            const int c = s / 9, tap = s - 9 * c;
+            const int younger = (s + 1 < nsteps ? my_dma : 0) + 2 * QI * ((halo_after(s - 2) ? 1 : 0) +
+                                                                          (halo_after(s - 1) ? 1 : 0));
+            wait_vm(younger);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();                // B(s) visible; stage (s + 2) % 3 free
+            asm volatile("" ::: "memory");
+            if (s + 2 < nsteps) dma_b(s + 2, (s + 2) % 3);
+            const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
+            compute(s % 3, dy, dx);
+            if (tap == 8 && c + 1 < CH) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();            // every wave is done with chunk c's halo
+                asm volatile("" ::: "memory");
+                store_halo();
+                if (c + 2 < CH) load_halo(c + 2);
+            }
+        }
+    } else
+    for (int s = 0; s < nsteps; ++s) {
+        const int c = s / 9, tap = s - 9 * c;
+        int younger = s + 1 < nsteps ? my_dma : 0;
+        if (s == 0 && CH > 1) younger += 2 * QI;
+        if (s == 1 && CH > 1) younger = 2 * QI + (s + 1 < nsteps ? my_dma : 0);
+        if (s >= 2 && tap == 0 && c + 1 < CH) younger += 2 * QI;
+        wait_vm(younger);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
+        compute(s & 1, dy, dx);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();                    // stage s & 1 (and, at tap 8, the halo) are free
+        asm volatile("" ::: "memory");
+        if (tap == 8 && c + 1 < CH) {
+            store_halo();                                // chunk c+1 (its loads were issued 9 steps ago)
+            if (c + 2 < CH) load_halo(c + 2);
+        }
+        if (s + 2 < nsteps) dma_b(s + 2, s & 1);
     }
+    __syncthreads();
+    x6_epilogue<S, 16>(a, acc, m0, n0, wm, wn, tid, lane, smem, amax_off);
 }
 
 // ---------------------------------------------------------------------------
@@ -1006,6 +1221,48 @@ static hipError_t launch_x6_big(const ConvArgs& a, hipStream_t s) {
     return launch_x6<256, BN2, 512, 2, TERMS, MF>(a, s, mb);
 }
 
+template <int BN, int NSB>
+static int x6_halo_lds(const ConvArgs& a) {
+    using S = X6Shape<256, BN, 512, 2, 2>;
+    const int HP = 256 + 2 * a.yw + 3;
+    return std::max(NSB * 2 * S::PL_B + 2 * HP * 64, S::EPR * S::EPLD * 4) + (a.ymax ? 4 * a.B : 0);
+}
+
+template <int BN, int NSB>
+static hipError_t launch_x6_halo_n(const ConvArgs& a0, hipStream_t s) {
+    ConvArgs a = a0;
+    a.w = a.wx3;
+    a.ntiles_n = (a.cout + BN - 1) / BN;
+    a.mbase = 0;
+    static const bool attr = [] {
+        (void)hipFuncSetAttribute((const void*)conv_x6_halo_kernel<BN, NSB>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        return true;
+    }();
+    (void)attr;
+    const int lds = x6_halo_lds<BN, NSB>(a);
+    if (lds > 160 * 1024) return hipErrorInvalidValue;
+    const int mt = (a.M + 255) / 256;
+    hipLaunchKernelGGL((conv_x6_halo_kernel<BN, NSB>), dim3(mt * a.ntiles_n), dim3(512), lds, s, a);
+    return hipGetLastError();
+}
+
+// option x6_halo: 1 two B stages, 2 three where they fit LDS beside the halo
+template <int BN>
+static hipError_t launch_x6_halo(const ConvArgs& a, hipStream_t s) {
+    if (a.tune->x6_halo >= 2 && x6_halo_lds<BN, 3>(a) <= 160 * 1024) return launch_x6_halo_n<BN, 3>(a, s);
+    return launch_x6_halo_n<BN, 2>(a, s);
+}
+
+// 3x3 / stride 1 / pad 1, same-size in and out, K = 9 x Cin in whole 32-channel chunks,
+// halo of at most 512 rows (W <= 126) that fits LDS beside the B stages
+static bool x6_halo_ok(const ConvArgs& a) {
+    if (!a.tune || !a.tune->x6_halo || a.kh != 3 || a.kw != 3 || a.stride != 1 || a.pad != 1) return false;
+    if (a.xh != a.yh || a.xw != a.yw || a.cin_pad % 32 || a.kpad != 9 * a.cin_pad) return false;
+    if (256 + 2 * a.yw + 2 > 512 || (a.ymax && a.B > kAmaxFrames)) return false;
+    return true;
+}
+
 // N tile follows Cout (weights are packed with Npad a multiple of 128, so every
 // tile's rows exist): 32 for the heads, 64 for the 64-channel convs, else 128.
 // The small single-stage tile takes the narrow (N <= 64) layers with K <= 256 or
@@ -1095,14 +1352,19 @@ static hipError_t launch_terms(const ConvArgs& a0, hipStream_t s) {
         // 100 tiles, 137 -> 199 us)
         const long t256 = (long)((a.M + 255) / 256) * (a.cout / 256);
         if (a.tune && a.tune->x6_bn256 && a.cout % 256 == 0 && t256 >= 192) {
+            if (x6_halo_ok(a)) return launch_x6_halo<256>(a, s);
             if (a.tune->x6_mf32) return launch_x6<256, 256, 512, 2, TERMS, 32>(a, s);
             return launch_x6_big<256, TERMS>(a, s);
         }
         // Cout 192 (the fused SSH conv5X5_1 + conv3X3): one 192-wide N tile instead of two
         // 128-wide ones with a quarter of the MFMAs on padding rows (level 0 1716 -> 1264 us,
         // level 1 526 -> 396; not for level 2's 100 tiles: 137 -> 178)
-        if (a.tune && a.tune->x6_bn256 && a.cout == 192 && (a.M + 255) / 256 >= 192)
+        if (a.tune && a.tune->x6_bn256 && a.cout == 192 && (a.M + 255) / 256 >= 192) {
+            if (x6_halo_ok(a)) return launch_x6_halo<192>(a, s);
             return launch_x6_big<192, TERMS>(a, s);
+        }
+        // every eligible layer on the halo form whatever the batch (its K order differs)
+        if (x6_halo_ok(a)) return launch_x6_halo<128>(a, s);
         if (a.tune && a.tune->x6_mf32) return launch_x6<256, 128, 512, 2, TERMS, 32>(a, s);
     }
     return launch_x6_big<128, TERMS>(a, s);
