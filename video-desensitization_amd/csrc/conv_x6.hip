@@ -615,6 +615,12 @@ __global__ __launch_bounds__(NT, NT == 256 && BM == 256 ? 1 : 2) void conv_x6_ke
 // with three, the stage a DMA refills was last read two tiles ago, so one barrier per
 // K tile (plus one per chunk before the halo is rewritten). Same products, same f32
 // accumulation, K summed in another order (chunk-major instead of tap-major).
+// Halo planes: A fragments start at any row (base + dy W + dx), so the chunk swizzle
+// keys on row bit 2 -- conflict-free ds_read_b128 fragment reads (16 rows, two chunks
+// per lane group) for every start row, where swz's bit-3 key is conflict-free only
+// for starts that are multiples of 8 (checked exhaustively over the 8 start residues)
+__device__ __forceinline__ int swzh(int row, int chunk) { return row * 64 + ((chunk ^ (((row >> 2) & 1) << 1)) << 4); }
+
 template <int BN, int NSB>
 __global__ __launch_bounds__(512, 2) void conv_x6_halo_kernel(ConvArgs a) {
     using S = X6Shape<256, BN, 512, 2, 2>;
@@ -669,8 +675,8 @@ __global__ __launch_bounds__(512, 2) void conv_x6_halo_kernel(ConvArgs a) {
                 }
                 u32x4 o[3];
                 split_pack<2>(e, hsa[q], o);
-                *(u32x4*)(Ah + swz(hr, pr)) = o[0];
-                *(u32x4*)(Ah + PL_H + swz(hr, pr)) = o[1];
+                *(u32x4*)(Ah + swzh(hr, pr)) = o[0];
+                *(u32x4*)(Ah + PL_H + swzh(hr, pr)) = o[1];
             }
         }
     };
@@ -726,7 +732,7 @@ __global__ __launch_bounds__(512, 2) void conv_x6_halo_kernel(ConvArgs a) {
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
             const int hr = (aflg[i] & need) == need ? arow[i] + shift : HR;
-            const int o = swz(hr, ch);
+            const int o = swzh(hr, ch);
             af[i][0] = *(const u32x4*)(Ah + o);
             af[i][1] = *(const u32x4*)(Ah + PL_H + o);
         }
@@ -744,7 +750,7 @@ __global__ __launch_bounds__(512, 2) void conv_x6_halo_kernel(ConvArgs a) {
     // chunk 1's halo loading into registers
     load_halo(0);
     store_halo();
-    if (tid < 8) *(u32x4*)(Ah + (tid >> 2) * PL_H + swz(HR, tid & 3)) = u32x4{0u, 0u, 0u, 0u};
+    if (tid < 8) *(u32x4*)(Ah + (tid >> 2) * PL_H + swzh(HR, tid & 3)) = u32x4{0u, 0u, 0u, 0u};
     dma_b(0, 0);
     if (nsteps > 1) dma_b(1, 1);
     if (CH > 1) load_halo(1);
@@ -753,28 +759,30 @@ __global__ __launch_bounds__(512, 2) void conv_x6_halo_kernel(ConvArgs a) {
     // B(s+1) (if issued) and the halo loads issued at the end of step s-1 or (s = 1)
     // in the prologue after B(1).
     if constexpr (NSB == 3) {
-        // VMEM issue order per step s: [top] B(s+2); [end, tap 8] halo loads of chunk
-        // c+2. Younger than B(s) (issued at the top of s-2): B(s+1) and the halo loads
-        // issued at the end of s-2 or s-1 (the prologue's chunk-1 loads count as "end
-        // of step -1").
-        auto halo_after = [&](int j) { return j == -1 ? CH > 1 : (j >= 0 && j % 9 == 8 && j / 9 + 2 < CH); };
+        // VMEM issue order per step s: [top] B(s+2), except on tap-8 steps, which issue
+        // it at the end, after the halo loads of chunk c+2 (the halo stores then wait
+        // only on B(s+1), issued a step earlier, not on a DMA just issued). Younger than
+        // B(s) at the top of s: B(s+1) and the halo loads issued at the end of s-1 (the
+        // prologue's chunk-1 loads follow B(1), so for s = 0 and 1 too).
         for (int s = 0; s < nsteps; ++s) {
             const int c = s / 9, tap = s - 9 * c;
-            const int younger = (s + 1 < nsteps ? my_dma : 0) + 2 * QI * ((halo_after(s - 2) ? 1 : 0) +
-                                                                          (halo_after(s - 1) ? 1 : 0));
+            const bool halo_prev = (s >= 1 && (s - 1) % 9 == 8 && (s - 1) / 9 + 2 < CH) || (s <= 1 && CH > 1);
+            const int younger = (s + 1 < nsteps ? my_dma : 0) + (halo_prev ? 2 * QI : 0);
             wait_vm(younger);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();                // B(s) visible; stage (s + 2) % 3 free
             asm volatile("" ::: "memory");
-            if (s + 2 < nsteps) dma_b(s + 2, (s + 2) % 3);
+            const bool rehalo = tap == 8 && c + 1 < CH;
+            if (!rehalo && s + 2 < nsteps) dma_b(s + 2, (s + 2) % 3);
             const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
             compute(s % 3, dy, dx);
-            if (tap == 8 && c + 1 < CH) {
+            if (rehalo) {
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 __builtin_amdgcn_s_barrier();            // every wave is done with chunk c's halo
                 asm volatile("" ::: "memory");
                 store_halo();
                 if (c + 2 < CH) load_halo(c + 2);
+                if (s + 2 < nsteps) dma_b(s + 2, (s + 2) % 3);
             }
         }
     } else

@@ -61,8 +61,8 @@ struct VdTune {
                               //   output's K order, so results do not depend on the split. Measured
                               //   slower (27.6 -> 28.5 / 28.9 ms per step for 1 / 2): the narrow tiles
                               //   fetch more per FLOP, and a partial round's workgroups run faster alone
-    int x6_halo = 1;          // fp16 pairs, 3x3 stride-1 convs: input split once per 32-channel chunk
-                              //   over the tile's linear halo (conv_x6_halo_kernel)
+    int x6_halo = 2;          // fp16 pairs, 3x3 stride-1 convs: input split once per 32-channel chunk
+                              //   over the tile's linear halo (conv_x6_halo_kernel); 2: three B stages, 1: two
     int x6_slots = 0;         //   workgroup slots of one round (0: the CU count; tests force small values)
     int f32_split = 2;        // plan (fp32, at weight load): 2 = operands scaled by powers of two
                               //   and split into fp16 pairs, 3 products on the f16 matrix cores;
