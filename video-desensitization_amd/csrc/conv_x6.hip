@@ -622,7 +622,7 @@ __global__ __launch_bounds__(NT, NT == 256 && BM == 256 ? 1 : 2) void conv_x6_ke
 __device__ __forceinline__ int swzh(int row, int chunk) { return row * 64 + ((chunk ^ (((row >> 2) & 1) << 1)) << 4); }
 
 template <int BN, int NSB>
-__global__ __launch_bounds__(512, 2) void conv_x6_halo_kernel(ConvArgs a) {
+__global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(ConvArgs a) {
     using S = X6Shape<256, BN, 512, 2, 2>;
     constexpr int BM = 256, NT = 512, TM = S::TM, TN = S::TN, WAVES = S::WAVES, PL_B = S::PL_B;
     constexpr int QI = 4;                           // halo items (row, 8 channels) per thread: HR <= 512
@@ -644,14 +644,14 @@ __global__ __launch_bounds__(512, 2) void conv_x6_halo_kernel(ConvArgs a) {
     const long xbytes = (long)a.B * a.xh * a.xw * a.ldx * 4;
     const __amdgpu_buffer_rsrc_t rsrc_x = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, (int)xbytes, 0x00020000);
     int hoff[QI];                                    // element offset of the item's pixel + channels
-    float hsa[QI];
+    unsigned hexp = 0;                              // the items' frame scale exponents, a byte each
 #pragma unroll
     for (int q = 0; q < QI; ++q) {
         const int it = tid + NT * q, hr = it >> 2, pr = it & 3;
         const int pix = m0 - W - 1 + hr;
         const bool ok = hr < HR && pix >= 0 && pix < a.M;
         hoff[q] = ok ? pix * a.ldx + a.xcoff + pr * 8 : -1;
-        hsa[q] = ok ? __builtin_ldexpf(1.f, act_scale_exp(a, pix / HW)) : 1.f;
+        hexp |= (unsigned)((ok ? act_scale_exp(a, pix / HW) : 0) & 0xff) << (8 * q);
     }
     u32x4 hx[QI][2];
     auto load_halo = [&](int c) {
@@ -674,7 +674,8 @@ __global__ __launch_bounds__(512, 2) void conv_x6_halo_kernel(ConvArgs a) {
                     e[4 + j] = __uint_as_float(hx[q][1][j]);
                 }
                 u32x4 o[3];
-                split_pack<2>(e, hsa[q], o);
+                const int ex = (int)(signed char)((hexp >> (8 * q)) & 0xff);
+                split_pack<2>(e, __builtin_ldexpf(1.f, ex), o);
                 *(u32x4*)(Ah + swzh(hr, pr)) = o[0];
                 *(u32x4*)(Ah + PL_H + swzh(hr, pr)) = o[1];
             }
@@ -728,21 +729,40 @@ __global__ __launch_bounds__(512, 2) void conv_x6_halo_kernel(ConvArgs a) {
         const int ch = lane >> 4;
         const int need = (dy < 0 ? 1 : 0) | (dy > 0 ? 2 : 0) | (dx < 0 ? 4 : 0) | (dx > 0 ? 8 : 0) | 16;
         const int shift = dy * W + dx;
-        u32x4 af[TM][3];
+        if constexpr (TN < TM) {   // narrow N: B fragments resident, A streamed (VGPRs at 4 waves / SIMD)
+            u32x4 bf[TN][3];
 #pragma unroll
-        for (int i = 0; i < TM; ++i) {
-            const int hr = (aflg[i] & need) == need ? arow[i] + shift : HR;
-            const int o = swzh(hr, ch);
-            af[i][0] = *(const u32x4*)(Ah + o);
-            af[i][1] = *(const u32x4*)(Ah + PL_H + o);
-        }
+            for (int j = 0; j < TN; ++j) {
+                bf[j][0] = *(const u32x4*)(Bs + swz(wn * S::WTN + j * 16 + (lane & 15), ch));
+                bf[j][1] = *(const u32x4*)(Bs + PL_B + swz(wn * S::WTN + j * 16 + (lane & 15), ch));
+            }
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            u32x4 bf[3];
-            bf[0] = *(const u32x4*)(Bs + swz(wn * S::WTN + j * 16 + (lane & 15), ch));
-            bf[1] = *(const u32x4*)(Bs + PL_B + swz(wn * S::WTN + j * 16 + (lane & 15), ch));
+            for (int i = 0; i < TM; ++i) {
+                const int hr = (aflg[i] & need) == need ? arow[i] + shift : HR;
+                const int o = swzh(hr, ch);
+                u32x4 af[3];
+                af[0] = *(const u32x4*)(Ah + o);
+                af[1] = *(const u32x4*)(Ah + PL_H + o);
 #pragma unroll
-            for (int i = 0; i < TM; ++i) acc[i][j] = mfma_terms<2>(af[i], bf, acc[i][j]);
+                for (int j = 0; j < TN; ++j) acc[i][j] = mfma_terms<2>(af, bf[j], acc[i][j]);
+            }
+        } else {
+            u32x4 af[TM][3];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int hr = (aflg[i] & need) == need ? arow[i] + shift : HR;
+                const int o = swzh(hr, ch);
+                af[i][0] = *(const u32x4*)(Ah + o);
+                af[i][1] = *(const u32x4*)(Ah + PL_H + o);
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                u32x4 bf[3];
+                bf[0] = *(const u32x4*)(Bs + swz(wn * S::WTN + j * 16 + (lane & 15), ch));
+                bf[1] = *(const u32x4*)(Bs + PL_B + swz(wn * S::WTN + j * 16 + (lane & 15), ch));
+#pragma unroll
+                for (int i = 0; i < TM; ++i) acc[i][j] = mfma_terms<2>(af[i], bf, acc[i][j]);
+            }
         }
     };
 
@@ -1338,6 +1358,10 @@ static hipError_t launch_terms(const ConvArgs& a0, hipStream_t s) {
     // (layer1 conv2 831 -> 603 us, SSH level-0 conv7X7 229 -> 163 us)
     const bool small = force_small || (bn <= 64 && (a.kpad <= (TERMS == 2 ? small_k2 : small_k) ||
                                                     big_tiles < small_tiles));
+    if constexpr (TERMS == 2) {   // narrow 3x3 stride-1 layers on the halo form too (two workgroups per CU)
+        if (bn <= 64 && a.tune && a.tune->x6_halo_narrow && x6_halo_ok(a))
+            return bn == 32 ? launch_x6_halo<32>(a, s) : launch_x6_halo<64>(a, s);
+    }
     if (small) {
         if (bn == 32) return launch_x6<128, 32, 256, 1, TERMS>(a, s);
         if constexpr (TERMS == 2) {   // the integer-valued face canvas: one A plane, two products (stem)
