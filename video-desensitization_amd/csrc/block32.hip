@@ -181,6 +181,27 @@ __global__ __launch_bounds__(512, 1) void bottleneck32_kernel(Block32Args a) {
     int ob = -1;            // output max bookkeeping: this wave's current frame and its max
     float om = 0.f;
 
+    // stage-1 x of halo pixel tiles w and 8 + w/2 (lane: pixel 16 p + li, channels 8 g..)
+    auto xoff = [&](int oy0, int ox0, int p, int li, int g) {
+        const int r = 16 * p + li;
+        const int hy = r / HWD, hx = r - hy * HWD;
+        const int iy = oy0 - 1 + hy, ix = ox0 - 1 + hx;
+        const bool in = r < HROWS && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
+        return in ? (unsigned)((iy * a.W + ix) * CIN + 8 * g) * 4u : 0x80000000u;
+    };
+    auto ldx = [&](__amdgpu_buffer_rsrc_t rx, unsigned offA, unsigned offB, int s, u32x4 (&ra)[2], u32x4 (&rb)[2]) {
+        const int so = s * 128;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            ra[q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, offA, so + 16 * q, 0));
+            rb[q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, offB, so + 16 * q, 0));
+        }
+    };
+    auto frame_rsrc = [&](int b) {
+        return __builtin_amdgcn_make_buffer_rsrc((void*)((const float*)a.x + (size_t)b * fpx * CIN), 0,
+                                                 (int)(fpx * CIN * 4), 0x00020000);
+    };
+
 #pragma unroll 1
     for (int t = t0; t < tend; t += tstep) {
         const int b = t / tpf, r0 = t - b * tpf;
@@ -188,8 +209,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck32_kernel(Block32Args a) {
         const int oy0 = ty * TH, ox0 = tx * TW;
         const int kx = scale_exp(__uint_as_float(a.xmax[b]));
         const float sax = __builtin_ldexpf(1.f, kx), invx = __builtin_ldexpf(1.f, -kx);
-        const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)((const float*)a.x + (size_t)b * fpx * CIN), 0, (int)(fpx * CIN * 4), 0x00020000);
+        const __amdgpu_buffer_rsrc_t rx = frame_rsrc(b);
         __syncthreads();   // B0: the previous tile is done with t1 / t2 / the max slots
         // lane coordinates made opaque per tile: keeps the per-lane LDS / global
         // addresses of the three stages from being hoisted out of the tile loop
@@ -200,32 +220,17 @@ __global__ __launch_bounds__(512, 1) void bottleneck32_kernel(Block32Args a) {
         float vA[4][4], vB[2][4];
         {
             const int pB = 8 + (w >> 1), hB = w & 1;
-            auto xoff = [&](int p) {
-                const int r = 16 * p + li;
-                const int hy = r / HWD, hx = r - hy * HWD;
-                const int iy = oy0 - 1 + hy, ix = ox0 - 1 + hx;
-                const bool in = r < HROWS && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
-                return in ? (unsigned)((iy * a.W + ix) * CIN + 8 * g) * 4u : 0x80000000u;
-            };
-            const unsigned offA = xoff(w), offB = xoff(pB);
+            const unsigned offA = xoff(oy0, ox0, w, li, g), offB = xoff(oy0, ox0, pB, li, g);
             f32x4_t accA[4], accB[2];
 #pragma unroll
             for (int c = 0; c < 4; ++c) accA[c] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int c = 0; c < 2; ++c) accB[c] = f32x4_t{0.f, 0.f, 0.f, 0.f};
             u32x4 xa[2][2], xb[2][2];                    // [set][half]: k-step s in set s & 1
-            auto ldx = [&](int s, u32x4 (&ra)[2], u32x4 (&rb)[2]) {
-                const int so = s * 128;
-#pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    ra[q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, offA, so + 16 * q, 0));
-                    rb[q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, offB, so + 16 * q, 0));
-                }
-            };
-            ldx(0, xa[0], xb[0]);
+            ldx(rx, offA, offB, 0, xa[0], xb[0]);
 #pragma unroll
             for (int s = 0; s < KS1; ++s) {
-                if (s + 1 < KS1) ldx(s + 1, xa[(s + 1) & 1], xb[(s + 1) & 1]);
+                if (s + 1 < KS1) ldx(rx, offA, offB, s + 1, xa[(s + 1) & 1], xb[(s + 1) & 1]);
                 u32x4 pa[2], pb[2];
                 split8(xa[s & 1][0], xa[s & 1][1], sax, pa);
                 split8(xb[s & 1][0], xb[s & 1][1], sax, pb);
@@ -376,39 +381,40 @@ __global__ __launch_bounds__(512, 1) void bottleneck32_kernel(Block32Args a) {
                             wdf[j][s][p] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rwd, lo, so, 0));
                     }
         }
+        // ---- stage 3 operands in flight across B5: the first identity row (below) ----
+        const int c0 = 32 * w + 8 * g;
+        const int ox = ox0 + li;
+        // per output row: identity x[px][c0..c0+7] (2 x 16 B), or the downsample
+        // input x[px][32 s + 8 g ..] (2 k-steps x 2 x 16 B); prefetched one row ahead
+        constexpr int NX = DS ? 4 : 2;
+        u32x4 xr[DS ? 1 : 2][NX];        // DS: no prefetch (registers)
+        auto ldr = [&](int m, u32x4 (&r)[NX]) {
+            const int oy = oy0 + m;
+            const bool in = oy < a.H && ox < a.W;
+            if constexpr (DS) {
+                const unsigned o = in ? (unsigned)((oy * a.W + ox) * CIN + 8 * g) * 4u : 0x80000000u;
+#pragma unroll
+                for (int s = 0; s < 2; ++s)
+#pragma unroll
+                    for (int q = 0; q < 2; ++q)
+                        r[2 * s + q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                            rx, o, s * 128 + 16 * q, 0));
+            } else {
+                const unsigned o = in ? (unsigned)((oy * a.W + ox) * CIN + c0) * 4u : 0x80000000u;
+#pragma unroll
+                for (int q = 0; q < 2; ++q)
+                    r[q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, o, 16 * q, 0));
+            }
+        };
+        if constexpr (!DS) ldr(0, xr[0]);
         __syncthreads();   // B5: t2 planes complete
 
         // ---- stage 3: out channels 32w + 8g .. +7 per lane, 8 output rows ----
         {
             const float inv2 = __builtin_ldexpf(1.f, -k2);
-            const int c0 = 32 * w + 8 * g;
-            const int ox = ox0 + li;
             const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
                 (void*)((float*)a.y + (size_t)b * fpx * CO), 0, (int)(fpx * CO * 4), 0x00020000);
             float om_t = 0.f;
-            // per output row: identity x[px][c0..c0+7] (2 x 16 B), or the downsample
-            // input x[px][32 s + 8 g ..] (2 k-steps x 2 x 16 B); prefetched one row ahead
-            constexpr int NX = DS ? 4 : 2;
-            u32x4 xr[DS ? 1 : 2][NX];            // DS: no prefetch (registers)
-            auto ldr = [&](int m, u32x4 (&r)[NX]) {
-                const int oy = oy0 + m;
-                const bool in = oy < a.H && ox < a.W;
-                if constexpr (DS) {
-                    const unsigned o = in ? (unsigned)((oy * a.W + ox) * CIN + 8 * g) * 4u : 0x80000000u;
-#pragma unroll
-                    for (int s = 0; s < 2; ++s)
-#pragma unroll
-                        for (int q = 0; q < 2; ++q)
-                            r[2 * s + q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                rx, o, s * 128 + 16 * q, 0));
-                } else {
-                    const unsigned o = in ? (unsigned)((oy * a.W + ox) * CIN + c0) * 4u : 0x80000000u;
-#pragma unroll
-                    for (int q = 0; q < 2; ++q)
-                        r[q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, o, 16 * q, 0));
-                }
-            };
-            if constexpr (!DS) ldr(0, xr[0]);
 #pragma unroll
             for (int m = 0; m < 8; ++m) {
                 __builtin_amdgcn_sched_barrier(0);   // keep rows apart (register pressure)
