@@ -47,7 +47,7 @@ def main(fetch_dir, write_dir, out=None, precision="bf16"):
     mw, mnw = per_launch_named(write_dir, "WRITE_SIZE", "mosaic_out_kernel")
     res = {
         "precision": precision,
-        "kernel": "RetinaFace conv launches on the face stream (" + ("conv_x6 / conv1x1_x6, fp32 plan (scaled fp16 pairs)" if precision == "fp32"
+        "kernel": "RetinaFace conv launches on the face stream (" + ("stem_pool32 / bottleneck32 / conv_x6 / conv_x6_halo / conv1x1_x6, fp32 plan (scaled fp16 pairs)" if precision == "fp32"
                   else "stem_pool / bottleneck / chain / conv_big / conv_igemm / conv1x1_stream") + ")",
         "launches": {"fetch_pass": nf, "write_pass": nw},
         "fetch_size_kib_per_launch": round(f_kib, 1),

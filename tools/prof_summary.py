@@ -12,7 +12,7 @@ import os
 import sys
 
 FAMILIES = [("conv", ("conv_igemm_kernel", "conv1x1_stream_kernel", "conv_big_kernel", "bottleneck_kernel",
-                       "bottleneck32_kernel", "stem_pool_kernel", "stem_pool32_kernel", "chain_kernel", "dwconv", "conv_x6_kernel",
+                       "bottleneck32_kernel", "stem_pool_kernel", "stem_pool32_kernel", "chain_kernel", "dwconv", "conv_x6_kernel", "conv_x6_halo_kernel",
                        "conv1x1_x6_kernel")),
             ("mosaic", ("mosaic_",)), ("letterbox", ("letterbox_kernel", "letterbox_s2d")),
             ("post", ("candidates_kernel", "nms_kernel")), ("other", ("maxpool", "upsample")),
