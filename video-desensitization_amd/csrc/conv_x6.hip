@@ -325,7 +325,8 @@ __device__ __forceinline__ void x6_epilogue(const ConvArgs& a, AccT (&acc)[S::TM
     }
 }
 
-template <int BM, int BN, int NT, int NST, int TERMS, int MF>
+template <int BM, int BN, int NT, int NST, int TERMS, int MF, int NA>
+// NA: A register sets (K tiles of A loads in flight: NA - 1 besides the one being split)
 // 8 waves: two workgroups' worth of waves per SIMD pair (256 VGPRs each); 4 waves (one
 // per SIMD, 128 x 128 wave tiles): the whole 512-register file per wave, the
 // accumulators in AGPRs
@@ -376,7 +377,7 @@ __global__ __launch_bounds__(NT, NT == 256 && BM == 256 ? 1 : 2) void conv_x6_ke
 
     // two register sets of A (8 f32 of each of 2 rows): tile t lives in set t & 1,
     // loaded two iterations before it is split into LDS
-    u32x4 ra[2][AIT][2];                            // [set][item][half]
+    u32x4 ra[NA][AIT][2];                           // [set][item][half]
     // per half h: the (dy, dx, c) of this thread's 4-channel chunk kt*8 + 2*apair + h,
     // advanced by 32 channels per load_a call (tiles are loaded in order): no
     // divisions and no branches in the load path
@@ -539,21 +540,23 @@ __global__ __launch_bounds__(NT, NT == 256 && BM == 256 ? 1 : 2) void conv_x6_ke
     };
 
     if constexpr (NST == 2) {
-    // ---- main loop. Per thread VMEM issue order: ... A(t+2) loads (4), B(t+1) DMA
-    // (my_dma) at the end of iteration t-1. At the top of iteration t the younger ops
-    // are those of iteration t-1's end -- A(t+2), B(t+1) -- so B(t) and A(t+1) retire
-    // at vmcnt(4 + my_dma) (fewer when the tail issued less).
+    // ---- main loop. A(t) lives in register set t % NA. Per thread VMEM issue order at
+    // the end of iteration t: A(t+1+NA) loads (2 AIT, into the set A(t+1) just left),
+    // B(t+2) DMA (my_dma); the prologue issues A(0) (split at once), A(1..NA-1), B(0),
+    // A(NA), B(1), i.e. the ends of iterations -2 and -1. At the top of iteration t the
+    // ops younger than B(t) are those of iteration t-1's end, and A(t+1) is older than
+    // B(t), so both retire at vmcnt(2 AIT + my_dma) (fewer when the tail issued less).
     load_a(ra[0]);
 #pragma unroll
     for (int q = 0; q < AIT; ++q) store_item(0, ra[0], q);
+#pragma unroll
+    for (int j = 1; j < NA; ++j)
+        if (j < nk) load_a(ra[j]);
     dma_b(0, 0);
-    if (nk > 1) load_a(ra[1]);
+    if (NA < nk) load_a(ra[0]);
     if (nk > 1) dma_b(1, 1);
-    if (nk > 2) load_a(ra[0]);
     auto iter = [&](int kt, const u32x4 (&rnext)[AIT][2], u32x4 (&rfree)[AIT][2]) {
-        // younger than B(kt) / A(kt+1): A(kt+2) loads (issued iff kt+2 < nk) and
-        // B(kt+1) DMA (iff kt+1 < nk)
-        const int younger = (kt + 2 < nk ? 2 * AIT : 0) + (kt + 1 < nk ? my_dma : 0);
+        const int younger = (kt + NA < nk ? 2 * AIT : 0) + (kt + 1 < nk ? my_dma : 0);
         wait_vm(younger);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this thread's A(kt) ds_writes
         __builtin_amdgcn_s_barrier();
@@ -562,14 +565,15 @@ __global__ __launch_bounds__(NT, NT == 256 && BM == 256 ? 1 : 2) void conv_x6_ke
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();                        // everyone done reading stage kt & 1
         asm volatile("" ::: "memory");
-        if (kt + 3 < nk) load_a(rfree);                       // A(kt+3) into the set A(kt+1) just left
+        if (kt + 1 + NA < nk) load_a(rfree);                  // A(kt+1+NA) into the set A(kt+1) just left
         if (kt + 2 < nk) dma_b(kt + 2, kt & 1);
     };
     // Raw barriers with counted waits: __syncthreads() would add vmcnt(0) and drain
-    // the prefetch. Unrolled by 2 so the register sets are indexed statically.
-    for (int kt = 0; kt < nk; kt += 2) {
-        iter(kt, ra[1], ra[1]);
-        if (kt + 1 < nk) iter(kt + 1, ra[0], ra[0]);
+    // the prefetch. Unrolled by NA so the register sets are indexed statically.
+    for (int kt = 0; kt < nk; kt += NA) {
+#pragma unroll
+        for (int u = 0; u < NA; ++u)
+            if (kt + u < nk) iter(kt + u, ra[(u + 1) % NA], ra[(u + 1) % NA]);
     }
     } else {
     // ---- one LDS stage: per tile, B(kt) DMA and the split A(kt) write, then
@@ -1194,11 +1198,16 @@ bool vd_conv_x6_ok(const ConvArgs& a) {
 }
 
 // rows [mbase, M) of the conv (mbase a multiple of the caller's tile rows)
-template <int BM, int BN, int NT, int NST, int TERMS, int MF = 16>
+template <int BM, int BN, int NT, int NST, int TERMS, int MF = 16, int NA = 2>
 static hipError_t launch_x6(const ConvArgs& a0, hipStream_t s, int mbase = 0, int mtiles = -1) {
+    if constexpr (NA == 2 && BM == 256 && BN <= 128 && NST == 2 && TERMS == 2 && MF == 16) {
+        // option x6_adepth: four A register sets (three K tiles of A loads in flight) on
+        // the 256 x {128, 64, 32} tiles, whose accumulators leave the registers for them
+        if (a0.tune && a0.tune->x6_adepth >= 4) return launch_x6<BM, BN, NT, NST, TERMS, MF, 4>(a0, s, mbase, mtiles);
+    }
     using S = X6Shape<BM, BN, NT, NST, TERMS, MF>;
     static const bool attr = [] {
-        (void)hipFuncSetAttribute((const void*)conv_x6_kernel<BM, BN, NT, NST, TERMS, MF>,
+        (void)hipFuncSetAttribute((const void*)conv_x6_kernel<BM, BN, NT, NST, TERMS, MF, NA>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS + 4 * kAmaxFrames);
         return true;
     }();
@@ -1209,7 +1218,7 @@ static hipError_t launch_x6(const ConvArgs& a0, hipStream_t s, int mbase = 0, in
     a.mbase = mbase;
     const int mt = mtiles >= 0 ? mtiles : (a.M - mbase + BM - 1) / BM;
     const int lds = S::LDS + (a.ymax ? 4 * a.B : 0);
-    hipLaunchKernelGGL((conv_x6_kernel<BM, BN, NT, NST, TERMS, MF>), dim3(mt * a.ntiles_n), dim3(NT), lds, s, a);
+    hipLaunchKernelGGL((conv_x6_kernel<BM, BN, NT, NST, TERMS, MF, NA>), dim3(mt * a.ntiles_n), dim3(NT), lds, s, a);
     return hipGetLastError();
 }
 

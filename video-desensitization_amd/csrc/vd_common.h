@@ -64,6 +64,7 @@ struct VdTune {
     int x6_halo = 2;          // fp16 pairs, 3x3 stride-1 convs: input split once per 32-channel chunk
                               //   over the tile's linear halo (conv_x6_halo_kernel); 2: three B stages, 1: two
     int x6_halo_narrow = 1;   // ... also for Cout <= 64 (N tiles of 32 / 64)
+    int x6_adepth = 2;        // A register sets of the 256 x {128, 64, 32} fp16-pair tiles (2 or 4; 4 measured level)
     int x6_slots = 0;         //   workgroup slots of one round (0: the CU count; tests force small values)
     int f32_split = 2;        // plan (fp32, at weight load): 2 = operands scaled by powers of two
                               //   and split into fp16 pairs, 3 products on the f16 matrix cores;
