@@ -264,8 +264,8 @@ __device__ __forceinline__ f32x4_t mfma16(const u32x4& a, const u32x4& b, const 
 
 __global__ __launch_bounds__(256, 2) void stem_pool32_kernel(StemPoolArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    char* lx = smem;                       // XBUF3
-    char* lst = smem + XBUF3;              // STB3
+    char* lx = smem;                       // 2 x XBUF3: X' of this tile and the next
+    char* lst = smem + 2 * XBUF3;          // STB3
     char* lscratch = lst + STB3;           // 1 KB sink of the padding DMA slots
     unsigned* s_amax = (unsigned*)(lscratch + 1024);
 
@@ -288,7 +288,7 @@ __global__ __launch_bounds__(256, 2) void stem_pool32_kernel(StemPoolArgs a) {
     for (int f = tid; f < a.B; f += 256) s_amax[f] = 0u;
     const size_t fx = (size_t)a.xh * a.xw * 16;
 
-    auto issue_x = [&](int t) {
+    auto issue_x = [&](int t, int buf) {
         const int b = t / tpf, r0 = t - b * tpf;
         const int ty = r0 / tpc, tx = r0 - ty * tpc;
         const int xr0 = 2 * PT3 * ty - 2, xc0 = 2 * PT3 * tx - 2;
@@ -303,11 +303,11 @@ __global__ __launch_bounds__(256, 2) void stem_pool32_kernel(StemPoolArgs a) {
             const int iy = xr0 + xr, ix = xc0 + xc;
             const bool in = real && xp < XP3 && (unsigned)iy < (unsigned)a.xh && (unsigned)ix < (unsigned)a.xw;
             const unsigned off = in ? (unsigned)(((iy * a.xw + ix) * 16 + ch * 8) * 2) : 0x80000000u;
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(real ? lx + i * 1024 : lscratch), 16, off, 0, 0,
-                                                     0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_t*)(real ? lx + buf * XBUF3 + i * 1024 : lscratch), 16,
+                                                     off, 0, 0, 0);
         }
     };
-    if (t0 < tend) issue_x(t0);
+    if (t0 < tend) issue_x(t0, 0);
 
     // stationary: hi / lo weight fragments of this wave's 32 channels and the BN terms
     const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)a.wf, 0, 0x7fffffff, 0x00020000);
@@ -327,14 +327,20 @@ __global__ __launch_bounds__(256, 2) void stem_pool32_kernel(StemPoolArgs a) {
         sh[e] = a.shift[32 * np + 8 * g0 + e];
     }
 
+    int xb = 0;                            // X' buffer of this tile
 #pragma unroll 1
-    for (int t = t0; t < tend; t += tstep) {
+    for (int t = t0; t < tend; t += tstep, xb ^= 1) {
         const int b = t / tpf, r0 = t - b * tpf;
         const int ty = r0 / tpc, tx = r0 - ty * tpc;
         const int sy0 = 2 * PT3 * ty - 1, sx0 = 2 * PT3 * tx - 1;
-        // this tile's X' (DMA); the previous tile's 4 stores per thread are the only younger ops
+        // this tile's X' (DMA, issued a whole tile ago); the previous tile's 4 stores per
+        // thread are the only younger ops
         __builtin_amdgcn_s_waitcnt(VMCNT4);
         __syncthreads();
+        // the next tile's X' into the other buffer (stage A of the previous tile, its
+        // last reader, finished before the barrier above)
+        if (t + tstep < tend) issue_x(t + tstep, xb ^ 1);
+        const char* lxt = lx + xb * XBUF3;
         int li = li0, g = g0;
         asm volatile("" : "+v"(li), "+v"(g));
 
@@ -349,7 +355,7 @@ __global__ __launch_bounds__(256, 2) void stem_pool32_kernel(StemPoolArgs a) {
             for (int s = 0; s < 8; ++s) {
                 const int tap = 2 * s + (g >> 1), ta = tap >> 2, tb = tap & 3;
                 const int rr = r + ta < XE3 ? r + ta : XE3 - 1;   // rows past the tile (p >= SP3): any X'
-                xf[s] = *(const u32x4*)(lx + (rr * XE3 + (c + tb < XE3 ? c + tb : XE3 - 1)) * 32 + (g & 1) * 16);
+                xf[s] = *(const u32x4*)(lxt + (rr * XE3 + (c + tb < XE3 ? c + tb : XE3 - 1)) * 32 + (g & 1) * 16);
             }
 #pragma unroll
             for (int s = 0; s < 8; ++s) {
@@ -371,7 +377,6 @@ __global__ __launch_bounds__(256, 2) void stem_pool32_kernel(StemPoolArgs a) {
             *(float4*)(lst + st_off3(p, cg + 1)) = make_float4(o[4], o[5], o[6], o[7]);
         }
         __syncthreads();
-        if (t + tstep < tend) issue_x(t + tstep);             // X' buffer free once stage A is done
 
         // ---- stage B: 3x3/2 max pool of the tile, 8 channels per item, 2 items per thread ----
         {
@@ -420,10 +425,10 @@ __global__ __launch_bounds__(256, 2) void stem_pool32_kernel(StemPoolArgs a) {
 hipError_t vd_launch_stem_pool32(const StemPoolArgs& a, hipStream_t s) {
     if (a.B <= 0) return hipSuccess;
     if (a.B > 1024) return hipErrorInvalidValue;
-    const size_t lds = XBUF3 + STB3 + 1024 + 4 * (size_t)a.B;
+    const size_t lds = 2 * XBUF3 + STB3 + 1024 + 4 * (size_t)a.B;
     static const int cus = [] {
         (void)hipFuncSetAttribute((const void*)stem_pool32_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  XBUF3 + STB3 + 1024 + 4 * 1024);
+                                  2 * XBUF3 + STB3 + 1024 + 4 * 1024);
         int dev = 0, n = 256;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
