@@ -191,6 +191,11 @@ CONV_CASES = [
     (2, 23, 21, 256, 192, 3, 1, 1, 1, 0),     # 192-wide N tile: fused SSH conv5X5_1 + conv3X3
     (2, 13, 11, 256, 512, 3, 1, 1, 1, 1),     # fp32 pairs: 256 x 256 tile, two N tiles, residual, M tail
     (1, 15, 17, 64, 160, 3, 1, 1, 2, 1),      # 192-wide N tile, cout 160, leaky + residual
+    # fp32 halo form (3x3 / stride 1, Cin % 32 == 0, W <= 126): the widest halo, N = 32 / 64
+    # tiles, frames smaller than a tile (one tile's halo straddles several frames), W past the limit
+    (1, 5, 126, 32, 64, 3, 1, 1, 1, 0),
+    (3, 7, 9, 64, 32, 3, 1, 1, 2, 1),
+    (2, 6, 127, 32, 128, 3, 1, 1, 1, 0),
     # 1x1 streaming kernel (bf16, K 64/128/256/512): bottleneck conv3 / conv1 / downsample shapes
     (2, 21, 23, 64, 256, 1, 1, 0, 1, 1),      # conv3 + residual, M not a multiple of 16
     (1, 18, 18, 256, 512, 1, 2, 0, 0, 0),     # stride-2 downsample
@@ -213,8 +218,8 @@ CONV_CASES = [
 ]
 
 
-@pytest.mark.parametrize("prec", ["fp32", "fp32-big", "fp32-mf32", "fp32-mid", "fp32-small", "fp32-exact", "fp32-x6", "fp32-x6-big",
-                                  "fp32-x6-small", "fp32-s128", "fp32-s256", "bf16", "fp16", "bf16-gemm64",
+@pytest.mark.parametrize("prec", ["fp32", "fp32-big", "fp32-mf32", "fp32-mid", "fp32-small", "fp32-halo1", "fp32-exact", "fp32-x6",
+                                  "fp32-x6-big", "fp32-x6-small", "fp32-s128", "fp32-s256", "bf16", "fp16", "bf16-gemm64",
                                   "bf16-gemm128"])
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv_matches_torch(gpu, face_ctx_factory, prec, case, options=None):
@@ -225,8 +230,16 @@ def test_conv_matches_torch(gpu, face_ctx_factory, prec, case, options=None):
     fp32-exact: exact-f32 MFMA (option f32_split=0); fp32-x6(-big/-small): the exact
     3-term bf16 split (option f32_split=1); bf16: the default dispatch
     (streaming 1x1 / streaming taps / phased / GEMM); bf16-gemm64 / -gemm128: the
-    implicit GEMM with 64- and 128-row tiles forced through vd_set_option."""
+    implicit GEMM with 64- and 128-row tiles forced through vd_set_option. The default
+    fp32 plan runs the 3x3 stride-1 shapes (Cin % 32 == 0, W <= 126) on the halo form
+    (three B stages; fp32-halo1: two); -big / -small / -mf32 switch it off so the
+    tap-major tiles keep their coverage on those shapes."""
     options = dict(options or {})
+    if prec == "fp32-halo1":
+        options.update(x6_halo=1)
+        prec = "fp32"
+    if prec in ("fp32-big", "fp32-small", "fp32-mf32"):
+        options.update(x6_halo=0)
     if prec in ("fp32-s128", "fp32-s256"):     # streaming 1x1 slices of 128 / 256 (default) channels, K 64 / 128
         options.update(x6_stream256=0 if prec == "fp32-s128" else 2)
         prec = "fp32"
