@@ -407,3 +407,30 @@ def test_heads_fp32_halo_conv(gpu):
     assert sum(len(x) for x in boxes[0]) > 0
     for a, b in zip(boxes[1], boxes[0]):
         np.testing.assert_array_equal(a, b)
+
+
+def test_heads_ssh_side_lane_bit_identical(gpu):
+    """Face net on two lanes (option ssh_side, default): SSH + heads of levels 1-2 on a
+    second stream beside FPN merge1 and level 0 (runtime.cpp Ctx::face_lanes). Same
+    kernels on the same operands, so heads and boxes equal the one-stream order bit for
+    bit, in both fp32 and bf16; repeated calls (events reused) stay identical."""
+    import vdmi
+    fr = _frames(3, 1080, 1920, seed=41)
+    for prec in ("fp32", "bf16"):
+        heads, boxes = {}, {}
+        for side in (1, 0):
+            ctx = vdmi.Context(precision=prec, max_batch=3, options={"ssh_side": side})
+            try:
+                ctx.load_weights(0, face_weights("default"))
+                heads[side] = ctx.forward_heads(fr)
+                again = ctx.forward_heads(fr)
+                for a, b in zip(again, heads[side]):
+                    np.testing.assert_array_equal(a, b)
+                r = ctx.detect(fr)
+                boxes[side] = [r.frame(b)[0].copy() for b in range(3)]
+            finally:
+                ctx.close()
+        for a, b in zip(heads[1], heads[0]):
+            np.testing.assert_array_equal(a, b)
+        for a, b in zip(boxes[1], boxes[0]):
+            np.testing.assert_array_equal(a, b)

@@ -113,6 +113,9 @@ int build_mnet_body(Ctx& c, const WMap& W, FaceNet& F, Act feats[3]) {
 
 int vd_build_face(Ctx& c, const WMap& W) {
     FaceNet& F = c.face;
+    for (hipEvent_t ev : c.lane_ev)   // a previous load's lane events (face_lanes re-creates them)
+        if (ev) hipEventDestroy(ev);
+    c.lane_ev.clear();
     F.in_h = c.cfg.input_h;
     F.in_w = c.cfg.input_w;
     const int H = F.in_h, Wd = F.in_w;
@@ -233,17 +236,26 @@ int vd_build_face(Ctx& c, const WMap& W) {
     if ((rc = c.act(m2, feats[1].h, feats[1].w, oc))) return rc;
     if ((rc = c.act(o1, feats[0].h, feats[0].w, oc))) return rc;
     if ((rc = c.act(m1, feats[0].h, feats[0].w, oc))) return rc;
+    int fpn_at[5];   // op index of o3, o2, m2, o1, m1 (face_lanes)
+    fpn_at[0] = (int)F.net.ops.size();
     if ((rc = c.add_conv(F.net, o3c, feats[2], 0, o3, 0))) return rc;
     // output2 = relu(bn(conv(C4))) + nearest_up(output3)   (layers.py:102-103)
+    fpn_at[1] = (int)F.net.ops.size();
     if ((rc = c.add_conv(F.net, o2c, feats[1], 0, o2, 0, &o3, 0, VD_RES_POST_ACT, 1))) return rc;
+    fpn_at[2] = (int)F.net.ops.size();
     if ((rc = c.add_conv(F.net, m2c, o2, 0, m2, 0))) return rc;
+    fpn_at[3] = (int)F.net.ops.size();
     if ((rc = c.add_conv(F.net, o1c, feats[0], 0, o1, 0, &m2, 0, VD_RES_POST_ACT, 1))) return rc;
+    fpn_at[4] = (int)F.net.ops.size();
     if ((rc = c.add_conv(F.net, m1c, o1, 0, m1, 0))) return rc;
+    if ((int)F.net.ops.size() != fpn_at[4] + 1) return vd_set_error(VD_ERR_STATE, "internal: FPN op count");
     const Act fpn_out[3] = {m1, m2, o3};
 
     // ---- SSH x3 + fused heads ----
     const bool ssh_fuse = c.tune.ssh_fuse != 0;   // 0: conv3X3 and conv5X5_1 as two convs
+    int ssh_b[3], ssh_e[3];                        // op range of each level's SSH + heads
     for (int l = 0; l < 3; ++l) {
+        ssh_b[l] = (int)F.net.ops.size();
         const std::string pre = "ssh" + std::to_string(l + 1);
         int s3, s51, s52, s72, s73;
         if ((rc = conv_bn(c, W, pre + ".conv3X3.0.weight", pre + ".conv3X3.1", 1, 1, VD_ACT_RELU, &s3))) return rc;
@@ -301,7 +313,9 @@ int vd_build_face(Ctx& c, const WMap& W) {
         if (c.convs[hc].cout != 32) return vd_set_error(VD_ERR_WEIGHTS, "heads of level %d: %d channels != 32", l, c.convs[hc].cout);
         if ((rc = c.act(F.heads[l], f.h, f.w, 32, true))) return rc;
         if ((rc = c.add_conv(F.net, hc, cat, hoff, F.heads[l], 0))) return rc;
+        ssh_e[l] = (int)F.net.ops.size();
     }
+    if (c.tune.ssh_side && (rc = c.face_lanes(fpn_at, ssh_b, ssh_e))) return rc;
 
     // ---- anchors (anchors.py:22-41, Python doubles -> float32) ----
     static const int steps[3] = {8, 16, 32};

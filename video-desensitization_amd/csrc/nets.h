@@ -77,6 +77,8 @@ struct Op {
     int blk = -1;                      // OP_BLOCK: index into Ctx::blocks (x -> y)
     void* wf = nullptr;                // OP_STEMPOOL: conv's weight fragments (conv = the stem conv)
     Act y2;                            // OP_CHAIN: conv = conv3 (x -> y, identity r), conv2 = next conv1 (y -> y2)
+    int lane = 0;                      // 1: runs on Ctx::stream_side (face SSH levels 1-2)
+    int dep = -1;                      // op index (other lane) whose completion this op waits for
 };
 
 struct Net {
@@ -164,6 +166,9 @@ struct Ctx {
     hipStream_t stream = nullptr, own_stream = nullptr;
     hipStream_t stream2 = nullptr;               // plate branch runs beside the face branch
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipStream_t stream_side = nullptr;           // the face net's second lane (SSH levels 1-2 beside level 0)
+    std::vector<hipEvent_t> lane_ev;             // per face op: completion event for the other lane
+    hipEvent_t ev_side = nullptr;                // side lane done (joined before the face decode)
     int fork_at = -1;                                // run_ops records ev_fork after this many face ops
     std::mutex mu;
     std::vector<void*> allocs;
@@ -239,6 +244,7 @@ struct Ctx {
     void t_end();
     int run_conv_op(const Op& op, int f0, int n, int fam = 0);
     int run_ops(const Net& net, int b, int e, int f0, int n);
+    int face_lanes(const int (&fpn)[5], const int (&ssh_b)[3], const int (&ssh_e)[3]);
     int run_net(const Net& net, int n, int mb = 0, int split = 0);
     const uint8_t* frames_to_device(const uint8_t* frames, int n, int h, size_t pitch, int where, int* rc);
     int check_frames(int n, int h, int w, size_t pitch);

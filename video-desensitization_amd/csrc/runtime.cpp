@@ -546,9 +546,20 @@ static hipError_t amax_follow_impl(const Op& op, int f0, int n, hipStream_t s) {
 }
 
 int Ctx::run_ops(const Net& net, int b, int e, int f0, int n) {
+    // two lanes (face net, option ssh_side): lane-1 ops run on stream_side; an op with
+    // dep >= 0 waits for that op's completion event first (recorded below on the
+    // producer's lane); after the net's last op the main lane waits for the side lane
+    const bool lanes = &net == &face.net && !lane_ev.empty();
+    hipStream_t main = stream;
+    bool side_used = false;
     for (int i = b; i < e; ++i) {
         const Op& op = net.ops[i];
         int rc = VD_OK;
+        if (lanes) {
+            stream = op.lane ? stream_side : main;
+            side_used |= op.lane != 0;
+            if (op.dep >= 0) VD_CHECK_HIP(hipStreamWaitEvent(stream, lane_ev[op.dep], 0));
+        }
         if (op.kind == OP_CONV) {
             rc = run_conv_op(op, f0, n, net.conv_fam);
         } else if (op.kind == OP_BLOCK) {
@@ -575,9 +586,52 @@ int Ctx::run_ops(const Net& net, int b, int e, int f0, int n) {
             if (er == hipSuccess) er = amax_follow_impl(op, f0, n, stream);
             if (er != hipSuccess) rc = vd_set_error(VD_ERR_HIP, "upsample: %s", hipGetErrorString(er));
         }
+        if (lanes && lane_ev[i]) VD_CHECK_HIP(hipEventRecord(lane_ev[i], stream));
+        if (lanes) stream = main;
         if (rc) return rc;
         if (&net == &face.net && i + 1 == fork_at) VD_CHECK_HIP(hipEventRecord(ev_fork, stream));
     }
+    if (lanes && side_used) {
+        VD_CHECK_HIP(hipEventRecord(ev_side, stream_side));
+        VD_CHECK_HIP(hipStreamWaitEvent(stream, ev_side, 0));
+    }
+    return VD_OK;
+}
+
+// The face net's op list as built (FPN o3 o2 m2 o1 m1, then SSH + heads of levels 0, 1,
+// 2) reordered into two lanes: level 2's chain right after o3 and level 1's after m2,
+// both on the side stream, so they fill the CUs that FPN merge1 and the level-0 SSH
+// convs (6x the pixels) leave idle in their last partial rounds. Same kernels and
+// operands: results are bit-identical to the one-lane order.
+int Ctx::face_lanes(const int (&fpn)[5], const int (&ssh_b)[3], const int (&ssh_e)[3]) {
+    Net& net = face.net;
+    std::vector<Op> out(net.ops.begin(), net.ops.begin() + fpn[0]);
+    auto take = [&](int b, int e, int lane, int dep) {
+        for (int i = b; i < e; ++i) {
+            Op op = net.ops[i];
+            op.lane = lane;
+            op.dep = i == b ? dep : -1;
+            out.push_back(op);
+        }
+    };
+    take(fpn[0], fpn[0] + 1, 0, -1);                      // o3
+    const int p_o3 = (int)out.size() - 1;
+    take(ssh_b[2], ssh_e[2], 1, p_o3);                     // level 2 (reads o3)
+    take(fpn[1], fpn[2] + 1, 0, -1);                       // o2, m2
+    const int p_m2 = (int)out.size() - 1;
+    take(ssh_b[1], ssh_e[1], 1, p_m2);                     // level 1 (reads m2)
+    take(fpn[3], fpn[4] + 1, 0, -1);                       // o1, m1
+    take(ssh_b[0], ssh_e[0], 0, -1);                       // level 0
+    if (out.size() != net.ops.size()) return vd_set_error(VD_ERR_STATE, "internal: face lanes lost ops");
+    net.ops.swap(out);
+    if (!stream_side) {
+        VD_CHECK_HIP(hipStreamCreateWithFlags(&stream_side, hipStreamNonBlocking));
+        VD_CHECK_HIP(hipEventCreateWithFlags(&ev_side, hipEventDisableTiming));
+    }
+    for (hipEvent_t ev : lane_ev)
+        if (ev) hipEventDestroy(ev);
+    lane_ev.assign(net.ops.size(), nullptr);
+    for (int i : {p_o3, p_m2}) VD_CHECK_HIP(hipEventCreateWithFlags(&lane_ev[i], hipEventDisableTiming));
     return VD_OK;
 }
 
@@ -863,6 +917,13 @@ int vd_destroy(vd_ctx* h) {
     if (ctx->jpeg_ev) hipEventDestroy(ctx->jpeg_ev);
     for (auto& t : ctx->ev_pool) { hipEventDestroy(t.a); hipEventDestroy(t.b); }
     hipStreamSynchronize(ctx->stream2);
+    if (ctx->stream_side) {
+        hipStreamSynchronize(ctx->stream_side);
+        hipStreamDestroy(ctx->stream_side);
+        hipEventDestroy(ctx->ev_side);
+    }
+    for (hipEvent_t ev : ctx->lane_ev)
+        if (ev) hipEventDestroy(ev);
     hipEventDestroy(ctx->ev_fork);
     hipEventDestroy(ctx->ev_join);
     hipStreamDestroy(ctx->stream2);
@@ -905,7 +966,7 @@ int vd_set_option(vd_ctx* h, const char* name, int value) {
         {"plate_s2d", &VdTune::plate_s2d}, {"f32_split", &VdTune::f32_split},
         {"x6_small_k", &VdTune::x6_small_k}, {"x6_small_tiles", &VdTune::x6_small_tiles},
         {"x6_stream", &VdTune::x6_stream}, {"x6_small_k2", &VdTune::x6_small_k2}, {"x6_bn256", &VdTune::x6_bn256},
-        {"x6_exact", &VdTune::x6_exact}, {"x6_mid", &VdTune::x6_mid}, {"block_fuse32", &VdTune::block_fuse32}, {"x6_mf32", &VdTune::x6_mf32}, {"x6_tail", &VdTune::x6_tail}, {"x6_stream_silu", &VdTune::x6_stream_silu}, {"x6_slots", &VdTune::x6_slots}, {"x6_halo", &VdTune::x6_halo}, {"x6_halo_narrow", &VdTune::x6_halo_narrow}, {"x6_adepth", &VdTune::x6_adepth}, {"x6_stream256", &VdTune::x6_stream256}, {"plate_stage", &VdTune::plate_stage},
+        {"x6_exact", &VdTune::x6_exact}, {"x6_mid", &VdTune::x6_mid}, {"block_fuse32", &VdTune::block_fuse32}, {"x6_mf32", &VdTune::x6_mf32}, {"x6_tail", &VdTune::x6_tail}, {"x6_stream_silu", &VdTune::x6_stream_silu}, {"x6_slots", &VdTune::x6_slots}, {"x6_halo", &VdTune::x6_halo}, {"x6_halo_narrow", &VdTune::x6_halo_narrow}, {"x6_adepth", &VdTune::x6_adepth}, {"x6_stream256", &VdTune::x6_stream256}, {"plate_stage", &VdTune::plate_stage}, {"ssh_side", &VdTune::ssh_side},
         {"jenc_gpu", &VdTune::jenc_gpu}, {"jdec_gpu", &VdTune::jdec_gpu}, {"jdec_chunk", &VdTune::jdec_chunk}, {"jdec_sync", &VdTune::jdec_sync}, {"jdec_group", &VdTune::jdec_group},
     };
     for (const Opt& o : opts)

@@ -42,6 +42,9 @@ struct VdTune {
     int jdec_sync = 128;      //   states recorded per chunk: passes stop at the previous trajectory (0: off)
     int jdec_chunk = 1024;    //   raw scan bytes per decoding thread (tests force small chunks)
     int jdec_group = 4;       //   resynchronisation passes launched between host convergence checks
+    int ssh_side = 0;         // 1: face SSH levels 1-2 (+ heads) on a second stream beside FPN merge / level 0
+                              //   (at weight load; measured -0.1 ms/step, but overlapping launches inflate
+                              //   the per-launch durations behind `roofline`: off by default)
     int plate_stage = 3;      // plate branch starts after face stage N (0: with the stem; 1-4: after
                               //   layerN; 5: after the whole face net). After layer3 its HBM-bound
                               //   convs overlap the MFMA-bound late face layers: 30.8 -> 30.0 ms/step
