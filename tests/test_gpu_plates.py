@@ -204,3 +204,27 @@ def test_process_plate_release_point(gpu, stage):
     for b in range(3):
         np.testing.assert_array_equal(res[stage][1][b], res[3][1][b])
         np.testing.assert_array_equal(res[stage][2][b], res[3][2][b])
+
+
+@pytest.mark.parametrize("h,w", [(1080, 1920), (720, 1280), (480, 640)])
+def test_plate_raw_fp32_s2d_matches_plain(gpu, h, w):
+    """fp32 plan: the plate canvas in space-to-depth form as integer pixel values in
+    fp16 (exact), model.0 as a 2x2 conv over it on one A plane with the / 255 folded
+    into its BN scale (plate_net.cpp yconv_s2d, option plate_s2d32); plate_s2d32=0
+    keeps the f32 canvas and the 3x3 conv. The same 27 products per output in another
+    f32 order: raw outputs within f32 rounding of each other and of the oracle."""
+    import vdmi
+    from vdmi import synth, weights
+    fr = synth.frames(2, h, w, seed=7)
+    out = {}
+    for s2d in (1, 0):
+        c = vdmi.Context(precision="fp32", max_batch=2, options={"plate_s2d32": s2d})
+        try:
+            c.load_weights(1, weights.yolov8n_state_dict(0))
+            out[s2d] = c.plate_raw(fr)
+        finally:
+            c.close()
+    exp, _, _ = _oracle_raw(fr)
+    assert out[1].shape == out[0].shape == exp.shape
+    assert _rel(out[1], out[0]) < 2e-5
+    assert _rel(out[1], exp) < 1e-4

@@ -1372,10 +1372,11 @@ static hipError_t launch_terms(const ConvArgs& a0, hipStream_t s) {
             return bn == 32 ? launch_x6_halo<32>(a, s) : launch_x6_halo<64>(a, s);
     }
     if (small) {
-        if (bn == 32) return launch_x6<128, 32, 256, 1, TERMS>(a, s);
-        if constexpr (TERMS == 2) {   // the integer-valued face canvas: one A plane, two products (stem)
+        if constexpr (TERMS == 2) {   // integer-valued canvases (face / plate stems): one A plane, two products
+            if (bn == 32 && a.x_exact) return launch_x6<128, 32, 256, 1, 1>(a, s);
             if (bn == 64 && a.x_exact) return launch_x6<128, 64, 256, 1, 1>(a, s);
         }
+        if (bn == 32) return launch_x6<128, 32, 256, 1, TERMS>(a, s);
         if (bn == 64) return launch_x6<128, 64, 256, 1, TERMS>(a, s);
         return launch_x6<128, 128, 256, 1, TERMS>(a, s);
     }

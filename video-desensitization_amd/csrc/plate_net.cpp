@@ -93,7 +93,9 @@ int yconv_s2d(Ctx& c, const WMap& W, const std::string& pre) {
                                 w->data[(((size_t)n * 3 + ch) * 3 + dy) * 3 + dx];
                         }
         const float alpha = g->data[n] / std::sqrt(v->data[n] + YOLO_BN_EPS);
-        sc[n] = alpha;
+        // fp32 plan: the canvas holds the integer pixel values (exact in fp16), the
+        // preprocessing's / 255 moves into the BN scale
+        sc[n] = c.f32 ? alpha / 255.f : alpha;
         sh[n] = b->data[n] - m->data[n] * alpha;
     }
     int rc = c.upload_conv(cv, wt, sc, sh);
@@ -262,8 +264,10 @@ int vd_build_plate(Ctx& c, const WMap& W) {
         return vd_set_error(VD_ERR_WEIGHTS, "plate weights have %d classes, cfg.plate_nc = %d", cls0->shape[0], P.nc);
     int rc;
     static const int strides[] = {2, 2, 1, 2, 1, 2, 1, 2, 1};
-    // bf16: the letterbox writes the stem input in space-to-depth form (option plate_s2d=0: off)
-    P.s2d = !c.f32 && !c.f16 && c.tune.plate_s2d;
+    // bf16 / fp32 (fp16 pairs): the letterbox writes the stem input in space-to-depth form
+    // (option plate_s2d=0: off); fp32 as integer pixel values in f32 (exact in fp16),
+    // model.0 then on one A plane (x_exact) with the / 255 in its BN scale
+    P.s2d = c.tune.plate_s2d && ((!c.f32 && !c.f16) || (c.f32 && c.tune.f32_split == 2 && c.tune.plate_s2d32));
     if (P.s2d && (rc = yconv_s2d(c, W, "model.0"))) return rc;
     for (int i : {0, 1, 3, 5, 7}) {
         if (i == 0 && P.s2d) continue;
@@ -290,11 +294,15 @@ int vd_build_plate(Ctx& c, const WMap& W) {
     // buffers for the imgsz x imgsz canvas
     const int cpad = c.f32 ? 4 : 8;
     c.amax_begin(1);
-    if (P.s2d) rc = c.act(P.input, P.imgsz / 2 + 1, P.imgsz / 2 + 1, 16);
+    if (P.s2d) rc = c.act(P.input, P.imgsz / 2 + 1, P.imgsz / 2 + 1, 16);   // fp32: f32 (conv_x6 reads f32 A)
     else rc = c.act(P.input, P.imgsz, P.imgsz, cpad);
     if (rc) return rc;
     P.input.amax = nullptr;            // letterboxed canvas / 255: in [0, 1]
     P.input.bound = 1.f;
+    if (P.s2d && c.f32) {              // fp32 s2d canvas: integer pixel values 0..255
+        P.input.bound = 255.f;
+        P.input.exact16 = true;
+    }
     for (const Buf& b : kBufs) {
         Act a;
         if ((rc = c.act(a, P.imgsz / b.div, P.imgsz / b.div, b.c))) return rc;
@@ -341,7 +349,7 @@ int vd_plate_letterbox_args(Ctx& c, const uint8_t* d, int n, int h, int w, size_
     vd_resize_mode(h, w, nh, nw, &a.mode, &a.scale_x, &a.scale_y);
     a.pad_value = 114.f;
     a.mean[0] = a.mean[1] = a.mean[2] = 0.f;
-    a.div = 255.f;
+    a.div = P.s2d && c.f32 ? 1.f : 255.f;   // fp32 s2d: integers, / 255 in model.0's BN scale
     a.flip = 1;   // im[..., ::-1]: the RGB frames are treated as BGR
     a.out = P.input.p; a.cpad = P.input.c; a.out_f32 = c.f32 ? 1 : 0; a.out_f16 = c.f16 ? 1 : 0;
     a.s2d = P.s2d ? 1 : 0;
@@ -357,7 +365,7 @@ int vd_plate_forward(Ctx& c, const uint8_t* d, int n, int h, int w, size_t pitch
     const int oh = a.oh, ow = a.ow;
     if (!letterboxed) {
         const double obytes =
-            P.s2d ? (double)(oh / 2 + 1) * (ow / 2 + 1) * 32 : (double)oh * ow * a.cpad * (c.f32 ? 4 : 2);
+            P.s2d ? (double)(oh / 2 + 1) * (ow / 2 + 1) * (c.f32 ? 64 : 32) : (double)oh * ow * a.cpad * (c.f32 ? 4 : 2);
         c.t_begin(2, (double)n * (a.nh * (double)w * 3 + obytes));
         hipError_t e = vd_launch_letterbox(a, c.stream);
         c.t_end();

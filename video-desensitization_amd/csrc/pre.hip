@@ -76,9 +76,15 @@ __device__ __forceinline__ void canvas_px(const LetterboxArgs& a, const uint8_t*
     }
 }
 
-// one 2x2 block's 16 values (4 sub-pixels x [3 channels, 0]): bf16, or fp16 (a.out_f16:
-// the fp32 plan's fused stem canvas, integer values, exact)
+// one 2x2 block's 16 values (4 sub-pixels x [3 channels, 0]): bf16, fp16 (a.out_f16:
+// the fp32 plan's fused face stem canvas, integer values, exact) or f32 (a.out_f32)
 __device__ __forceinline__ void store_s2d(const LetterboxArgs& a, size_t idx, const float (&v)[16]) {
+    if (a.out_f32) {   // the fp32 plan's plate canvas: integer values as f32, 64 B per block
+        float4* o = (float4*)((float*)a.out + idx * 16);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+        return;
+    }
     uint4 u[2];
     if (a.out_f16) {
         _Float16 t[16];

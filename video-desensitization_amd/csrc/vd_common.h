@@ -45,6 +45,7 @@ struct VdTune {
     int ssh_side = 0;         // 1: face SSH levels 1-2 (+ heads) on a second stream beside FPN merge / level 0
                               //   (at weight load; measured -0.1 ms/step, but overlapping launches inflate
                               //   the per-launch durations behind `roofline`: off by default)
+    int plate_s2d32 = 1;      // fp32 plan: the plate stem on the fp16 space-to-depth canvas (with plate_s2d)
     int plate_stage = 3;      // plate branch starts after face stage N (0: with the stem; 1-4: after
                               //   layerN; 5: after the whole face net). After layer3 its HBM-bound
                               //   convs overlap the MFMA-bound late face layers: 30.8 -> 30.0 ms/step
