@@ -249,7 +249,7 @@ def test_conv_matches_torch(gpu, face_ctx_factory, prec, case, options=None):
     if prec == "fp32-exact":
         options.update(f32_split=0)
         prec = "fp32"
-    if prec == "fp32-mid":                    # 1x1 convs on the 128 x 128 two-stage tile (option x6_mid)
+    if prec == "fp32-mid":                    # 1x1 Cout-128 convs on the 128 x 128 two-stage tile (option x6_mid)
         options.update(x6_mid=1 << 20, x6_stream=0)
         prec = "fp32"
     if prec == "fp32-mf32":                   # the big tile on v_mfma_f32_32x32x16_f16 (option x6_mf32)

@@ -1386,7 +1386,9 @@ static hipError_t launch_terms(const ConvArgs& a0, hipStream_t s) {
         // short-K 1x1 layers (HBM-bound f32 tensors): a 128 x 128 two-stage tile at two
         // workgroups per CU, so one workgroup's epilogue / prologue overlaps the other's
         // main loop, and 4x the tiles of the 256 x 256 form balance the last round
-        if (a.tune && a.tune->x6_mid && a.kh == 1 && a.kw == 1 && a.kpad <= a.tune->x6_mid && a.cout % 128 == 0)
+        // (Cout 128 only: layer2 conv1 at K = 512 340 -> 305 us; the Cout 256 layers at
+        // K = 512, FPN output1 / layer3.0 conv1, measured 7-13 % slower on it)
+        if (a.tune && a.tune->x6_mid && a.kh == 1 && a.kw == 1 && a.kpad <= a.tune->x6_mid && a.cout == 128)
             return launch_x6<128, 128, 256, 2, TERMS>(a, s);
     }
     if constexpr (TERMS == 2) {   // 64 x 128 wave tiles: 2/3 of the LDS fragment reads per MFMA

@@ -58,7 +58,7 @@ struct VdTune {
     int x6_small_k2 = 1 << 20;//   fp16 pairs: K at or below which N <= 64 layers take the small tile
     int x6_bn256 = 1;         // fp16 pairs: 256 x 256 tile for Cout % 256 == 0
     int x6_exact = 1;         // fp16 pairs: one A plane for inputs exact in fp16 (the face stem)
-    int x6_mid = 0;           // fp16 pairs: 1x1 convs with K <= this on the 128 x 128 two-stage tile (0: off)
+    int x6_mid = 512;         // fp16 pairs: 1x1 Cout-128 convs with K <= this on the 128 x 128 two-stage tile (0: off)
     int x6_mf32 = 0;          // fp16 pairs: 256 x {256,128} tiles on v_mfma_f32_32x32x16_f16 (else 16x16x32)
     int x6_tail = 0;          // fp16 pairs, big tiles: rows past the last full round of 256-row tiles on
                               //   narrower tiles (1: BN/2, 2: BN/4 columns, 0: off); N splits keep every
