@@ -24,10 +24,19 @@ Rank 0 prints one JSON line.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 64] [--precision fp32]
     torchrun --nproc-per-node N bench.py --gpus N ...
+
+`python bench.py --gpus N` (N > 1) with no WORLD_SIZE in the environment starts the
+N ranks itself: the parent makes no GPU call, runs torch.distributed.run as a child
+process (127.0.0.1 rendezvous, a free port) with the same arguments and exits with
+its status. A rank errors out when WORLD_SIZE != --gpus. `--force-dist` takes the
+distributed path (process group, record all-gather) even at one rank, so the RCCL
+branch can be exercised on a one-GPU box.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -37,13 +46,14 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "video-desensitization_amd"))
 sys.path.insert(0, ROOT)
 
-# MI355X_MICROARCH.md dense MFMA peaks. fp32 (default plan, conv_x6.hip): f32 FLOPs on the bf16
-# matrix cores at six products per multiply-add -> 2500 / 6; fp32_exact: v_mfma_f32_16x16x4_f32.
+# MI355X_MICROARCH.md dense MFMA peaks. fp32 (default plan, conv_x6.hip): f32 FLOPs on the f16
+# matrix cores at three products per multiply-add (scaled fp16 pairs) -> 2500 / 3; fp32_x6 (exact
+# 3-term bf16 split, six products) -> 2500 / 6; fp32_exact: v_mfma_f32_16x16x4_f32.
 PEAK_TFLOPS = {"bf16": 2500.0, "fp16": 2500.0, "fp32": 2500.0 / 3, "fp32_x6": 2500.0 / 6, "fp32_exact": 157.3}
 PEAK_HBM_GBS = 8000.0                           # MI355X_MICROARCH.md: HBM3E spec
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -74,7 +84,34 @@ def parse():
     ap.add_argument("--microbatch-stage", type=int, default=2, help="micro-batch the backbone through layer<N>")
     ap.add_argument("--faces", type=int, default=1, help="0: plates only, no mosaic (profiling the plate net)")
     ap.add_argument("--host-pipeline", type=int, default=1, help="1: also time the host-frame pipeline (PCIe incl.)")
-    return ap.parse_args()
+    ap.add_argument("--force-dist", action="store_true",
+                    help="process group + record all-gather even at one rank (exercises the RCCL branch at world 1)")
+    ap.add_argument("--launch-probe", action="store_true",
+                    help="each rank prints its rank / world as JSON and exits, no GPU work (launcher test)")
+    return ap.parse_args(argv)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_cmd(argv, gpus, port):
+    """The child command that starts `gpus` ranks of this script on one node (what the
+    driver runs for N > 1): torch.distributed.run, 127.0.0.1 rendezvous."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(gpus),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(argv, gpus):
+    """Start the ranks as a child process (the parent has made no GPU call and is never
+    replaced by exec) and return its exit status."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(launch_cmd(argv, gpus, _free_port()), env=env)
 
 
 def cpu_model():
@@ -130,7 +167,8 @@ def cpu_baseline(frames, sd, seconds, plates=True):
     rec = {"value": done / dt, "unit": "frames/s", "cores": cores, "kind": "port", "cpu_model": cpu_model(),
            "sample": f"{done} x {frames.shape[2]}x{frames.shape[1]} synthetic frames through the oracle "
                      f"(torch-CPU fp32 RetinaFace-R50 + numpy decode/NMS/mosaic"
-                     f"{' + YOLOv8n plate forward/NMS' if plates else ''}; one frame at a time), {dt:.1f} s"}
+                     f"{' + YOLOv8n plate forward/NMS' if plates else ''}; one frame at a time, where the reference "
+                     f"forwards 64-frame batches, combine_detect.py:204,216), {dt:.1f} s"}
     return rec, ref
 
 
@@ -200,18 +238,30 @@ class Mode:
 
 
 def main():
-    a = parse()
+    argv = sys.argv[1:]
+    a = parse(argv)
+    if a.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and (a.gpus > 1 or a.force_dist):
+        # not started by torchrun: start the ranks now, before anything touches the GPU
+        sys.exit(launch_ranks(argv, a.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {a.gpus}")
+    if a.launch_probe:
+        print(json.dumps({"rank": rank, "world": world, "local_rank": local}), flush=True)
+        return
     import torch
     import torch.distributed as dist
     from vdmi import _lib, synth, weights
     from vdmi.dist import all_gather_records, pack_records, shard_range
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if a.same_device:
         local = 0
-    if world > 1:
+    dist_on = world > 1 or a.force_dist
+    if dist_on:
         if a.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
         else:
@@ -249,11 +299,11 @@ def main():
             for s, n in batches:
                 fr, o = (frames, out) if n == B else (frames[:n], out[:n])
                 mode.process(fr, o)
-                if world > 1 or a.records_out:
+                if dist_on or a.records_out:
                     recs.append(pack_records(mode.faces.count[:n], mode.faces.xyxy[:n], rec_cap,
                                              mode.faces.score[:n], mode.faces.label[:n],
                                              torch.arange(f0 + s, f0 + s + n, dtype=torch.int32, device=dev)))
-            if world > 1:   # per-frame box records -> every rank (RCCL all-gather over xGMI)
+            if dist_on:     # per-frame box records -> every rank (RCCL all-gather over xGMI)
                 rec = torch.cat(recs) if recs else torch.zeros((0, 2 + 6 * rec_cap), dtype=torch.int32, device=dev)
                 if rec.shape[0] < per_rank:                       # uneven shards: padding rows (frame = -1)
                     pad = torch.zeros((per_rank - rec.shape[0], rec.shape[1]), dtype=torch.int32, device=dev)
@@ -267,17 +317,17 @@ def main():
 
     def timed(mode):
         torch.cuda.synchronize(dev)
-        if world > 1:
+        if dist_on:
             dist.barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         run(mode, a.steps)
         torch.cuda.synchronize(dev)
-        if world > 1:
+        if dist_on:
             dist.barrier()
         torch.cuda.synchronize(dev)
         d = time.perf_counter() - t0
-        if world > 1:
+        if dist_on:
             t = torch.tensor([d], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             d = float(t.item())
@@ -483,7 +533,8 @@ def main():
                                f"write-back, {total} frames of {W}x{H} per step over {world} GPU(s) "
                                f"(batches of {B} per GPU)",
                    "global_batch": total, "frame": f"{W}x{H}", "net_input": "640x640",
-                   "parallelism": f"frame-sharded x{world}" + (", RCCL all-gather of box records" if world > 1 else ""),
+                   "parallelism": f"frame-sharded x{world}" + (
+                       f", {'RCCL' if a.backend == 'nccl' else 'gloo'} all-gather of box records" if dist_on else ""),
                    "plates": plates},
     }
     for k in ("roofline", "blur_roofline", "faces_per_frame", "instrumented_ms_per_step", "plate_conv",
@@ -522,7 +573,7 @@ def main():
         np.save(a.records_out, gathered["rec"].cpu().numpy())
     if rank == 0:
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

@@ -11,7 +11,9 @@ package [ext], not installed here; no .record fixture ships with the reference):
     bytes (the writer's `blank` buffer: '0' then zeros); then Channel, ChunkHeader +
     ChunkBody pairs and finally the Index, whose SingleIndex entries hold each
     section's position and a cache (channel: message count, name, type; chunk header:
-    message count, begin / end time, raw size; chunk body: message count);
+    message count, begin / end time, raw size; chunk body: message count); raw size
+    is the running sum of the chunk's SingleMessage.content sizes, as Chunk::add
+    (cyber/record/file/chunk) accumulates it, not the serialised body size;
   * protobuf wire encoding of those messages (field numbers from record.proto) and
     of apollo.drivers.CompressedImage (frame_id 2, format 3, data 4,
     measurement_time 5);
@@ -120,8 +122,9 @@ def write_record(channels, chunks, compress=0):
                 written.add(name)
         cb = b"".join(field_bytes(1, single_message(*m)) for m in ch)
         t0, t1 = min(m[1] for m in ch), max(m[1] for m in ch)
-        chh = field_varint(1, t0) + field_varint(2, t1) + field_varint(3, len(ch)) + field_varint(4, len(cb))
-        index.append((CHUNK_HEADER, pos, (len(ch), t0, t1, len(cb))))
+        raw = sum(len(m[2]) for m in ch)          # Chunk::add: raw_size += message.content().size()
+        chh = field_varint(1, t0) + field_varint(2, t1) + field_varint(3, len(ch)) + field_varint(4, raw)
+        index.append((CHUNK_HEADER, pos, (len(ch), t0, t1, raw)))
         body += section(CHUNK_HEADER, chh)
         pos += 16 + len(chh)
         index.append((CHUNK_BODY, pos, len(ch)))

@@ -46,3 +46,31 @@ def test_bench_two_ranks_strong_equals_single_rank(gpu, tmp_path):
     assert list(r1) == list(range(6)) and list(r2) == list(range(6))
     assert sum(v[3] for v in r1.values()) > 0
     assert r2 == r1
+
+
+def test_bench_self_launch_two_ranks_equals_single_rank(gpu, tmp_path):
+    """`python bench.py --gpus 2` with no torchrun around it starts both ranks itself."""
+    from vdmi.dist import unpack_records
+    one = str(tmp_path / "one.npy")
+    two = str(tmp_path / "two.npy")
+    _run([sys.executable, "bench.py"] + COMMON, one)
+    out = _run([sys.executable, "bench.py", "--gpus", "2", "--backend", "gloo", "--same-device"] + COMMON, two)
+    assert '"n_gpus": 2' in out and "gloo all-gather" in out
+    r1, r2 = unpack_records(np.load(one)), unpack_records(np.load(two))
+    assert list(r2) == list(range(6)) and sum(v[3] for v in r1.values()) > 0
+    assert r2 == r1
+
+
+def test_bench_rccl_world1_equals_no_dist(gpu, tmp_path):
+    """The nccl (= RCCL) branch of bench.py -- init_process_group("nccl", device_id=...)
+    and all_gather_into_tensor of the box records on the device -- at one rank: the
+    gathered records equal the no-dist run's."""
+    from vdmi.dist import unpack_records
+    one = str(tmp_path / "one.npy")
+    rc = str(tmp_path / "rccl.npy")
+    _run([sys.executable, "bench.py"] + COMMON, one)
+    out = _run([sys.executable, "bench.py", "--gpus", "1", "--force-dist", "--backend", "nccl"] + COMMON, rc)
+    assert '"n_gpus": 1' in out and "RCCL all-gather" in out
+    r1, r2 = unpack_records(np.load(one)), unpack_records(np.load(rc))
+    assert list(r2) == list(range(6)) and sum(v[3] for v in r1.values()) > 0
+    assert r2 == r1

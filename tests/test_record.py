@@ -132,11 +132,12 @@ def test_repack_replaces_camera_data_and_relayouts(rec):
             f = orec.parse(e[2])
             t, pos = orec.get(f, 1), orec.get(f, 2)
             assert by_pos[pos][0] == t
-            if t == orec.CHUNK_HEADER:
+            if t == orec.CHUNK_HEADER:      # raw size = summed SingleMessage.content sizes (Chunk::add)
                 raw = orec.get(orec.parse(orec.get(f, 102)), 4)
                 nxt = [s for s in secs if s[1] > pos][0]
-                assert nxt[0] == orec.CHUNK_BODY and raw == len(nxt[2])
-                assert orec.get(orec.parse(by_pos[pos][1]), 4) == len(nxt[2])
+                content = sum(len(orec.get(orec.parse(m[2]), 3)) for m in orec.parse(nxt[2]))
+                assert nxt[0] == orec.CHUNK_BODY and raw == content
+                assert orec.get(orec.parse(by_pos[pos][1]), 4) == content
         a, b = orec.messages(data), orec.messages(out)
         assert [(c, t) for c, t, _ in a] == [(c, t) for c, t, _ in b]
         for (ch, _, ca), (_, _, cb) in zip(a, b):
@@ -155,23 +156,77 @@ def test_repack_replaces_camera_data_and_relayouts(rec):
                 assert [x for x in fa if x[0] != 4] == [x for x in fb if x[0] != 4]
 
 
-def test_repack_short_stream_keeps_the_rest(rec):
+def _new_streams(blobs, rng, vids, name="{cam}_processed.h265", cams=None):
+    """one replacement access unit per extracted message, with new payloads / lengths"""
+    orig = orec.extract(blobs, set(CAMS))
+    out = {}
+    for cam in orig:
+        if cams is not None and cam not in cams:
+            continue
+        units = [orec.get(orec.parse(c), 4) for d in blobs for ch, _, c in orec.messages(d) if ch.split("/")[3] == cam]
+        first = next(i for i, u in enumerate(units) if orec.is_key_frame(u))
+        repl = [au(rng, orec.is_key_frame(u), n=int(rng.integers(5, 400))) for u in units[first:]]
+        (vids / name.format(cam=cam)).write_bytes(b"".join(repl))
+        out[cam] = (first, repl)
+    return out
+
+
+def test_repack_reference_output_names(rec):
+    """combine_detect.py:658 names each desensitised stream <camera>_processed.<ext>
+    in the directory it hands to write_allH265_record_all (:958): those are found and
+    every extracted message is replaced."""
+    from vdmi import record
+    tmp, src, blobs, names = rec
+    vids = tmp / "videos"
+    vids.mkdir()
+    new = _new_streams(blobs, np.random.default_rng(4), vids)
+    assert record.write_allH265_record_all(str(src), str(vids), str(tmp / "out")) == len(names)
+    for cam, (first, repl) in new.items():
+        topic = f"/drivers/camera/{cam}/compressed/image"
+        got = [orec.get(orec.parse(c), 4) for d in names for ch, _, c in orec.messages((tmp / "out" / d).read_bytes())
+               if ch == topic]
+        assert got[first:] == repl
+
+
+def test_repack_short_stream_is_an_error(rec):
+    """Fewer access units than extracted messages: refused, nothing written (a record
+    with original frames left in would not be desensitised)."""
+    import vdmi
     from vdmi import record
     tmp, src, blobs, names = rec
     vids = tmp / "videos"
     vids.mkdir()
     rng = np.random.default_rng(1)
+    _new_streams(blobs, rng, vids)
     cam = CAMS[0].split("/")[3]
-    repl = [au(rng, True, n=50), au(rng, False, n=60)]
-    (vids / f"{cam}.h265").write_bytes(b"".join(repl))
-    record.write_allH265_record_all(str(src), str(vids), str(tmp / "out"))
-    got = [orec.get(orec.parse(c), 4) for d in names for ch, _, c in orec.messages((tmp / "out" / d).read_bytes())
-           if ch == CAMS[0]]
-    exp = [orec.get(orec.parse(c), 4) for d in blobs for ch, _, c in orec.messages(d) if ch == CAMS[0]]
-    first = next(i for i, u in enumerate(exp) if orec.is_key_frame(u))
-    assert got[:first] == exp[:first]
-    assert got[first:first + 2] == repl
-    assert got[first + 2:] == exp[first + 2:]
+    (vids / f"{cam}_processed.h265").write_bytes(au(rng, True, n=50) + au(rng, False, n=60))
+    with pytest.raises(vdmi.VdError, match="access units"):
+        record.write_allH265_record_all(str(src), str(vids), str(tmp / "out"))
+    assert not any((tmp / "out" / n).exists() for n in names)
+
+
+def test_repack_missing_camera_stream_is_an_error(rec):
+    import vdmi
+    from vdmi import record
+    tmp, src, blobs, names = rec
+    vids = tmp / "videos"
+    vids.mkdir()
+    _new_streams(blobs, np.random.default_rng(2), vids, cams={CAMS[0].split("/")[3], CAMS[1].split("/")[3]})
+    with pytest.raises(vdmi.VdError, match="no desensitised stream for camera rear"):
+        record.write_allH265_record_all(str(src), str(vids), str(tmp / "out"))
+
+
+def test_non_segment_files_are_skipped(rec):
+    """Only <stem>.record and <stem>.record.<digits> are CyberRT segments."""
+    from vdmi import record
+    tmp, src, blobs, _ = rec
+    (src / "notes.record.bak").write_bytes(b"junk" * 50)
+    (src / "x.recording").write_bytes(b"junk" * 50)
+    (src / "y.record.01a").write_bytes(b"junk" * 50)
+    n = record.read_record2h265_all(str(src), str(tmp / "h265"))
+    assert n == 3
+    for cam, data in orec.extract(blobs, set(CAMS)).items():
+        assert (tmp / "h265" / "hevcs" / f"{cam}.h265").read_bytes() == data
 
 
 def test_record_errors(tmp_path):
@@ -209,3 +264,15 @@ def test_oracle_layout_known_answer():
     assert [s[0] for s in secs] == [orec.CHANNEL, orec.CHUNK_HEADER, orec.CHUNK_BODY, orec.INDEX]
     assert orec.get(hdr, 12) == len(data) and orec.get(hdr, 6) == secs[-1][1]
     assert orec.messages(data) == [("/a", 5, b"xy")]
+
+
+def test_chunk_raw_size_is_summed_content_known_answer():
+    """ChunkHeader.raw_size (and its index cache) = the sum of the chunk's
+    SingleMessage.content sizes, as CyberRT's Chunk::add accumulates it."""
+    data = orec.write_record([("/a", "T")], [[("/a", 5, b"xy"), ("/a", 6, b"abcde")]])
+    hdr, secs = orec.read_sections(data)
+    ch = orec.parse(secs[1][2])
+    assert orec.get(ch, 4) == 7 and orec.get(ch, 3) == 2
+    idx = [orec.parse(e[2]) for e in orec.parse(secs[-1][2])]
+    cache = [orec.parse(orec.get(f, 102)) for f in idx if orec.get(f, 1) == orec.CHUNK_HEADER]
+    assert orec.get(cache[0], 4) == 7

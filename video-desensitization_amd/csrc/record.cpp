@@ -22,10 +22,15 @@
 //   of every message from the topic's first key frame (an access unit holding a VPS /
 //   SPS / PPS or IRAP slice NAL) on, concatenated into <out>/hevcs/<camera>.h265.
 // repack:  the same records rewritten with each extracted message's data replaced by
-//   the matching access unit of <videos>/<camera>.h265 (the desensitised stream, split
-//   at access-unit boundaries); every other byte is carried over, and the positions /
-//   sizes that move (chunk raw sizes, index positions and caches, header size and
-//   index position) are recomputed. Written as <name>.tmp_record, then renamed.
+//   the matching access unit of <videos>/<camera>_processed.h265 (the name the
+//   reference's create_video gives it, combine_detect.py:658; <camera>.h265 also
+//   accepted), the desensitised stream split at access-unit boundaries; a topic with
+//   extracted messages and no stream, or a stream whose access-unit count differs
+//   from the topic's extracted message count, is an error (no record is written with
+//   original frames left in). Every other byte is carried over, and the positions /
+//   sizes that move (chunk raw sizes = summed message content sizes, index positions
+//   and caches, header size and index position) are recomputed. Written as
+//   <name>.tmp_record, then renamed.
 // Protobuf messages are edited as field lists and re-serialised in their original
 // field order, so a record written by a canonical protobuf encoder and repacked with
 // its own extracted streams comes back byte-identical (tests/test_record.py).
@@ -266,12 +271,25 @@ std::vector<std::string> access_units(const std::string& s) {
     return out;
 }
 
+// CyberRT segment names: <stem>.record or <stem>.record.<digits> (the recorder's
+// split segments); anything else (foo.record.bak, x.recording, .tmp_record) is skipped
+bool is_segment_name(const std::string& name) {
+    const size_t k = name.rfind(".record");
+    if (k == std::string::npos || k == 0) return false;
+    const size_t e = k + 7;
+    if (e == name.size()) return true;
+    if (name[e] != '.' || e + 1 == name.size()) return false;
+    for (size_t i = e + 1; i < name.size(); ++i)
+        if (name[i] < '0' || name[i] > '9') return false;
+    return true;
+}
+
 int list_records(const char* dir, std::vector<std::string>& files) {
     DIR* d = opendir(dir);
     if (!d) return vd_set_error(VD_ERR_ARG, "record: cannot open directory %s", dir);
     while (dirent* e = readdir(d)) {
         const std::string name = e->d_name;
-        if (name.find(".record") == std::string::npos || name.find(".tmp_record") != std::string::npos) continue;
+        if (!is_segment_name(name)) continue;
         const std::string path = std::string(dir) + "/" + name;
         struct stat st;
         if (stat(path.c_str(), &st) == 0 && S_ISREG(st.st_mode)) files.push_back(name);
@@ -328,25 +346,44 @@ int for_camera_messages(Record& r, Fn&& fn, bool rewrite) {
     return VD_OK;
 }
 
+// ChunkHeader.raw_size as CyberRT's Chunk::add keeps it: the running sum of the
+// chunk's SingleMessage.content sizes (not the serialised body size)
+int content_bytes(const std::string& body, uint64_t& total) {
+    std::vector<Field> fs;
+    if (!parse(body, fs)) return vd_set_error(VD_ERR_ARG, "record: bad chunk body");
+    total = 0;
+    for (Field& m : fs) {
+        if (m.num != 1 || m.wt != 2) continue;
+        std::vector<Field> msg;
+        if (!parse(m.b, msg)) return vd_set_error(VD_ERR_ARG, "record: bad message in chunk body");
+        if (const Field* c = find(msg, 3))
+            if (c->wt == 2) total += c->b.size();
+    }
+    return VD_OK;
+}
+
 // positions and sizes after bodies changed: chunk headers' raw_size, the index's
 // positions and chunk-header caches, the header's size and index position
 int relayout(Record& r, std::string& out) {
     std::map<uint64_t, uint64_t> moved;                   // old section position -> new
-    std::map<uint64_t, uint64_t> body_size;               // new position of a chunk header -> its body size
+    std::map<uint64_t, uint64_t> body_size;               // old position of a chunk header -> its raw size
     uint64_t at = 16 + kHeaderLength;
     for (size_t i = 0; i < r.secs.size(); ++i) {
         Section& s = r.secs[i];
         if (s.type == SEC_CHUNK_HEADER && i + 1 < r.secs.size() && r.secs[i + 1].type == SEC_CHUNK_BODY) {
+            uint64_t raw_size = 0;
+            int rc = content_bytes(r.secs[i + 1].body, raw_size);
+            if (rc) return rc;
+            body_size[s.pos] = raw_size;
             std::vector<Field> ch;
             if (parse(s.body, ch)) {
                 if (Field* raw = find(ch, 4)) {
-                    raw->v = r.secs[i + 1].body.size();
+                    raw->v = raw_size;
                     s.body = serialize(ch);
                 }
             }
         }
         moved[s.pos] = at;
-        if (s.type == SEC_CHUNK_HEADER && i + 1 < r.secs.size()) body_size[s.pos] = r.secs[i + 1].body.size();
         at += 16 + s.body.size();
     }
     uint64_t index_pos = 0;
@@ -444,11 +481,33 @@ extern "C" int vd_record_repack_h265(const char* record_dir, const char* videos_
     std::vector<std::string> files;
     int rc = list_records(record_dir, files);
     if (rc) return rc;
-    // the desensitised streams, split into access units
+    // per camera topic, how many messages the extract step put into its stream
+    std::vector<size_t> count(kNumTopics, 0);
+    {
+        std::vector<int> started(kNumTopics, 0);
+        for (const std::string& name : files) {
+            Record r;
+            if ((rc = load_record(std::string(record_dir) + "/" + name, r))) return rc;
+            rc = for_camera_messages(r, [&](int t, std::vector<Field>& img) {
+                const Field* data = find(img, 4);
+                if (!data || data->wt != 2) return false;
+                if (!started[t] && !is_key_frame(data->b)) return false;
+                started[t] = 1;
+                ++count[t];
+                return false;
+            }, false);
+            if (rc) return rc;
+        }
+    }
+    // the desensitised streams (combine_detect.py:658 writes <camera>_processed.<ext>),
+    // split into access units; every extracted topic needs one with exactly one access
+    // unit per extracted message -- a record is never written with original frames left in
     std::vector<std::vector<std::string>> aus(kNumTopics);
     std::vector<int> have(kNumTopics, 0);
     for (int t = 0; t < kNumTopics; ++t) {
-        for (const char* pat : {"%s/%s.h265", "%s/%s.hevc", "%s/processed_%s.h265"}) {
+        if (!count[t]) continue;
+        for (const char* pat : {"%s/%s_processed.h265", "%s/%s_processed.hevc", "%s/%s.h265", "%s/%s.hevc",
+                                "%s/processed_%s.h265"}) {
             char p[4096];
             std::snprintf(p, sizeof p, pat, videos_dir, camera_of(t).c_str());
             struct stat st;
@@ -457,8 +516,15 @@ extern "C" int vd_record_repack_h265(const char* record_dir, const char* videos_
             if ((rc = read_file(p, s))) return rc;
             aus[t] = access_units(s);
             have[t] = 1;
+            if (aus[t].size() != count[t])
+                return vd_set_error(VD_ERR_ARG, "record: %s holds %zu access units but the records hold %zu extracted "
+                                    "messages of camera %s", p, aus[t].size(), count[t], camera_of(t).c_str());
             break;
         }
+        if (!have[t])
+            return vd_set_error(VD_ERR_ARG, "record: no desensitised stream for camera %s in %s (looked for "
+                                "%s_processed.h265 / .hevc, %s.h265 / .hevc)", camera_of(t).c_str(), videos_dir,
+                                camera_of(t).c_str(), camera_of(t).c_str());
     }
     make_dirs(out_dir);
     std::vector<size_t> next(kNumTopics, 0);
@@ -473,8 +539,7 @@ extern "C" int vd_record_repack_h265(const char* record_dir, const char* videos_
             if (!data || data->wt != 2) return false;
             if (!started[t] && !is_key_frame(data->b)) return false;   // not in the extracted stream
             started[t] = 1;
-            if (next[t] >= aus[t].size()) return false;             // the stream ran out: keep the original
-            data->b = aus[t][next[t]++];
+            data->b = aus[t][next[t]++];                            // counts checked above
             return true;
         }, true);
         if (rc) return rc;

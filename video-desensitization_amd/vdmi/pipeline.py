@@ -434,11 +434,13 @@ def _gpu_codec_batches(batches, output_dir, face_detector, plate_detector, batch
                     f0, c0 = enc.pop(0)
                     if collect(f0):
                         totals[0] += c0[0]; totals[1] += c0[1]; totals[2] += c0[2]
+    finally:
+        # every batch already handed to the encoder is finished (its errors logged, its
+        # writes queued) before the saves are waited on -- also when a load failure aborts
         while enc:
             f0, c0 = enc.pop(0)
             if collect(f0):
                 totals[0] += c0[0]; totals[1] += c0[1]; totals[2] += c0[2]
-    finally:
         ahead.shutdown()
         behind.shutdown()
         dctx.close()
