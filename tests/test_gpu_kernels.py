@@ -472,3 +472,35 @@ def test_postprocess_ties_and_capacity(gpu, face_ctx_factory):
     assert full.cap == len(e[0])
     np.testing.assert_array_equal(full.frame(0)[3], e[0])
     np.testing.assert_array_equal(full.frame(0)[0], e[2])
+
+
+TR_CASES = [
+    # 1x1 convs on the TR tiles (option x6_gemm1x1): 256 x 256 (Cout % 256, >= 192 tiles), 256 x 128,
+    # 128 x 128 (Cout 128, K <= 512); M tails, stride 2, residual before / after the activation
+    (2, 37, 41, 512, 256, 1, 1, 0, 1, 1),
+    (1, 33, 35, 1024, 512, 1, 2, 0, 0, 0),
+    (3, 19, 23, 512, 128, 1, 1, 0, 1, 0),
+    (1, 21, 19, 256, 384, 1, 1, 0, 2, 2),
+    (2, 45, 47, 512, 2048, 1, 1, 0, 1, 1),
+]
+
+
+@pytest.mark.parametrize("case", TR_CASES)
+def test_conv_tr_tiles_bit_identical(gpu, face_ctx_factory, case):
+    """The TR tiles (D^T accumulators, register epilogue) compute the same products in
+    the same order as the untransposed tiles: outputs (and the per-frame max slots the
+    hook checks) are bit-identical, and within the fp32 tolerance of torch."""
+    n, h, w, cin, cout, k, s, p, act, res_mode = case
+    rng = np.random.default_rng(cin + 3 * cout)
+    x = np.maximum(rng.standard_normal((n, h, w, cin)), 0).astype(F32)
+    wt = (rng.standard_normal((cout, cin, k, k)) * np.sqrt(2.0 / cin)).astype(F32)
+    scale = rng.uniform(0.5, 1.5, cout).astype(F32)
+    shift = rng.standard_normal(cout).astype(F32) * F32(0.1)
+    oh, ow = (h - 1) // s + 1, (w - 1) // s + 1
+    res = rng.standard_normal((n, oh, ow, cout)).astype(F32) if res_mode else None
+    outs = []
+    for tr in (0, 1):
+        ctx = face_ctx_factory("fp32", 8, options=(("x6_gemm1x1", tr), ("x6_stream", 0)))
+        outs.append(ctx.conv2d(x, wt, s, p, scale, shift, act, 0.1, res, res_mode))
+    assert np.array_equal(outs[0], outs[1])
+    test_conv_matches_torch(gpu, face_ctx_factory, "fp32", case, options=dict(x6_gemm1x1=1, x6_stream=0))

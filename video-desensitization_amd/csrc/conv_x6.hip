@@ -173,6 +173,20 @@ __device__ __forceinline__ f32x4_t mfma_terms<2>(const u32x4 (&a)[3], const u32x
     return acc;
 }
 
+// The same three products in the same order with the operands exchanged: the MFMA
+// computes D^T (rows = weight rows / output channels, columns = pixels), so a lane's
+// accumulator holds 4 consecutive channels of one pixel (register epilogue, TR tiles)
+__device__ __forceinline__ f32x4_t mfma_pair_tr(const u32x4 (&a)[3], const u32x4 (&b)[3], f32x4_t acc) {
+#define VDT_MFMA(pa, pb)                                                                                 \
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, b[pb]),                    \
+                                                 __builtin_bit_cast(f16x8_t, a[pa]), acc, 0, 0, 0)
+    VDT_MFMA(1, 0);
+    VDT_MFMA(0, 1);
+    VDT_MFMA(0, 0);
+#undef VDT_MFMA
+    return acc;
+}
+
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
 
 // fp16 pair on the 32x32x16 matrix-core form: the same three products per K step of
@@ -189,9 +203,34 @@ __device__ __forceinline__ f32x16_t mfma_pair32(const u32x4 (&a)[3], const u32x4
     return acc;
 }
 
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+
+// 8 f32 -> the scaled fp16 pair as two packed 16-B planes, element pairs built in
+// half2 registers (v_fma_mixlo / v_fma_mixhi write the halves in place: no shifts or
+// ORs); the same roundings as split2h
+__device__ __forceinline__ void split_pair8(const float (&e)[8], float sa, u32x4& H, u32x4& L) {
+    unsigned hv[4], lv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        half2_t h, l;
+        h[0] = (_Float16)__builtin_fmaf(e[2 * j], sa, 0.f);
+        h[1] = (_Float16)__builtin_fmaf(e[2 * j + 1], sa, 0.f);
+        l[0] = (_Float16)__builtin_fmaf(e[2 * j], sa, -(float)h[0]);
+        l[1] = (_Float16)__builtin_fmaf(e[2 * j + 1], sa, -(float)h[1]);
+        hv[j] = __builtin_bit_cast(unsigned, h);
+        lv[j] = __builtin_bit_cast(unsigned, l);
+    }
+    H = u32x4{hv[0], hv[1], hv[2], hv[3]};
+    L = u32x4{lv[0], lv[1], lv[2], lv[3]};
+}
+
 // 8 f32 -> TERMS packed 16-B planes (bf16 truncation split, or scaled fp16 pair)
 template <int TERMS>
 __device__ __forceinline__ void split_pack(const float (&e)[8], float sa, u32x4 (&o)[3]) {
+    if constexpr (TERMS == 2) {
+        split_pair8(e, sa, o[0], o[1]);
+        return;
+    }
     unsigned hv[8], mv[8], lv[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -214,6 +253,10 @@ __device__ __forceinline__ void x6_epilogue(const ConvArgs& a, AccT (&acc)[S::TM
                                             int wn, int tid, int lane, char* smem, int amax_off) {
     constexpr int BM = S::BM, BN = S::BNV, NT = S::NT, TM = S::TM, TN = S::TN, TERMS = S::TERMSV;
     const int ohw = a.yh * a.yw;
+    if (a.dbg & 1) {                                   // timing experiment: main loop only
+        if (acc[0][0][0] == 1234.5f) ((float*)a.y)[tid] = 1.f;
+        return;
+    }
     // ---- fused epilogue: BM / EPR passes of EPR rows through LDS ([EPR][BN+4] f32)
     constexpr int EPLD = S::EPLD, EPR = S::EPR, CG = BN / 8, ITEMS = EPR * CG / NT;
     static_assert(ITEMS >= 1 && (EPR * CG) % NT == 0, "epilogue items");
@@ -325,13 +368,99 @@ __device__ __forceinline__ void x6_epilogue(const ConvArgs& a, AccT (&acc)[S::TM
     }
 }
 
-template <int BM, int BN, int NT, int NST, int TERMS, int MF, int NA>
+// Epilogue of the transposed (TR) tiles straight from registers: the weight rows were
+// loaded permuted (x6_tr_row), so MFMA blocks 2jp, 2jp+1 give lane (p = l % 16, q = l / 16)
+// the 8 consecutive channels 32 jp + 8 q .. +7 of pixel 16 i + p: BN + residual +
+// activation on 8 values, two 16-B stores, no LDS staging and no workgroup barrier
+// (only the per-frame max goes through LDS). Same arithmetic as x6_epilogue.
+template <class S>
+__device__ __forceinline__ void x6_epilogue_tr(const ConvArgs& a, f32x4_t (&acc)[S::TM][S::TN], int m0, int n0,
+                                               int wm, int wn, int lane, unsigned* s_amax) {
+    constexpr int TM = S::TM, TN = S::TN;
+    static_assert(TN % 2 == 0, "TR tiles pair the channel blocks");
+    const int ohw = a.yh * a.yw;
+    const int q = lane >> 4, pl = lane & 15;
+    const int cb = n0 + wn * S::WTN + 8 * q;
+    int mrow[TM], fbs[TM];
+    float inv[TM], vmax[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int m = m0 + wm * S::WTM + 16 * i + pl;
+        mrow[i] = m;
+        fbs[i] = m < a.M ? m / ohw : -1;
+        inv[i] = __builtin_ldexpf(1.f, -act_scale_exp(a, fbs[i] < 0 ? 0 : fbs[i]));
+        vmax[i] = 0.f;
+    }
+#pragma unroll
+    for (int jp = 0; jp < TN / 2; ++jp) {
+        const int c = cb + 32 * jp;
+        if (c >= a.cout) continue;
+        const float4 s0 = *(const float4*)(a.scale + c), s1 = *(const float4*)(a.scale + c + 4);
+        const float4 h0 = *(const float4*)(a.shift + c), h1 = *(const float4*)(a.shift + c + 4);
+        const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+        const float sh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int m = mrow[i];
+            if (m >= a.M) continue;
+            float rv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            if (a.res_mode != VD_RES_NONE) {
+                size_t roff;
+                if (a.res_up) {
+                    const int b = fbs[i], rem = m - b * ohw;
+                    const int oy = rem / a.yw, ox = rem - oy * a.yw;
+                    roff = ((size_t)(b * a.rh + (oy >> 1)) * a.rw + (ox >> 1)) * a.res_ld;
+                } else {
+                    roff = (size_t)m * a.res_ld;
+                }
+                roff += a.res_coff + c;
+                const float4 r0 = *(const float4*)((const float*)a.res + roff);
+                const float4 r1 = *(const float4*)((const float*)a.res + roff + 4);
+                rv[0] = r0.x; rv[1] = r0.y; rv[2] = r0.z; rv[3] = r0.w;
+                rv[4] = r1.x; rv[5] = r1.y; rv[6] = r1.z; rv[7] = r1.w;
+            }
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float ev = e < 4 ? acc[i][2 * jp][e] : acc[i][2 * jp + 1][e - 4];
+                float t = (ev * inv[i]) * sc[e] + sh[e];
+                if (a.res_mode == VD_RES_PRE_ACT) t += rv[e];
+                t = act_apply(t, a.act, a.slope);
+                if (a.res_mode == VD_RES_POST_ACT) t += rv[e];
+                v[e] = t;
+                vmax[i] = fmaxf(vmax[i], fabsf(t));
+            }
+            float* yp = (float*)a.y + (size_t)m * a.ldy + a.ycoff + c;
+            *(float4*)yp = make_float4(v[0], v[1], v[2], v[3]);
+            *(float4*)(yp + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        }
+    }
+    if (a.ymax) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) amax_lds_add(s_amax, fbs[i], vmax[i]);
+        __syncthreads();
+        amax_lds_flush(s_amax, a.ymax, a.B);
+    }
+}
+
+// LDS row -> weight row of a TR tile: row 16 j + i of each 32-row group holds channel
+// 8 (i >> 2) + 4 (j & 1) + (i & 3) of the group, so blocks 2jp, 2jp+1 give a lane 8
+// consecutive channels (conv1x1_x6_kernel's permutation)
+__device__ __forceinline__ int x6_tr_row(int row) {
+    const int j = (row >> 4) & 1, i = row & 15;
+    return (row & ~31) + 8 * (i >> 2) + 4 * j + (i & 3);
+}
+
+template <int BM, int BN, int NT, int NST, int TERMS, int MF, int NA, bool TR = false>
 // NA: A register sets (K tiles of A loads in flight: NA - 1 besides the one being split)
 // 8 waves: two workgroups' worth of waves per SIMD pair (256 VGPRs each); 4 waves (one
 // per SIMD, 128 x 128 wave tiles): the whole 512-register file per wave, the
 // accumulators in AGPRs
+// TR: transposed accumulators (D^T, weight rows permuted by x6_tr_row) and the register
+// epilogue x6_epilogue_tr; fp16 pairs on the 16x16x32 form only
 __global__ __launch_bounds__(NT, NT == 256 && BM == 256 ? 1 : 2) void conv_x6_kernel(ConvArgs a) {
     static_assert(MF == 16 || (MF == 32 && TERMS == 2), "32x32x16 form: fp16 pairs only");
+    static_assert(!TR || (MF == 16 && TERMS == 2), "TR tiles: fp16 pairs on 16x16x32");
     using S = X6Shape<BM, BN, NT, NST, TERMS, MF>;
     constexpr int STAGE = S::STAGE, PL_A = S::PL_A, PL_B = S::PL_B, TM = S::TM, TN = S::TN, WAVES = S::WAVES;
     constexpr int AROWS = S::AROWS, AIT = S::AITEMS;
@@ -448,7 +577,8 @@ __global__ __launch_bounds__(NT, NT == 256 && BM == 256 ? 1 : 2) void conv_x6_ke
                 const int p = j / RB, r0 = (j % RB) * 16;
                 const int row = r0 + (lane >> 2), slot = lane & 3;
                 const int chunk = slot ^ (((row >> 3) & 1) * 3);
-                const unsigned off = (unsigned)((((long)(n0 + row) * nk + kt) * S::TB + p) * 64 + chunk * 16);
+                const int wrow = TR ? x6_tr_row(row) : row;
+                const unsigned off = (unsigned)((((long)(n0 + wrow) * nk + kt) * S::TB + p) * 64 + chunk * 16);
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_w, (lds_void_t*)(Bs + p * PL_B + r0 * 64), 16, off, 0,
                                                          0, 0);
             }
@@ -507,7 +637,10 @@ __global__ __launch_bounds__(NT, NT == 256 && BM == 256 ? 1 : 2) void conv_x6_ke
                 for (int p = 0; p < S::TB; ++p)
                     bf[p] = *(const u32x4*)(Bs + p * PL_B + swz(wn * S::WTN + j * 16 + (lane & 15), ch));
 #pragma unroll
-                for (int i = 0; i < TM; ++i) acc[i][j] = mfma_terms<TERMS>(af[i], bf, acc[i][j]);
+                for (int i = 0; i < TM; ++i) {
+                    if constexpr (TR) acc[i][j] = mfma_pair_tr(af[i], bf, acc[i][j]);
+                    else acc[i][j] = mfma_terms<TERMS>(af[i], bf, acc[i][j]);
+                }
 #pragma unroll
                 for (int q = 0; q < AIT; ++q)
                     if (split_next && j == q * TN / AIT) store_item(st_next, rn, q);
@@ -526,7 +659,10 @@ __global__ __launch_bounds__(NT, NT == 256 && BM == 256 ? 1 : 2) void conv_x6_ke
                 for (int p = 0; p < S::TA; ++p)
                     af[p] = *(const u32x4*)(A + p * PL_A + swz(wm * S::WTM + i * 16 + (lane & 15), ch));
 #pragma unroll
-                for (int j = 0; j < TN; ++j) acc[i][j] = mfma_terms<TERMS>(af, bf[j], acc[i][j]);
+                for (int j = 0; j < TN; ++j) {
+                    if constexpr (TR) acc[i][j] = mfma_pair_tr(af, bf[j], acc[i][j]);
+                    else acc[i][j] = mfma_terms<TERMS>(af, bf[j], acc[i][j]);
+                }
                 if constexpr (AIT == 2) {
                     if (split_next && i == 0) store_item(st_next, rn, 0);
                     if (split_next && i == (TM > 2 ? 2 : 1)) store_item(st_next, rn, 1);
@@ -598,9 +734,16 @@ __global__ __launch_bounds__(NT, NT == 256 && BM == 256 ? 1 : 2) void conv_x6_ke
         if (kt + 1 < nk) iter1(kt + 1, ra[1], ra[0]);
     }
     }
-    __syncthreads();
-
-    x6_epilogue<S, MF>(a, acc, m0, n0, wm, wn, tid, lane, smem, S::LDS);
+    if constexpr (TR) {
+        if (a.dbg & 1) {                               // timing experiment: main loop only
+            if (acc[0][0][0] == 1234.5f) ((float*)a.y)[tid] = 1.f;
+            return;
+        }
+        x6_epilogue_tr<S>(a, acc, m0, n0, wm, wn, lane, (unsigned*)(smem + S::LDS));
+    } else {
+        __syncthreads();
+        x6_epilogue<S, MF>(a, acc, m0, n0, wm, wn, tid, lane, smem, S::LDS);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -923,7 +1066,9 @@ __global__ __launch_bounds__(512) void conv1x1_x6_kernel(ConvArgs a, int nchunks
             }
         }
         float vmax = 0.f;
-        if (mu < a.M) {
+        if (a.dbg & 1) {                                   // timing experiment: no epilogue
+            if (acc[0][0] == 1234.5f) ((float*)a.y)[tid] = 1.f;
+        } else if (mu < a.M) {
             const int m = mu;
             size_t roff = 0;
             if constexpr (RES != VD_RES_NONE) {
@@ -1198,16 +1343,16 @@ bool vd_conv_x6_ok(const ConvArgs& a) {
 }
 
 // rows [mbase, M) of the conv (mbase a multiple of the caller's tile rows)
-template <int BM, int BN, int NT, int NST, int TERMS, int MF = 16, int NA = 2>
+template <int BM, int BN, int NT, int NST, int TERMS, int MF = 16, int NA = 2, bool TR = false>
 static hipError_t launch_x6(const ConvArgs& a0, hipStream_t s, int mbase = 0, int mtiles = -1) {
-    if constexpr (NA == 2 && BM == 256 && BN <= 128 && NST == 2 && TERMS == 2 && MF == 16) {
+    if constexpr (NA == 2 && BM == 256 && BN <= 128 && NST == 2 && TERMS == 2 && MF == 16 && !TR) {
         // option x6_adepth: four A register sets (three K tiles of A loads in flight) on
         // the 256 x {128, 64, 32} tiles, whose accumulators leave the registers for them
         if (a0.tune && a0.tune->x6_adepth >= 4) return launch_x6<BM, BN, NT, NST, TERMS, MF, 4>(a0, s, mbase, mtiles);
     }
     using S = X6Shape<BM, BN, NT, NST, TERMS, MF>;
     static const bool attr = [] {
-        (void)hipFuncSetAttribute((const void*)conv_x6_kernel<BM, BN, NT, NST, TERMS, MF, NA>,
+        (void)hipFuncSetAttribute((const void*)conv_x6_kernel<BM, BN, NT, NST, TERMS, MF, NA, TR>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS + 4 * kAmaxFrames);
         return true;
     }();
@@ -1218,7 +1363,7 @@ static hipError_t launch_x6(const ConvArgs& a0, hipStream_t s, int mbase = 0, in
     a.mbase = mbase;
     const int mt = mtiles >= 0 ? mtiles : (a.M - mbase + BM - 1) / BM;
     const int lds = S::LDS + (a.ymax ? 4 * a.B : 0);
-    hipLaunchKernelGGL((conv_x6_kernel<BM, BN, NT, NST, TERMS, MF, NA>), dim3(mt * a.ntiles_n), dim3(NT), lds, s, a);
+    hipLaunchKernelGGL((conv_x6_kernel<BM, BN, NT, NST, TERMS, MF, NA, TR>), dim3(mt * a.ntiles_n), dim3(NT), lds, s, a);
     return hipGetLastError();
 }
 
@@ -1321,6 +1466,29 @@ static int stream_x6_nch(const ConvArgs& a, int terms) {
     return a.cout % 64 == 0 && a.cin_pad <= 128 ? 64 : 0;
 }
 
+// TR tiles (option x6_gemm1x1, default): the 1x1 convs the streaming form does not take
+// (K >= 512, strided downsamples) on conv_x6_kernel with D^T accumulators and the
+// register epilogue (x6_epilogue_tr). Same tiles and products as the untransposed form,
+// bit-identical results (tests/test_gpu_kernels.py); the epilogue skips the LDS round
+// trip and its two barriers per pass (tools/x6bench, B = 64: layer4 conv3 334 -> 304 us,
+// layer3.0 downsample 528 -> 472, layer3 conv1 263 -> 243, FPN output1 553 -> 512).
+// Measured and not kept: the pixel operand loaded straight into registers by the two
+// waves of its row band (no LDS image, one barrier per K tile with three weight
+// stages): its main loop ran 5-10 % slower than the LDS-staged one (layer3 conv1
+// 215 -> 235 us without epilogue). Needs 8-channel 16-B output / residual vectors.
+static bool x6_tr_ok(const ConvArgs& a) {
+    if (a.kh != 1 || a.kw != 1 || a.pad != 0 || a.cout % 128) return false;
+    if ((a.ldy | a.ycoff) & 7) return false;
+    return a.res_mode == VD_RES_NONE || !((a.res_ld | a.res_coff) & 7);
+}
+
+static hipError_t launch_tr(const ConvArgs& a, hipStream_t s) {
+    const long t256 = (long)((a.M + 255) / 256) * (a.cout / 256);
+    if (a.cout % 256 == 0 && t256 >= 192) return launch_x6<256, 256, 512, 2, 2, 16, 2, true>(a, s);
+    if (a.cout == 128 && a.tune->x6_mid && a.kpad <= a.tune->x6_mid) return launch_x6<128, 128, 256, 2, 2, 16, 2, true>(a, s);
+    return launch_x6<256, 128, 512, 2, 2, 16, 2, true>(a, s);
+}
+
 template <int TERMS>
 static hipError_t launch_terms(const ConvArgs& a0, hipStream_t s) {
     ConvArgs a = a0;
@@ -1346,6 +1514,11 @@ static hipError_t launch_terms(const ConvArgs& a0, hipStream_t s) {
             }
         }
     }
+    if constexpr (TERMS == 2) {
+        // option x6_gemm1x1 = 2 (experiments): the K <= 256 layers of the streaming form on the
+        // TR tiles as well (measured 20-35 % slower than the streaming form)
+        if (a.tune && a.tune->x6_gemm1x1 == 2 && x6_tr_ok(a)) return launch_tr(a, s);
+    }
     if (const int nch = stream_x6_nch(a, TERMS)) {
         if constexpr (TERMS == 2) {   // 256-channel slices: each pixel read by half as many workgroups
             if (a.tune && a.tune->x6_stream256 && a.cout % 256 == 0) {
@@ -1357,6 +1530,9 @@ static hipError_t launch_terms(const ConvArgs& a0, hipStream_t s) {
         if (a.cin_pad == 128) return nch == 128 ? stream_mode_x6<4, 8, TERMS>(a, s) : stream_mode_x6<4, 4, TERMS>(a, s);
         if constexpr (TERMS == 2) return stream_mode_x6<8, 8, TERMS>(a, s);
         return stream_mode_x6<8, 4, TERMS>(a, s);
+    }
+    if constexpr (TERMS == 2) {
+        if (a.tune && a.tune->x6_gemm1x1 && x6_tr_ok(a)) return launch_tr(a, s);
     }
     const int bn = a.cout <= 32 ? 32 : (a.cout <= 64 ? 64 : 128);
     const long big_tiles = (long)((a.M + 255) / 256) * ((a.cout + bn - 1) / bn);
@@ -1427,7 +1603,9 @@ bool vd_conv1x1_x6_dual_ok(const ConvArgs& a) {
     return a.cin_pad == 64 && a.kpad2 == 64 && a.cout % 128 == 0;
 }
 
-hipError_t vd_launch_conv_x6(const ConvArgs& a, hipStream_t s) {
+hipError_t vd_launch_conv_x6(const ConvArgs& a0, hipStream_t s) {
+    ConvArgs a = a0;
+    a.dbg = a.tune ? a.tune->x6_dbg : 0;
     if (a.x2) {
         if (!vd_conv1x1_x6_dual_ok(a) || (a.ymax && a.B > kAmaxFrames)) return hipErrorInvalidValue;
         return launch_dual_x6<2, 2, 8>(a, s);

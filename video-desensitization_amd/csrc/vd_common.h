@@ -70,6 +70,9 @@ struct VdTune {
     int x6_halo_narrow = 1;   // ... also for Cout <= 64 (N tiles of 32 / 64)
     int x6_adepth = 2;        // A register sets of the 256 x {128, 64, 32} fp16-pair tiles (2 or 4; 4 measured level)
     int x6_slots = 0;         //   workgroup slots of one round (0: the CU count; tests force small values)
+    int x6_gemm1x1 = 1;       // fp16 pairs: GEMM 1x1 convs on the TR tiles (D^T accumulators, register epilogue;
+                              //   2: also the streaming form's K <= 256 layers, 0: off)
+    int x6_dbg = 0;           // timing experiments only (tools/x6bench; WRONG results): 1 = no epilogue
     int f32_split = 2;        // plan (fp32, at weight load): 2 = operands scaled by powers of two
                               //   and split into fp16 pairs, 3 products on the f16 matrix cores;
                               //   1 = exact 3-term bf16 split, 6 products (conv_x6.hip);
@@ -111,6 +114,7 @@ struct ConvArgs {
     const unsigned* x2max; float x2bound;
     int x_exact;                                 // fp16 pairs: input values exact in fp16 (integer canvas)
     int mbase;                                   // conv_x6 tiles: first output row of the launch (tail split)
+    int dbg;                                     // VdTune::x6_dbg (timing experiments; 0 in production)
 };
 
 // One fused layer1 bottleneck (block.hip): x [B][H][W][cin] -> y [B][H][W][256],
