@@ -347,6 +347,10 @@ def main():
         if world == 1 and precision == a.precision and a.host_pipeline:
             res["host_pipeline"] = host_pipeline(mode)
             res["jpeg_pipeline"] = jpeg_pipeline(mode)
+            if (H, W) == (1080, 1920):   # realistic entropy: smooth structure + sensor noise, ~0.45 MB per q95 frame
+                sf = synth.structured_frames(min(B, 8), H, W, seed=0)
+                sf = np.concatenate([sf] * (-(-B // len(sf))))[:B]
+                res["jpeg_pipeline_structured"] = jpeg_pipeline(mode, torch.from_numpy(sf).to(dev), "structured")
         mode.close()
         return res, lists
 
@@ -378,92 +382,45 @@ def main():
                 "what": "pinned host frames -> H2D -> vd_process -> D2H of mosaicked frames + box lists, "
                         "copies and compute on separate streams (FramePipeline, depth 2)"}
 
-    def jpeg_pipeline(mode):
-        """Frame I/O included: the B frames as in-memory JPEG files
-        (q95 4:2:0, what the reference's ffmpeg split and cv2.imwrite produce) ->
+    def jpeg_pipeline(mode, src=None, what="noise"):
+        """Frame I/O included: B frames as in-memory JPEG files (q95
+        4:2:0, what the reference's ffmpeg split and cv2.imwrite produce) ->
         vd_jpeg_decode (device entropy decode + HIP IDCT) into device frames ->
-        vd_process -> vd_jpeg_encode (HIP FDCT + device Huffman coding) -> JPEG bytes
-        in host memory. Three stages in flight, as batch_process_images' GPU codec
-        path runs them: batch s+1 decoded on a second context, batch s processed,
-        batch s-1 encoded on a third (each context has its own stream and lock)."""
+        vd_process -> vd_jpeg_encode (HIP FDCT + device Huffman coding) -> JPEG bytes in
+        host memory, as batch_process_images' GPU codec path runs it
+        (vdmi.pipeline.GpuJpegStages): decode, process and encode of consecutive
+        batches in flight on three contexts, chained by events (no device-wide syncs)."""
+        from vdmi.pipeline import GpuJpegStages
         ctx = mode.ctx
         ctx.set_stream(stream.cuda_stream)
-        jp = ctx.jpeg_encode(frames[:B], quality=95, subsampling=2)
-        steps = max(1, min(a.steps, 5))
-        import vdmi
-        dctx = vdmi.Context(device=dev.index or 0, precision="fp32", max_batch=B)
-        ectx = vdmi.Context(device=dev.index or 0, precision="fp32", max_batch=B)
-        d_in = [torch.empty_like(frames[:B]) for _ in range(2)]
-        d_out = [torch.empty_like(frames[:B]) for _ in range(2)]
-        stage = {"decode_wait": 0.0, "process": 0.0, "encode_wait": 0.0}
-        spent = {"decode": 0.0, "encode": 0.0}
+        if src is None:
+            src = frames[:B]
+        jp = ctx.jpeg_encode(src, quality=95, subsampling=2)
+        steps = max(1, min(a.steps, 8))
+        st = GpuJpegStages(ctx, B, mode.flags, quality=95, subsampling=2)
         outj = []
-
-        def decode(i):
-            t = time.perf_counter()
-            dctx.jpeg_decode(jp, out=d_in[i % 2])
-            dctx.sync()
-            return time.perf_counter() - t
-
-        def encode(i):
-            t = time.perf_counter()
-            r = ectx.jpeg_encode(d_out[i % 2], quality=95, subsampling=2, copy=False)
-            return r, time.perf_counter() - t
-
-        from concurrent.futures import ThreadPoolExecutor
-        dpool, epool = ThreadPoolExecutor(1), ThreadPoolExecutor(1)
-
-        def run(nsteps):
-            fut = dpool.submit(decode, 0)
-            enc = [None, None]
-            for s in range(nsteps):
-                t = time.perf_counter()
-                spent["decode"] += fut.result()
-                t1 = time.perf_counter()
-                if s + 1 < nsteps:
-                    fut = dpool.submit(decode, s + 1)     # d_in[(s+1)%2]: process(s-1) has finished
-                if enc[s % 2] is not None:                # encode(s-2) is done with d_out[s%2]
-                    r, dt = enc[s % 2].result()
-                    spent["encode"] += dt
-                    outj[:] = r
-                t2 = time.perf_counter()
-                mode.process(d_in[s % 2], d_out[s % 2])
-                torch.cuda.synchronize(dev)
-                t3 = time.perf_counter()
-                enc[s % 2] = epool.submit(encode, s)
-                stage["decode_wait"] += t1 - t
-                stage["encode_wait"] += t2 - t1
-                stage["process"] += t3 - t2
-            for e in enc:
-                if e is not None:
-                    r, dt = e.result()
-                    spent["encode"] += dt
-                    outj[:] = r
+        done = lambda key, res, nf, npl: outj.__setitem__(slice(None), res[0][1])
         try:
-            run(2)
+            st.run(((s, lambda: jp, None) for s in range(3)), done)       # warm-up
             torch.cuda.synchronize(dev)
-            for k in stage:
-                stage[k] = 0.0
-            for k in spent:
-                spent[k] = 0.0
+            for k in st.stats:
+                st.stats[k] = 0.0
             t0 = time.perf_counter()
-            run(steps)
+            st.run(((s, lambda: jp, None) for s in range(steps)), done)
             d = time.perf_counter() - t0
-            passes = dctx.jdec_passes()
+            passes = st.dctx.jdec_passes()
         finally:
-            dpool.shutdown()
-            epool.shutdown()
-            dctx.close()
-            ectx.close()
-        st = {k: round(v / steps * 1e3, 2) for k, v in stage.items()}
-        st.update({k: round(v / steps * 1e3, 2) for k, v in spent.items()})
+            st.close()
+        ctx.set_stream(stream.cuda_stream)
+        stg = {k: round(v / steps * 1e3, 2) for k, v in st.stats.items()}
         return {"value": round(B * steps / d, 2), "unit": "frames/s", "ms_per_step": round(d / steps * 1e3, 3),
-                "stage_ms_per_step": st, "decode_sync_passes": passes,
-                "steps": steps, "jpeg_bytes_in_per_frame": int(np.mean([len(j) for j in jp])),
+                "frames": what, "stage_ms_per_step": stg, "decode_sync_passes": passes, "steps": steps,
+                "jpeg_bytes_in_per_frame": int(np.mean([len(j) for j in jp])),
                 "jpeg_bytes_out_per_frame": int(np.mean([len(j) for j in outj])),
                 "what": "in-memory q95 4:2:0 JPEG frames -> GPU decode (device entropy decode + HIP IDCT, second "
                         "context) -> vd_process -> GPU encode (HIP FDCT + device Huffman coding, third context) -> "
-                        "JPEG bytes in host memory; decode of s+1, process of s and encode of s-1 in flight together"}
+                        "JPEG bytes in host memory; decode, process and encode of consecutive batches in flight, "
+                        "chained by events (vdmi.pipeline.GpuJpegStages)"}
 
     def instrumented(mode, precision):
         """Per-kernel-family durations: the same K steps again, each launch bracketed
@@ -538,7 +495,7 @@ def main():
                    "plates": plates},
     }
     for k in ("roofline", "blur_roofline", "faces_per_frame", "instrumented_ms_per_step", "plate_conv",
-              "ms_breakdown_per_step", "host_pipeline", "jpeg_pipeline"):
+              "ms_breakdown_per_step", "host_pipeline", "jpeg_pipeline", "jpeg_pipeline_structured"):
         if k in head:
             res[k] = head[k]
     parity = {}

@@ -80,23 +80,35 @@ def _iou_match(e, g, thr=0.9):
 
 
 # ------------------------------------------------------------------ C2
+# bf16 C2 box agreement with the f32 oracle over the 32 frames of seed 31: (batch share,
+# worst frame share) floors, ~the measured values less a margin (r04 GPU run)
+C2_BOX_FLOOR = (0.90, 0.70)
+
+
 def test_c2_bf16_720p_heads_and_boxes(gpu, face_ctx_factory):
-    """bf16 at 1280x720 (ratio-2 area letterbox): heads within the bf16 bound,
-    >= 90 % of oracle boxes matched at IoU >= 0.9."""
-    ctx = face_ctx_factory("bf16", 8)
-    fr = _frames720(3, seed=31)
+    """bf16 at 1280x720 (ratio-2 area letterbox), the whole C2 batch of 32 frames: heads
+    within the bf16 bound, and the share of oracle boxes matched at IoU >= 0.9 above
+    its measured floor (C2_BOX_FLOOR), per batch and per frame."""
+    ctx = face_ctx_factory("bf16", 32)
+    fr = _frames720(32, seed=31)
     loc, conf, _ = ctx.forward_heads(fr)
     eloc, econf = _oracle_heads(fr)
     assert _rel(loc, eloc) < 2e-2 and _rel(conf, econf) < 2e-2      # observed <= 0.0116 (~1.5x)
     got = ctx.detect(fr)
     pri = oanchors.get_anchors((640, 640))
     matched = total = 0
-    for b in range(3):
+    worst = 1.0
+    for b in range(32):
         _, boxes, _ = obbox.postprocess_frame(eloc[b], econf[b], pri, 0.5, 0.4)
         e = obbox.correct_and_scale(boxes, 720, 1280)
+        mb = _iou_match(e, got.frame(b)[1])
         total += len(e)
-        matched += _iou_match(e, got.frame(b)[1])
-    assert total > 0 and matched / total >= 0.9, (matched, total)
+        matched += mb
+        if len(e):
+            worst = min(worst, mb / len(e))
+    print(f"C2 bf16 boxes matched at IoU >= 0.9: {matched}/{total}, worst frame {worst:.3f}")
+    assert total > 0 and matched / total >= C2_BOX_FLOOR[0], (matched, total)
+    assert worst >= C2_BOX_FLOOR[1], worst
 
 
 def test_c2_bf16_720p_b32_process_mosaic_exact(gpu):

@@ -47,8 +47,8 @@ pytestmark = [pytest.mark.gpu, pytest.mark.parity]
 # order (difference of two scores), IoU (ratio), trunc (source pixels). The score
 # bound is ~340 f32 ulps at 0.5 and ~1.4x the largest score difference the two
 # forwards show over ALL candidates of all cases (1.48e-5, r03 GPU run); the pixel
-# bound is ~65 ulps at 1920 px (observed: 2.1e-4 px at x = 273).
-F32_BOUND = {"score": 2e-5, "order": 2e-5, "iou": 2e-5, "trunc": 2e-3}
+# bound is 1.5x the largest observed (2.1e-4 px at x = 273, ~7 ulps at 1920 px).
+F32_BOUND = {"score": 2e-5, "order": 2e-5, "iou": 2e-5, "trunc": 3.2e-4}
 # heads: max |gpu - oracle| / max |oracle| per tensor, ~1.5x the largest observed
 # over the cases (r03, R50: pairs 3.9e-6, exact 3.2e-6, bf16 triples 4.4e-6; MobileNet-0.25:
 # pairs 2.6e-6, exact 2.3e-6)

@@ -9,7 +9,7 @@
 // double-precision nearest index rule. This is a pure gather -> |delta| = 0.
 //
 // Kernels per call (two launches; every output byte is written exactly once):
-//  mosaic_cell_kernel  CELL_BLOCKS workgroups per frame. Each clips the frame's
+//  mosaic_cell_kernel  cell_blocks workgroups per frame (option mosaic_cells). Each clips the frame's
 //                      boxes and precomputes their resizeNN factors (boxes in call
 //                      order: faces first, then plates, combine_detect.py:242-244)
 //                      into LDS -- workgroup 0 also writes them, and the cell-count
@@ -37,7 +37,6 @@ namespace {
 constexpr int ROWS = 16;        // rows per output band
 constexpr int TB_CAP = 64;      // band-list capacity; fuller bands walk the global table
 constexpr int BOX_FAST = 256;   // frames with at most this many boxes get the overlap graph + cell table
-constexpr int CELL_BLOCKS = 32; // workgroups per frame sharing its mosaic cells
 constexpr int CELL_CAP = 1 << 18;   // cell-table entries per frame (packed RGB)
 constexpr int MAPBOX = 32;      // band boxes the fast path's column maps can name (5 bits)
 constexpr int VMAPCAP = 3072;   // vector descriptors per band (row classes x vectors per row)
@@ -705,8 +704,9 @@ size_t vd_mosaic_table_bytes(int n, int tcap) {
 hipError_t vd_launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w, size_t pitch,
                             const int* cnt0, const int* xy0, int cap0,
                             const int* cnt1, const int* xy1, int cap1, int level, void* table,
-                            int stages, int map_on, hipStream_t s) {
+                            int stages, int map_on, int cell_blocks, hipStream_t s) {
     if (n <= 0 || h <= 0 || w <= 0) return hipSuccess;
+    cell_blocks = std::min(std::max(cell_blocks, 1), 256);
     const int vec_ok = (pitch % 16 == 0) && ((uintptr_t)in % 16 == 0) && ((uintptr_t)out % 16 == 0);
     const int tcap = (cnt0 ? cap0 : 0) + (cnt1 ? cap1 : 0);
     char* cpre = (char*)table + (size_t)n * tcap * sizeof(MBox);
@@ -715,7 +715,7 @@ hipError_t vd_launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w
     MosaicArgs a{in, out, n, h, w, pitch, cnt0, xy0, cap0, cnt1, xy1, cap1, level, vec_ok, (MBox*)table, tcap,
                  (int*)cpre, (uint32_t*)cel, 1};
     a.map_on = map_on;
-    if (stages & 1) hipLaunchKernelGGL(mosaic_cell_kernel, dim3(CELL_BLOCKS, n), dim3(256), 0, s, a);
+    if (stages & 1) hipLaunchKernelGGL(mosaic_cell_kernel, dim3(cell_blocks, n), dim3(256), 0, s, a);
     if (stages & 2) hipLaunchKernelGGL(mosaic_out_kernel, dim3((h + ROWS - 1) / ROWS, n), dim3(256), 0, s, a);
     return hipGetLastError();
 }

@@ -128,6 +128,12 @@ class Context:
     def stream(self):
         return self._lib.vd_get_stream(self._h)
 
+    def stream_wait_event(self, event):
+        """Queue a wait for a torch.cuda.Event on this context's stream (orders its next
+        launches behind work recorded on another context's or torch's stream)."""
+        import torch
+        torch.cuda.ExternalStream(self.stream(), device=torch.device(f"cuda:{self.device}")).wait_event(event)
+
     def sync(self):
         check(self._lib.vd_sync(self._h))
 

@@ -202,6 +202,184 @@ class FramePipeline:
         self.ctx.set_stream(None)
 
 
+class GpuJpegStages:
+    """JPEG frames in, JPEG frames out, three stages in flight on three contexts.
+
+    Job i (slot i % depth): decode on a weight-less context (decode thread; device
+    entropy decode + HIP IDCT into the device frame slot), one vd_process on the
+    caller's context (faces | plates | mosaic, caller thread), encode on a third
+    context (encode thread; HIP FDCT + device Huffman coding). The stages are chained
+    by HIP events on the contexts' streams, not by host waits on the device:
+
+        decode(i)  --ev_dec-->  process(i)  --ev_proc-->  encode(i)
+        process(i) --ev_proc--> decode(i + depth)   (its input slot is free again)
+
+    so process(i + 1) is queued behind process(i) as soon as decode(i + 1)'s host
+    stages are done, and the GPU runs the three contexts' kernels side by side. The
+    caller thread waits only on host futures: decode(i) queued, and encode(i - depth)
+    finished before process(i) reuses its output slot and box lists.
+    combine_detect.py:204-262 is the loop this replaces (cv2.imread -> detect ->
+    mosaic -> cv2.imwrite per batch)."""
+
+    def __init__(self, ctx, max_batch, flags, quality=95, subsampling=2, depth=3, cap=256):
+        import torch
+        from .context import Context, DeviceBoxes
+        self.torch = torch
+        self.ctx = ctx
+        self.B = int(max_batch)
+        self.flags = flags
+        self.quality, self.subsampling = int(quality), int(subsampling)
+        self.depth = max(2, int(depth))
+        dev = self.dev = torch.device(f"cuda:{ctx.device}")
+        self.dctx = Context(device=ctx.device, precision="fp32", max_batch=self.B)
+        self.ectx = Context(device=ctx.device, precision="fp32", max_batch=self.B)
+        self.s_dec = torch.cuda.ExternalStream(self.dctx.stream(), device=dev)
+        self.s_enc = torch.cuda.ExternalStream(self.ectx.stream(), device=dev)
+        self.faces = [DeviceBoxes(self.B, cap, dev) for _ in range(self.depth)]
+        self.plates = [DeviceBoxes(self.B, cap, dev) for _ in range(self.depth)]
+        self.ev_dec = [torch.cuda.Event() for _ in range(self.depth)]
+        self.ev_proc = [torch.cuda.Event() for _ in range(self.depth)]
+        self.buf = {}                                   # (h, w) -> ([d_in] * depth, [d_out] * depth)
+        self.dpool, self.epool = ThreadPoolExecutor(1), ThreadPoolExecutor(1)
+        self.stats = {"decode_wait": 0.0, "encode_wait": 0.0, "queue": 0.0, "decode": 0.0, "encode": 0.0}
+
+    def _buffers(self, h, w):
+        if (h, w) not in self.buf:
+            t = self.torch
+            mk = lambda: [t.empty((self.B, h, w, 3), dtype=t.uint8, device=self.dev) for _ in range(self.depth)]
+            self.buf[(h, w)] = (mk(), mk())
+        return self.buf[(h, w)]
+
+    def _decode(self, i, fetch, fallback, wait_ev):
+        """-> [(frame indices, h, w)] per frame size of job i, decoded into slot i % depth."""
+        import time
+        from .context import jpeg_info
+        t0 = time.perf_counter()
+        blobs = fetch()
+        groups = {}
+        for k, b in enumerate(blobs):
+            try:
+                key = jpeg_info(b)[:2]
+            except Exception:
+                if fallback is None:
+                    raise
+                key = fallback(k).shape[:2]
+            groups.setdefault(key, []).append(k)
+        if wait_ev is not None:
+            self.s_dec.wait_event(wait_ev)              # process(i - depth) is done with the slot
+        slot = i % self.depth
+        out = []
+        for (h, w), idx in groups.items():
+            din = self._buffers(h, w)[0][slot][:len(idx)]
+            try:
+                self.dctx.jpeg_decode([blobs[k] for k in idx], out=din)
+            except Exception:                           # not a layout the GPU decoder takes: host decode
+                if fallback is None:
+                    raise
+                host = np.stack([fallback(k) for k in idx])
+                with self.torch.cuda.stream(self.s_dec):
+                    din.copy_(self.torch.from_numpy(host))
+            out.append((idx, h, w))
+        self.ev_dec[slot].record(self.s_dec)
+        self.stats["decode"] += time.perf_counter() - t0
+        return out
+
+    def _encode(self, i, groups):
+        """-> [(frame indices, JPEG views)], face / plate counts of job i."""
+        import time
+        t0 = time.perf_counter()
+        slot = i % self.depth
+        self.s_enc.wait_event(self.ev_proc[slot])
+        res, nf, npl = [], 0, 0
+        for idx, h, w in groups:
+            if idx is None:
+                continue
+            jp = self.ectx.jpeg_encode(self._buffers(h, w)[1][slot][:len(idx)], quality=self.quality,
+                                       subsampling=self.subsampling, copy=False)
+            res.append((idx, jp))
+        for idx, h, w in groups:                        # the encode synchronised: process(i) is complete
+            if idx is not None:
+                nf += int(self.faces[slot].count[:len(idx)].sum().item())
+                npl += int(self.plates[slot].count[:len(idx)].sum().item())
+        self.stats["encode"] += time.perf_counter() - t0
+        return res, nf, npl
+
+    def run(self, jobs, done, on_error=None):
+        """jobs: iterable of (key, fetch, fallback): fetch() -> list of JPEG bytes;
+        fallback(k) -> host-decoded RGB frame k or None. done(key, [(frame indices,
+        JPEG views)], faces, plates) is called in order on the caller thread. A fetch /
+        decode error propagates after every job already processed has been encoded
+        and handed to done; a process error drops that job (on_error(key, exc))."""
+        import collections
+        import time
+        jobs = iter(jobs)
+        dec = collections.deque()                       # (i, key, future)
+        enc = collections.deque()                       # (i, key, future)
+        nxt = [0]
+        D = self.depth
+
+        def submit_decode():
+            job = next(jobs, None)
+            if job is None:
+                return
+            key, fetch, fallback = job
+            i = nxt[0]
+            nxt[0] += 1
+            wait_ev = self.ev_proc[i % D] if i >= D else None
+            dec.append((i, key, self.dpool.submit(self._decode, i, fetch, fallback, wait_ev)))
+
+        def finish_one():
+            i, key, fut = enc.popleft()
+            t = time.perf_counter()
+            res, nf, npl = fut.result()
+            self.stats["encode_wait"] += time.perf_counter() - t
+            done(key, res, nf, npl)
+
+        try:
+            submit_decode()
+            submit_decode()
+            while dec:
+                i, key, fut = dec.popleft()
+                t = time.perf_counter()
+                groups = fut.result()                   # a fetch / decode failure propagates
+                t1 = time.perf_counter()
+                self.stats["decode_wait"] += t1 - t
+                while enc and enc[0][0] <= i - D:       # encode(i - depth) frees the output slot
+                    finish_one()
+                t2 = time.perf_counter()
+                slot = i % D
+                self.ctx.stream_wait_event(self.ev_dec[slot])
+                ok = []
+                for idx, h, w in groups:
+                    din, dout = self._buffers(h, w)
+                    n = len(idx)
+                    try:
+                        self.ctx.process(din[slot][:n], dout[slot][:n], faces=self.faces[slot],
+                                         plates=self.plates[slot], flags=self.flags)
+                        ok.append((idx, h, w))
+                    except Exception as e:              # combine_detect.py:226-228: the batch is dropped
+                        if on_error is None:
+                            raise
+                        on_error(key, e)
+                        ok.append((None, h, w))
+                self.ev_proc[slot].record(self.torch.cuda.ExternalStream(self.ctx.stream(), device=self.dev))
+                self.stats["queue"] += time.perf_counter() - t2
+                enc.append((i, key, self.epool.submit(self._encode, i, ok)))
+                submit_decode()
+        finally:
+            for _, _, fut in dec:                        # decodes queued behind a failure: not processed
+                fut.cancel()
+            while enc:
+                finish_one()
+
+    def close(self):
+        self.dpool.shutdown()
+        self.epool.shutdown()
+        self.torch.cuda.synchronize(self.dev)
+        self.dctx.close()
+        self.ectx.close()
+
+
 def fused_context(face_detector, plate_detector, batch_size):
     """One context holding both drop-ins' weights and the face detector's knobs
     (cached on the face detector)."""
@@ -354,97 +532,39 @@ def _write_bytes(data, path):
 
 def _gpu_codec_batches(batches, output_dir, face_detector, plate_detector, batch_size, mosaic_plates, io, logger,
                        quality):
-    """Frame I/O on the GPU: file bytes (reader threads) -> vd_jpeg_decode into
-    device frames -> one vd_process (faces | plates | mosaic) -> vd_jpeg_encode from
-    device memory -> writer threads. Batch i+1 is read and decoded (its host Huffman
-    threads and IDCT kernels, on a second weight-less context and stream) while
-    batch i is processed and encoded. A frame the GPU decoder does not take
-    (progressive, other layout) is decoded by the host loader; a batch whose
-    inference fails is dropped (combine_detect.py:226-228)."""
-    import torch
-    from .context import Context, DeviceBoxes, jpeg_info
+    """Frame I/O on the GPU (GpuJpegStages): file bytes (reader threads) ->
+    vd_jpeg_decode into device frames -> one vd_process (faces | plates | mosaic) ->
+    vd_jpeg_encode from device memory -> writer threads, the three stages of
+    consecutive batches in flight together, chained by events. A frame the GPU
+    decoder does not take (progressive, other layout) is decoded by the host loader;
+    a batch whose inference fails is dropped (combine_detect.py:226-228); a read
+    failure aborts the call after the batches before it are written (:209-211)."""
     ctx = fused_context(face_detector, plate_detector, batch_size)
-    dev = torch.device(f"cuda:{ctx.device}")
-    dctx = Context(device=ctx.device, precision="fp32", max_batch=max(int(batch_size), 1))
     flags = _lib.VD_PROC_FACES | _lib.VD_PROC_MOSAIC | _lib.VD_PROC_PLATES
     if mosaic_plates:
         flags |= _lib.VD_PROC_MOSAIC_PLATES
-    faces = DeviceBoxes(batch_size, 256, dev)
-    plates = DeviceBoxes(batch_size, 256, dev)
     totals = [0, 0, 0]
     save_futs = []
 
-    def load(files):
-        """files -> [(items, device frames)] per frame size, decoded and synchronised"""
-        blobs = list(io.map(_read_bytes, files))
-        groups = {}
-        for f, b in zip(files, blobs):
-            try:
-                key = jpeg_info(b)[:2]
-            except Exception:
-                key = load_image_rgb(f).shape[:2]
-            groups.setdefault(key, []).append((f, b))
-        out = []
-        for (h, w), items in groups.items():
-            d_in = torch.empty((len(items), h, w, 3), dtype=torch.uint8, device=dev)
-            try:
-                dctx.jpeg_decode([b for _, b in items], out=d_in)
-                dctx.sync()
-            except Exception:                # not a layout the GPU decoder takes: host decode
-                d_in.copy_(torch.from_numpy(np.stack([load_image_rgb(f) for f, _ in items])))
-                torch.cuda.synchronize(dev)  # the copy ran on torch's stream, not a context's
-            out.append((items, d_in))
-        return out
+    def job(files):
+        return (files, lambda: list(io.map(_read_bytes, files)), lambda k: load_image_rgb(files[k]))
 
-    # batch i+1 decoded (dctx), batch i processed (ctx), batch i-1 encoded (ectx): three
-    # contexts, each with its own stream and lock, so the three stages overlap
-    ectx = Context(device=ctx.device, precision="fp32", max_batch=max(int(batch_size), 1))
+    def done(files, res, nf, npl):
+        for idx, jpegs in res:
+            for k, data in zip(idx, jpegs):
+                dst = os.path.join(output_dir, f"processed_{os.path.basename(files[k])}")
+                save_futs.append(io.submit(_write_bytes, data, dst))
+            totals[0] += len(idx)
+        totals[1] += nf
+        if mosaic_plates:                # the reference's tuple check discards plate boxes otherwise
+            totals[2] += npl
 
-    def encode(items, out):
-        jpgs = ectx.jpeg_encode(out, quality=quality, subsampling=2, copy=False)
-        return [io.submit(_write_bytes, data, os.path.join(output_dir, f"processed_{os.path.basename(path)}"))
-                for (path, _), data in zip(items, jpgs)]
-
-    def collect(fut):
-        try:
-            save_futs.extend(fut.result())
-        except Exception as e:           # combine_detect.py:226-228: the batch is dropped
-            logger.error(f"parallel inference failed: {e}")
-            return False
-        return True
-
-    ahead, behind = ThreadPoolExecutor(1), ThreadPoolExecutor(1)
-    enc = []                             # (future, counts) of batches being encoded
+    stages = GpuJpegStages(ctx, max(int(batch_size), 1), flags, quality=quality, subsampling=2)
     try:
-        fut = ahead.submit(load, batches[0]) if batches else None
-        for bi in range(len(batches)):
-            decoded = fut.result()       # a load failure propagates (combine_detect.py:209-211)
-            fut = ahead.submit(load, batches[bi + 1]) if bi + 1 < len(batches) else None
-            for items, d_in in decoded:
-                try:
-                    out, fc, pc = ctx.process(d_in, faces=faces, plates=plates, flags=flags)
-                    ctx.sync()           # the encode context reads `out` on its own stream
-                except Exception as e:   # combine_detect.py:226-228: the batch is dropped
-                    logger.error(f"parallel inference failed: {e}")
-                    continue
-                n = len(items)
-                counts = (n, int(fc.count[:n].sum().item()), int(pc.count[:n].sum().item()) if mosaic_plates else 0)
-                enc.append((behind.submit(encode, items, out), counts))
-                while len(enc) > 1:      # at most one batch encoding behind the one just processed
-                    f0, c0 = enc.pop(0)
-                    if collect(f0):
-                        totals[0] += c0[0]; totals[1] += c0[1]; totals[2] += c0[2]
+        stages.run((job(files) for files in batches), done,
+                   on_error=lambda files, e: logger.error(f"parallel inference failed: {e}"))
     finally:
-        # every batch already handed to the encoder is finished (its errors logged, its
-        # writes queued) before the saves are waited on -- also when a load failure aborts
-        while enc:
-            f0, c0 = enc.pop(0)
-            if collect(f0):
-                totals[0] += c0[0]; totals[1] += c0[1]; totals[2] += c0[2]
-        ahead.shutdown()
-        behind.shutdown()
-        dctx.close()
-        ectx.close()
+        stages.close()
         _save_all(save_futs, logger)
     return tuple(totals)
 

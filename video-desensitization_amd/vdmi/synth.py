@@ -39,6 +39,25 @@ def frames(n, h, w, seed=0, start=0):
     return out
 
 
+def structured_frames(n, h, w, seed=0, noise=1.5):
+    """uint8 [n,h,w,3] frames with the entropy of real video frames: per channel four
+    seeded low-frequency plane waves around mid-grey plus N(0, noise) sensor noise
+    (~0.45 MB per 1080p frame at JPEG q95 4:2:0, where the counter-hash frames are
+    ~2.4 MB). For frame-I/O timing (bench.py jpeg_pipeline_structured)."""
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float32)
+    out = np.empty((n, h, w, 3), np.uint8)
+    for f in range(n):
+        img = np.empty((h, w, 3), np.float32)
+        for c in range(3):
+            fr = rng.uniform(0.002, 0.02, (4, 2)).astype(np.float32)
+            ph = rng.uniform(0, 6.28, 4).astype(np.float32)
+            img[..., c] = 128 + sum(40 * np.sin(fr[k, 0] * xx + fr[k, 1] * yy + ph[k]) for k in range(4))
+        img += rng.normal(0, noise, (h, w, 1)).astype(np.float32)
+        out[f] = np.clip(img, 0, 255).astype(np.uint8)
+    return out
+
+
 def box_lists(n, h, w, per_frame=8, seed=1):
     """int32 [n][per_frame][4] (x1,y1,x2,y2) lists for blur-only runs."""
     rng = np.random.default_rng(seed)
