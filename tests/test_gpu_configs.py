@@ -81,8 +81,8 @@ def _iou_match(e, g, thr=0.9):
 
 # ------------------------------------------------------------------ C2
 # bf16 C2 box agreement with the f32 oracle over the 32 frames of seed 31: (batch share,
-# worst frame share) floors, ~the measured values less a margin (r04 GPU run)
-C2_BOX_FLOOR = (0.90, 0.70)
+# worst frame share) floors; measured 893/928 = 0.962 and 0.792 (r04 GPU run)
+C2_BOX_FLOOR = (0.93, 0.75)
 
 
 def test_c2_bf16_720p_heads_and_boxes(gpu, face_ctx_factory):

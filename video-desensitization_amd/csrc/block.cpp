@@ -57,7 +57,6 @@ bool is_conv(const Conv& c, int cin, int cout, int k, int stride, int pad, int a
 bool Ctx::block_ok(int c1, int c2, int c3, int cd, const Act& x) const {
     const bool ds = cd >= 0;
     const int cin = x.c;
-    if (f16) return false;
     if (f32) {   // fp32 plan: the fp16-pair block (block32.hip), on pair-packed convs with range slots
         if (!tune.block_fuse32 || !x.f32 || !x.amax || !vd_block32_ok(cin, ds, x.h, x.w)) return false;
         for (int c : {c1, c2, c3, cd})
@@ -237,7 +236,7 @@ int Ctx::add_block(Net& net, int bi, const Act& x, Act& y) {
 int Ctx::add_stem_pool(Net& net, int ci, const Act& x, Act& y) {
     const Conv& cv = convs[ci];
     const bool pair = f32 && cv.split == 2;             // fp32 plan: fp16 pair weights, f32 pooled map
-    if ((f32 && !pair) || f16 || x.f32 || y.f32 != pair || (pair && !cv.wx3) || cv.cin != 16 || cv.cin_pad != 16 || cv.cout != 64 || cv.kh != 4 || cv.kw != 4 ||
+    if ((f32 && !pair) || x.f32 || y.f32 != pair || (pair && !cv.wx3) || cv.cin != 16 || cv.cin_pad != 16 || cv.cout != 64 || cv.kh != 4 || cv.kw != 4 ||
         cv.stride != 1 || cv.pad != 1 || cv.act != VD_ACT_RELU || cv.kpad != 256 || x.c != 16 || y.c != 64 ||
         !vd_stem_pool_ok(x.h, x.w, y.h, y.w))
         return vd_set_error(VD_ERR_ARG, "fused stem plan shape mismatch");
@@ -302,6 +301,7 @@ int Ctx::run_block_op(const Op& op, int f0, int n, int fam) {
     a.tiles_x = (a.W + 15) / 16;
     a.tiles_y = (a.H + 7) / 8;
     a.w1 = bk.w1; a.w2 = bk.w2; a.w3 = bk.w3; a.wd = bk.wd; a.bn = bk.bn;
+    a.f16 = f16 ? 1 : 0;
     t_begin(fam, fpp * n * a.H * a.W);
     hipError_t e = vd_launch_block(a, stream);
     t_end();
@@ -315,6 +315,7 @@ int Ctx::run_stem_pool_op(const Op& op, int f0, int n, int fam) {
     a.x = foff_b(op.x, f0); a.B = n; a.xh = op.x.h; a.xw = op.x.w;
     a.y = (void*)((char*)op.y.p + (size_t)f0 * op.y.h * op.y.w * op.y.c * (op.y.f32 ? 4 : 2)); a.ph = op.y.h; a.pw = op.y.w;
     a.wf = op.wf; a.scale = cv.scale; a.shift = cv.shift;
+    a.f16 = f16 ? 1 : 0;
     const bool pair = op.y.f32;
     if (pair) {
         a.scale = cv.scale_x;                           // BN scale with the weights' power-of-two folded in

@@ -49,7 +49,6 @@ __device__ __forceinline__ int lds_off(int row, int chunk) {
 }
 
 typedef __attribute__((address_space(3))) void lds_void_t;
-typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
 
 // physical 16-B chunk of logical chunk c in row r of the x halo image: 512-B rows
 // (CIN 256) XOR the low 4 chunk bits with r&15, 128-B rows (CIN 64) with (r>>1)&7 --
@@ -63,16 +62,13 @@ __device__ __forceinline__ int lx_chunk(int r, int c) {
 constexpr int VMCNT0 = 0x0F70;                  // s_waitcnt vmcnt(0) (expcnt / lgkmcnt: no wait)
 constexpr int VMCNT8 = 0x0F78;                  // s_waitcnt vmcnt(8)
 
-__device__ __forceinline__ float bf_lo(unsigned u) { return __uint_as_float(u << 16); }
-__device__ __forceinline__ float bf_hi(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
-
-__device__ __forceinline__ f32x4_t mfma(const u32x4& a, const u32x4& b, const f32x4_t& c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
-                                                   c, 0, 0, 0);
-}
-
-template <int CIN, bool DS>
+// F16: the fp16 plan (VD_PREC_FP16) -- the same kernel on fp16 operands / activations
+template <int CIN, bool DS, bool F16>
 __global__ __launch_bounds__(512, 1) void bottleneck_kernel(BlockArgs a) {
+    using HT = Half16<F16>;
+    typedef typename HT::T E16;
+    typedef E16 t16x4_t __attribute__((ext_vector_type(4)));
+    const auto mfma = [](const u32x4& x, const u32x4& y, const f32x4_t& c) { return HT::mfma(x, y, c); };
     constexpr int KS1 = CIN / 32;                         // stage-1 k-steps
     constexpr int XROW = CIN * 2;                         // bytes per halo pixel in LX
     constexpr int RPI = 1024 / XROW;                      // pixels per 1-KB DMA instruction
@@ -113,7 +109,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck_kernel(BlockArgs a) {
         const int ty = r0 / a.tiles_x, tx = r0 - ty * a.tiles_x;
         const int oy0 = ty * TH, ox0 = tx * TW;
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)((const __bf16*)a.x + (size_t)b * fpx * CIN), 0, (int)(fpx * CIN * 2), 0x00020000);
+            (void*)((const E16*)a.x + (size_t)b * fpx * CIN), 0, (int)(fpx * CIN * 2), 0x00020000);
         // every wave issues exactly DPW DMAs (slots past NDMA read zeros into a 1-KB
         // scratch line): a compile-time count keeps the compiler's vmcnt bookkeeping
         // exact, so later waits on W2 / residual loads do not also wait for this DMA
@@ -245,9 +241,9 @@ __global__ __launch_bounds__(512, 1) void bottleneck_kernel(BlockArgs a) {
                 const bool in = r < HROWS && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W;
                 const float v0 = acc[k][0] * s1v.x + h1v.x, v1 = acc[k][1] * s1v.y + h1v.y;
                 const float v2 = acc[k][2] * s1v.z + h1v.z, v3 = acc[k][3] * s1v.w + h1v.w;
-                const bf16x4_t o = {(__bf16)(in && v0 > 0.f ? v0 : 0.f), (__bf16)(in && v1 > 0.f ? v1 : 0.f),
-                                    (__bf16)(in && v2 > 0.f ? v2 : 0.f), (__bf16)(in && v3 > 0.f ? v3 : 0.f)};
-                *(bf16x4_t*)(lt1 + lds_off(r, 2 * jn + (g >> 1)) + (g & 1) * 8) = o;
+                const t16x4_t o = {(E16)(in && v0 > 0.f ? v0 : 0.f), (E16)(in && v1 > 0.f ? v1 : 0.f),
+                                   (E16)(in && v2 > 0.f ? v2 : 0.f), (E16)(in && v3 > 0.f ? v3 : 0.f)};
+                *(t16x4_t*)(lt1 + lds_off(r, 2 * jn + (g >> 1)) + (g & 1) * 8) = o;
             }
         }
         // the stage-3 identity, x at this wave's 32 channels for the 8 tile rows, taken
@@ -309,9 +305,9 @@ __global__ __launch_bounds__(512, 1) void bottleneck_kernel(BlockArgs a) {
             for (int m = 0; m < 4; ++m) {
                 const float v0 = acc[m][0] * s2v.x + h2v.x, v1 = acc[m][1] * s2v.y + h2v.y;
                 const float v2 = acc[m][2] * s2v.z + h2v.z, v3 = acc[m][3] * s2v.w + h2v.w;
-                const bf16x4_t o = {(__bf16)(v0 > 0.f ? v0 : 0.f), (__bf16)(v1 > 0.f ? v1 : 0.f),
-                                    (__bf16)(v2 > 0.f ? v2 : 0.f), (__bf16)(v3 > 0.f ? v3 : 0.f)};
-                *(bf16x4_t*)(lt2 + lds_off(16 * (4 * half + m) + li, 2 * jn + (g >> 1)) + (g & 1) * 8) = o;
+                const t16x4_t o = {(E16)(v0 > 0.f ? v0 : 0.f), (E16)(v1 > 0.f ? v1 : 0.f),
+                                   (E16)(v2 > 0.f ? v2 : 0.f), (E16)(v3 > 0.f ? v3 : 0.f)};
+                *(t16x4_t*)(lt2 + lds_off(16 * (4 * half + m) + li, 2 * jn + (g >> 1)) + (g & 1) * 8) = o;
             }
         }
         VD_STAMP(4);
@@ -325,7 +321,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck_kernel(BlockArgs a) {
         // ---- stage 3: out channels 32w..32w+31 (8 consecutive per lane), 8 tile rows ----
         {
             const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
-                (void*)((__bf16*)a.y + (size_t)b * fpx * CO), 0, (int)(fpx * CO * 2), 0x00020000);
+                (void*)((E16*)a.y + (size_t)b * fpx * CO), 0, (int)(fpx * CO * 2), 0x00020000);
             const int ox = ox0 + li;
             const unsigned yo = ox < a.W ? (unsigned)((oy0 * a.W + ox) * CO + 32 * w + 8 * g) * 2u : 0x80000000u;
             // t2 (and, DS, x) fragments of row m+1 go out before the MFMAs of row m
@@ -370,13 +366,13 @@ __global__ __launch_bounds__(512, 1) void bottleneck_kernel(BlockArgs a) {
                 } else {              // + identity
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
-                        v[2 * e] += bf_lo(rf[m][e]);
-                        v[2 * e + 1] += bf_hi(rf[m][e]);
+                        v[2 * e] += HT::lo(rf[m][e]);
+                        v[2 * e + 1] += HT::hi(rf[m][e]);
                     }
                 }
-                bf16x8_t o;
+                typename HT::V8 o;
 #pragma unroll
-                for (int e = 0; e < 8; ++e) o[e] = (__bf16)(v[e] > 0.f ? v[e] : 0.f);
+                for (int e = 0; e < 8; ++e) o[e] = (E16)(v[e] > 0.f ? v[e] : 0.f);
                 // pixels past the frame: out-of-range lane offset, the store is dropped
                 const unsigned so = oy0 + m < a.H ? yo + (unsigned)(m * a.W * CO * 2) : 0x80000000u;
                 __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), ry, so, 0, 0);
@@ -395,13 +391,13 @@ __global__ __launch_bounds__(512, 1) void bottleneck_kernel(BlockArgs a) {
 #undef VD_STAMP
 }
 
-template <int CIN, bool DS>
+template <int CIN, bool DS, bool F16>
 hipError_t launch(const BlockArgs& a, hipStream_t s) {
     constexpr int RPI = 1024 / (CIN * 2);
     constexpr size_t xb = (size_t)((HROWS + RPI - 1) / RPI * RPI) * CIN * 2;
     constexpr size_t lds = (DS ? 2 : 1) * xb + 192 * 128 + 128 * 128 + 1024;
     static const int cus = [] {
-        (void)hipFuncSetAttribute((const void*)bottleneck_kernel<CIN, DS>,
+        (void)hipFuncSetAttribute((const void*)bottleneck_kernel<CIN, DS, F16>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         int dev = 0, n = 256;
         (void)hipGetDevice(&dev);
@@ -410,7 +406,7 @@ hipError_t launch(const BlockArgs& a, hipStream_t s) {
     }();
     const int tiles = a.B * a.tiles_x * a.tiles_y;
     const int grid = tiles < cus ? tiles : cus;            // persistent: one workgroup per CU
-    hipLaunchKernelGGL((bottleneck_kernel<CIN, DS>), dim3(grid), dim3(512), lds, s, a);
+    hipLaunchKernelGGL((bottleneck_kernel<CIN, DS, F16>), dim3(grid), dim3(512), lds, s, a);
     return hipGetLastError();
 }
 
@@ -423,7 +419,7 @@ bool vd_block_ok(int cin, bool ds, int h, int w) {
 
 hipError_t vd_launch_block(const BlockArgs& a, hipStream_t s) {
     if (a.B <= 0) return hipSuccess;
-    if (a.cin == 256 && !a.ds) return launch<256, false>(a, s);
-    if (a.cin == 64 && a.ds) return launch<64, true>(a, s);
+    if (a.cin == 256 && !a.ds) return a.f16 ? launch<256, false, true>(a, s) : launch<256, false, false>(a, s);
+    if (a.cin == 64 && a.ds) return a.f16 ? launch<64, true, true>(a, s) : launch<64, true, false>(a, s);
     return hipErrorInvalidValue;
 }

@@ -48,13 +48,6 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-__device__ __forceinline__ f32x4_t mfma(const u32x4& a, const u32x4& b, const f32x4_t& c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
-                                                   c, 0, 0, 0);
-}
-
-__device__ __forceinline__ float bf_lo(unsigned u) { return __uint_as_float(u << 16); }
-__device__ __forceinline__ float bf_hi(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
 
 constexpr int C_MID = 128, C_OUT = 512;   // layer2 widths
 constexpr int D = 3;                      // groups in flight ahead of the computing one
@@ -64,7 +57,12 @@ constexpr int SLOT = SLOT_T2 + 16 * 1024; // + identity rows (16 KB)
 // s_waitcnt vmcnt(N) with expcnt / lgkmcnt left alone (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4] << 14)
 constexpr int vmcnt_imm(int n) { return (n & 15) | ((n >> 4) << 14) | 0x0F70 & ~15; }
 
+// F16: the fp16 plan (VD_PREC_FP16) on fp16 operands / activations
+template <bool F16>
 __global__ __launch_bounds__(512, 1) void chain_kernel(ChainArgs a) {
+    using HT = Half16<F16>;
+    typedef typename HT::T T;
+    const auto mfma = [](const u32x4& x, const u32x4& y, const f32x4_t& c) { return HT::mfma(x, y, c); };
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* ring = smem;                                     // R x SLOT
     u32x4* xch = (u32x4*)(smem + R * SLOT);                // exchange [16 k-steps][64 lanes]
@@ -93,13 +91,13 @@ __global__ __launch_bounds__(512, 1) void chain_kernel(ChainArgs a) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int ch = 64 * w + 32 * (j >> 1) + 8 * (p >> 2) + 4 * (j & 1) + (p & 3);
-        const __bf16* wp = (const __bf16*)a.w3 + (size_t)ch * a.kpad3 + 8 * q;
+        const T* wp = (const T*)a.w3 + (size_t)ch * a.kpad3 + 8 * q;
 #pragma unroll
         for (int s = 0; s < 4; ++s) w3f[j][s] = *(const u32x4*)(wp + 32 * s);
     }
     u32x4 w1f[16];     // conv1': row i = channel 16w + i, 16 k-steps
     {
-        const __bf16* wp = (const __bf16*)a.w1 + (size_t)(16 * w + p) * a.kpad1 + 8 * q;
+        const T* wp = (const T*)a.w1 + (size_t)(16 * w + p) * a.kpad1 + 8 * q;
 #pragma unroll
         for (int s = 0; s < 16; ++s) w1f[s] = *(const u32x4*)(wp + 32 * s);
     }
@@ -179,13 +177,13 @@ __global__ __launch_bounds__(512, 1) void chain_kernel(ChainArgs a) {
             const float* sh = sh3[h];
             const float v[8] = {lo[0] * sc[0] + sh[0], lo[1] * sc[1] + sh[1], lo[2] * sc[2] + sh[2], lo[3] * sc[3] + sh[3],
                                 hi[0] * sc[4] + sh[4], hi[1] * sc[5] + sh[5], hi[2] * sc[6] + sh[6], hi[3] * sc[7] + sh[7]};
-            bf16x8_t o;
+            typename HT::V8 o;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                const float t0 = v[2 * e] + bf_lo(rf[e]);
-                const float t1 = v[2 * e + 1] + bf_hi(rf[e]);
-                o[2 * e] = (__bf16)(t0 > 0.f ? t0 : 0.f);
-                o[2 * e + 1] = (__bf16)(t1 > 0.f ? t1 : 0.f);
+                const float t0 = v[2 * e] + HT::lo(rf[e]);
+                const float t1 = v[2 * e + 1] + HT::hi(rf[e]);
+                o[2 * e] = (T)(t0 > 0.f ? t0 : 0.f);
+                o[2 * e + 1] = (T)(t1 > 0.f ? t1 : 0.f);
             }
             const u32x4 ou = __builtin_bit_cast(u32x4, o);
             const unsigned yoff = ok ? (mrow * (unsigned)a.ld_y + (unsigned)c) * 2u : 0x80000000u;
@@ -197,11 +195,11 @@ __global__ __launch_bounds__(512, 1) void chain_kernel(ChainArgs a) {
         f32x4_t acc2 = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int s = 0; s < 16; ++s) acc2 = mfma(w1f[s], xch[s * 64 + lane], acc2);
-        __bf16 o2[4];
+        T o2[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const float t = acc2[r] * sc1[r] + sh1[r];
-            o2[r] = (__bf16)(t > 0.f ? t : 0.f);
+            o2[r] = (T)(t > 0.f ? t : 0.f);
         }
         const unsigned y2off = ok ? (mrow * (unsigned)a.ld_y2 + (unsigned)(16 * w + 4 * qq)) * 2u : 0x80000000u;
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o2), ry2, y2off, 0, 0);
@@ -224,7 +222,8 @@ hipError_t vd_launch_chain(const ChainArgs& a, hipStream_t s) {
     if (a.M <= 0) return hipSuccess;
     constexpr size_t lds = (size_t)R * SLOT + 16 * 1024 + 1024;
     static const int cus = [] {
-        (void)hipFuncSetAttribute((const void*)chain_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute((const void*)chain_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute((const void*)chain_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         int dev = 0, n = 256;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
@@ -232,6 +231,7 @@ hipError_t vd_launch_chain(const ChainArgs& a, hipStream_t s) {
     }();
     const int groups = (a.M + 15) / 16;
     const int grid = groups < cus ? groups : cus;   // persistent: one workgroup per CU
-    hipLaunchKernelGGL(chain_kernel, dim3(grid), dim3(512), lds, s, a);
+    if (a.f16) hipLaunchKernelGGL(chain_kernel<true>, dim3(grid), dim3(512), lds, s, a);
+    else hipLaunchKernelGGL(chain_kernel<false>, dim3(grid), dim3(512), lds, s, a);
     return hipGetLastError();
 }

@@ -390,21 +390,11 @@ hipError_t vd_launch_conv(const ConvArgs& a0, bool f32, hipStream_t s) {
     const bool dense = (a.cin_pad % bke) == 0;
     if (a.x2) {   // fused conv3 + downsample: planned only where a dual streaming kernel applies
         if (f32) return vd_launch_conv_x6(a, s);
-        if (a.f16 || !vd_conv1x1_dual_ok(a)) return hipErrorInvalidValue;
+        if (!vd_conv1x1_dual_ok(a)) return hipErrorInvalidValue;
         return vd_launch_conv1x1_stream(a, s);
     }
     const int bn = a.cout <= 32 ? 32 : (a.cout <= 64 ? 64 : 128);
     const long tiles128 = (long)((a.M + 127) / 128) * ((a.cout + bn - 1) / bn);
-    if (a.f16) {   // fp16 mode (VD_PREC_FP16): the implicit GEMM on v_mfma_f32_16x16x32_f16
-        if (tiles128 < 512) {
-            if (bn == 32) return launch_bn<_Float16, 64, 32>(a, dense, s);
-            if (bn == 64) return launch_bn<_Float16, 64, 64>(a, dense, s);
-            return launch_bn<_Float16, 64, 128>(a, dense, s);
-        }
-        if (bn == 32) return launch_bn<_Float16, 128, 32>(a, dense, s);
-        if (bn == 64) return launch_bn<_Float16, 128, 64>(a, dense, s);
-        return launch_bn<_Float16, 128, 128>(a, dense, s);
-    }
     if (f32) {
         if (vd_conv_x6_ok(a)) return vd_launch_conv_x6(a, s);
         if (a.cout <= 32) return launch_bn<float, 128, 32>(a, dense, s);
@@ -419,6 +409,18 @@ hipError_t vd_launch_conv(const ConvArgs& a0, bool f32, hipStream_t s) {
     // Cout 129-192 (the fused SSH conv5X5_1 + conv3X3): one 192-wide N tile instead
     // of two 128-wide ones, so each A tile is staged once.
     const bool n192 = a.cout > 128 && a.cout <= 192 && t.conv_n192;
+    if (a.f16) {   // fp16 plan (VD_PREC_FP16): the same tiles on v_mfma_f32_16x16x32_f16
+        if (tiles128 < t.conv_small) {
+            if (n192) return launch_bn<_Float16, 64, 192>(a, dense, s);
+            if (bn == 32) return launch_bn<_Float16, 64, 32>(a, dense, s);
+            if (bn == 64) return launch_bn<_Float16, 64, 64>(a, dense, s);
+            return launch_bn<_Float16, 64, 128>(a, dense, s);
+        }
+        if (bn == 32) return launch_bn<_Float16, 128, 32>(a, dense, s);
+        if (bn == 64) return launch_bn<_Float16, 128, 64>(a, dense, s);
+        if (n192) return launch_bn<_Float16, 128, 192>(a, dense, s);
+        return launch_bn<_Float16, 128, 128>(a, dense, s);
+    }
     if (tiles128 < t.conv_small) {
         if (n192) return launch_bn<__bf16, 64, 192>(a, dense, s);
         if (bn == 32) return launch_bn<__bf16, 64, 32>(a, dense, s);

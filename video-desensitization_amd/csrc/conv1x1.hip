@@ -37,8 +37,6 @@ __device__ __forceinline__ float act_apply(float v, float slope) {
     return v;
 }
 
-__device__ __forceinline__ float bf_lo(unsigned u) { return __uint_as_float(u << 16); }
-__device__ __forceinline__ float bf_hi(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
 
 // KS: K / 32 (k-steps), NTT: 16-channel tiles per wave (NCH = 16 * NTT channels per
 // workgroup), ACT / RES: activation and residual mode (compile-time: no per-element branches).
@@ -47,8 +45,11 @@ __device__ __forceinline__ float bf_hi(unsigned u) { return __uint_as_float(u & 
 // (kh, kw, c) order, gathered per pixel with zero padding (and zero past the last tap).
 // KS2 > 0: DUAL — a second 1x1 conv (K2 = 32*KS2, weights w2, its own BN) over x2
 // at stride2 is summed before the activation (bottleneck conv3 + downsample).
-template <int KS, int NTT, int ACT, int RES, bool TAPS, int KS2 = 0>
+// F16: the fp16 plan (VD_PREC_FP16) on fp16 operands / activations, else bf16.
+template <int KS, int NTT, int ACT, int RES, bool TAPS, int KS2, bool F16>
 __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvArgs a, int nchunks, int groups) {
+    using HT = Half16<F16>;
+    typedef typename HT::T T;
     constexpr int NCH = 16 * NTT;
     constexpr int KT = (KS + 1) / 2;                      // 128-byte K tiles per weight row
     constexpr int KT2 = (KS2 + 1) / 2;
@@ -71,7 +72,7 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvArgs a, int nch
     // weights [n0, n0+NCH) x [0, K) -> LDS image [kt][row][128 B] with the chunk swizzle;
     // LDS row 16j + i (tile j, MFMA row i) holds channel 32(j>>1) + 8(i>>2) + 4(j&1) + (i&3)
     {
-        const __bf16* w = (const __bf16*)a.w;
+        const T* w = (const T*)a.w;
         constexpr int CPR = KS * 4;                       // 16-B chunks per weight row (K/8)
         for (int i = tid; i < NCH * CPR; i += 512) {
             const int row = i / CPR, c = i - row * CPR;
@@ -85,7 +86,7 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvArgs a, int nch
             s_shift[i] = a.shift[n0 + i];
         }
         if constexpr (KS2 > 0) {
-            const __bf16* w2 = (const __bf16*)a.w2;
+            const T* w2 = (const T*)a.w2;
             constexpr int CPR2 = KS2 * 4;
             for (int i = tid; i < NCH * CPR2; i += 512) {
                 const int row = i / CPR2, c = i - row * CPR2;
@@ -135,17 +136,17 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvArgs a, int nch
             _Pragma("unroll") for (int ks = 0; ks < KS; ++ks) {                                \
                 const int iy = iy0 + tdy[ks], ix = ix0 + tdx[ks];                              \
                 const bool in = (unsigned)iy < (unsigned)a.xh && (unsigned)ix < (unsigned)a.xw;\
-                const __bf16* src = (const __bf16*)a.x + (in ? base + toff[ks] : 0);           \
+                const T* src = (const T*)a.x + (in ? base + toff[ks] : 0);                     \
                 const u32x4 v = *(const u32x4*)src;                                            \
                 XF[ks] = in ? v : u32x4{0u, 0u, 0u, 0u};                                       \
             }                                                                                  \
         } else {                                                                               \
-            const __bf16* xp = (const __bf16*)a.x +                                            \
+            const T* xp = (const T*)a.x +                                                      \
                 (((size_t)b_ * a.xh + oy_ * a.stride) * a.xw + ox_ * a.stride) * a.ldx + a.xcoff + q * 8; \
             _Pragma("unroll") for (int ks = 0; ks < KS; ++ks) XF[ks] = *(const u32x4*)(xp + ks * 32); \
         }                                                                                      \
         if constexpr (KS2 > 0) {                                                               \
-            const __bf16* xp2 = (const __bf16*)a.x2 +                                          \
+            const T* xp2 = (const T*)a.x2 +                                                    \
                 (((size_t)b_ * a.xh2 + oy_ * a.stride2) * a.xw2 + ox_ * a.stride2) * a.ldx2 + a.xcoff2 + q * 8; \
             _Pragma("unroll") for (int ks = 0; ks < (KS2 > 0 ? KS2 : 1); ++ks) XF2[ks] = *(const u32x4*)(xp2 + ks * 32); \
         }                                                                                      \
@@ -154,10 +155,10 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvArgs a, int nch
             if (a.res_up) roff = ((size_t)(b_ * a.rh + (oy_ >> 1)) * a.rw + (ox_ >> 1)) * a.res_ld; \
             else roff = (size_t)m_ * a.res_ld;                                                 \
             if constexpr (NTT == 1) {                                                          \
-                const unsigned* rp = (const unsigned*)((const __bf16*)a.res + roff + a.res_coff + n0 + q * 4); \
+                const unsigned* rp = (const unsigned*)((const T*)a.res + roff + a.res_coff + n0 + q * 4); \
                 RF[0] = u32x4{rp[0], rp[1], 0u, 0u};                                           \
             } else {                                                                           \
-                const __bf16* rp = (const __bf16*)a.res + roff + a.res_coff + n0 + q * 8;      \
+                const T* rp = (const T*)a.res + roff + a.res_coff + n0 + q * 8;                \
                 _Pragma("unroll") for (int i = 0; i < NR; ++i) RF[i] = *(const u32x4*)(rp + 32 * i); \
             }                                                                                  \
         }                                                                                      \
@@ -192,8 +193,7 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvArgs a, int nch
 #pragma unroll
                 for (int j = 0; j < NTT; ++j) {
                     const u32x4 wf = *(const u32x4*)(wt + lds_off(16 * j + p_lane, ch));
-                    acc2[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, wf),
-                                                                      __builtin_bit_cast(bf16x8_t, xf2[ks]), acc2[j], 0, 0, 0);
+                    acc2[j] = HT::mfma(wf, xf2[ks], acc2[j]);
                 }
             }
         }
@@ -204,8 +204,7 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvArgs a, int nch
 #pragma unroll
             for (int j = 0; j < NTT; ++j) {
                 const u32x4 wf = *(const u32x4*)(wt + lds_off(16 * j + p_lane, ch));
-                acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, wf),
-                                                                 __builtin_bit_cast(bf16x8_t, xf[ks]), acc[j], 0, 0, 0);
+                acc[j] = HT::mfma(wf, xf[ks], acc[j]);
             }
         }
         if (ok) {
@@ -216,7 +215,7 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvArgs a, int nch
                           acc[0][3] * sc.w + sh.w};
             float rv[4] = {0.f, 0.f, 0.f, 0.f};
             if constexpr (RES != VD_RES_NONE) {
-                rv[0] = bf_lo(rf[0][0]); rv[1] = bf_hi(rf[0][0]); rv[2] = bf_lo(rf[0][1]); rv[3] = bf_hi(rf[0][1]);
+                rv[0] = HT::lo(rf[0][0]); rv[1] = HT::hi(rf[0][0]); rv[2] = HT::lo(rf[0][1]); rv[3] = HT::hi(rf[0][1]);
             }
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -229,9 +228,9 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvArgs a, int nch
             if (a.out_f32) {
                 *(float4*)((float*)a.y + yo) = make_float4(v[0], v[1], v[2], v[3]);
             } else {
-                typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
-                const bf16x4_t o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
-                *(bf16x4_t*)((__bf16*)a.y + yo) = o;
+                typedef T t16x4_t __attribute__((ext_vector_type(4)));
+                const t16x4_t o = {(T)v[0], (T)v[1], (T)v[2], (T)v[3]};
+                *(t16x4_t*)((T*)a.y + yo) = o;
             }
         } else {
         // lane holds channels n0 + 32i + 8q + (0..3 from tile 2i, 4..7 from tile 2i+1) of pixel m
@@ -258,7 +257,7 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvArgs a, int nch
             float rv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
             if constexpr (RES != VD_RES_NONE) {
 #pragma unroll
-                for (int e = 0; e < 4; ++e) { rv[2 * e] = bf_lo(rf[i][e]); rv[2 * e + 1] = bf_hi(rf[i][e]); }
+                for (int e = 0; e < 4; ++e) { rv[2 * e] = HT::lo(rf[i][e]); rv[2 * e + 1] = HT::hi(rf[i][e]); }
             }
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
@@ -272,10 +271,10 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvArgs a, int nch
                 *(float4*)((float*)a.y + yo + 32 * i) = make_float4(v[0], v[1], v[2], v[3]);
                 *(float4*)((float*)a.y + yo + 32 * i + 4) = make_float4(v[4], v[5], v[6], v[7]);
             } else {
-                bf16x8_t o;
+                typename HT::V8 o;
 #pragma unroll
-                for (int e = 0; e < 8; ++e) o[e] = (__bf16)v[e];
-                *(bf16x8_t*)((__bf16*)a.y + yo + 32 * i) = o;
+                for (int e = 0; e < 8; ++e) o[e] = (T)v[e];
+                *(typename HT::V8*)((T*)a.y + yo + 32 * i) = o;
             }
         }
         }
@@ -292,12 +291,12 @@ __global__ __launch_bounds__(512) void conv1x1_stream_kernel(ConvArgs a, int nch
 #undef VD_SLOAD
 }
 
-template <int KS, int NTT, int ACT, int RES, bool TAPS, int KS2 = 0>
-hipError_t launch_stream(const ConvArgs& a, hipStream_t s) {
+template <int KS, int NTT, int ACT, int RES, bool TAPS, int KS2, bool F16>
+hipError_t launch_stream_t(const ConvArgs& a, hipStream_t s) {
     constexpr int NCH = 16 * NTT, KT = (KS + 1) / 2, KT2 = (KS2 + 1) / 2;
     constexpr size_t lds = (size_t)(KT + KT2) * NCH * 128 + 4 * NCH * sizeof(float);
     static const bool attr = [] {
-        (void)hipFuncSetAttribute((const void*)conv1x1_stream_kernel<KS, NTT, ACT, RES, TAPS, KS2>,
+        (void)hipFuncSetAttribute((const void*)conv1x1_stream_kernel<KS, NTT, ACT, RES, TAPS, KS2, F16>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         return true;
     }();
@@ -308,7 +307,8 @@ hipError_t launch_stream(const ConvArgs& a, hipStream_t s) {
         int dev = 0, cus = 256, per_cu = 1;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv1x1_stream_kernel<KS, NTT, ACT, RES, TAPS, KS2>, 512, lds);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv1x1_stream_kernel<KS, NTT, ACT, RES, TAPS, KS2, F16>,
+                                                           512, lds);
         return std::max(1, cus * std::max(1, per_cu));
     }();
     const int nchunks = a.cout / NCH;
@@ -316,8 +316,14 @@ hipError_t launch_stream(const ConvArgs& a, hipStream_t s) {
     int k = std::max(1, resident / (8 * nchunks));
     k = std::min(k, std::max(1, (groups + 63) / 64));
     dim3 grid(8 * nchunks * k), block(512);
-    hipLaunchKernelGGL((conv1x1_stream_kernel<KS, NTT, ACT, RES, TAPS, KS2>), grid, block, lds, s, a, nchunks, groups);
+    hipLaunchKernelGGL((conv1x1_stream_kernel<KS, NTT, ACT, RES, TAPS, KS2, F16>), grid, block, lds, s, a, nchunks, groups);
     return hipGetLastError();
+}
+
+template <int KS, int NTT, int ACT, int RES, bool TAPS, int KS2 = 0>
+hipError_t launch_stream(const ConvArgs& a, hipStream_t s) {
+    return a.f16 ? launch_stream_t<KS, NTT, ACT, RES, TAPS, KS2, true>(a, s)
+                 : launch_stream_t<KS, NTT, ACT, RES, TAPS, KS2, false>(a, s);
 }
 
 template <int KS, int NTT, bool TAPS>

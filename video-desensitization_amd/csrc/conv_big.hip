@@ -82,7 +82,11 @@ __device__ __forceinline__ void wait_vm(int n) {
     }
 }
 
+// F16: the fp16 plan (VD_PREC_FP16) on fp16 operands / activations, else bf16
+template <bool F16>
 __global__ __launch_bounds__(512) void conv_big_kernel(ConvArgs a) {
+    using H16 = Half16<F16>;
+    typedef typename H16::T T;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wr = wid >> 2, wc = wid & 3;            // wave row (0..1) / column (0..3)
@@ -224,9 +228,7 @@ __global__ __launch_bounds__(512) void conv_big_kernel(ConvArgs a) {
         _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                       \
         _Pragma("unroll") for (int i = 0; i < 4; ++i)                                          \
         _Pragma("unroll") for (int j = 0; j < 2; ++j)                                          \
-            acc[MH][NH][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(                       \
-                __builtin_bit_cast(bf16x8_t, af[i][ks]),                                       \
-                __builtin_bit_cast(bf16x8_t, (NH) ? b1[j][ks] : b0[j][ks]), acc[MH][NH][i][j], 0, 0, 0); \
+            acc[MH][NH][i][j] = H16::mfma(af[i][ks], (NH) ? b1[j][ks] : b0[j][ks], acc[MH][NH][i][j]); \
         __builtin_amdgcn_s_setprio(0);                                                         \
         asm volatile("" ::: "memory");                                                         \
         VDB_STAMP();                                                                           \
@@ -304,20 +306,20 @@ __global__ __launch_bounds__(512) void conv_big_kernel(ConvArgs a) {
                 } else {
                     roff = (size_t)m * a.res_ld + a.res_coff + nb;
                 }
-                const bf16x8_t r8 = *(const bf16x8_t*)((const __bf16*)a.res + roff);
+                const typename H16::V8 r8 = *(const typename H16::V8*)((const T*)a.res + roff);
 #pragma unroll
                 for (int e = 0; e < 8; ++e) rv[e] = (float)r8[e];
             }
-            bf16x8_t o;
+            typename H16::V8 o;
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
                 float t = v[e];
                 if (a.res_mode == VD_RES_PRE_ACT) t += rv[e];
                 t = act_apply(t, a.act, a.slope);
                 if (a.res_mode == VD_RES_POST_ACT) t += rv[e];
-                o[e] = (__bf16)t;
+                o[e] = (T)t;
             }
-            *(bf16x8_t*)((__bf16*)a.y + (size_t)m * a.ldy + a.ycoff + nb) = o;
+            *(typename H16::V8*)((T*)a.y + (size_t)m * a.ldy + a.ycoff + nb) = o;
         }
     }
 }
@@ -341,13 +343,15 @@ bool vd_conv_big_ok(const ConvArgs& a) {
 
 hipError_t vd_launch_conv_big(const ConvArgs& a0, hipStream_t s) {
     static const bool attr = [] {
-        (void)hipFuncSetAttribute((const void*)conv_big_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)conv_big_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)conv_big_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
         return true;
     }();
     (void)attr;
     ConvArgs a = a0;
     a.ntiles_n = a.cout / 256;
     dim3 grid(((a.M + 255) / 256) * a.ntiles_n), block(512);
-    hipLaunchKernelGGL(conv_big_kernel, grid, block, LDS_BYTES, s, a);
+    if (a.f16) hipLaunchKernelGGL(conv_big_kernel<true>, grid, block, LDS_BYTES, s, a);
+    else hipLaunchKernelGGL(conv_big_kernel<false>, grid, block, LDS_BYTES, s, a);
     return hipGetLastError();
 }

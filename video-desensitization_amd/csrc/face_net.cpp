@@ -125,7 +125,7 @@ int vd_build_face(Ctx& c, const WMap& W) {
     // fp32 plan (fp16 pairs): the fused stem + pool on an fp16 space-to-depth canvas
     const bool s2d32 = c.f32 && c.tune.f32_split == 2 && c.tune.stem_pool &&
                        vd_stem_pool_ok(H / 2 + 1, Wd / 2 + 1, H / 4, Wd / 4);
-    F.s2d = ((!c.f32 && !c.f16) || s2d32) && !F.mnet && H % 2 == 0 && Wd % 2 == 0;
+    F.s2d = (!c.f32 || s2d32) && !F.mnet && H % 2 == 0 && Wd % 2 == 0;   // bf16 / fp16 / fp32 pairs
     c.amax_begin(0);
     if (F.s2d) rc = c.act(F.input, H / 2 + 1, Wd / 2 + 1, 16, false, c.f32);
     else rc = c.act(F.input, H, Wd, cpad);
@@ -195,7 +195,7 @@ int vd_build_face(Ctx& c, const WMap& W) {
             const Act* idt = &x;
             if (has_ds && c.dual_ok(c3, cd, out)) {
                 // relu(bn3(conv3(t2)) + bn(downsample(x))) in one streaming pass: the
-                // downsample output never goes through HBM (bf16 fast path only)
+                // downsample output never goes through HBM (16-bit and fp32-pair plans)
                 if ((rc = c.add_conv_dual(F.net, c3, t2, cd, x, out))) return rc;
                 x = out;
                 continue;

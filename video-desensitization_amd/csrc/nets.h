@@ -114,7 +114,7 @@ struct PostScratch {   // per-net candidate / NMS scratch sized for max_batch x 
 struct FaceNet {
     bool loaded = false;
     int in_h = 640, in_w = 640;
-    bool s2d = false;               // bf16: stem input in space-to-depth form (pre.hip letterbox_s2d_kernel)
+    bool s2d = false;               // 16-bit / fp32-pair plans: stem input in space-to-depth form (pre.hip letterbox_s2d_kernel)
     bool mnet = false;              // MobileNetV1-0.25 backbone (cfg_mnet) instead of ResNet-50
     Act input;
     Net net;
@@ -131,7 +131,7 @@ struct PlateNet {
     int imgsz = 640;
     int hstride = 0;                // head channel stride (64 DFL + nc, padded to 8)
     Act input;                      // letterboxed canvas, allocated for imgsz x imgsz
-    bool s2d = false;               // bf16: canvas in space-to-depth form, model.0 as a 2x2 conv
+    bool s2d = false;               // 16-bit / fp32-pair plans: canvas in space-to-depth form, model.0 as a 2x2 conv
     std::vector<std::pair<std::string, Act>> bufs;   // named activation buffers (max canvas)
     std::vector<std::pair<std::string, int>> conv_idx;
     std::vector<std::pair<long long, Net>> plans;    // per canvas (h<<32|w)
@@ -161,7 +161,7 @@ struct Ctx {
     vd_cfg cfg{};
     int device = 0;
     bool f32 = false;
-    bool f16 = false;                             // VD_PREC_FP16: fp16 operands/activations (GEMM path only)
+    bool f16 = false;                             // VD_PREC_FP16: fp16 operands/activations (the bf16 plan's kernels)
     VdTune tune;                                  // kernel-selection switches (vd_set_option)
     hipStream_t stream = nullptr, own_stream = nullptr;
     hipStream_t stream2 = nullptr;               // plate branch runs beside the face branch

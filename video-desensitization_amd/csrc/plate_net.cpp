@@ -267,7 +267,7 @@ int vd_build_plate(Ctx& c, const WMap& W) {
     // bf16 / fp32 (fp16 pairs): the letterbox writes the stem input in space-to-depth form
     // (option plate_s2d=0: off); fp32 as integer pixel values in f32 (exact in fp16),
     // model.0 then on one A plane (x_exact) with the / 255 in its BN scale
-    P.s2d = c.tune.plate_s2d && ((!c.f32 && !c.f16) || (c.f32 && c.tune.f32_split == 2 && c.tune.plate_s2d32));
+    P.s2d = c.tune.plate_s2d && (!c.f32 || (c.tune.f32_split == 2 && c.tune.plate_s2d32));
     if (P.s2d && (rc = yconv_s2d(c, W, "model.0"))) return rc;
     for (int i : {0, 1, 3, 5, 7}) {
         if (i == 0 && P.s2d) continue;

@@ -269,7 +269,7 @@ __global__ __launch_bounds__(256) void letterbox_s2d_pair_kernel(LetterboxArgs a
             if (!(cv ? yb : ya) || (unsigned)XX >= (unsigned)(cv ? OWb : OWa)) continue;
             const Tap* ty = cv ? tyb : tya;
             const bool* rin = cv ? rinb : rina;
-            __bf16 t[16];
+            float t[16];
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
                 const int h = s >> 1;
@@ -278,12 +278,10 @@ __global__ __launch_bounds__(256) void letterbox_s2d_pair_kernel(LetterboxArgs a
                 const int y = 2 * YY + h - 1;
                 if ((unsigned)y < (unsigned)c.oh && (unsigned)x < (unsigned)c.ow)
                     lb_px_lds(c, lrow + (2 * h) * RS, lrow + (2 * h + 1) * RS, ty[h], x, rin[h], v);
-                t[4 * s + 0] = (__bf16)v[0]; t[4 * s + 1] = (__bf16)v[1]; t[4 * s + 2] = (__bf16)v[2];
-                t[4 * s + 3] = (__bf16)0.f;
+                t[4 * s + 0] = v[0]; t[4 * s + 1] = v[1]; t[4 * s + 2] = v[2];
+                t[4 * s + 3] = 0.f;
             }
-            __bf16* out = (__bf16*)c.out + (((size_t)f * (cv ? OHb : OHa) + YY) * (cv ? OWb : OWa) + XX) * 16;
-            *(uint4*)out = *(const uint4*)t;
-            *(uint4*)(out + 8) = *(const uint4*)(t + 8);
+            store_s2d(c, ((size_t)f * (cv ? OHb : OHa) + YY) * (cv ? OWb : OWa) + XX, t);   // bf16 or fp16
         }
     }
 }
@@ -374,10 +372,10 @@ __global__ __launch_bounds__(256) void upsample2x_kernel(const T* x, int xh, int
 
 }  // namespace
 
-// Same frames, both bf16 space-to-depth canvases, the same resize (nw, nh, filter)
-// and even relative offsets of the pasted images.
+// Same frames, both 16-bit (bf16 / fp16) space-to-depth canvases, the same resize
+// (nw, nh, filter) and even relative offsets of the pasted images.
 bool vd_letterbox_pair_ok(const LetterboxArgs& a, const LetterboxArgs& b) {
-    return a.s2d && b.s2d && !a.out_f32 && !b.out_f32 && !a.out_f16 && !b.out_f16 && a.src == b.src && a.n == b.n &&
+    return a.s2d && b.s2d && !a.out_f32 && !b.out_f32 && a.src == b.src && a.n == b.n &&
            a.ih == b.ih && a.iw == b.iw && a.pitch == b.pitch && a.iw * 3 <= LB_LDS_MAX && a.nw == b.nw &&
            a.nh == b.nh && a.mode == b.mode && a.scale_x == b.scale_x && a.scale_y == b.scale_y &&
            ((a.top - b.top) & 1) == 0 && ((a.left - b.left) & 1) == 0;

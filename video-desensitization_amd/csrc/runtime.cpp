@@ -355,7 +355,6 @@ int Ctx::make_conv_cat(const WMap& W, const std::vector<std::string>& wkeys, con
 
 // Bottleneck conv3 (ci on x) + downsample (c2 on x2, strided 1x1) in one op.
 bool Ctx::dual_ok(int ci, int c2, const Act& y) const {
-    if (f16) return false;
     const Conv& a = convs[ci];
     const Conv& b = convs[c2];
     if (f32) {   // fp16-pair plan: conv1x1_x6_dual_kernel
@@ -482,6 +481,7 @@ int Ctx::run_chain_op(const Op& op, int f0, int n, int fam) {
     a.y = (void*)foff(op.y, f0); a.ld_y = op.y.c;
     a.y2 = (void*)foff(op.y2, f0); a.ld_y2 = op.y2.c;
     a.M = n * op.y.h * op.y.w;
+    a.f16 = f16 ? 1 : 0;
     t_begin(fam, (c3.flops_per_px + c1.flops_per_px) * a.M);
     hipError_t e = vd_launch_chain(a, stream);
     t_end();
@@ -489,11 +489,11 @@ int Ctx::run_chain_op(const Op& op, int f0, int n, int fam) {
     return VD_OK;
 }
 
-// Peephole over ops [begin, end) of a bf16 plan: a bottleneck conv3 (1x1, + identity
+// Peephole over ops [begin, end) of a bf16 / fp16 plan: a bottleneck conv3 (1x1, + identity
 // before the ReLU) immediately followed by a 1x1 conv that reads exactly its output
 // (the next bottleneck's conv1) becomes one OP_CHAIN where chain.hip covers the shape.
 void Ctx::fuse_chains(Net& net, size_t begin) {
-    if (f32 || f16) return;
+    if (f32) return;
     std::vector<Op> out(net.ops.begin(), net.ops.begin() + begin);
     for (size_t i = begin; i < net.ops.size(); ++i) {
         const Op& a = net.ops[i];

@@ -44,22 +44,22 @@ __device__ __forceinline__ int st_off(int row, int chunk) {
     return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
 }
 
-__device__ __forceinline__ f32x4_t mfma(const u32x4& a, const u32x4& b, const f32x4_t& c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
-                                                   c, 0, 0, 0);
-}
-
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
-// max of two pairs of non-negative bf16 (their bit patterns order as unsigned
-// 16-bit integers): one v_pk_max_u16
+// max of two pairs of non-negative bf16 -- or fp16: both formats' non-negative bit
+// patterns order as unsigned 16-bit integers: one v_pk_max_u16
 __device__ __forceinline__ unsigned max_bf16x2(unsigned a, unsigned b) {
     return __builtin_bit_cast(unsigned, __builtin_elementwise_max(__builtin_bit_cast(u16x2, a),
                                                                  __builtin_bit_cast(u16x2, b)));
 }
 
-template <int NXB>   // X' tile buffers: 2 = next tile's DMA overlaps this tile, 1 = more workgroups per CU
+// NXB: X' tile buffers (2 = next tile's DMA overlaps this tile, 1 = more workgroups per
+// CU); F16: the fp16 plan (VD_PREC_FP16: fp16 canvas, weights and pooled map)
+template <int NXB, bool F16>
 __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemPoolArgs a) {
+    using HT = Half16<F16>;
+    typedef typename HT::T E16;
+    const auto mfma = [](const u32x4& x, const u32x4& y, const f32x4_t& c) { return HT::mfma(x, y, c); };
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* lx = smem;                       // NXB x XBUF
     char* lst = smem + NXB * XBUF;         // STB
@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemPoolArgs a) {
         const int ty = r0 / tpc, tx = r0 - ty * tpc;
         const int xr0 = 2 * PT * ty - 2, xc0 = 2 * PT * tx - 2;   // X' origin of the tile
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)((const __bf16*)a.x + (size_t)b * fx), 0, (int)(fx * 2), 0x00020000);
+            (void*)((const E16*)a.x + (size_t)b * fx), 0, (int)(fx * 2), 0x00020000);
         char* dst = lx + buf * XBUF;
 #pragma unroll
         for (int k = 0; k < DPW; ++k) {
@@ -155,13 +155,13 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemPoolArgs a) {
             }
             const int sy = sy0 + r, sx = sx0 + c;
             const bool in = p < SP && (unsigned)sy < (unsigned)SH && (unsigned)sx < (unsigned)SW;
-            bf16x8_t o;
+            typename HT::V8 o;
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
                 const float v = acc[e >> 2][e & 3] * sc[e] + sh[e];
-                o[e] = (__bf16)(in && v > 0.f ? v : 0.f);
+                o[e] = (E16)(in && v > 0.f ? v : 0.f);
             }
-            *(bf16x8_t*)(lst + st_off(p, 4 * np + g)) = o;
+            *(typename HT::V8*)(lst + st_off(p, 4 * np + g)) = o;
         }
         __syncthreads();
         if (NXB == 1 && t + tstep < tend) issue_x(t + tstep, 0);   // X' buffer free once stage A is done
@@ -171,7 +171,7 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemPoolArgs a) {
             // stores through a descriptor, unconditional (past the frame: out-of-range
             // offset, dropped) so every thread issues exactly 2 per tile (see vmcnt above)
             const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
-                (void*)((__bf16*)a.y + (size_t)b * a.ph * a.pw * 64), 0, (int)((size_t)a.ph * a.pw * 128), 0x00020000);
+                (void*)((E16*)a.y + (size_t)b * a.ph * a.pw * 64), 0, (int)((size_t)a.ph * a.pw * 128), 0x00020000);
 #pragma unroll
             for (int pass = 0; pass < 2; ++pass) {
                 const int q = pass * 32 + (tid >> 3), ch = tid & 7;
@@ -194,11 +194,11 @@ __global__ __launch_bounds__(256, 2) void stem_pool_kernel(StemPoolArgs a) {
     }
 }
 
-template <int NXB>
+template <int NXB, bool F16>
 hipError_t launch_stem(const StemPoolArgs& a, hipStream_t s) {
     constexpr size_t lds = NXB * XBUF + STB + 1024;
     static const int cus = [] {
-        (void)hipFuncSetAttribute((const void*)stem_pool_kernel<NXB>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)stem_pool_kernel<NXB, F16>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds);
         int dev = 0, n = 256;
         (void)hipGetDevice(&dev);
@@ -208,7 +208,7 @@ hipError_t launch_stem(const StemPoolArgs& a, hipStream_t s) {
     const int per_cu = NXB == 2 ? 2 : 3;                 // LDS: 66 KB / 53 KB per workgroup
     const int tiles = a.B * ((a.ph + PT - 1) / PT) * ((a.pw + PT - 1) / PT);
     const int grid = tiles < per_cu * cus ? tiles : per_cu * cus;   // persistent
-    hipLaunchKernelGGL(stem_pool_kernel<NXB>, dim3(grid), dim3(256), lds, s, a);
+    hipLaunchKernelGGL((stem_pool_kernel<NXB, F16>), dim3(grid), dim3(256), lds, s, a);
     return hipGetLastError();
 }
 
@@ -225,7 +225,7 @@ hipError_t vd_launch_stem_pool(const StemPoolArgs& a, hipStream_t s) {
     // one X' buffer and three workgroups per CU measured 9 % faster than two buffers
     // (DMA overlapping the whole tile) at two workgroups per CU: the kernel is
     // latency-bound, occupancy wins
-    return launch_stem<1>(a, s);
+    return a.f16 ? launch_stem<1, true>(a, s) : launch_stem<1, false>(a, s);
 }
 
 // ---------------------------------------------------------------------------

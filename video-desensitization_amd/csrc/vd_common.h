@@ -9,6 +9,35 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
+typedef unsigned vd_u32x4 __attribute__((ext_vector_type(4)));
+
+// The 16-bit operand type of the bf16 plan (F16 = false) and the fp16 plan (VD_PREC_FP16,
+// F16 = true): element type, 8-vector, the 16x16x32 matrix-core product, and the two
+// elements of a packed 32-bit word as f32. Conversions to T are round-to-nearest-even.
+template <bool F16> struct Half16;
+template <> struct Half16<false> {
+    typedef __bf16 T;
+    typedef bf16x8_t V8;
+    static __device__ __forceinline__ f32x4_t mfma(const vd_u32x4& a, const vd_u32x4& b, const f32x4_t& c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
+                                                       c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ float lo(unsigned u) { return __uint_as_float(u << 16); }
+    static __device__ __forceinline__ float hi(unsigned u) { return __uint_as_float(u & 0xFFFF0000u); }
+};
+template <> struct Half16<true> {
+    typedef _Float16 T;
+    typedef f16x8_t V8;
+    static __device__ __forceinline__ f32x4_t mfma(const vd_u32x4& a, const vd_u32x4& b, const f32x4_t& c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b),
+                                                      c, 0, 0, 0);
+    }
+    static __device__ __forceinline__ float lo(unsigned u) {
+        return (float)__builtin_bit_cast(_Float16, (unsigned short)(u & 0xFFFFu));
+    }
+    static __device__ __forceinline__ float hi(unsigned u) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(u >> 16)); }
+};
+
 enum VdAct { VD_ACT_NONE = 0, VD_ACT_RELU = 1, VD_ACT_LEAKY = 2, VD_ACT_SILU = 3 };
 enum VdResMode { VD_RES_NONE = 0, VD_RES_PRE_ACT = 1, VD_RES_POST_ACT = 2 };
 
@@ -131,6 +160,7 @@ struct BlockArgs {
     const float* bn;             // s1 t1 s2 t2 (64 each) s3 t3 sd td (256 each)
     unsigned long long* diag;    // optional: per-stage cycle sums of workgroup 0, wave 0 (tools/convbench)
     int mode;                    // experiments (tools/convbench VD_BLOCK_MODE); 0 in production
+    int f16;                     // fp16 plan: fp16 operands / activations (else bf16)
 };
 
 // One fused layer1 bottleneck in the fp32 plan (block32.hip): x f32 [B][H][W][cin]
@@ -161,6 +191,7 @@ struct ChainArgs {
     void* y; int ld_y;                    // block output [M][512]
     void* y2; int ld_y2;                  // next block's t1 [M][128]
     int M;
+    int f16;                              // fp16 plan: fp16 operands / activations (else bf16)
 };
 
 // Depthwise 3x3 conv (pad 1) + BN + activation, NHWC (dwconv.hip): MobileNetV1 conv_dw.
@@ -182,6 +213,7 @@ struct StemPoolArgs {
                                  //   (fp32 plan: [2 planes: hi, lo] of that, fp16; x = X' in fp16, exact)
     const float* scale; const float* shift;
     unsigned* ymax;              // fp32 plan: per-frame max |y| slots of the pooled map
+    int f16;                     // fp16 plan (stem_pool_kernel): fp16 canvas, weights and pooled map
 };
 
 // Device buffers + parameters for one frame batch's detection post-processing.

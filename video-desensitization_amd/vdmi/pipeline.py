@@ -233,8 +233,14 @@ class GpuJpegStages:
         dev = self.dev = torch.device(f"cuda:{ctx.device}")
         self.dctx = Context(device=ctx.device, precision="fp32", max_batch=self.B)
         self.ectx = Context(device=ctx.device, precision="fp32", max_batch=self.B)
-        self.s_dec = torch.cuda.ExternalStream(self.dctx.stream(), device=dev)
-        self.s_enc = torch.cuda.ExternalStream(self.ectx.stream(), device=dev)
+        # the codec contexts run on high-priority streams: their small, latency-bound
+        # kernels (entropy-decode passes between host convergence checks) are dispatched
+        # ahead of the queued workgroups of the process context's convs
+        hi = torch.cuda.Stream.priority_range()[1]
+        self.s_dec = torch.cuda.Stream(device=dev, priority=hi)
+        self.s_enc = torch.cuda.Stream(device=dev, priority=hi)
+        self.dctx.set_stream(self.s_dec.cuda_stream)
+        self.ectx.set_stream(self.s_enc.cuda_stream)
         self.faces = [DeviceBoxes(self.B, cap, dev) for _ in range(self.depth)]
         self.plates = [DeviceBoxes(self.B, cap, dev) for _ in range(self.depth)]
         self.ev_dec = [torch.cuda.Event() for _ in range(self.depth)]
