@@ -5,6 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 OUT=gpurun_out/r4d
 mkdir -p $OUT
 export TMPDIR=/tmp
+timeout -k 10 120 tools/x6bench 20 all > $OUT/x6.txt 2>&1 || exit 1
 timeout -k 10 700 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_e2e.py tests/test_gpu_configs.py tests/test_gpu_plates.py tests/test_gpu_kernels.py -k "16bit or fp16 or c5 or 4k or plate" -p no:cacheprovider > $OUT/tests.log 2>&1; rc=$?
 tail -3 $OUT/tests.log
 [ $rc -eq 0 ] || exit $rc

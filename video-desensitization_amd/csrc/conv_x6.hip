@@ -102,6 +102,13 @@ __device__ __forceinline__ void wait_vm(int n) {
     }
 }
 
+// s_waitcnt vmcnt(N) for a compile-time N (no branch tree)
+template <int N>
+__device__ __forceinline__ void wait_vm_k() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 __device__ __forceinline__ float act_apply(float v, int act, float slope) {
     if (act == VD_ACT_RELU) return v > 0.f ? v : 0.f;
     if (act == VD_ACT_LEAKY) return v > 0.f ? v : v * slope;
@@ -692,8 +699,14 @@ __global__ __launch_bounds__(NT, NT == 256 && BM == 256 ? 1 : 2) void conv_x6_ke
     if (NA < nk) load_a(ra[0]);
     if (nk > 1) dma_b(1, 1);
     auto iter = [&](int kt, const u32x4 (&rnext)[AIT][2], u32x4 (&rfree)[AIT][2]) {
-        const int younger = (kt + NA < nk ? 2 * AIT : 0) + (kt + 1 < nk ? my_dma : 0);
-        wait_vm(younger);
+        if (S::NDMA % WAVES == 0 && !(a.dbg & 2)) {   // immediates: no runtime wait_vm branch tree
+            constexpr int MYD = S::NDMA % WAVES == 0 ? S::NDMA / WAVES : 0;
+            if (kt + NA < nk) wait_vm_k<2 * AIT + MYD>();
+            else if (kt + 1 < nk) wait_vm_k<MYD>();
+            else wait_vm_k<0>();
+        } else {
+            wait_vm((kt + NA < nk ? 2 * AIT : 0) + (kt + 1 < nk ? my_dma : 0));
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this thread's A(kt) ds_writes
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
@@ -720,7 +733,8 @@ __global__ __launch_bounds__(NT, NT == 256 && BM == 256 ? 1 : 2) void conv_x6_ke
 #pragma unroll
         for (int q = 0; q < AIT; ++q) store_item(0, rcur, q);   // compiler waits for A(kt)'s loads
         if (kt + 1 < nk) load_a(rnext);
-        wait_vm(kt + 1 < nk ? 2 * AIT : 0);                   // B(kt) landed (older than A(kt+1))
+        if (kt + 1 < nk) wait_vm_k<2 * AIT>();                // B(kt) landed (older than A(kt+1))
+        else wait_vm_k<0>();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
@@ -925,7 +939,41 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
     // 9c+8], B(s+2) at the end of step s. At the top of step s, younger than B(s):
     // B(s+1) (if issued) and the halo loads issued at the end of step s-1 or (s = 1)
     // in the prologue after B(1).
-    if constexpr (NSB == 3) {
+    if (NSB == 3 && S::NDMA % WAVES == 0 && !(a.dbg & 2)) {
+        // This wave's DMA count per step is a compile-time constant, so each step's vmcnt
+        // is one of four immediates chosen by two uniform branches (the runtime wait_vm
+        // switch costs a tree of scalar branches per step). (Unrolling the nine taps of a
+        // chunk as well measured no better and spills on the 192 / 256-wide tiles.)
+        constexpr int MYD = S::NDMA % WAVES == 0 ? S::NDMA / WAVES : 0;
+        for (int s = 0; s < nsteps; ++s) {
+            const int c = s / 9, tap = s - 9 * c;
+            // halo loads younger than B(s): chunk c+1's, issued at the end of step s-1
+            // (tap 0, c >= 1) or in the prologue after B(1) (s = 0, 1)
+            const bool halo_prev = tap == 0 ? c + 1 < CH : (s == 1 && CH > 1);
+            if (halo_prev) {
+                if (s + 1 < nsteps) wait_vm_k<MYD + 2 * QI>();
+                else wait_vm_k<2 * QI>();
+            } else {
+                if (s + 1 < nsteps) wait_vm_k<MYD>();
+                else wait_vm_k<0>();
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();                // B(s) visible; stage (s + 2) % 3 free
+            asm volatile("" ::: "memory");
+            const bool rehalo = tap == 8 && c + 1 < CH;
+            if (!rehalo && s + 2 < nsteps) dma_b(s + 2, (s + 2) % 3);
+            const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
+            compute(s % 3, dy, dx);
+            if (rehalo) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();            // every wave is done with chunk c's halo
+                asm volatile("" ::: "memory");
+                store_halo();
+                if (c + 2 < CH) load_halo(c + 2);
+                if (s + 2 < nsteps) dma_b(s + 2, (s + 2) % 3);
+            }
+        }
+    } else if (NSB == 3) {
         // VMEM issue order per step s: [top] B(s+2), except on tap-8 steps, which issue
         // it at the end, after the halo loads of chunk c+2 (the halo stores then wait
         // only on B(s+1), issued a step earlier, not on a DMA just issued). Younger than

@@ -102,7 +102,7 @@ struct VdTune {
     int x6_slots = 0;         //   workgroup slots of one round (0: the CU count; tests force small values)
     int x6_gemm1x1 = 1;       // fp16 pairs: GEMM 1x1 convs on the TR tiles (D^T accumulators, register epilogue;
                               //   2: also the streaming form's K <= 256 layers, 0: off)
-    int x6_dbg = 0;           // timing experiments only (tools/x6bench; WRONG results): 1 = no epilogue
+    int x6_dbg = 0;           // experiments (tools/x6bench): 1 = no epilogue (WRONG results), 2 = runtime vmcnt waits
     int f32_split = 2;        // plan (fp32, at weight load): 2 = operands scaled by powers of two
                               //   and split into fp16 pairs, 3 products on the f16 matrix cores;
                               //   1 = exact 3-term bf16 split, 6 products (conv_x6.hip);
