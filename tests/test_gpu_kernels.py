@@ -504,3 +504,28 @@ def test_conv_tr_tiles_bit_identical(gpu, face_ctx_factory, case):
         outs.append(ctx.conv2d(x, wt, s, p, scale, shift, act, 0.1, res, res_mode))
     assert np.array_equal(outs[0], outs[1])
     test_conv_matches_torch(gpu, face_ctx_factory, "fp32", case, options=dict(x6_gemm1x1=1, x6_stream=0))
+
+
+@pytest.mark.parametrize("copy", [0, 1])
+def test_mosaic_output_forms_match_oracle(gpu, copy):
+    """Option mosaic_copy: 1 (default) = copy-first (one plain copy pass, the cell
+    kernel writes each box cell's owned pixel runs, the band output pass only for
+    frames without a cell table); 0 = the band output pass writes every byte. Both
+    exact against the oracle on overlapping / nested boxes, > 256 boxes (no cell
+    table), a cell-table overflow and frames with no boxes."""
+    import vdmi
+    from vdmi import mosaic_frames, synth
+    ctx = vdmi.Context(precision="bf16", max_batch=4, options={"mosaic_copy": copy})
+    try:
+        rng = np.random.default_rng(21)
+        frames = synth.frames(4, 480, 720, seed=21)
+        nested = [(10 + 3 * i, 5 + 9 * i, 700 - 2 * i, 470 - i) for i in range(25)]
+        many = [tuple(int(v) for v in (x, y, x + rng.integers(4, 60), y + rng.integers(4, 60)))
+                for x, y in zip(rng.integers(-20, 720, 300), rng.integers(-20, 480, 300))]
+        boxes = [_rand_boxes(rng, 1, 480, 720, 30)[0], nested, many, []]
+        for level in (1, 3, 8):
+            got = mosaic_frames(frames, boxes, level, ctx=ctx)
+            for i in range(4):
+                np.testing.assert_array_equal(got[i], omosaic.mosaic_frame(frames[i], boxes[i], level))
+    finally:
+        ctx.close()

@@ -61,6 +61,7 @@ struct VdTune {
     int mosaic_map = 1;       // mosaic output pass: per-band vector maps (0: generic path)
     int mosaic_nt = 0;        //   non-temporal output stores (1), and source loads (3)
     int mosaic_cells = 32;    //   cell-table kernel: workgroups per frame
+    int mosaic_copy = 1;      //   copy-first output: one plain copy pass, the cell kernel writes the box pixels
     int block_fuse = 1;       // plan: fused layer1 bottlenecks (block.hip)
     int block_fuse32 = 1;     // plan, fp32 (fp16 pairs): fused layer1 bottlenecks (block32.hip)
     int chain = 1;            // plan: layer2 conv3 + next conv1 (chain.hip)
@@ -462,7 +463,7 @@ hipError_t vd_launch_jpeg(const JpegArgs& a, hipStream_t s);
 hipError_t vd_launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w, size_t pitch,
                             const int* cnt0, const int* xy0, int cap0,
                             const int* cnt1, const int* xy1, int cap1, int level, void* table,
-                            int stages, int map_on, int cell_blocks, hipStream_t s);   // stages: 1 = cell table, 2 = output pass
+                            int stages, int map_on, int cell_blocks, hipStream_t s);   // stages: 1 = cell table, 2 = output pass, 4 = copy
 size_t vd_mosaic_table_bytes(int n, int tcap);
 
 #define VD_CHECK_HIP(expr)                                                     \
