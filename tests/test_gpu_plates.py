@@ -146,19 +146,21 @@ def test_plate_raw_bf16_s2d_matches_plain(gpu, h, w):
     assert _rel(out["1"][:, 64:], exp[:, 64:]) < 8e-2
 
 
-@pytest.mark.parametrize("h,w", [(1080, 1920), (720, 1280), (480, 640), (1080, 1440)])
-def test_process_paired_letterbox_matches_separate(gpu, h, w):
+@pytest.mark.parametrize("prec,h,w", [("bf16", 1080, 1920), ("bf16", 720, 1280), ("bf16", 480, 640),
+                                       ("bf16", 1080, 1440), ("fp32", 1080, 1920), ("fp16", 720, 1280)])
+def test_process_paired_letterbox_matches_separate(gpu, prec, h, w):
     """With faces and plates in one vd_process call, both s2d canvases come from one
     read of the frames (pre.hip letterbox_s2d_pair_kernel) where the resize geometry
-    matches; option lb_pair=0 runs the two letterboxes apart. Same per-pixel arithmetic:
-    box lists and mosaicked frames are identical."""
+    matches; option lb_pair=0 runs the two letterboxes apart. Same per-pixel arithmetic
+    (fp32 plan: fp16 face canvas + f32 plate canvas from the one staged read): box lists
+    and mosaicked frames are identical."""
     import vdmi
     from vdmi import _lib, synth, weights
     fr = synth.frames(2, h, w, seed=21)
     flags = _lib.VD_PROC_FACES | _lib.VD_PROC_PLATES | _lib.VD_PROC_MOSAIC | _lib.VD_PROC_MOSAIC_PLATES
     res = {}
     for pair in ("1", "0"):
-        c = vdmi.Context(precision="bf16", max_batch=2, options={"lb_pair": int(pair)})
+        c = vdmi.Context(precision=prec, max_batch=2, options={"lb_pair": int(pair)})
         try:
             c.load_weights(0, weights.retinaface_state_dict(0))
             c.load_weights(1, weights.yolov8n_state_dict(0))

@@ -170,6 +170,13 @@ __global__ __launch_bounds__(512, 1) void bottleneck32_kernel(Block32Args a) {
     const __amdgpu_buffer_rsrc_t rwd = __builtin_amdgcn_make_buffer_rsrc((void*)(DS ? a.wd : a.w3), 0, 0x7fffffff,
                                                                           0x00020000);
     const unsigned lo16 = (unsigned)lane * 16u;
+    u32x4 w2f[9][2];
+#pragma unroll
+    for (int tp = 0; tp < 9; ++tp)
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+            w2f[tp][p] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                rw2, lo16, ((((jn * 2 + hf) * 9 + tp) * 2 + p) * 64) * 16, 0));
     const size_t fpx = (size_t)a.H * a.W;
     int ob = -1;            // output max bookkeeping: this wave's current frame and its max
     float om = 0.f;
@@ -194,33 +201,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck32_kernel(Block32Args a) {
         return __builtin_amdgcn_make_buffer_rsrc((void*)((const float*)a.x + (size_t)b * fpx * CIN), 0,
                                                  (int)(fpx * CIN * 4), 0x00020000);
     };
-    // The stage-1 x of a whole tile (both pixel tiles, all k-steps) is loaded into
-    // registers one stage ahead: the next tile's loads are issued during this tile's
-    // stage 3 (after its last identity load), so their HBM latency hides under stage 3
-    // and the barrier; W2 is not stationary but re-read from L2 per tile after stage 1
-    // (its 72 registers are the x buffers' during stage 1 / 3)
-    // XPF k-steps cross the tile boundary (the rest are loaded at the top of stage 1,
-    // XPF k-steps ahead of their use): all of them at CIN 64, 6 of 8 at CIN 256 (all 8
-    // spills at 256 VGPRs beside stage 3's operands)
-    constexpr int XPF = KS1 <= 2 ? KS1 : 6;
-    u32x4 xq[KS1][2][2];                            // [k-step][pixel tile A / B][half]
-    auto x_offsets = [&](int tt, unsigned& offA, unsigned& offB) {
-        const int rr = tt % tpf;
-        const int yy = rr / a.tiles_x, xx = rr - yy * a.tiles_x;
-        int li = li0, g = g0;
-        asm volatile("" : "+v"(li), "+v"(g));
-        offA = xoff(yy * TH, xx * TW, w, li, g);
-        offB = xoff(yy * TH, xx * TW, 8 + (w >> 1), li, g);
-    };
-    auto load_x_tile = [&](int tt) {
-        unsigned offA, offB;
-        x_offsets(tt, offA, offB);
-        const __amdgpu_buffer_rsrc_t rxx = frame_rsrc(tt / tpf);
-#pragma unroll
-        for (int s2 = 0; s2 < XPF; ++s2) ldx(rxx, offA, offB, s2, xq[s2][0], xq[s2][1]);
-    };
 
-    load_x_tile(t0);
 #pragma unroll 1
     for (int t = t0; t < tend; t += tstep) {
         const int b = t / tpf, r0 = t - b * tpf;
@@ -239,22 +220,20 @@ __global__ __launch_bounds__(512, 1) void bottleneck32_kernel(Block32Args a) {
         float vA[4][4], vB[2][4];
         {
             const int pB = 8 + (w >> 1), hB = w & 1;
+            const unsigned offA = xoff(oy0, ox0, w, li, g), offB = xoff(oy0, ox0, pB, li, g);
             f32x4_t accA[4], accB[2];
 #pragma unroll
             for (int c = 0; c < 4; ++c) accA[c] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int c = 0; c < 2; ++c) accB[c] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-            if constexpr (XPF < KS1) {                  // the k-steps not prefetched across tiles
-                unsigned offA, offB;
-                x_offsets(t, offA, offB);
-#pragma unroll
-                for (int s2 = XPF; s2 < KS1; ++s2) ldx(rx, offA, offB, s2, xq[s2][0], xq[s2][1]);
-            }
+            u32x4 xa[2][2], xb[2][2];                    // [set][half]: k-step s in set s & 1
+            ldx(rx, offA, offB, 0, xa[0], xb[0]);
 #pragma unroll
             for (int s = 0; s < KS1; ++s) {
+                if (s + 1 < KS1) ldx(rx, offA, offB, s + 1, xa[(s + 1) & 1], xb[(s + 1) & 1]);
                 u32x4 pa[2], pb[2];
-                split8(xq[s][0][0], xq[s][0][1], sax, pa);
-                split8(xq[s][1][0], xq[s][1][1], sax, pb);
+                split8(xa[s & 1][0], xa[s & 1][1], sax, pa);
+                split8(xb[s & 1][0], xb[s & 1][1], sax, pb);
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
                     u32x4 wf[2];
@@ -286,19 +265,6 @@ __global__ __launch_bounds__(512, 1) void bottleneck32_kernel(Block32Args a) {
             for (int c = 0; c < 2; ++c) finish(accB[c], 2 * hB + c, pB, vB[c]);
             m = wave_max(m);
             if (lane == 0 && m > 0.f) atomicMax(s_max, __float_as_uint(m));
-        }
-        // this tile's W2 fragments (this wave's 16 channels x its input half, 9 taps x 2
-        // planes), from L2, landing under B1 / the t1 split / B2
-        u32x4 w2f[9][2];
-        {
-            unsigned lo = lo16;
-            asm volatile("" : "+v"(lo));
-#pragma unroll
-            for (int tp = 0; tp < 9; ++tp)
-#pragma unroll
-                for (int p = 0; p < 2; ++p)
-                    w2f[tp][p] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                        rw2, lo, ((((jn * 2 + hf) * 9 + tp) * 2 + p) * 64) * 16, 0));
         }
         __syncthreads();   // B1: the tile's t1 max is complete
         {
@@ -453,8 +419,6 @@ __global__ __launch_bounds__(512, 1) void bottleneck32_kernel(Block32Args a) {
             for (int m = 0; m < 8; ++m) {
                 __builtin_amdgcn_sched_barrier(0);   // keep rows apart (register pressure)
                 if constexpr (DS) ldr(m, xr[0]); else if (m + 1 < 8) ldr(m + 1, xr[(m + 1) & 1]);
-                // the next tile's stage-1 x, once this tile's last identity load is issued
-                if (m == (DS ? 7 : 6) && t + tstep < tend) load_x_tile(t + tstep);
                 u32x4 tfr[2][2];
 #pragma unroll
                 for (int s = 0; s < 2; ++s) {

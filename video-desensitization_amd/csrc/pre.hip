@@ -281,7 +281,7 @@ __global__ __launch_bounds__(256) void letterbox_s2d_pair_kernel(LetterboxArgs a
                 t[4 * s + 0] = v[0]; t[4 * s + 1] = v[1]; t[4 * s + 2] = v[2];
                 t[4 * s + 3] = 0.f;
             }
-            store_s2d(c, ((size_t)f * (cv ? OHb : OHa) + YY) * (cv ? OWb : OWa) + XX, t);   // bf16 or fp16
+            store_s2d(c, ((size_t)f * (cv ? OHb : OHa) + YY) * (cv ? OWb : OWa) + XX, t);   // bf16, fp16 or f32
         }
     }
 }
@@ -375,7 +375,7 @@ __global__ __launch_bounds__(256) void upsample2x_kernel(const T* x, int xh, int
 // Same frames, both 16-bit (bf16 / fp16) space-to-depth canvases, the same resize
 // (nw, nh, filter) and even relative offsets of the pasted images.
 bool vd_letterbox_pair_ok(const LetterboxArgs& a, const LetterboxArgs& b) {
-    return a.s2d && b.s2d && !a.out_f32 && !b.out_f32 && a.src == b.src && a.n == b.n &&
+    return a.s2d && b.s2d && a.src == b.src && a.n == b.n &&
            a.ih == b.ih && a.iw == b.iw && a.pitch == b.pitch && a.iw * 3 <= LB_LDS_MAX && a.nw == b.nw &&
            a.nh == b.nh && a.mode == b.mode && a.scale_x == b.scale_x && a.scale_y == b.scale_y &&
            ((a.top - b.top) & 1) == 0 && ((a.left - b.left) & 1) == 0;

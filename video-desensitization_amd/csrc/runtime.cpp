@@ -1136,8 +1136,8 @@ int vd_process(vd_ctx* h, const uint8_t* in, uint8_t* out, int n, int fh, int fw
         ctx->face_letterbox_args(d, n, fh, fw, pitch, &fa);
         if (ctx->tune.lb_pair && vd_plate_letterbox_args(*ctx, d, n, fh, fw, pitch, &pa) == VD_OK &&
             vd_letterbox_pair_ok(fa, pa)) {
-            ctx->t_begin(2, (double)n * (fa.nh * (double)fw * 3 + ((double)(fa.oh / 2 + 1) * (fa.ow / 2 + 1) +
-                                                                    (double)(pa.oh / 2 + 1) * (pa.ow / 2 + 1)) * 32));
+            ctx->t_begin(2, (double)n * (fa.nh * (double)fw * 3 + (double)(fa.oh / 2 + 1) * (fa.ow / 2 + 1) * (fa.out_f32 ? 64 : 32) +
+                                         (double)(pa.oh / 2 + 1) * (pa.ow / 2 + 1) * (pa.out_f32 ? 64 : 32)));
             hipError_t e = vd_launch_letterbox_pair(fa, pa, ctx->stream);
             ctx->t_end();
             if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "letterbox pair: %s", hipGetErrorString(e));

@@ -61,7 +61,7 @@ struct VdTune {
     int mosaic_map = 1;       // mosaic output pass: per-band vector maps (0: generic path)
     int mosaic_nt = 0;        //   non-temporal output stores (1), and source loads (3)
     int mosaic_cells = 32;    //   cell-table kernel: workgroups per frame
-    int mosaic_copy = 1;      //   copy-first output: one plain copy pass, the cell kernel writes the box pixels
+    int mosaic_copy = 0;      //   copy-first output: one plain copy pass, the cell kernel writes the box pixels (measured slower)
     int block_fuse = 1;       // plan: fused layer1 bottlenecks (block.hip)
     int block_fuse32 = 1;     // plan, fp32 (fp16 pairs): fused layer1 bottlenecks (block32.hip)
     int chain = 1;            // plan: layer2 conv3 + next conv1 (chain.hip)
