@@ -224,6 +224,7 @@ class Mode:
         if plates:
             self.ctx.load_weights(_lib.VD_NET_YOLOV8N, weights.yolov8n_state_dict(0))
         self.precision = precision
+        self.face_groups = opts.get("face_groups", 2)   # runtime default (vd_common.h VdTune)
         self.faces = vdmi.DeviceBoxes(a.batch, 256, dev)
         self.pboxes = vdmi.DeviceBoxes(a.batch, 256, dev) if plates else None
         self.flags = _lib.VD_PROC_FACES | _lib.VD_PROC_MOSAIC | (_lib.VD_PROC_PLATES if plates else 0)
@@ -342,6 +343,13 @@ def main():
         res = {"value": round(total * a.steps / dt, 2), "ms_per_step": round(dt / a.steps * 1e3, 3)}
         if not a.no_timing:
             res.update(instrumented(mode, precision))
+            rf = res["roofline"]
+            # the timed steps' face-conv FLOPs over their whole wall time (every other
+            # kernel of the step, the plate net included, counted against them)
+            sa = rf["flop_per_step"] / (res["ms_per_step"] * 1e-3) / 1e12
+            rf["step"] = {"achieved": round(sa, 2), "frac": round(sa / rf["peak"], 4),
+                          "face_groups": mode.face_groups,
+                          "what": "face-conv FLOP per step / ms_per_step of the timed steps"}
         res["faces_per_frame"] = round(float(mode.faces.count.float().mean().item()), 2)
         lists = frame_lists(mode.ctx, batches[-1][1]) if batches and a.faces else []
         if world == 1 and precision == a.precision and a.host_pipeline:
@@ -424,11 +432,16 @@ def main():
 
     def instrumented(mode, precision):
         """Per-kernel-family durations: the same K steps again, each launch bracketed
-        by HIP events on the stream it runs on (runtime.cpp t_begin / t_end)."""
+        by HIP events on the stream it runs on (runtime.cpp t_begin / t_end). The face
+        net runs as one launch per layer over the whole batch here (face_groups = 1):
+        with frame groups on concurrent streams each launch's events would also span
+        the other groups' work. The timed steps' own rate is `roofline.step`."""
         ctx = mode.ctx
+        ctx.set_option("face_groups", 1)
         ctx.timing(True)
         ctx.timing_reset()
         dt_ev = timed(mode)
+        ctx.set_option("face_groups", mode.face_groups)
         r = {"instrumented_ms_per_step": round(dt_ev / a.steps * 1e3, 3)}
         cms, cn, cflop = ctx.timing_read(_lib.FAM_CONV)
         mms, mn, mbytes = ctx.timing_read(_lib.FAM_MOSAIC)
@@ -456,7 +469,9 @@ def main():
                                    "concurrently on a second stream)",
                          "avg_launch_ms": round(cms / max(cn, 1), 4), "launches": cn,
                          "flop_per_launch": round(cflop / max(cn, 1)), "traffic_unit": "bytes per launch (HBM, PMC)",
-                         "traffic_source": tsrc}
+                         "traffic_source": tsrc,
+                         "measured_with": "face_groups=1 (one launch per layer over the batch, face stream)",
+                         "flop_per_step": round(cflop / max(a.steps, 1))}
         # blur: the output pass (mosaic_out_kernel) dominates; algorithmic bytes per launch =
         # 2*W*H*3 per frame (out-of-place, reference new-array semantics); the family adds
         # the cell-table kernel (box prep + walked cell colours)

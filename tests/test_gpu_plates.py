@@ -208,6 +208,39 @@ def test_process_plate_release_point(gpu, stage):
         np.testing.assert_array_equal(res[stage][2][b], res[3][2][b])
 
 
+@pytest.mark.parametrize("prec,plates,groups", [("fp32", True, 2), ("fp32", False, 2), ("bf16", True, 2),
+                                               ("fp32", True, 3), ("fp16", False, 4)])
+def test_process_face_groups_bit_identical(gpu, prec, plates, groups):
+    """Option face_groups runs the face net as G frame groups on G streams (runtime.cpp
+    Ctx::face_forward; default 2). Every kernel is batch-invariant, so the float boxes,
+    scores and mosaicked frames equal the one-launch schedule's (face_groups=1)
+    exactly; an odd batch splits unevenly (5 frames: 2 + 3, 1 + 2 + 2, 1 + 1 + 1 + 2)."""
+    import vdmi
+    from vdmi import _lib, synth, weights
+    fr = synth.frames(5, 1080, 1920, seed=23)
+    flags = _lib.VD_PROC_FACES | _lib.VD_PROC_MOSAIC
+    if plates:
+        flags |= _lib.VD_PROC_PLATES | _lib.VD_PROC_MOSAIC_PLATES
+    res = {}
+    for hv in (groups, 1):
+        c = vdmi.Context(precision=prec, max_batch=5, options={"face_groups": hv})
+        try:
+            c.load_weights(0, weights.retinaface_state_dict(0))
+            if plates:
+                c.load_weights(1, weights.yolov8n_state_dict(0))
+            for _ in range(2):                                     # a second call reuses the events
+                out, faces, pl = c.process(fr, flags=flags)
+            res[hv] = (out.copy(), [faces.frame(b)[0].copy() for b in range(5)],
+                       [np.concatenate([faces.frame(b)[1].ravel(), faces.frame(b)[2]]) for b in range(5)])
+        finally:
+            c.close()
+    np.testing.assert_array_equal(res[groups][0], res[1][0])
+    assert sum(len(x) for x in res[1][1]) > 0
+    for b in range(5):
+        np.testing.assert_array_equal(res[groups][1][b], res[1][1][b])
+        np.testing.assert_array_equal(res[groups][2][b], res[1][2][b])
+
+
 @pytest.mark.parametrize("h,w", [(1080, 1920), (720, 1280), (480, 640)])
 def test_plate_raw_fp32_s2d_matches_plain(gpu, h, w):
     """fp32 plan: the plate canvas in space-to-depth form as integer pixel values in

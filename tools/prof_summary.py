@@ -5,8 +5,15 @@ its own stream (the plate network's convs run on a second stream), so the
 per-launch averages can be checked against bench.py's in-process HIP-event
 numbers (`roofline.avg_launch_ms` is the face conv family).
 
-    python tools/prof_summary.py gpurun_out/prof/run_kernel_stats.csv [out.md]
+    python tools/prof_summary.py gpurun_out/prof/run_kernel_stats.csv [out.md] [bench.json]
+
+With bench.json (the same run's JSON line) the last `roofline.launches` face-stream
+conv launches -- bench.py's instrumented pass, which runs last and issues the face net
+as one launch per layer over the batch (face_groups = 1) -- are averaged on their own:
+that is the number `roofline.avg_launch_ms` must agree with. The timed steps before it
+run the face net as frame groups on two streams (both count as face streams).
 """
+import json
 import csv
 import os
 import sys
@@ -40,20 +47,25 @@ def face_stream(rows):
     return face
 
 
-def face_stream_convs(trace_path):
-    """[count, total ns] of conv launches on the face stream, and on the others."""
-    rows = list(csv.DictReader(open(trace_path)))
+def face_stream_convs(trace_path, last=0):
+    """[count, total ns] of conv launches on the face stream(s), on the others, and of
+    the last `last` face-stream launches by start time."""
+    rows = sorted(csv.DictReader(open(trace_path)), key=lambda r: int(r["Start_Timestamp"]))
     face = face_stream(rows)
-    f, o = [0, 0], [0, 0]
+    f, o, tail = [0, 0], [0, 0], []
     for r in rows:
         if any(k in r["Kernel_Name"] for k in CONV):
+            d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
             acc = f if r["Stream_Id"] in face else o
             acc[0] += 1
-            acc[1] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-    return f, o
+            acc[1] += d
+            if r["Stream_Id"] in face:
+                tail.append(d)
+    tail = tail[-last:] if last else []
+    return f, o, [len(tail), sum(tail)]
 
 
-def main(path, out=None):
+def main(path, out=None, bench=None):
     rows = list(csv.DictReader(open(path)))
     lines = ["| family | kernel | calls | total ms | avg us |", "|---|---|---:|---:|---:|"]
     fam_tot = {}
@@ -75,7 +87,11 @@ def main(path, out=None):
         lines.append(f"| {fam} | {c} | {t:.3f} | {t / c * 1e3:.1f} |")
     trace = os.path.join(os.path.dirname(path), os.path.basename(path).replace("kernel_stats", "kernel_trace"))
     if os.path.exists(trace):
-        (fc, ft), (oc, ot) = face_stream_convs(trace)
+        last = 0
+        if bench:
+            line = [x for x in open(bench).read().splitlines() if x.startswith("{")][-1]
+            last = int(json.loads(line)["roofline"]["launches"])
+        (fc, ft), (oc, ot), (lc, lt) = face_stream_convs(trace, last)
         lines.append("")
         lines.append("| conv launches by stream | calls | total ms | avg us per launch |")
         lines.append("|---|---:|---:|---:|")
@@ -83,6 +99,9 @@ def main(path, out=None):
             lines.append(f"| RetinaFace (face stream) | {fc} | {ft / 1e6:.3f} | {ft / fc / 1e3:.1f} |")
         if oc:
             lines.append(f"| YOLOv8n (plate stream) | {oc} | {ot / 1e6:.3f} | {ot / oc / 1e3:.1f} |")
+        if lc:
+            lines.append(f"| RetinaFace, bench.py's instrumented pass (last {lc}, face_groups = 1) | {lc} | "
+                         f"{lt / 1e6:.3f} | {lt / lc / 1e3:.1f} |")
     txt = "\n".join(lines) + "\n"
     if out:
         open(out, "w").write(txt)
@@ -90,4 +109,4 @@ def main(path, out=None):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None, sys.argv[3] if len(sys.argv) > 3 else None)

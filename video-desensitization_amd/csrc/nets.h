@@ -169,6 +169,9 @@ struct Ctx {
     hipStream_t stream_side = nullptr;           // the face net's second lane (SSH levels 1-2 beside level 0)
     std::vector<hipEvent_t> lane_ev;             // per face op: completion event for the other lane
     hipEvent_t ev_side = nullptr;                // side lane done (joined before the face decode)
+    hipEvent_t ev_half = nullptr;                // option face_groups: fork of the frame groups
+    std::vector<hipStream_t> group_streams;      // option face_groups: streams of frame groups 1..G-1
+    std::vector<hipEvent_t> group_events;        //   and their completion events (joined by the context stream)
     int fork_at = -1;                                // run_ops records ev_fork after this many face ops
     std::mutex mu;
     std::vector<void*> allocs;

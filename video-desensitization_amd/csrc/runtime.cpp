@@ -763,6 +763,40 @@ int Ctx::face_forward(int n) {
     const int mb = cfg.reserved[0];                       // frames per micro-batch (0 = off)
     const int stage = cfg.reserved[1] > 0 ? cfg.reserved[1] : 2;   // micro-batch through layer<stage>
     const int split = face.net.stage_end[std::min(std::max(stage, 0), 4)];
+    const int G = std::min(std::min(tune.face_groups, 4), n);
+    if (G >= 2 && mb <= 0 && lane_ev.empty()) {
+        // G frame groups on G streams (group 0 on the context stream): each layer's last
+        // partial round of workgroups leaves CUs that the other groups' launches take.
+        // Every kernel is batch-invariant (a frame's sums do not depend on its batch
+        // position or the launch's frame count), so the results are bit-identical to
+        // one launch over n frames.
+        const Net& net = face.net;
+        while ((int)group_streams.size() < G - 1) {
+            hipStream_t st;
+            hipEvent_t ev;
+            VD_CHECK_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+            VD_CHECK_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            group_streams.push_back(st);
+            group_events.push_back(ev);
+        }
+        if (!ev_half) VD_CHECK_HIP(hipEventCreateWithFlags(&ev_half, hipEventDisableTiming));
+        if (net.amax) VD_CHECK_HIP(hipMemsetAsync(net.amax, 0, net.amax_bytes, stream));
+        VD_CHECK_HIP(hipEventRecord(ev_half, stream));
+        hipStream_t main = stream;
+        for (int g = 0; g < G; ++g) {
+            const int f0 = (int)((long)n * g / G), f1 = (int)((long)n * (g + 1) / G);
+            stream = g ? group_streams[g - 1] : main;
+            if (g) VD_CHECK_HIP(hipStreamWaitEvent(stream, ev_half, 0));
+            int rc = run_ops(net, 0, (int)net.ops.size(), f0, f1 - f0);
+            if (!rc && g) {
+                if (hipEventRecord(group_events[g - 1], stream) != hipSuccess) rc = vd_set_error(VD_ERR_HIP, "group event");
+            }
+            stream = main;
+            if (rc) return rc;
+        }
+        for (int g = 1; g < G; ++g) VD_CHECK_HIP(hipStreamWaitEvent(stream, group_events[g - 1], 0));
+        return VD_OK;
+    }
     return run_net(face.net, n, mb, split);
 }
 
@@ -946,6 +980,12 @@ int vd_destroy(vd_ctx* h) {
         if (ev) hipEventDestroy(ev);
     hipEventDestroy(ctx->ev_fork);
     hipEventDestroy(ctx->ev_join);
+    if (ctx->ev_half) hipEventDestroy(ctx->ev_half);
+    for (size_t g = 0; g < ctx->group_streams.size(); ++g) {
+        hipStreamSynchronize(ctx->group_streams[g]);
+        hipStreamDestroy(ctx->group_streams[g]);
+        hipEventDestroy(ctx->group_events[g]);
+    }
     hipStreamDestroy(ctx->stream2);
     hipStreamDestroy(ctx->own_stream);
     delete ctx;
@@ -986,7 +1026,7 @@ int vd_set_option(vd_ctx* h, const char* name, int value) {
         {"plate_s2d", &VdTune::plate_s2d}, {"f32_split", &VdTune::f32_split},
         {"x6_small_k", &VdTune::x6_small_k}, {"x6_small_tiles", &VdTune::x6_small_tiles},
         {"x6_stream", &VdTune::x6_stream}, {"x6_small_k2", &VdTune::x6_small_k2}, {"x6_bn256", &VdTune::x6_bn256},
-        {"x6_exact", &VdTune::x6_exact}, {"x6_mid", &VdTune::x6_mid}, {"block_fuse32", &VdTune::block_fuse32}, {"x6_mf32", &VdTune::x6_mf32}, {"x6_tail", &VdTune::x6_tail}, {"x6_stream_silu", &VdTune::x6_stream_silu}, {"x6_slots", &VdTune::x6_slots}, {"x6_halo", &VdTune::x6_halo}, {"x6_halo_narrow", &VdTune::x6_halo_narrow}, {"x6_adepth", &VdTune::x6_adepth}, {"x6_gemm1x1", &VdTune::x6_gemm1x1}, {"x6_stream256", &VdTune::x6_stream256}, {"plate_stage", &VdTune::plate_stage}, {"ssh_side", &VdTune::ssh_side}, {"plate_s2d32", &VdTune::plate_s2d32},
+        {"x6_exact", &VdTune::x6_exact}, {"x6_mid", &VdTune::x6_mid}, {"block_fuse32", &VdTune::block_fuse32}, {"x6_mf32", &VdTune::x6_mf32}, {"x6_tail", &VdTune::x6_tail}, {"x6_stream_silu", &VdTune::x6_stream_silu}, {"x6_slots", &VdTune::x6_slots}, {"x6_halo", &VdTune::x6_halo}, {"x6_halo_narrow", &VdTune::x6_halo_narrow}, {"x6_adepth", &VdTune::x6_adepth}, {"x6_gemm1x1", &VdTune::x6_gemm1x1}, {"x6_stream256", &VdTune::x6_stream256}, {"plate_stage", &VdTune::plate_stage}, {"ssh_side", &VdTune::ssh_side}, {"face_groups", &VdTune::face_groups}, {"plate_s2d32", &VdTune::plate_s2d32},
         {"jenc_gpu", &VdTune::jenc_gpu}, {"jdec_gpu", &VdTune::jdec_gpu}, {"jdec_chunk", &VdTune::jdec_chunk}, {"jdec_sync", &VdTune::jdec_sync}, {"jdec_group", &VdTune::jdec_group},
     };
     for (const Opt& o : opts)

@@ -77,6 +77,8 @@ struct VdTune {
                               //   (at weight load; measured -0.1 ms/step, but overlapping launches inflate
                               //   the per-launch durations behind `roofline`: off by default)
     int plate_s2d32 = 1;      // fp32 plan: the plate stem on the fp16 space-to-depth canvas (with plate_s2d)
+    int face_groups = 2;      // face net as G frame groups on G streams (the tails of one group's launches
+                              //   fill with the others'; bit-identical; 0 / 1: one launch over the batch)
     int plate_stage = 3;      // plate branch starts after face stage N (0: with the stem; 1-4: after
                               //   layerN; 5: after the whole face net). After layer3 its HBM-bound
                               //   convs overlap the MFMA-bound late face layers: 30.8 -> 30.0 ms/step
