@@ -263,3 +263,35 @@ def test_plate_raw_fp32_s2d_matches_plain(gpu, h, w):
     assert out[1].shape == out[0].shape == exp.shape
     assert _rel(out[1], out[0]) < 2e-5
     assert _rel(out[1], exp) < 1e-4
+
+
+@pytest.mark.parametrize("h,w", [(1080, 1920), (720, 1280), (480, 640)])
+def test_plate_raw_fp32_taps_matches_gemm(gpu, h, w):
+    """fp32 plan: the YOLO net's narrow KxK layers (model.0 on its integer s2d canvas,
+    model.1 / model.3 and the C2f bottleneck 3x3 convs with K <= 288) on the streaming
+    TAPS form (conv_x6.hip conv1x1_x6_kernel<..., TAPS>, option x6_taps); x6_taps=0 runs
+    them on the GEMM / halo tiles. The same fp16-pair products per output in another f32
+    order: raw outputs within f32 rounding of each other and of the oracle, the same
+    int boxes, float corners within f32 rounding."""
+    import vdmi
+    from vdmi import synth, weights
+    fr = synth.frames(3, h, w, seed=9)
+    out, boxes = {}, {}
+    for t in (1, 0):
+        c = vdmi.Context(precision="fp32", max_batch=3, options={"x6_taps": t})
+        try:
+            c.load_weights(1, weights.yolov8n_state_dict(0))
+            c.timing(True)
+            c.timing_reset()
+            out[t] = c.plate_raw(fr)
+            got = c.detect_plates(fr)
+            boxes[t] = [(got.frame(b)[0].copy(), got.frame(b)[1].copy()) for b in range(3)]
+        finally:
+            c.close()
+    exp, _, _ = _oracle_raw(fr)
+    assert out[1].shape == out[0].shape == exp.shape
+    assert _rel(out[1], out[0]) < 2e-5
+    assert _rel(out[1], exp) < 1e-4
+    for b in range(3):   # same boxes; float corners within f32 rounding (observed 2e-7)
+        np.testing.assert_array_equal(boxes[1][b][0], boxes[0][b][0])
+        np.testing.assert_allclose(boxes[1][b][1], boxes[0][b][1], rtol=2e-6, atol=0)

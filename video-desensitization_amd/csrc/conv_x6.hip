@@ -1035,11 +1035,20 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
 // 16 pixels' 8 channels per lane loaded as 2 x 16 B f32 straight from NHWC and
 // split in registers; weight rows are permuted so tiles 2i, 2i+1 give a lane 8
 // consecutive output channels (two 16-B f32 stores, residual read in the same shape).
-template <int KS, int NTT, int ACT, int RES, int TERMS>
-__global__ __launch_bounds__(512) void conv1x1_x6_kernel(ConvArgs a, int nchunks, int groups) {
+//
+// TAPS form (round 4, the YOLO net's narrow KxK layers, K <= 288): each lane's 8-channel
+// K chunk of every k-step is one (dy, dx, c) of the filter, fixed per lane, so the
+// tap table sits in registers; a pixel's chunk is loaded through a buffer descriptor
+// (off the frame -> zeros, conv padding) for every k-step. TERMS = 1: integer-valued
+// input (x_exact canvases) on one plane against both weight planes. NTT = 1: 16
+// output channels, a lane stores 4 consecutive ones.
+template <int KS, int NTT, int ACT, int RES, int TERMS, bool TAPS = false>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(TAPS ? 4 : 1)))   // TAPS: two workgroups per CU
+void conv1x1_x6_kernel(ConvArgs a, int nchunks, int groups) {
+    constexpr int WT = TERMS == 1 ? 2 : TERMS;             // weight planes
     constexpr int NCH = 16 * NTT, PL = KS * NCH * 64;     // bytes per weight plane
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    float* s_scale = (float*)(smem + TERMS * PL);
+    float* s_scale = (float*)(smem + WT * PL);
     float* s_shift = s_scale + NCH;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int bid = blockIdx.x, xcd = bid & 7, local = bid >> 3;
@@ -1050,11 +1059,11 @@ __global__ __launch_bounds__(512) void conv1x1_x6_kernel(ConvArgs a, int nchunks
     {   // split weights [n0, n0 + NCH) x K -> LDS [plane][ks][row][64 B]; row 16j + i holds
         // channel 32(j>>1) + 8(i>>2) + 4(j&1) + (i&3)
         const int nk = a.kpad / KT;
-        for (int i = tid; i < TERMS * KS * NCH * 4; i += 512) {
+        for (int i = tid; i < WT * KS * NCH * 4; i += 512) {
             const int c = i & 3, row = (i >> 2) % NCH, pk = (i >> 2) / NCH, ks = pk % KS, p = pk / KS;
             const int j = row >> 4, ii = row & 15;
             const int chn = NTT == 1 ? row : 32 * (j >> 1) + 8 * (ii >> 2) + 4 * (j & 1) + (ii & 3);
-            const u32x4 v = *(const u32x4*)((const char*)a.wx3 + ((((size_t)(n0 + chn) * nk + ks) * TERMS + p) * 64 + c * 16));
+            const u32x4 v = *(const u32x4*)((const char*)a.wx3 + ((((size_t)(n0 + chn) * nk + ks) * WT + p) * 64 + c * 16));
             *(u32x4*)(smem + p * PL + ks * NCH * 64 + swz(row, c)) = v;
         }
         for (int i = tid; i < NCH; i += 512) {
@@ -1069,19 +1078,47 @@ __global__ __launch_bounds__(512) void conv1x1_x6_kernel(ConvArgs a, int nchunks
     const int p_lane = lane & 15, q = lane >> 4;
     const int ohw = a.yh * a.yw;
     const int wstride = nmblk * 8;
+    // TAPS: this lane's (dy, dx, c) per k-step; a chunk past K gets dy far off the frame
+    int tdy[TAPS ? KS : 1], tdx[TAPS ? KS : 1], toff[TAPS ? KS : 1];
+    if constexpr (TAPS) {
+        const int kreal = a.kh * a.kw * a.cin_pad;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            const int k = ks * 32 + q * 8, t = k / a.cin_pad, c = k - t * a.cin_pad;
+            const int dy = t / a.kw, dx = t - dy * a.kw;
+            tdy[ks] = k < kreal ? dy : (1 << 28);
+            tdx[ks] = dx;
+            toff[ks] = (dy * a.xw + dx) * a.ldx + c;
+        }
+    }
+    const __amdgpu_buffer_rsrc_t rsrc_x = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)a.x, 0, (int)((long)a.B * a.xh * a.xw * a.ldx * 4), 0x00020000);
     auto load = [&](int g, u32x4 (&xf)[KS][2]) {
         const int mu = g * 16 + p_lane;
         const int m = mu < a.M ? mu : a.M - 1;
         const int b = m / ohw, rem = m - b * ohw;
         const int oy = rem / a.yw, ox = rem - oy * a.yw;
-        const float* xp = (const float*)a.x + (((size_t)b * a.xh + oy * a.stride) * a.xw + ox * a.stride) * a.ldx +
-                          a.xcoff + q * 8;
+        if constexpr (TAPS) {
+            const int iy0 = oy * a.stride - a.pad, ix0 = ox * a.stride - a.pad;
+            const int pbase = ((b * a.xh + iy0) * a.xw + ix0) * a.ldx + a.xcoff;
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-            xf[ks][0] = *(const u32x4*)(xp + ks * 32);
-            xf[ks][1] = *(const u32x4*)(xp + ks * 32 + 4);
+            for (int ks = 0; ks < KS; ++ks) {
+                const bool ok = ((unsigned)(iy0 + tdy[ks]) < (unsigned)a.xh) & ((unsigned)(ix0 + tdx[ks]) < (unsigned)a.xw);
+                const unsigned off = ok ? (unsigned)(pbase + toff[ks]) * 4u : 0x80000000u;
+                xf[ks][0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc_x, (int)off, 0, 0));
+                xf[ks][1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc_x, (int)(off + 16u), 0, 0));
+            }
+        } else {
+            const float* xp = (const float*)a.x + (((size_t)b * a.xh + oy * a.stride) * a.xw + ox * a.stride) * a.ldx +
+                              a.xcoff + q * 8;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                xf[ks][0] = *(const u32x4*)(xp + ks * 32);
+                xf[ks][1] = *(const u32x4*)(xp + ks * 32 + 4);
+            }
         }
     };
+    (void)rsrc_x;
     u32x4 xf[KS][2];
     int g = mblk * 8 + wid;
     if (g < groups) load(g, xf);
@@ -1108,9 +1145,16 @@ __global__ __launch_bounds__(512) void conv1x1_x6_kernel(ConvArgs a, int nchunks
             for (int j = 0; j < NTT; ++j) {
                 u32x4 wf[3];
 #pragma unroll
-                for (int p = 0; p < TERMS; ++p)
+                for (int p = 0; p < WT; ++p)
                     wf[p] = *(const u32x4*)(smem + p * PL + ks * NCH * 64 + swz(16 * j + p_lane, q));
-                acc[j] = mfma_terms<TERMS>(wf, xb, acc[j]);
+                if constexpr (TERMS == 1) {   // w_lo x + w_hi x (x exact on one plane)
+                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, wf[1]),
+                                                                    __builtin_bit_cast(f16x8_t, xb[0]), acc[j], 0, 0, 0);
+                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, wf[0]),
+                                                                    __builtin_bit_cast(f16x8_t, xb[0]), acc[j], 0, 0, 0);
+                } else {
+                    acc[j] = mfma_terms<TERMS>(wf, xb, acc[j]);
+                }
             }
         }
         float vmax = 0.f;
@@ -1128,6 +1172,25 @@ __global__ __launch_bounds__(512) void conv1x1_x6_kernel(ConvArgs a, int nchunks
                     roff = (size_t)m * a.res_ld;
                 }
                 roff += a.res_coff + n0 + q * 8;
+            }
+            if constexpr (NTT == 1) {   // rows = channels: a lane holds channels 4q .. 4q + 3
+                if constexpr (RES != VD_RES_NONE) roff -= q * 4;
+                const size_t yo1 = (size_t)m * a.ldy + a.ycoff + n0 + q * 4;
+                const int c = q * 4;
+                float v[4];
+                float4 r4 = make_float4(0.f, 0.f, 0.f, 0.f);
+                if constexpr (RES != VD_RES_NONE) r4 = *(const float4*)((const float*)a.res + roff);
+                const float rv[4] = {r4.x, r4.y, r4.z, r4.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float t = (acc[0][e] * inv_sa) * s_scale[c + e] + s_shift[c + e];
+                    if constexpr (RES == VD_RES_PRE_ACT) t += rv[e];
+                    t = act_apply(t, ACT, a.slope);
+                    if constexpr (RES == VD_RES_POST_ACT) t += rv[e];
+                    v[e] = t;
+                    vmax = fmaxf(vmax, fabsf(t));
+                }
+                *(float4*)((float*)a.y + yo1) = make_float4(v[0], v[1], v[2], v[3]);
             }
             const size_t yo = (size_t)m * a.ldy + a.ycoff + n0 + q * 8;
 #pragma unroll
@@ -1335,27 +1398,61 @@ hipError_t launch_dual_x6(const ConvArgs& a0, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <int KS, int NTT, int ACT, int RES, int TERMS>
+template <int KS, int NTT, int ACT, int RES, int TERMS, bool TAPS = false>
 hipError_t launch_stream_x6(const ConvArgs& a, hipStream_t s) {
     constexpr int NCH = 16 * NTT;
-    constexpr int lds = TERMS * KS * NCH * 64 + 2 * NCH * 4;
+    constexpr int lds = (TERMS == 1 ? 2 : TERMS) * KS * NCH * 64 + 2 * NCH * 4;
     static const int resident = [] {
-        (void)hipFuncSetAttribute((const void*)conv1x1_x6_kernel<KS, NTT, ACT, RES, TERMS>,
+        (void)hipFuncSetAttribute((const void*)conv1x1_x6_kernel<KS, NTT, ACT, RES, TERMS, TAPS>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds + 4 * kAmaxFrames);
         int dev = 0, cus = 256, per_cu = 1;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv1x1_x6_kernel<KS, NTT, ACT, RES, TERMS>, 512,
-                                                           lds);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv1x1_x6_kernel<KS, NTT, ACT, RES, TERMS, TAPS>,
+                                                           512, lds);
         return std::max(1, cus * std::max(1, per_cu));
     }();
     const int nchunks = a.cout / NCH;
     const int groups = (a.M + 15) / 16;
     int k = std::max(1, resident / (8 * nchunks));
     k = std::min(k, std::max(1, (groups + 63) / 64));
-    hipLaunchKernelGGL((conv1x1_x6_kernel<KS, NTT, ACT, RES, TERMS>), dim3(8 * nchunks * k), dim3(512),
+    hipLaunchKernelGGL((conv1x1_x6_kernel<KS, NTT, ACT, RES, TERMS, TAPS>), dim3(8 * nchunks * k), dim3(512),
                        lds + (a.ymax ? 4 * a.B : 0), s, a, nchunks, groups);
     return hipGetLastError();
+}
+
+// TAPS streaming form (fp16 pairs): the narrow KxK layers of the YOLO net -- Cin a
+// multiple of 8, K (padded) <= 160, Cout 16 / 32 as one channel slice, SiLU (the
+// C2f bottleneck's shortcut as a post-activation residual) -- and the space-to-depth
+// model.0 on its integer canvas (x_exact: one A plane). Returns false when not taken.
+static bool launch_taps_x6(const ConvArgs& a, hipStream_t s, hipError_t* err) {
+    if (!a.tune || !a.tune->x6_taps || (a.kh == 1 && a.kw == 1 && a.pad == 0 && a.stride == 1)) return false;
+    if (a.act != VD_ACT_SILU || (a.res_mode != VD_RES_NONE && a.res_mode != VD_RES_POST_ACT)) return false;
+    if ((a.cin_pad & 7) || ((a.ldx | a.xcoff) & 3) || ((a.ldy | a.ycoff) & 7)) return false;
+    if (a.res_mode != VD_RES_NONE && (a.res_up || ((a.res_ld | a.res_coff) & 7))) return false;
+    if (a.kpad > 160 || a.kpad % 32) return false;
+    const int ks = a.kpad / 32, co = a.cout;
+    const bool post = a.res_mode == VD_RES_POST_ACT;
+#define VD_TAPS(KS, NTT, T)                                                                                        \
+    do {                                                                                                           \
+        *err = post ? launch_stream_x6<KS, NTT, VD_ACT_SILU, VD_RES_POST_ACT, T, true>(a, s)                       \
+                    : launch_stream_x6<KS, NTT, VD_ACT_SILU, VD_RES_NONE, T, true>(a, s);                          \
+        return true;                                                                                               \
+    } while (0)
+    if (a.x_exact) {
+        if (ks == 2 && co == 16 && !post) {
+            *err = launch_stream_x6<2, 1, VD_ACT_SILU, VD_RES_NONE, 1, true>(a, s);
+            return true;
+        }
+        return false;
+    }
+    // K <= 160 only: at K = 288 (model.3, the 32-channel bottlenecks at 80x48) the
+    // two register sets of x need ~210 VGPRs, one workgroup per CU, and the form
+    // measured 5-40 % slower than the GEMM / halo tiles
+    if (ks == 5 && co == 16) VD_TAPS(5, 1, 2);
+    if (ks == 5 && co == 32) VD_TAPS(5, 2, 2);
+#undef VD_TAPS
+    return false;
 }
 
 template <int KS, int NTT, int TERMS>
@@ -1541,6 +1638,10 @@ template <int TERMS>
 static hipError_t launch_terms(const ConvArgs& a0, hipStream_t s) {
     ConvArgs a = a0;
     if (TERMS == 2) a.scale = a.scale_x;              // the fp16 pair's per-channel rescaled BN scale
+    if constexpr (TERMS == 2) {
+        hipError_t err = hipSuccess;
+        if (launch_taps_x6(a, s, &err)) return err;
+    }
     if constexpr (TERMS == 2) {   // YOLO's SiLU 1x1 convs (C2f cv1 / cv2, SPPF cv1) on the streaming form
         if (a.tune && a.tune->x6_stream_silu && a.act == VD_ACT_SILU && a.res_mode == VD_RES_NONE && a.kh == 1 &&
             a.kw == 1 && a.pad == 0 && a.kpad == a.cin_pad && !((a.ldx | a.xcoff | a.ldy | a.ycoff) & 7)) {

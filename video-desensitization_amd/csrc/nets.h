@@ -172,6 +172,7 @@ struct Ctx {
     hipEvent_t ev_half = nullptr;                // option face_groups: fork of the frame groups
     std::vector<hipStream_t> group_streams;      // option face_groups: streams of frame groups 1..G-1
     std::vector<hipEvent_t> group_events;        //   and their completion events (joined by the context stream)
+    std::vector<hipEvent_t> group_lag_events;    //   group g done with its first face_group_lag ops
     int fork_at = -1;                                // run_ops records ev_fork after this many face ops
     std::mutex mu;
     std::vector<void*> allocs;

@@ -782,15 +782,26 @@ int Ctx::face_forward(int n) {
         if (!ev_half) VD_CHECK_HIP(hipEventCreateWithFlags(&ev_half, hipEventDisableTiming));
         if (net.amax) VD_CHECK_HIP(hipMemsetAsync(net.amax, 0, net.amax_bytes, stream));
         VD_CHECK_HIP(hipEventRecord(ev_half, stream));
+        // option face_group_lag = L: group g starts once group g - 1 has finished its
+        // first L ops (0: all groups start together)
+        const int ne = (int)net.ops.size();
+        const int lag = std::min(std::max(tune.face_group_lag, 0), ne);
+        while ((int)group_lag_events.size() < G - 1) {
+            hipEvent_t ev;
+            VD_CHECK_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            group_lag_events.push_back(ev);
+        }
         hipStream_t main = stream;
         for (int g = 0; g < G; ++g) {
             const int f0 = (int)((long)n * g / G), f1 = (int)((long)n * (g + 1) / G);
             stream = g ? group_streams[g - 1] : main;
-            if (g) VD_CHECK_HIP(hipStreamWaitEvent(stream, ev_half, 0));
-            int rc = run_ops(net, 0, (int)net.ops.size(), f0, f1 - f0);
-            if (!rc && g) {
-                if (hipEventRecord(group_events[g - 1], stream) != hipSuccess) rc = vd_set_error(VD_ERR_HIP, "group event");
-            }
+            if (g) VD_CHECK_HIP(hipStreamWaitEvent(stream, lag ? group_lag_events[g - 1] : ev_half, 0));
+            int rc = run_ops(net, 0, lag, f0, f1 - f0);
+            if (!rc && lag && g + 1 < G && hipEventRecord(group_lag_events[g], stream) != hipSuccess)
+                rc = vd_set_error(VD_ERR_HIP, "group lag event");
+            if (!rc) rc = run_ops(net, lag, ne, f0, f1 - f0);
+            if (!rc && g && hipEventRecord(group_events[g - 1], stream) != hipSuccess)
+                rc = vd_set_error(VD_ERR_HIP, "group event");
             stream = main;
             if (rc) return rc;
         }
@@ -986,6 +997,7 @@ int vd_destroy(vd_ctx* h) {
         hipStreamDestroy(ctx->group_streams[g]);
         hipEventDestroy(ctx->group_events[g]);
     }
+    for (hipEvent_t ev : ctx->group_lag_events) hipEventDestroy(ev);
     hipStreamDestroy(ctx->stream2);
     hipStreamDestroy(ctx->own_stream);
     delete ctx;
@@ -1026,7 +1038,7 @@ int vd_set_option(vd_ctx* h, const char* name, int value) {
         {"plate_s2d", &VdTune::plate_s2d}, {"f32_split", &VdTune::f32_split},
         {"x6_small_k", &VdTune::x6_small_k}, {"x6_small_tiles", &VdTune::x6_small_tiles},
         {"x6_stream", &VdTune::x6_stream}, {"x6_small_k2", &VdTune::x6_small_k2}, {"x6_bn256", &VdTune::x6_bn256},
-        {"x6_exact", &VdTune::x6_exact}, {"x6_mid", &VdTune::x6_mid}, {"block_fuse32", &VdTune::block_fuse32}, {"x6_mf32", &VdTune::x6_mf32}, {"x6_tail", &VdTune::x6_tail}, {"x6_stream_silu", &VdTune::x6_stream_silu}, {"x6_slots", &VdTune::x6_slots}, {"x6_halo", &VdTune::x6_halo}, {"x6_halo_narrow", &VdTune::x6_halo_narrow}, {"x6_adepth", &VdTune::x6_adepth}, {"x6_gemm1x1", &VdTune::x6_gemm1x1}, {"x6_stream256", &VdTune::x6_stream256}, {"plate_stage", &VdTune::plate_stage}, {"ssh_side", &VdTune::ssh_side}, {"face_groups", &VdTune::face_groups}, {"plate_s2d32", &VdTune::plate_s2d32},
+        {"x6_exact", &VdTune::x6_exact}, {"x6_mid", &VdTune::x6_mid}, {"block_fuse32", &VdTune::block_fuse32}, {"x6_mf32", &VdTune::x6_mf32}, {"x6_tail", &VdTune::x6_tail}, {"x6_stream_silu", &VdTune::x6_stream_silu}, {"x6_slots", &VdTune::x6_slots}, {"x6_halo", &VdTune::x6_halo}, {"x6_halo_narrow", &VdTune::x6_halo_narrow}, {"x6_adepth", &VdTune::x6_adepth}, {"x6_gemm1x1", &VdTune::x6_gemm1x1}, {"x6_taps", &VdTune::x6_taps}, {"x6_stream256", &VdTune::x6_stream256}, {"plate_stage", &VdTune::plate_stage}, {"ssh_side", &VdTune::ssh_side}, {"face_groups", &VdTune::face_groups}, {"face_group_lag", &VdTune::face_group_lag}, {"plate_s2d32", &VdTune::plate_s2d32},
         {"jenc_gpu", &VdTune::jenc_gpu}, {"jdec_gpu", &VdTune::jdec_gpu}, {"jdec_chunk", &VdTune::jdec_chunk}, {"jdec_sync", &VdTune::jdec_sync}, {"jdec_group", &VdTune::jdec_group},
     };
     for (const Opt& o : opts)

@@ -79,6 +79,7 @@ struct VdTune {
     int plate_s2d32 = 1;      // fp32 plan: the plate stem on the fp16 space-to-depth canvas (with plate_s2d)
     int face_groups = 2;      // face net as G frame groups on G streams (the tails of one group's launches
                               //   fill with the others'; bit-identical; 0 / 1: one launch over the batch)
+    int face_group_lag = 0;   //   group g starts after group g - 1's first N ops (0: together)
     int plate_stage = 3;      // plate branch starts after face stage N (0: with the stem; 1-4: after
                               //   layerN; 5: after the whole face net). After layer3 its HBM-bound
                               //   convs overlap the MFMA-bound late face layers: 30.8 -> 30.0 ms/step
@@ -103,6 +104,7 @@ struct VdTune {
     int x6_halo_narrow = 1;   // ... also for Cout <= 64 (N tiles of 32 / 64)
     int x6_adepth = 2;        // A register sets of the 256 x {128, 64, 32} fp16-pair tiles (2 or 4; 4 measured level)
     int x6_slots = 0;         //   workgroup slots of one round (0: the CU count; tests force small values)
+    int x6_taps = 1;          // fp32 plan: narrow KxK YOLO layers (K <= 288) on the streaming TAPS form
     int x6_gemm1x1 = 1;       // fp16 pairs: GEMM 1x1 convs on the TR tiles (D^T accumulators, register epilogue;
                               //   2: also the streaming form's K <= 256 layers, 0: off)
     int x6_dbg = 0;           // experiments (tools/x6bench): 1 = no epilogue (WRONG results), 2 = runtime vmcnt waits
