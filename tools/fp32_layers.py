@@ -12,17 +12,21 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from conv_layers import face_plan  # noqa: E402
 
 
-def main(path, B=64, block=True):
+def main(path, B=64, block=True, chain=True):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     # fp32 plan: layer1 bottlenecks fused (block32.hip) unless option block_fuse32=0
-    plan = face_plan(B, fused=True, block=block, chain=False, ssh_fused=True, dual=(0,))
-    # the face stream: the stream with the most conv launches (73 per step vs the plate net's 60);
-    # its last len(plan) conv launches are the last step's layers
+    plan = face_plan(B, fused=True, block=block, chain=(0, 1, 2) if chain else (), ssh_fused=True, dual=(0,))
+    # the face streams run the fused stem / layer1 kernels (with face_groups both group
+    # streams do); the one with the latest launch is the context stream, which runs
+    # bench.py's instrumented pass (face_groups = 1) last: its last len(plan) conv
+    # launches are that pass's last step
     per = {}
     for r in rows:
-        if "conv" in r["Kernel_Name"] or "stem_pool" in r["Kernel_Name"] or "bottleneck" in r["Kernel_Name"]:
+        if "conv" in r["Kernel_Name"] or "stem_pool" in r["Kernel_Name"] or "bottleneck" in r["Kernel_Name"] \
+                or "chain" in r["Kernel_Name"]:
             per.setdefault(r["Stream_Id"], []).append(r)
-    convs = max(per.values(), key=len)[-len(plan):]
+    face = [v for v in per.values() if any("stem_pool" in r["Kernel_Name"] for r in v)] or list(per.values())
+    convs = max(face, key=lambda v: int(v[-1]["End_Timestamp"]))[-len(plan):]
     tot = fl_tot = 0
     for (name, M, N, K), r in zip(plan, convs):
         dt = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
@@ -36,4 +40,5 @@ def main(path, B=64, block=True):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 64, (sys.argv[3] != "0") if len(sys.argv) > 3 else True)
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 64, (sys.argv[3] != "0") if len(sys.argv) > 3 else True,
+         (sys.argv[4] != "0") if len(sys.argv) > 4 else True)

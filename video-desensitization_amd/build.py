@@ -23,7 +23,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("VD_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["conv.hip", "conv1x1.hip", "conv_big.hip", "pre.hip", "post.hip", "mosaic.hip", "block.hip", "block32.hip", "block.cpp",
-           "chain.hip", "stem.hip", "dwconv.hip", "conv_x6.hip", "jpeg.hip", "jpeg_dec.hip", "jpeg_host.cpp", "jpeg_enc.hip", "jpeg_enc.cpp", "runtime.cpp", "face_net.cpp", "plate_net.cpp", "record.cpp"]
+           "chain.hip", "chain32.hip", "stem.hip", "dwconv.hip", "conv_x6.hip", "jpeg.hip", "jpeg_dec.hip", "jpeg_host.cpp", "jpeg_enc.hip", "jpeg_enc.cpp", "runtime.cpp", "face_net.cpp", "plate_net.cpp", "record.cpp"]
 HEADERS = ["vd_common.h", "vd_math.h", "nets.h"]
 FLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-ffp-contract=off",
          "-Wall", "-Wno-unused-function", f"-I{os.path.join(ROOT, 'include')}"]

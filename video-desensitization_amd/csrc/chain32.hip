@@ -1,0 +1,330 @@
+// chain32.hip — fp32 plan: a layer2 bottleneck's conv3 and the NEXT bottleneck's
+// conv1 in one streaming pass (128 -> 512 -> 128 channels).
+//
+// torchvision Bottleneck [ext] as built from the reference's body.layer2.* weights
+// (detect_face/retinaface.py:53-60, IntermediateLayerGetter over resnet50), in the
+// arithmetic of the fp32 plan (conv_x6.hip: f32 activations, each product as three
+// fp16 MFMA products of power-of-two-scaled hi/lo pairs, f32 accumulation):
+//   y   = relu(bn3(conv3(t2)) + idt)        512 ch: this block's output (and the next
+//                                            block's identity), written once
+//   t1' = relu(bn1'(conv1'(y)))             128 ch: the next block's conv1
+// The two-launch plan writes y (840 MB per 64 frames at 80x80) and reads it straight
+// back for conv1'; here conv1' consumes it from registers.
+//
+// One persistent workgroup of 8 waves per CU walks super-groups of 128 pixels, wave w
+// taking 16 of them; weights stream through LDS in 8 chunks of 64 conv3 output channels
+// (the conv3 rows of the chunk + the conv1' columns that read them: 32 + 32 KB per
+// chunk, double-buffered by LDS-DMA with a source-side chunk swizzle):
+//   conv3    D^T = W3 . T2^T on 16x16x32 f16 MFMAs (A = weight rows from LDS, B = the
+//            wave's 16 pixels, split once per super-group with t2's per-frame scale, as
+//            the streaming 1x1 kernel does: y is bit-identical to the two-launch plan);
+//            BN + identity + ReLU, 16-B f32 stores of y, per-frame max |y|.
+//   conv1'   the lane's y values of conv3 blocks 2i, 2i+1 (channels 32i + 4q + e and
+//            32i + 16 + 4q + e of pixel p) are exactly the B fragment of conv1' k-step i
+//            once conv1's weights are packed with that K order inside each 32-channel step
+//            (Ctx::fuse_chains32). They are split with a per-(pixel, chunk) power of two
+//            from the pixel's chunk maximum (two lane shuffles); the pixel's running sum
+//            is kept at the current chunk's scale (re-based by an exact power-of-two
+//            multiply when the scale changes), so all of conv1's K accumulates in one
+//            chain as in the two-launch plan, only the split points differ: f32-level
+//            differences (tests/test_gpu_e2e.py), batch-invariant (nothing depends on
+//            the pixel's neighbours in the batch).
+// vmcnt counts LDS-DMA, loads and stores together in issue order; every wave issues the
+// same count of each per chunk (8 DMA, 4 identity loads, 4 y stores), so the waits are
+// fixed immediates.
+#include "vd_common.h"
+
+namespace {
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+constexpr int CM = 128, CO = 512;     // t2 / t1' channels, block output channels
+constexpr int NCH = 64;               // conv3 output channels per weight chunk
+constexpr int NCHUNK = CO / NCH;      // 8
+constexpr int W3B = NCH * 512;        // W3 chunk: 64 rows x (4 k-steps x 2 planes x 64 B)
+constexpr int W1B = CM * 256;         // W1 chunk: 128 rows x (2 k-steps x 2 planes x 64 B)
+constexpr int STAGE = W3B + W1B;      // 64 KB
+constexpr int LDS_FIXED = 2 * STAGE + (2 * CO + 2 * CM) * 4;
+
+// s_waitcnt vmcnt(N), expcnt / lgkmcnt left alone (gfx9 encoding)
+constexpr int vmcnt_imm(int n) { return (n & 15) | ((n >> 4) << 14) | 0x0F70; }
+
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// 8 f32 -> fp16 hi / lo planes of x * sa (conv_x6.hip split_pair8: the same roundings)
+__device__ __forceinline__ void split8(const float (&e)[8], float sa, u32x4& H, u32x4& L) {
+    unsigned hv[4], lv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        half2_t h, l;
+        h[0] = (_Float16)__builtin_fmaf(e[2 * j], sa, 0.f);
+        h[1] = (_Float16)__builtin_fmaf(e[2 * j + 1], sa, 0.f);
+        l[0] = (_Float16)__builtin_fmaf(e[2 * j], sa, -(float)h[0]);
+        l[1] = (_Float16)__builtin_fmaf(e[2 * j + 1], sa, -(float)h[1]);
+        hv[j] = __builtin_bit_cast(unsigned, h);
+        lv[j] = __builtin_bit_cast(unsigned, l);
+    }
+    H = u32x4{hv[0], hv[1], hv[2], hv[3]};
+    L = u32x4{lv[0], lv[1], lv[2], lv[3]};
+}
+
+// w_lo x_hi + w_hi x_lo + w_hi x_hi (conv_x6.hip mfma_terms<2>, small terms first)
+__device__ __forceinline__ f32x4_t mfma3(const u32x4& wh, const u32x4& wl, const u32x4& xh, const u32x4& xl,
+                                         f32x4_t acc) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, wl), __builtin_bit_cast(f16x8_t, xh), acc,
+                                                 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, wh), __builtin_bit_cast(f16x8_t, xl), acc,
+                                                 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, wh), __builtin_bit_cast(f16x8_t, xh), acc,
+                                                 0, 0, 0);
+    return acc;
+}
+
+// power-of-two exponent k with m * 2^k in [2^14, 2^15) (act_scale_exp's rule)
+__device__ __forceinline__ int pow2_exp(float m) {
+    if (!(m > 0.f) || !(m < 3.0e38f)) return 0;
+    int e;
+    (void)frexpf(m, &e);
+    const int k = 15 - e;
+    return k < -100 ? -100 : (k > 100 ? 100 : k);
+}
+
+__global__ __launch_bounds__(512, 1) void chain32_kernel(Chain32Args a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* s_sc3 = (float*)(smem + 2 * STAGE);
+    float* s_sh3 = s_sc3 + CO;
+    float* s_sc1 = s_sh3 + CO;
+    float* s_sh1 = s_sc1 + CM;
+    unsigned* s_ymax = (unsigned*)(s_sh1 + CM);            // [B] then [B]
+    unsigned* s_y2max = s_ymax + a.B;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int p = lane & 15, q = lane >> 4;
+    const int nsg = (a.M + 127) / 128;
+    const int G = gridDim.x, sg0 = blockIdx.x;
+    if (sg0 >= nsg) return;                                 // uniform over the workgroup
+    const int nmine = (nsg - sg0 + G - 1) / G;
+
+    for (int i = tid; i < CO; i += 512) { s_sc3[i] = a.sc3[i]; s_sh3[i] = a.sh3[i]; }
+    for (int i = tid; i < CM; i += 512) { s_sc1[i] = a.sc1[i]; s_sh1[i] = a.sh1[i]; }
+    for (int f = tid; f < 2 * a.B; f += 512) s_ymax[f] = 0u;
+
+    const __amdgpu_buffer_rsrc_t rw3 = __builtin_amdgcn_make_buffer_rsrc((void*)a.w3, 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw1 = __builtin_amdgcn_make_buffer_rsrc((void*)a.w1, 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)a.t2, 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc((void*)a.res, 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t ry =
+        __builtin_amdgcn_make_buffer_rsrc(a.y, 0, (int)((long)a.M * a.ld_y * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t ry2 =
+        __builtin_amdgcn_make_buffer_rsrc(a.y2, 0, (int)((long)a.M * a.ld_y2 * 4), 0x00020000);
+
+    // DMA of weight chunk c into stage st: 64 instructions of 1 KB, wave w issues 8 of
+    // them (waves 0-3: the W3 rows 64c .. 64c+63, two 512-B rows per instruction; waves
+    // 4-7: the 256-B slice [256c, 256c + 256) of each of the 128 W1 rows, four per
+    // instruction). LDS position pos of a row holds logical 16-B chunk pos ^ (row & 15).
+    auto dma = [&](int c, int st) {
+        char* base = smem + st * STAGE;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int k = w * 8 + u;
+            if (k < 32) {
+                const int r = 2 * k + (lane >> 5), ci = (lane & 31) ^ (r & 15);
+                const unsigned off = (unsigned)(((64 * c + r) * 32 + ci) * 16);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rw3, (lds_void_t*)(base + k * 1024), 16, off, 0, 0, 0);
+            } else {
+                const int kk = k - 32;
+                const int r = 4 * kk + (lane >> 4), ci = (lane & 15) ^ (r & 15);
+                const unsigned off = (unsigned)(r * 2048 + c * 256 + ci * 16);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rw1, (lds_void_t*)(base + W3B + kk * 1024), 16, off, 0, 0, 0);
+            }
+        }
+    };
+    // this lane's pixel of wave group g (clamped; stores past M are dropped by ry / ry2)
+    auto pixel = [&](int g) {
+        const int m = g * 16 + p;
+        return m < a.M ? m : a.M - 1;
+    };
+    auto load_x = [&](int g, u32x4 (&xr)[4][2]) {
+        const unsigned base = (unsigned)(pixel(g) * a.ld_t2 + 8 * q) * 4u;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            xr[s][0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(base + 128u * s), 0, 0));
+            xr[s][1] =
+                __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(base + 128u * s + 16u), 0, 0));
+        }
+    };
+    // identity of chunk c: channels 64c + 16j + 4q .. +3, j = 0..3
+    auto load_idt = [&](int g, int c, u32x4 (&r)[4]) {
+        const unsigned base = (unsigned)(pixel(g) * a.ld_res + 64 * c + 4 * q) * 4u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            r[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, (int)(base + 64u * j), 0, 0));
+    };
+
+    int g = sg0 * 8 + w;
+    u32x4 xr[4][2], idt[2][4];
+    dma(0, 0);
+    load_idt(g, 0, idt[0]);
+    load_x(g, xr);
+#pragma unroll 1
+    for (int it = 0; it < nmine; ++it) {
+        const int gn = it + 1 < nmine ? (sg0 + (it + 1) * G) * 8 + w : g;   // next super-group's group
+        __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));          // x, identity(0), weight chunk 0
+        const int m = g * 16 + p;
+        const bool ok = m < a.M;
+        const int fb = (ok ? m : a.M - 1) / a.hw;           // this lane's pixel's frame
+        const float mx = a.xmax ? __uint_as_float(a.xmax[fb]) : a.xbound;
+        const int kx = pow2_exp(mx);
+        const float sa = __builtin_ldexpf(1.f, kx), inv_sa = __builtin_ldexpf(1.f, -kx);
+        u32x4 xb[4][2];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            float e8[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) e8[e] = __uint_as_float(xr[s][e >> 2][e & 3]);
+            split8(e8, sa, xb[s][0], xb[s][1]);
+        }
+        f32x4_t acc1[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc1[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        float vmax_y = 0.f;
+        int ks = 0;                                         // scale exponent of acc1
+#pragma unroll 1
+        for (int cp = 0; cp < NCHUNK / 2; ++cp)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int c = 2 * cp + h, st = h;   // chunk c in stage c & 1
+            if (c > 0) __builtin_amdgcn_s_waitcnt(vmcnt_imm(8));   // chunk c landed (younger: identity(c), y(c-1))
+            lds_barrier();                                  // every wave's DMA of chunk c landed; stage st^1 free
+            dma((c + 1) & 7, st ^ 1);
+            load_idt(c == 7 ? gn : g, (c + 1) & 7, idt[h ^ 1]);
+            const char* w3s = smem + st * STAGE;
+            const char* w1s = w3s + W3B;
+            // ---- conv3, channels 64c .. 64c+63 of the 16 pixels ----
+            f32x4_t acc3[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc3[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const char* row = w3s + (16 * j + p) * 512;
+                    const u32x4 wh = *(const u32x4*)(row + ((((2 * s) * 4 + q) ^ p) << 4));
+                    const u32x4 wl = *(const u32x4*)(row + ((((2 * s + 1) * 4 + q) ^ p) << 4));
+                    acc3[j] = mfma3(wh, wl, xb[s][0], xb[s][1], acc3[j]);
+                }
+            }
+            // ---- epilogue: bn3 + identity + relu, store y, split for conv1' ----
+            __builtin_amdgcn_s_waitcnt(vmcnt_imm(16));      // identity(c) (younger: y(c-1), DMA(c+1), identity(c+1))
+            float yv[4][4];
+            float cmax = 0.f;
+            const unsigned ybase = ok ? (unsigned)(m * a.ld_y + 64 * c + 4 * q) * 4u : 0x80000000u;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int ch = 64 * c + 16 * j + 4 * q;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float v = (acc3[j][e] * inv_sa) * s_sc3[ch + e] + s_sh3[ch + e];
+                    float t = v + __uint_as_float(idt[h][j][e]);
+                    t = t > 0.f ? t : 0.f;
+                    yv[j][e] = t;
+                    cmax = fmaxf(cmax, t);
+                }
+                __builtin_amdgcn_raw_buffer_store_b128(
+                    __builtin_bit_cast(u32x4, f32x4_t{yv[j][0], yv[j][1], yv[j][2], yv[j][3]}), ry,
+                    (int)(ybase + (ok ? 64u * j : 0u)), 0, 0);
+            }
+            vmax_y = fmaxf(vmax_y, cmax);
+            cmax = fmaxf(cmax, __shfl_xor(cmax, 16));
+            cmax = fmaxf(cmax, __shfl_xor(cmax, 32));       // the pixel's max over the chunk's 64 channels
+            // the pixel's conv1' sum runs at scale 2^ks: re-based exactly (a power of two)
+            // when this chunk's split scale differs; an all-zero chunk keeps the scale
+            const int ky = cmax > 0.f ? pow2_exp(cmax) : ks;
+            const float rebase = __builtin_ldexpf(1.f, ky - ks);
+            ks = ky;
+            const float sy = __builtin_ldexpf(1.f, ky);
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) acc1[j][e] *= rebase;
+            u32x4 yb[2][2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const float e8[8] = {yv[2 * i][0], yv[2 * i][1], yv[2 * i][2], yv[2 * i][3],
+                                     yv[2 * i + 1][0], yv[2 * i + 1][1], yv[2 * i + 1][2], yv[2 * i + 1][3]};
+                split8(e8, sy, yb[i][0], yb[i][1]);
+            }
+            // ---- conv1' over the chunk's 64 input channels, into the running sum ----
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const char* row = w1s + (16 * j + p) * 256;
+                    const u32x4 wh = *(const u32x4*)(row + ((((2 * i) * 4 + q) ^ p) << 4));
+                    const u32x4 wl = *(const u32x4*)(row + ((((2 * i + 1) * 4 + q) ^ p) << 4));
+                    acc1[j] = mfma3(wh, wl, yb[i][0], yb[i][1], acc1[j]);
+                }
+            }
+        }
+        const float inv_s1 = __builtin_ldexpf(1.f, -ks);
+        // ---- conv1' epilogue: bn1' + relu, t1' stores ----
+        float vmax_t = 0.f;
+        const unsigned y2base = ok ? (unsigned)(m * a.ld_y2 + 4 * q) * 4u : 0x80000000u;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float o[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int ch = 16 * j + 4 * q + e;
+                const float t = (acc1[j][e] * inv_s1) * s_sc1[ch] + s_sh1[ch];
+                o[e] = t > 0.f ? t : 0.f;
+                vmax_t = fmaxf(vmax_t, o[e]);
+            }
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f32x4_t{o[0], o[1], o[2], o[3]}), ry2,
+                                                   (int)(y2base + (ok ? 64u * j : 0u)), 0, 0);
+        }
+        amax_lds_add(s_ymax, ok ? fb : -1, vmax_y);
+        amax_lds_add(s_y2max, ok ? fb : -1, vmax_t);
+        g = gn;
+        load_x(g, xr);
+    }
+    __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));               // trailing DMA / loads land before the workgroup exits
+    __syncthreads();
+    if (a.ymax) amax_lds_flush(s_ymax, a.ymax, a.B);
+    if (a.y2max) amax_lds_flush(s_y2max, a.y2max, a.B);
+}
+
+}  // namespace
+
+// Eligible: the layer2 shape (128 -> 512 -> 128) with dense rows, fp16-pair weights,
+// frames within the LDS max slots, byte offsets within 2^31.
+bool vd_chain32_ok(int cmid, int cout, int kpad3, int kpad1, int ld_t2, int ld_res, int ld_y, int ld_y2, long M,
+                   int frames) {
+    if (cmid != CM || cout != CO || kpad3 != CM || kpad1 != CO) return false;
+    if (ld_t2 != CM || ld_res != CO || ld_y != CO || ld_y2 != CM) return false;
+    return M > 0 && M * CO * 4 < 0x7fffffffL && frames > 0 && frames <= 1024;
+}
+
+hipError_t vd_launch_chain32(const Chain32Args& a, hipStream_t s) {
+    if (a.M <= 0) return hipSuccess;
+    if (a.B <= 0 || a.B > 1024 || a.hw <= 0) return hipErrorInvalidValue;
+    static const int cus = [] {
+        (void)hipFuncSetAttribute((const void*)chain32_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  LDS_FIXED + 8 * 1024);
+        int dev = 0, n = 256;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        return n > 0 ? n : 256;
+    }();
+    const int nsg = (a.M + 127) / 128;
+    const int grid = nsg < cus ? nsg : cus;                 // persistent: one workgroup per CU
+    hipLaunchKernelGGL(chain32_kernel, dim3(grid), dim3(512), LDS_FIXED + 8 * a.B, s, a);
+    return hipGetLastError();
+}

@@ -36,6 +36,7 @@ struct Conv {
     void* w = nullptr;
     void* wx3 = nullptr;       // fp32 + f32_split: [npad][kpad/32][3][32] bf16 / [..][2][32] fp16 planes (conv_x6.hip)
     float* scale_x = nullptr;  // fp16 pairs: BN scale times the row's 2^-e
+    void* wx3_chain = nullptr; // fp16 pairs as chain32.hip's conv1': K permuted inside each 32-step
     int split = 0;             // fp32: VdTune::f32_split when the weights were packed
     float* scale = nullptr;
     float* shift = nullptr;
@@ -249,6 +250,8 @@ struct Ctx {
     int run_conv_op(const Op& op, int f0, int n, int fam = 0);
     int run_ops(const Net& net, int b, int e, int f0, int n);
     int face_lanes(const int (&fpn)[5], const int (&ssh_b)[3], const int (&ssh_e)[3]);
+    int chain32_weights(Conv& c1);
+    void fuse_chains32(Net& net, size_t begin);
     int run_net(const Net& net, int n, int mb = 0, int split = 0);
     const uint8_t* frames_to_device(const uint8_t* frames, int n, int h, size_t pitch, int where, int* rc);
     int check_frames(int n, int h, int w, size_t pitch);

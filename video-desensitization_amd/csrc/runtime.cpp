@@ -473,6 +473,26 @@ int Ctx::run_conv_op(const Op& op, int f0, int n, int fam) {
 int Ctx::run_chain_op(const Op& op, int f0, int n, int fam) {
     const Conv& c3 = convs[op.conv];
     const Conv& c1 = convs[op.conv2];
+    if (f32) {   // fp16-pair plan (chain32.hip)
+        Chain32Args a{};
+        a.t2 = foff(op.x, f0); a.ld_t2 = op.x.c;
+        a.res = foff(op.r, f0); a.ld_res = op.r.c;
+        a.w3 = c3.wx3; a.w1 = c1.wx3_chain;
+        a.sc3 = c3.scale_x; a.sh3 = c3.shift; a.sc1 = c1.scale_x; a.sh1 = c1.shift;
+        a.y = (void*)foff(op.y, f0); a.ld_y = op.y.c;
+        a.y2 = (void*)foff(op.y2, f0); a.ld_y2 = op.y2.c;
+        a.hw = op.y.h * op.y.w;
+        a.M = n * a.hw;
+        a.B = n;
+        a.xmax = op.x.amax ? op.x.amax + f0 : nullptr; a.xbound = op.x.bound;
+        a.ymax = op.y.amax ? op.y.amax + f0 : nullptr;
+        a.y2max = op.y2.amax ? op.y2.amax + f0 : nullptr;
+        t_begin(fam, (c3.flops_per_px + c1.flops_per_px) * a.M);
+        hipError_t e = vd_launch_chain32(a, stream);
+        t_end();
+        if (e != hipSuccess) return vd_set_error(VD_ERR_HIP, "chain32 launch: %s", hipGetErrorString(e));
+        return VD_OK;
+    }
     ChainArgs a{};
     a.t2 = foff(op.x, f0); a.ld_t2 = op.x.c;
     a.res = foff(op.r, f0); a.ld_res = op.r.c;
@@ -492,8 +512,32 @@ int Ctx::run_chain_op(const Op& op, int f0, int n, int fam) {
 // Peephole over ops [begin, end) of a bf16 / fp16 plan: a bottleneck conv3 (1x1, + identity
 // before the ReLU) immediately followed by a 1x1 conv that reads exactly its output
 // (the next bottleneck's conv1) becomes one OP_CHAIN where chain.hip covers the shape.
+// fp32 plan (chain32.hip): the same peephole on the layer2 shape with fp16-pair weights;
+// conv1's planes are copied with K permuted inside each 32-channel step (position 8q + e
+// <- channel 4q + e, 8q + 4 + e <- 16 + 4q + e) so conv3's accumulator lanes are its B
+// fragments.
+int Ctx::chain32_weights(Conv& c1) {
+    if (c1.wx3_chain) return VD_OK;
+    const size_t rows = (size_t)c1.npad, nk = (size_t)c1.kpad / 32, bytes = rows * nk * 2 * 64;
+    std::vector<uint16_t> src(bytes / 2), dst(bytes / 2);
+    VD_CHECK_HIP(hipMemcpy(src.data(), c1.wx3, bytes, hipMemcpyDeviceToHost));
+    for (size_t blk = 0; blk < rows * nk * 2; ++blk)       // one 32-entry plane of one k-step of one row
+        for (int qq = 0; qq < 4; ++qq)
+            for (int e = 0; e < 4; ++e) {
+                dst[blk * 32 + 8 * qq + e] = src[blk * 32 + 4 * qq + e];
+                dst[blk * 32 + 8 * qq + 4 + e] = src[blk * 32 + 16 + 4 * qq + e];
+            }
+    int rc = dalloc(&c1.wx3_chain, bytes);
+    if (rc) return rc;
+    VD_CHECK_HIP(hipMemcpy(c1.wx3_chain, dst.data(), bytes, hipMemcpyHostToDevice));
+    return VD_OK;
+}
+
 void Ctx::fuse_chains(Net& net, size_t begin) {
-    if (f32) return;
+    if (f32) {
+        fuse_chains32(net, begin);
+        return;
+    }
     std::vector<Op> out(net.ops.begin(), net.ops.begin() + begin);
     for (size_t i = begin; i < net.ops.size(); ++i) {
         const Op& a = net.ops[i];
@@ -509,6 +553,40 @@ void Ctx::fuse_chains(Net& net, size_t begin) {
                                c1.cin_pad == c3.cout && a.r.h == a.y.h && a.r.w == a.y.w;
             const long M = (long)cfg.max_batch * a.y.h * a.y.w;
             if (shape && tune.chain && vd_chain_ok(c3.cin_pad, c3.cout, c3.kpad, c1.kpad, a.x.c, a.r.c, a.y.c, b.y.c, M)) {
+                Op op = a;
+                op.kind = OP_CHAIN;
+                op.conv2 = b.conv;
+                op.y2 = b.y;
+                out.push_back(op);
+                ++i;
+                continue;
+            }
+        }
+        out.push_back(a);
+    }
+    net.ops.swap(out);
+}
+
+void Ctx::fuse_chains32(Net& net, size_t begin) {
+    if (!tune.chain) return;
+    std::vector<Op> out(net.ops.begin(), net.ops.begin() + begin);
+    for (size_t i = begin; i < net.ops.size(); ++i) {
+        const Op& a = net.ops[i];
+        if (i + 1 < net.ops.size() && a.kind == OP_CONV && net.ops[i + 1].kind == OP_CONV && a.conv2 < 0) {
+            const Op& b = net.ops[i + 1];
+            const Conv& c3 = convs[a.conv];
+            Conv& c1 = convs[b.conv];
+            const bool shape = c3.kh == 1 && c3.kw == 1 && c3.stride == 1 && c3.pad == 0 && c3.act == VD_ACT_RELU &&
+                               c1.kh == 1 && c1.kw == 1 && c1.stride == 1 && c1.pad == 0 && c1.act == VD_ACT_RELU &&
+                               c3.split == 2 && c1.split == 2 && c3.wx3 && c1.wx3 && c3.scale_x && c1.scale_x &&
+                               a.r.p && a.rmode == VD_RES_PRE_ACT && !a.rup && a.rcoff == 0 && a.xcoff == 0 &&
+                               a.ycoff == 0 && b.conv2 < 0 && !b.r.p && b.x.p == a.y.p && b.xcoff == 0 &&
+                               b.ycoff == 0 && a.x.f32 && a.y.f32 && b.y.f32 && a.r.f32 && c3.cin_pad == a.x.c &&
+                               c1.cin_pad == c3.cout && a.r.h == a.y.h && a.r.w == a.y.w;
+            const long M = (long)cfg.max_batch * a.y.h * a.y.w;
+            if (shape && vd_chain32_ok(c3.cin_pad, c3.cout, c3.kpad, c1.kpad, a.x.c, a.r.c, a.y.c, b.y.c, M,
+                                       cfg.max_batch) &&
+                chain32_weights(c1) == VD_OK) {
                 Op op = a;
                 op.kind = OP_CHAIN;
                 op.conv2 = b.conv;

@@ -199,6 +199,22 @@ struct ChainArgs {
     int f16;                              // fp16 plan: fp16 operands / activations (else bf16)
 };
 
+// fp32 plan (chain32.hip): layer2 conv3 (+ identity, ReLU) and the next conv1 in one pass,
+// fp16-pair weights: y = relu(bn3(w3 . t2) + res) [M][512], y2 = relu(bn1'(w1 . y)) [M][128].
+struct Chain32Args {
+    const void* t2; int ld_t2;            // [M][128] f32
+    const void* res; int ld_res;          // identity [M][512] f32
+    const void* w3;                       // conv3 planes [>= 512][4 k-steps][2][32] fp16 (conv_x6 wx3)
+    const void* w1;                       // next conv1 planes [>= 128][16][2][32], K permuted per 32-step
+    const float* sc3; const float* sh3;   // bn3 (scale times the row's 2^-e)
+    const float* sc1; const float* sh1;   // next bn1
+    void* y; int ld_y;                    // block output [M][512]
+    void* y2; int ld_y2;                  // next block's t1 [M][128]
+    int M, B, hw;                         // pixels, frames, pixels per frame
+    const unsigned* xmax; float xbound;   // t2's per-frame max |x| slots (frame 0 of this call)
+    unsigned* ymax; unsigned* y2max;      // y's / y2's slots (atomic max)
+};
+
 // Depthwise 3x3 conv (pad 1) + BN + activation, NHWC (dwconv.hip): MobileNetV1 conv_dw.
 struct DwConvArgs {
     const void* x; int xh, xw, ldx, xcoff;
@@ -454,6 +470,9 @@ hipError_t vd_launch_stem_pool32(const StemPoolArgs& a, hipStream_t s);   // fp1
 hipError_t vd_launch_block(const BlockArgs& a, hipStream_t s);
 bool vd_chain_ok(int cmid, int cout, int kpad3, int kpad1, int ld_t2, int ld_res, int ld_y, int ld_y2, long M);
 hipError_t vd_launch_chain(const ChainArgs& a, hipStream_t s);
+bool vd_chain32_ok(int cmid, int cout, int kpad3, int kpad1, int ld_t2, int ld_res, int ld_y, int ld_y2, long M,
+                   int frames);
+hipError_t vd_launch_chain32(const Chain32Args& a, hipStream_t s);
 hipError_t vd_launch_letterbox(const LetterboxArgs& a, hipStream_t s);
 bool vd_letterbox_pair_ok(const LetterboxArgs& a, const LetterboxArgs& b);
 hipError_t vd_launch_letterbox_pair(const LetterboxArgs& a, const LetterboxArgs& b, hipStream_t s);
