@@ -361,17 +361,19 @@ def test_heads_fp32_fused_layer1_matches_unfused(gpu):
         np.testing.assert_array_equal(a, b)
 
 
-def test_heads_fp32_chain_matches_unfused(gpu):
+@pytest.mark.parametrize("chain", [2, 1])
+def test_heads_fp32_chain_matches_unfused(gpu, chain):
     """fp32 plan, default: layer2's conv3 (+bn3 + identity + relu) and the next block's
     conv1 (+bn1 + relu) as one kernel (chain32.hip: the block output goes to HBM once
     and reaches conv1 from registers, split per (pixel, 64-channel chunk)); option
     chain=0 keeps the two launches (per-frame split). The block outputs are the same;
     conv1's products are rounded at other points: heads within f32 rounding of each
-    other, identical boxes."""
+    other, identical boxes. chain=2 (default): layer2's three pairs; chain=1 also layer3's
+    five (chain32.hip's 256 -> 1024 -> 256 shape)."""
     import vdmi
     fr = _frames(3, 1080, 1920, seed=37)
     heads, boxes = {}, {}
-    for ch in (1, 0):
+    for ch in (chain, 0):
         ctx = vdmi.Context(precision="fp32", max_batch=3, options={"chain": ch})
         try:
             ctx.load_weights(0, face_weights("default"))
@@ -380,10 +382,10 @@ def test_heads_fp32_chain_matches_unfused(gpu):
             boxes[ch] = [r.frame(b)[0].copy() for b in range(3)]
         finally:
             ctx.close()
-    for a, b in zip(heads[1], heads[0]):
+    for a, b in zip(heads[chain], heads[0]):
         assert np.abs(a - b).max() <= 6e-6 * (np.abs(b).max() + 1e-6), np.abs(a - b).max() / np.abs(b).max()
     assert sum(len(x) for x in boxes[0]) > 0
-    for a, b in zip(boxes[1], boxes[0]):
+    for a, b in zip(boxes[chain], boxes[0]):
         np.testing.assert_array_equal(a, b)
 
 

@@ -17,12 +17,16 @@ def face_plan(B=64, H=640, W=640, fused=True, block=True, chain=True, ssh_fused=
     three layer1 bottlenecks are one launch each (block.hip), K = their summed
     reduction depth per output channel of 256 (same FLOPs); with `chain`
     layer2.1/2.2's conv3 runs with the next block's conv1 (chain.hip, N=512 K=256
-    carries both layers' FLOPs; a tuple names the blocks bi whose conv3 chains with
-    block bi+1's conv1: the fp32 plan's chain32.hip takes (0, 1, 2)); with `ssh_fused` each SSH's conv5X5_1 and conv3X3
+    carries both layers' FLOPs; a tuple names the layer2 blocks bi whose conv3 chains with
+    block bi+1's conv1, a dict {layer index: blocks} any layer's: the fp32 plan's chain32.hip
+    takes {1: (0, 1, 2), 2: (0, 1, 2, 3, 4)}); with `ssh_fused` each SSH's conv5X5_1 and conv3X3
     are one 192-channel conv; `dual`: the layers whose block 0 runs conv3 + downsample
     as one launch (bf16: layer1/2; fp32: layer1)."""
     L = []
-    chained = tuple(chain) if isinstance(chain, (tuple, list)) else ((1, 2) if chain else ())
+    if isinstance(chain, dict):          # {layer index: blocks whose conv3 chains with the next conv1}
+        chained = {li: tuple(v) for li, v in chain.items()}
+    else:
+        chained = {1: tuple(chain) if isinstance(chain, (tuple, list)) else ((1, 2) if chain else ())}
     h, w = H // 2, W // 2
     L.append(("stem7x7", B * h * w, 64, 3 * 49))
     h, w = h // 2, w // 2
@@ -35,7 +39,7 @@ def face_plan(B=64, H=640, W=640, fused=True, block=True, chain=True, ssh_fused=
                 L.append((f"l1.{bi}.block", B * h * w, 256, k))
                 cin = planes * 4
                 continue
-            if li == 1 and bi - 1 in chained:
+            if bi - 1 in chained.get(li, ()):
                 pass                            # ran inside the previous block's chain launch
             else:
                 L.append((f"l{li+1}.{bi}.c1", B * h * w, planes, cin))
@@ -46,8 +50,8 @@ def face_plan(B=64, H=640, W=640, fused=True, block=True, chain=True, ssh_fused=
             else:
                 if bi == 0:
                     L.append((f"l{li+1}.{bi}.ds", B * oh * ow, planes * 4, cin))
-                if li == 1 and bi in chained:
-                    L.append((f"l2.{bi}.c3+l2.{bi+1}.c1", B * oh * ow, planes * 4, 2 * planes))
+                if bi in chained.get(li, ()):
+                    L.append((f"l{li+1}.{bi}.c3+c1", B * oh * ow, planes * 4, 2 * planes))
                 else:
                     L.append((f"l{li+1}.{bi}.c3", B * oh * ow, planes * 4, planes))
             cin = planes * 4

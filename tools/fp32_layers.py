@@ -12,10 +12,10 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from conv_layers import face_plan  # noqa: E402
 
 
-def main(path, B=64, block=True, chain=True):
+def main(path, B=64, block=True, chain=2):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     # fp32 plan: layer1 bottlenecks fused (block32.hip) unless option block_fuse32=0
-    plan = face_plan(B, fused=True, block=block, chain=(0, 1, 2) if chain else (), ssh_fused=True, dual=(0,))
+    plan = face_plan(B, fused=True, block=block, chain={1: (0, 1, 2), 2: (0, 1, 2, 3, 4)} if chain == 1 else ({1: (0, 1, 2)} if chain == 2 else {}), ssh_fused=True, dual=(0,))
     # the face streams run the fused stem / layer1 kernels (with face_groups both group
     # streams do); the one with the latest launch is the context stream, which runs
     # bench.py's instrumented pass (face_groups = 1) last: its last len(plan) conv
@@ -41,4 +41,4 @@ def main(path, B=64, block=True, chain=True):
 
 if __name__ == "__main__":
     main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 64, (sys.argv[3] != "0") if len(sys.argv) > 3 else True,
-         (sys.argv[4] != "0") if len(sys.argv) > 4 else True)
+         int(sys.argv[4]) if len(sys.argv) > 4 else 2)   # the plan's option chain (fp32: 2 = layer2 chains)

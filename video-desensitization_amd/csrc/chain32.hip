@@ -40,13 +40,27 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-constexpr int CM = 128, CO = 512;     // t2 / t1' channels, block output channels
-constexpr int NCH = 64;               // conv3 output channels per weight chunk
-constexpr int NCHUNK = CO / NCH;      // 8
-constexpr int W3B = NCH * 512;        // W3 chunk: 64 rows x (4 k-steps x 2 planes x 64 B)
-constexpr int W1B = CM * 256;         // W1 chunk: 128 rows x (2 k-steps x 2 planes x 64 B)
-constexpr int STAGE = W3B + W1B;      // 64 KB
-constexpr int LDS_FIXED = 2 * STAGE + (2 * CO + 2 * CM) * 4;
+// Shapes: layer2 (t2 128 -> y 512 -> t1' 128; weight chunks of 64 conv3 channels) and
+// layer3 (256 -> 1024 -> 256; chunks of 32). Either way a chunk is 32 KB of W3 rows and
+// 32 KB of W1 columns, and a wave runs 48 + 48 MFMAs on it.
+template <int CM_, int CO_, int NCH_, int GPW_> struct ChainShape {
+    static constexpr int CM = CM_, CO = CO_, NCH = NCH_;
+    static constexpr int GPW = GPW_;             // 16-pixel groups per wave (8 groups per super-group)
+    static constexpr int THREADS = 64 * 8 / GPW; // 8 or 4 waves
+    static constexpr int ND = 64 / (8 / GPW);    // weight DMA instructions per wave per chunk
+    static constexpr int KS3 = CM / 32;          // conv3 k-steps
+    static constexpr int T3 = NCH / 16;          // conv3 tiles per chunk
+    static constexpr int KC = NCH / 32;          // conv1' k-steps per chunk
+    static constexpr int T1 = CM / 16;           // conv1' output tiles
+    static constexpr int NCHUNK = CO / NCH;
+    static constexpr int RB3 = KS3 * 128;        // W3 row bytes (k-steps x 2 planes x 64 B)
+    static constexpr int RB1 = KC * 128;         // W1 row slice bytes of one chunk
+    static constexpr int W3B = NCH * RB3, W1B = CM * RB1, STAGE = W3B + W1B;
+    static constexpr int LDS = 2 * STAGE + (2 * CO + 2 * CM) * 4;
+    static_assert(W3B == 32768 && W1B == 32768, "64-KB stages");
+};
+using L2Shape = ChainShape<128, 512, 64, 1>;    // 8 waves, 2 per SIMD
+using L3Shape = ChainShape<256, 1024, 32, 1>;
 
 // s_waitcnt vmcnt(N), expcnt / lgkmcnt left alone (gfx9 encoding)
 constexpr int vmcnt_imm(int n) { return (n & 15) | ((n >> 4) << 14) | 0x0F70; }
@@ -95,7 +109,14 @@ __device__ __forceinline__ int pow2_exp(float m) {
     return k < -100 ? -100 : (k > 100 ? 100 : k);
 }
 
-__global__ __launch_bounds__(512, 1) void chain32_kernel(Chain32Args a) {
+template <class S>
+__global__ __launch_bounds__(S::THREADS, 1) void chain32_kernel(Chain32Args a) {
+    constexpr int CM = S::CM, CO = S::CO, NCH = S::NCH, KS3 = S::KS3, T3 = S::T3, KC = S::KC, T1 = S::T1;
+    constexpr int NCHUNK = S::NCHUNK, RB3 = S::RB3, RB1 = S::RB1, W3B = S::W3B, STAGE = S::STAGE;
+    constexpr int GPW = S::GPW, NT = S::THREADS, ND = S::ND;
+    // LDS row -> swizzle key: 16-B chunk ci of a row sits at ci ^ key (conflict-free
+    // fragment reads of 16 consecutive rows; rows of 128 B pair up in a 256-B bank line)
+    constexpr int R1PL = 256 / (RB1 < 256 ? RB1 : 256), C1 = RB1 / 16;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     float* s_sc3 = (float*)(smem + 2 * STAGE);
     float* s_sh3 = s_sc3 + CO;
@@ -112,9 +133,9 @@ __global__ __launch_bounds__(512, 1) void chain32_kernel(Chain32Args a) {
     if (sg0 >= nsg) return;                                 // uniform over the workgroup
     const int nmine = (nsg - sg0 + G - 1) / G;
 
-    for (int i = tid; i < CO; i += 512) { s_sc3[i] = a.sc3[i]; s_sh3[i] = a.sh3[i]; }
-    for (int i = tid; i < CM; i += 512) { s_sc1[i] = a.sc1[i]; s_sh1[i] = a.sh1[i]; }
-    for (int f = tid; f < 2 * a.B; f += 512) s_ymax[f] = 0u;
+    for (int i = tid; i < CO; i += NT) { s_sc3[i] = a.sc3[i]; s_sh3[i] = a.sh3[i]; }
+    for (int i = tid; i < CM; i += NT) { s_sc1[i] = a.sc1[i]; s_sh1[i] = a.sh1[i]; }
+    for (int f = tid; f < 2 * a.B; f += NT) s_ymax[f] = 0u;
 
     const __amdgpu_buffer_rsrc_t rw3 = __builtin_amdgcn_make_buffer_rsrc((void*)a.w3, 0, 0x7fffffff, 0x00020000);
     const __amdgpu_buffer_rsrc_t rw1 = __builtin_amdgcn_make_buffer_rsrc((void*)a.w1, 0, 0x7fffffff, 0x00020000);
@@ -125,175 +146,217 @@ __global__ __launch_bounds__(512, 1) void chain32_kernel(Chain32Args a) {
     const __amdgpu_buffer_rsrc_t ry2 =
         __builtin_amdgcn_make_buffer_rsrc(a.y2, 0, (int)((long)a.M * a.ld_y2 * 4), 0x00020000);
 
-    // DMA of weight chunk c into stage st: 64 instructions of 1 KB, wave w issues 8 of
-    // them (waves 0-3: the W3 rows 64c .. 64c+63, two 512-B rows per instruction; waves
-    // 4-7: the 256-B slice [256c, 256c + 256) of each of the 128 W1 rows, four per
-    // instruction). LDS position pos of a row holds logical 16-B chunk pos ^ (row & 15).
+    // DMA of weight chunk c into stage st: 64 instructions of 1 KB, ND per wave
+    // (instructions 0-31: the chunk's W3 rows NCH c .. +NCH; 32-63: the RB1-byte slice
+    // [RB1 c, RB1 (c + 1)) of each of the CM W1 rows). LDS position pos of a row holds
+    // logical 16-B chunk pos ^ key(row).
     auto dma = [&](int c, int st) {
         char* base = smem + st * STAGE;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int k = w * 8 + u;
+        for (int u = 0; u < ND; ++u) {
+            const int k = w * ND + u;
             if (k < 32) {
-                const int r = 2 * k + (lane >> 5), ci = (lane & 31) ^ (r & 15);
-                const unsigned off = (unsigned)(((64 * c + r) * 32 + ci) * 16);
+                constexpr int RPI = 1024 / RB3;             // rows per instruction
+                const int r = RPI * k + lane / (64 / RPI), pos = lane % (64 / RPI);
+                const int ci = pos ^ (r & 15);
+                const unsigned off = (unsigned)((NCH * c + r) * RB3 + ci * 16);
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rw3, (lds_void_t*)(base + k * 1024), 16, off, 0, 0, 0);
             } else {
+                constexpr int RPI = 1024 / RB1;
                 const int kk = k - 32;
-                const int r = 4 * kk + (lane >> 4), ci = (lane & 15) ^ (r & 15);
-                const unsigned off = (unsigned)(r * 2048 + c * 256 + ci * 16);
+                const int r = RPI * kk + lane / C1, pos = lane % C1;
+                const int ci = pos ^ ((r / R1PL) & (C1 - 1));
+                const unsigned off = (unsigned)(r * (CO / 32) * 128 + c * RB1 + ci * 16);
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rw1, (lds_void_t*)(base + W3B + kk * 1024), 16, off, 0, 0, 0);
             }
         }
     };
-    // this lane's pixel of wave group g (clamped; stores past M are dropped by ry / ry2)
+    // this lane's pixel of 16-pixel group g (clamped; stores past M are dropped by ry / ry2)
     auto pixel = [&](int g) {
         const int m = g * 16 + p;
         return m < a.M ? m : a.M - 1;
     };
-    auto load_x = [&](int g, u32x4 (&xr)[4][2]) {
+    auto load_x = [&](int g, u32x4 (&xr)[KS3][2]) {
         const unsigned base = (unsigned)(pixel(g) * a.ld_t2 + 8 * q) * 4u;
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
+        for (int s = 0; s < KS3; ++s) {
             xr[s][0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(base + 128u * s), 0, 0));
             xr[s][1] =
                 __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rx, (int)(base + 128u * s + 16u), 0, 0));
         }
     };
-    // identity of chunk c: channels 64c + 16j + 4q .. +3, j = 0..3
-    auto load_idt = [&](int g, int c, u32x4 (&r)[4]) {
-        const unsigned base = (unsigned)(pixel(g) * a.ld_res + 64 * c + 4 * q) * 4u;
+    // identity of chunk c: channels NCH c + 16j + 4q .. +3, j < T3
+    auto load_idt = [&](int g, int c, u32x4 (&r)[T3]) {
+        const unsigned base = (unsigned)(pixel(g) * a.ld_res + NCH * c + 4 * q) * 4u;
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < T3; ++j)
             r[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, (int)(base + 64u * j), 0, 0));
     };
 
-    int g = sg0 * 8 + w;
-    u32x4 xr[4][2], idt[2][4];
+    // wave w takes groups GPW w .. +GPW of each super-group of 8 groups
+    int g0 = sg0 * 8 + GPW * w;
+    u32x4 xr[GPW][KS3][2], idt[2][GPW][T3];
     dma(0, 0);
-    load_idt(g, 0, idt[0]);
-    load_x(g, xr);
+#pragma unroll
+    for (int u = 0; u < GPW; ++u) load_idt(g0 + u, 0, idt[0][u]);
 #pragma unroll 1
     for (int it = 0; it < nmine; ++it) {
-        const int gn = it + 1 < nmine ? (sg0 + (it + 1) * G) * 8 + w : g;   // next super-group's group
-        __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));          // x, identity(0), weight chunk 0
-        const int m = g * 16 + p;
-        const bool ok = m < a.M;
-        const int fb = (ok ? m : a.M - 1) / a.hw;           // this lane's pixel's frame
-        const float mx = a.xmax ? __uint_as_float(a.xmax[fb]) : a.xbound;
-        const int kx = pow2_exp(mx);
-        const float sa = __builtin_ldexpf(1.f, kx), inv_sa = __builtin_ldexpf(1.f, -kx);
-        u32x4 xb[4][2];
+        const int gn = it + 1 < nmine ? (sg0 + (it + 1) * G) * 8 + GPW * w : g0;   // next super-group
+        // x of this super-group (GPW = 1: loaded at the end of the previous one)
+        if (GPW > 1 || it == 0) {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            float e8[8];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) e8[e] = __uint_as_float(xr[s][e >> 2][e & 3]);
-            split8(e8, sa, xb[s][0], xb[s][1]);
+            for (int u = 0; u < GPW; ++u) load_x(g0 + u, xr[u]);
         }
-        f32x4_t acc1[8];
+        __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));          // x, identity(0), weight chunk 0
+        int m[GPW], fb[GPW];
+        bool ok[GPW];
+        float inv_sa[GPW];
+        u32x4 xb[GPW][KS3][2];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc1[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        float vmax_y = 0.f;
-        int ks = 0;                                         // scale exponent of acc1
+        for (int u = 0; u < GPW; ++u) {
+            m[u] = (g0 + u) * 16 + p;
+            ok[u] = m[u] < a.M;
+            fb[u] = (ok[u] ? m[u] : a.M - 1) / a.hw;        // this lane's pixel's frame
+            const float mx = a.xmax ? __uint_as_float(a.xmax[fb[u]]) : a.xbound;
+            const int kx = pow2_exp(mx);
+            const float sa = __builtin_ldexpf(1.f, kx);
+            inv_sa[u] = __builtin_ldexpf(1.f, -kx);
+#pragma unroll
+            for (int s = 0; s < KS3; ++s) {
+                float e8[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) e8[e] = __uint_as_float(xr[u][s][e >> 2][e & 3]);
+                split8(e8, sa, xb[u][s][0], xb[u][s][1]);
+            }
+        }
+        f32x4_t acc1[GPW][T1];
+#pragma unroll
+        for (int u = 0; u < GPW; ++u)
+#pragma unroll
+            for (int j = 0; j < T1; ++j) acc1[u][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        float vmax_y[GPW];
+        int ks[GPW];                                        // scale exponent of acc1
+#pragma unroll
+        for (int u = 0; u < GPW; ++u) { vmax_y[u] = 0.f; ks[u] = 0; }
 #pragma unroll 1
         for (int cp = 0; cp < NCHUNK / 2; ++cp)
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            const int c = 2 * cp + h, st = h;   // chunk c in stage c & 1
-            if (c > 0) __builtin_amdgcn_s_waitcnt(vmcnt_imm(8));   // chunk c landed (younger: identity(c), y(c-1))
+            const int c = 2 * cp + h, st = h;               // chunk c in stage c & 1
+            // chunk c landed (younger: identity(c), y(c-1))
+            if (c > 0) __builtin_amdgcn_s_waitcnt(vmcnt_imm(2 * GPW * T3));
             lds_barrier();                                  // every wave's DMA of chunk c landed; stage st^1 free
-            dma((c + 1) & 7, st ^ 1);
-            load_idt(c == 7 ? gn : g, (c + 1) & 7, idt[h ^ 1]);
+            const int cn = c + 1 < NCHUNK ? c + 1 : 0;
+            dma(cn, st ^ 1);
+#pragma unroll
+            for (int u = 0; u < GPW; ++u) load_idt((cn == 0 ? gn : g0) + u, cn, idt[h ^ 1][u]);
             const char* w3s = smem + st * STAGE;
             const char* w1s = w3s + W3B;
-            // ---- conv3, channels 64c .. 64c+63 of the 16 pixels ----
-            f32x4_t acc3[4];
+            // ---- conv3, channels NCH c .. +NCH of the wave's pixels ----
+            f32x4_t acc3[GPW][T3];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc3[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+            for (int u = 0; u < GPW; ++u)
 #pragma unroll
-            for (int s = 0; s < 4; ++s) {
+                for (int j = 0; j < T3; ++j) acc3[u][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const char* row = w3s + (16 * j + p) * 512;
+            for (int s = 0; s < KS3; ++s) {
+#pragma unroll
+                for (int j = 0; j < T3; ++j) {
+                    const char* row = w3s + (16 * j + p) * RB3;
                     const u32x4 wh = *(const u32x4*)(row + ((((2 * s) * 4 + q) ^ p) << 4));
                     const u32x4 wl = *(const u32x4*)(row + ((((2 * s + 1) * 4 + q) ^ p) << 4));
-                    acc3[j] = mfma3(wh, wl, xb[s][0], xb[s][1], acc3[j]);
+#pragma unroll
+                    for (int u = 0; u < GPW; ++u) acc3[u][j] = mfma3(wh, wl, xb[u][s][0], xb[u][s][1], acc3[u][j]);
                 }
+                // GPW = 2: keep each k-step's fragment reads next to its MFMAs (read ahead,
+                // the whole chunk's fragments would need another 128 VGPRs)
+                if constexpr (GPW > 1 || KS3 > 4) __builtin_amdgcn_sched_barrier(0);
             }
             // ---- epilogue: bn3 + identity + relu, store y, split for conv1' ----
-            __builtin_amdgcn_s_waitcnt(vmcnt_imm(16));      // identity(c) (younger: y(c-1), DMA(c+1), identity(c+1))
-            float yv[4][4];
-            float cmax = 0.f;
-            const unsigned ybase = ok ? (unsigned)(m * a.ld_y + 64 * c + 4 * q) * 4u : 0x80000000u;
+            // identity(c) (younger: y(c-1), DMA(c+1), identity(c+1))
+            __builtin_amdgcn_s_waitcnt(vmcnt_imm(ND + 2 * GPW * T3));
+            u32x4 yb[GPW][KC][2];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int ch = 64 * c + 16 * j + 4 * q;
+            for (int u = 0; u < GPW; ++u) {
+                float yv[T3][4];
+                float cmax = 0.f;
+                const unsigned ybase = ok[u] ? (unsigned)(m[u] * a.ld_y + NCH * c + 4 * q) * 4u : 0x80000000u;
+#pragma unroll
+                for (int j = 0; j < T3; ++j) {
+                    const int ch = NCH * c + 16 * j + 4 * q;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float v = (acc3[u][j][e] * inv_sa[u]) * s_sc3[ch + e] + s_sh3[ch + e];
+                        float t = v + __uint_as_float(idt[h][u][j][e]);
+                        t = t > 0.f ? t : 0.f;
+                        yv[j][e] = t;
+                        cmax = fmaxf(cmax, t);
+                    }
+                    __builtin_amdgcn_raw_buffer_store_b128(
+                        __builtin_bit_cast(u32x4, f32x4_t{yv[j][0], yv[j][1], yv[j][2], yv[j][3]}), ry,
+                        (int)(ybase + (ok[u] ? 64u * j : 0u)), 0, 0);
+                }
+                vmax_y[u] = fmaxf(vmax_y[u], cmax);
+                cmax = fmaxf(cmax, __shfl_xor(cmax, 16));
+                cmax = fmaxf(cmax, __shfl_xor(cmax, 32));   // the pixel's max over the chunk's NCH channels
+                // the pixel's conv1' sum runs at scale 2^ks: re-based exactly (a power of
+                // two) when this chunk's split scale differs; an all-zero chunk keeps it
+                const int ky = cmax > 0.f ? pow2_exp(cmax) : ks[u];
+                const float rebase = __builtin_ldexpf(1.f, ky - ks[u]);
+                ks[u] = ky;
+                const float sy = __builtin_ldexpf(1.f, ky);
+#pragma unroll
+                for (int j = 0; j < T1; ++j)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) acc1[u][j][e] *= rebase;
+#pragma unroll
+                for (int i = 0; i < KC; ++i) {
+                    const float e8[8] = {yv[2 * i][0], yv[2 * i][1], yv[2 * i][2], yv[2 * i][3],
+                                         yv[2 * i + 1][0], yv[2 * i + 1][1], yv[2 * i + 1][2], yv[2 * i + 1][3]};
+                    split8(e8, sy, yb[u][i][0], yb[u][i][1]);
+                }
+            }
+            // ---- conv1' over the chunk's NCH input channels, into the running sums ----
+#pragma unroll
+            for (int i = 0; i < KC; ++i) {
+#pragma unroll
+                for (int j = 0; j < T1; ++j) {
+                    const int r = 16 * j + p, key = (r / R1PL) & (C1 - 1);
+                    const char* row = w1s + r * RB1;
+                    const u32x4 wh = *(const u32x4*)(row + ((((2 * i) * 4 + q) ^ key) << 4));
+                    const u32x4 wl = *(const u32x4*)(row + ((((2 * i + 1) * 4 + q) ^ key) << 4));
+#pragma unroll
+                    for (int u = 0; u < GPW; ++u) acc1[u][j] = mfma3(wh, wl, yb[u][i][0], yb[u][i][1], acc1[u][j]);
+                    if constexpr (GPW > 1 || T1 > 8) {
+                        if ((j & 1) == 1) __builtin_amdgcn_sched_barrier(0);
+                    }
+                }
+            }
+        }
+        // ---- conv1' epilogue: bn1' + relu, t1' stores ----
+#pragma unroll
+        for (int u = 0; u < GPW; ++u) {
+            const float inv_s1 = __builtin_ldexpf(1.f, -ks[u]);
+            float vmax_t = 0.f;
+            const unsigned y2base = ok[u] ? (unsigned)(m[u] * a.ld_y2 + 4 * q) * 4u : 0x80000000u;
+#pragma unroll
+            for (int j = 0; j < T1; ++j) {
+                float o[4];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    const float v = (acc3[j][e] * inv_sa) * s_sc3[ch + e] + s_sh3[ch + e];
-                    float t = v + __uint_as_float(idt[h][j][e]);
-                    t = t > 0.f ? t : 0.f;
-                    yv[j][e] = t;
-                    cmax = fmaxf(cmax, t);
+                    const int ch = 16 * j + 4 * q + e;
+                    const float t = (acc1[u][j][e] * inv_s1) * s_sc1[ch] + s_sh1[ch];
+                    o[e] = t > 0.f ? t : 0.f;
+                    vmax_t = fmaxf(vmax_t, o[e]);
                 }
-                __builtin_amdgcn_raw_buffer_store_b128(
-                    __builtin_bit_cast(u32x4, f32x4_t{yv[j][0], yv[j][1], yv[j][2], yv[j][3]}), ry,
-                    (int)(ybase + (ok ? 64u * j : 0u)), 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f32x4_t{o[0], o[1], o[2], o[3]}), ry2,
+                                                       (int)(y2base + (ok[u] ? 64u * j : 0u)), 0, 0);
             }
-            vmax_y = fmaxf(vmax_y, cmax);
-            cmax = fmaxf(cmax, __shfl_xor(cmax, 16));
-            cmax = fmaxf(cmax, __shfl_xor(cmax, 32));       // the pixel's max over the chunk's 64 channels
-            // the pixel's conv1' sum runs at scale 2^ks: re-based exactly (a power of two)
-            // when this chunk's split scale differs; an all-zero chunk keeps the scale
-            const int ky = cmax > 0.f ? pow2_exp(cmax) : ks;
-            const float rebase = __builtin_ldexpf(1.f, ky - ks);
-            ks = ky;
-            const float sy = __builtin_ldexpf(1.f, ky);
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-#pragma unroll
-                for (int e = 0; e < 4; ++e) acc1[j][e] *= rebase;
-            u32x4 yb[2][2];
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                const float e8[8] = {yv[2 * i][0], yv[2 * i][1], yv[2 * i][2], yv[2 * i][3],
-                                     yv[2 * i + 1][0], yv[2 * i + 1][1], yv[2 * i + 1][2], yv[2 * i + 1][3]};
-                split8(e8, sy, yb[i][0], yb[i][1]);
-            }
-            // ---- conv1' over the chunk's 64 input channels, into the running sum ----
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const char* row = w1s + (16 * j + p) * 256;
-                    const u32x4 wh = *(const u32x4*)(row + ((((2 * i) * 4 + q) ^ p) << 4));
-                    const u32x4 wl = *(const u32x4*)(row + ((((2 * i + 1) * 4 + q) ^ p) << 4));
-                    acc1[j] = mfma3(wh, wl, yb[i][0], yb[i][1], acc1[j]);
-                }
-            }
+            amax_lds_add(s_ymax, ok[u] ? fb[u] : -1, vmax_y[u]);
+            amax_lds_add(s_y2max, ok[u] ? fb[u] : -1, vmax_t);
         }
-        const float inv_s1 = __builtin_ldexpf(1.f, -ks);
-        // ---- conv1' epilogue: bn1' + relu, t1' stores ----
-        float vmax_t = 0.f;
-        const unsigned y2base = ok ? (unsigned)(m * a.ld_y2 + 4 * q) * 4u : 0x80000000u;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            float o[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int ch = 16 * j + 4 * q + e;
-                const float t = (acc1[j][e] * inv_s1) * s_sc1[ch] + s_sh1[ch];
-                o[e] = t > 0.f ? t : 0.f;
-                vmax_t = fmaxf(vmax_t, o[e]);
-            }
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, f32x4_t{o[0], o[1], o[2], o[3]}), ry2,
-                                                   (int)(y2base + (ok ? 64u * j : 0u)), 0, 0);
-        }
-        amax_lds_add(s_ymax, ok ? fb : -1, vmax_y);
-        amax_lds_add(s_y2max, ok ? fb : -1, vmax_t);
-        g = gn;
-        load_x(g, xr);
+        g0 = gn;
+        if constexpr (GPW == 1) load_x(g0, xr[0]);
     }
     __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));               // trailing DMA / loads land before the workgroup exits
     __syncthreads();
@@ -303,21 +366,21 @@ __global__ __launch_bounds__(512, 1) void chain32_kernel(Chain32Args a) {
 
 }  // namespace
 
-// Eligible: the layer2 shape (128 -> 512 -> 128) with dense rows, fp16-pair weights,
-// frames within the LDS max slots, byte offsets within 2^31.
+// Eligible: the layer2 (128 -> 512 -> 128) or layer3 (256 -> 1024 -> 256) shape with
+// dense rows, frames within the LDS max slots, byte offsets within 2^31.
 bool vd_chain32_ok(int cmid, int cout, int kpad3, int kpad1, int ld_t2, int ld_res, int ld_y, int ld_y2, long M,
                    int frames) {
-    if (cmid != CM || cout != CO || kpad3 != CM || kpad1 != CO) return false;
-    if (ld_t2 != CM || ld_res != CO || ld_y != CO || ld_y2 != CM) return false;
-    return M > 0 && M * CO * 4 < 0x7fffffffL && frames > 0 && frames <= 1024;
+    const bool l2 = cmid == 128 && cout == 512, l3 = cmid == 256 && cout == 1024;
+    if (!(l2 || l3) || kpad3 != cmid || kpad1 != cout) return false;
+    if (ld_t2 != cmid || ld_res != cout || ld_y != cout || ld_y2 != cmid) return false;
+    return M > 0 && M * cout * 4 < 0x7fffffffL && frames > 0 && frames <= 1024;
 }
 
-hipError_t vd_launch_chain32(const Chain32Args& a, hipStream_t s) {
-    if (a.M <= 0) return hipSuccess;
-    if (a.B <= 0 || a.B > 1024 || a.hw <= 0) return hipErrorInvalidValue;
+template <class S>
+static hipError_t launch_chain32_t(const Chain32Args& a, hipStream_t s) {
     static const int cus = [] {
-        (void)hipFuncSetAttribute((const void*)chain32_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  LDS_FIXED + 8 * 1024);
+        (void)hipFuncSetAttribute((const void*)chain32_kernel<S>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  S::LDS + 8 * 1024);
         int dev = 0, n = 256;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
@@ -325,6 +388,14 @@ hipError_t vd_launch_chain32(const Chain32Args& a, hipStream_t s) {
     }();
     const int nsg = (a.M + 127) / 128;
     const int grid = nsg < cus ? nsg : cus;                 // persistent: one workgroup per CU
-    hipLaunchKernelGGL(chain32_kernel, dim3(grid), dim3(512), LDS_FIXED + 8 * a.B, s, a);
+    hipLaunchKernelGGL(chain32_kernel<S>, dim3(grid), dim3(S::THREADS), S::LDS + 8 * a.B, s, a);
     return hipGetLastError();
+}
+
+hipError_t vd_launch_chain32(const Chain32Args& a, hipStream_t s) {
+    if (a.M <= 0) return hipSuccess;
+    if (a.B <= 0 || a.B > 1024 || a.hw <= 0) return hipErrorInvalidValue;
+    if (a.ld_t2 == 128 && a.ld_res == 512) return launch_chain32_t<L2Shape>(a, s);
+    if (a.ld_t2 == 256 && a.ld_res == 1024) return launch_chain32_t<L3Shape>(a, s);
+    return hipErrorInvalidValue;
 }

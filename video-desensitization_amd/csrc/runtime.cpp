@@ -584,7 +584,8 @@ void Ctx::fuse_chains32(Net& net, size_t begin) {
                                b.ycoff == 0 && a.x.f32 && a.y.f32 && b.y.f32 && a.r.f32 && c3.cin_pad == a.x.c &&
                                c1.cin_pad == c3.cout && a.r.h == a.y.h && a.r.w == a.y.w;
             const long M = (long)cfg.max_batch * a.y.h * a.y.w;
-            if (shape && vd_chain32_ok(c3.cin_pad, c3.cout, c3.kpad, c1.kpad, a.x.c, a.r.c, a.y.c, b.y.c, M,
+            const bool take = tune.chain == 1 || c3.cin_pad == 128;   // option chain=2 (default): layer2 only
+            if (shape && take && vd_chain32_ok(c3.cin_pad, c3.cout, c3.kpad, c1.kpad, a.x.c, a.r.c, a.y.c, b.y.c, M,
                                        cfg.max_batch) &&
                 chain32_weights(c1) == VD_OK) {
                 Op op = a;

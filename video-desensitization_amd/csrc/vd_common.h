@@ -64,7 +64,8 @@ struct VdTune {
     int mosaic_copy = 0;      //   copy-first output: one plain copy pass, the cell kernel writes the box pixels (measured slower)
     int block_fuse = 1;       // plan: fused layer1 bottlenecks (block.hip)
     int block_fuse32 = 1;     // plan, fp32 (fp16 pairs): fused layer1 bottlenecks (block32.hip)
-    int chain = 1;            // plan: layer2 conv3 + next conv1 (chain.hip)
+    int chain = 2;            // plan: conv3 + next conv1 as one kernel (chain.hip; fp32: chain32.hip: 2 = layer2,
+                              //   1 = layer2 + layer3 -- level on the grouped headline, slower per launch)
     int stem_pool = 1;        // plan: stem conv + maxpool (stem.hip)
     int ssh_fuse = 1;         // plan: SSH conv3X3 + conv5X5_1 as one conv
     int plate_s2d = 1;        // plan: YOLO space-to-depth stem input
