@@ -409,6 +409,26 @@ def test_heads_fp32_tail_split_bit_identical(gpu):
             np.testing.assert_array_equal(a, b)
 
 
+def test_heads_fp32_halo_tr_bit_identical(gpu):
+    """fp32 plan: the halo 3x3 tiles with the MFMA operands exchanged (D^T accumulators,
+    weight rows permuted in the DMA, register epilogue; option x6_halo_tr, 1 = the
+    128 / 192 / 256-wide tiles, 2 = the narrow 32 / 64-wide ones too) against the
+    LDS-staged epilogue (0): the same products in the same order, heads bit-identical."""
+    import vdmi
+    fr = _frames(2, 1080, 1920, seed=41)
+    heads = {}
+    for tr in (0, 1, 2):
+        ctx = vdmi.Context(precision="fp32", max_batch=2, options={"x6_halo_tr": tr})
+        try:
+            ctx.load_weights(0, face_weights("default"))
+            heads[tr] = ctx.forward_heads(fr)
+        finally:
+            ctx.close()
+    for t in (1, 2):
+        for a, b in zip(heads[t], heads[0]):
+            np.testing.assert_array_equal(a, b)
+
+
 def test_heads_fp32_halo_conv(gpu):
     """fp32 plan: the 3x3 stride-1 convs with W <= 126 (layer2-4 conv2, FPN merges, SSH
     conv5X5_1 + conv3X3 at levels 0-2) run on conv_x6_halo_kernel (input split once per

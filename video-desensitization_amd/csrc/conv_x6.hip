@@ -782,7 +782,10 @@ __global__ __launch_bounds__(NT, NT == 256 && BM == 256 ? 1 : 2) void conv_x6_ke
 // for starts that are multiples of 8 (checked exhaustively over the 8 start residues)
 __device__ __forceinline__ int swzh(int row, int chunk) { return row * 64 + ((chunk ^ (((row >> 2) & 1) << 1)) << 4); }
 
-template <int BN, int NSB>
+// TR (round 4, option x6_halo_tr): the MFMA operands exchanged as on the TR GEMM tiles
+// (weight rows permuted by x6_tr_row in the DMA, D^T accumulators), so the epilogue runs
+// from registers (x6_epilogue_tr) with no LDS staging passes: bit-identical.
+template <int BN, int NSB, bool TR = false>
 __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(ConvArgs a) {
     using S = X6Shape<256, BN, 512, 2, 2>;
     constexpr int BM = 256, NT = 512, TM = S::TM, TN = S::TN, WAVES = S::WAVES, PL_B = S::PL_B;
@@ -857,7 +860,8 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
                 const int p = j / RB, r0 = (j % RB) * 16;
                 const int row = r0 + (lane >> 2), slot = lane & 3;
                 const int chunk = slot ^ (((row >> 3) & 1) * 3);
-                const unsigned off = (unsigned)((((long)(n0 + row) * nk + kt) * 2 + p) * 64 + chunk * 16);
+                const int wrow = TR ? x6_tr_row(row) : row;
+                const unsigned off = (unsigned)((((long)(n0 + wrow) * nk + kt) * 2 + p) * 64 + chunk * 16);
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_w, (lds_void_t*)(Bs + p * PL_B + r0 * 64), 16, off, 0,
                                                          0, 0);
             }
@@ -905,7 +909,10 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
                 af[0] = *(const u32x4*)(Ah + o);
                 af[1] = *(const u32x4*)(Ah + PL_H + o);
 #pragma unroll
-                for (int j = 0; j < TN; ++j) acc[i][j] = mfma_terms<2>(af, bf[j], acc[i][j]);
+                for (int j = 0; j < TN; ++j) {
+                    if constexpr (TR) acc[i][j] = mfma_pair_tr(af, bf[j], acc[i][j]);
+                    else acc[i][j] = mfma_terms<2>(af, bf[j], acc[i][j]);
+                }
             }
         } else {
             u32x4 af[TM][3];
@@ -922,7 +929,10 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
                 bf[0] = *(const u32x4*)(Bs + swz(wn * S::WTN + j * 16 + (lane & 15), ch));
                 bf[1] = *(const u32x4*)(Bs + PL_B + swz(wn * S::WTN + j * 16 + (lane & 15), ch));
 #pragma unroll
-                for (int i = 0; i < TM; ++i) acc[i][j] = mfma_terms<2>(af[i], bf, acc[i][j]);
+                for (int i = 0; i < TM; ++i) {
+                    if constexpr (TR) acc[i][j] = mfma_pair_tr(af[i], bf, acc[i][j]);
+                    else acc[i][j] = mfma_terms<2>(af[i], bf, acc[i][j]);
+                }
             }
         }
     };
@@ -939,7 +949,7 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
     // 9c+8], B(s+2) at the end of step s. At the top of step s, younger than B(s):
     // B(s+1) (if issued) and the halo loads issued at the end of step s-1 or (s = 1)
     // in the prologue after B(1).
-    if (NSB == 3 && S::NDMA % WAVES == 0 && !(a.dbg & 2)) {
+    if constexpr (NSB == 3 && S::NDMA % WAVES == 0) {
         // This wave's DMA count per step is a compile-time constant, so each step's vmcnt
         // is one of four immediates chosen by two uniform branches (the runtime wait_vm
         // switch costs a tree of scalar branches per step). (Unrolling the nine taps of a
@@ -973,7 +983,7 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
                 if (s + 2 < nsteps) dma_b(s + 2, (s + 2) % 3);
             }
         }
-    } else if (NSB == 3) {
+    } else if constexpr (NSB == 3) {
         // VMEM issue order per step s: [top] B(s+2), except on tap-8 steps, which issue
         // it at the end, after the halo loads of chunk c+2 (the halo stores then wait
         // only on B(s+1), issued a step earlier, not on a DMA just issued). Younger than
@@ -1000,7 +1010,7 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
                 if (s + 2 < nsteps) dma_b(s + 2, (s + 2) % 3);
             }
         }
-    } else
+    } else {
     for (int s = 0; s < nsteps; ++s) {
         const int c = s / 9, tap = s - 9 * c;
         int younger = s + 1 < nsteps ? my_dma : 0;
@@ -1022,8 +1032,13 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
         }
         if (s + 2 < nsteps) dma_b(s + 2, s & 1);
     }
-    __syncthreads();
-    x6_epilogue<S, 16>(a, acc, m0, n0, wm, wn, tid, lane, smem, amax_off);
+    }
+    if constexpr (TR) {
+        x6_epilogue_tr<S>(a, acc, m0, n0, wm, wn, lane, (unsigned*)(smem + amax_off));
+    } else {
+        __syncthreads();
+        x6_epilogue<S, 16>(a, acc, m0, n0, wm, wn, tid, lane, smem, amax_off);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1555,14 +1570,14 @@ static int x6_halo_lds(const ConvArgs& a) {
     return std::max(NSB * 2 * S::PL_B + 2 * HP * 64, S::EPR * S::EPLD * 4) + (a.ymax ? 4 * a.B : 0);
 }
 
-template <int BN, int NSB>
-static hipError_t launch_x6_halo_n(const ConvArgs& a0, hipStream_t s) {
+template <int BN, int NSB, bool TR = false>
+static hipError_t launch_x6_halo_t(const ConvArgs& a0, hipStream_t s) {
     ConvArgs a = a0;
     a.w = a.wx3;
     a.ntiles_n = (a.cout + BN - 1) / BN;
     a.mbase = 0;
     static const bool attr = [] {
-        (void)hipFuncSetAttribute((const void*)conv_x6_halo_kernel<BN, NSB>,
+        (void)hipFuncSetAttribute((const void*)conv_x6_halo_kernel<BN, NSB, TR>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         return true;
     }();
@@ -1570,8 +1585,18 @@ static hipError_t launch_x6_halo_n(const ConvArgs& a0, hipStream_t s) {
     const int lds = x6_halo_lds<BN, NSB>(a);
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     const int mt = (a.M + 255) / 256;
-    hipLaunchKernelGGL((conv_x6_halo_kernel<BN, NSB>), dim3(mt * a.ntiles_n), dim3(512), lds, s, a);
+    hipLaunchKernelGGL((conv_x6_halo_kernel<BN, NSB, TR>), dim3(mt * a.ntiles_n), dim3(512), lds, s, a);
     return hipGetLastError();
+}
+
+// TR form where the output (and residual) rows take 8-channel 16-B vectors (option
+// x6_halo_tr: 1 the 128 / 192 / 256-wide tiles, 2 the narrow ones too)
+template <int BN, int NSB>
+static hipError_t launch_x6_halo_n(const ConvArgs& a, hipStream_t s) {
+    const bool tr = a.tune && a.tune->x6_halo_tr >= (BN >= 128 ? 1 : 2) && !((a.ldy | a.ycoff) & 7) &&
+                    (a.res_mode == VD_RES_NONE || !((a.res_ld | a.res_coff) & 7));
+    if (tr) return launch_x6_halo_t<BN, NSB, true>(a, s);
+    return launch_x6_halo_t<BN, NSB, false>(a, s);
 }
 
 // option x6_halo: 1 two B stages, 2 three where they fit LDS beside the halo

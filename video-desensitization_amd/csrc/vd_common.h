@@ -105,6 +105,8 @@ struct VdTune {
     int x6_halo_narrow = 1;   // ... also for Cout <= 64 (N tiles of 32 / 64)
     int x6_adepth = 2;        // A register sets of the 256 x {128, 64, 32} fp16-pair tiles (2 or 4; 4 measured level)
     int x6_slots = 0;         //   workgroup slots of one round (0: the CU count; tests force small values)
+    int x6_halo_tr = 2;       // fp32 plan: halo 3x3 tiles with D^T accumulators and the register epilogue
+                              //   (1: the 128-256-wide tiles, 2: all; bit-identical)
     int x6_taps = 1;          // fp32 plan: narrow KxK YOLO layers (K <= 288) on the streaming TAPS form
     int x6_gemm1x1 = 1;       // fp16 pairs: GEMM 1x1 convs on the TR tiles (D^T accumulators, register epilogue;
                               //   2: also the streaming form's K <= 256 layers, 0: off)
