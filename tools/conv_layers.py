@@ -66,8 +66,11 @@ def face_plan(B=64, H=640, W=640, fused=True, block=True, chain=True, ssh_fused=
         m = B * hh * hh
         L += ([(f"ssh{l}.c51+c3", m, 192, 2304)] if ssh_fused else
               [(f"ssh{l}.c3", m, 128, 2304), (f"ssh{l}.c51", m, 64, 2304)])
-        L += [(f"ssh{l}.c52", m, 64, 576),
-              (f"ssh{l}.c72", m, 64, 576), (f"ssh{l}.c73", m, 64, 576), (f"head{l}", m, 32, 256)]
+        if ssh_fused == 2:   # conv5X5_2 + conv7X7_2 as one conv too (option ssh_fuse=2)
+            L += [(f"ssh{l}.c52+c72", m, 128, 576), (f"ssh{l}.c73", m, 64, 576), (f"head{l}", m, 32, 256)]
+        else:
+            L += [(f"ssh{l}.c52", m, 64, 576),
+                  (f"ssh{l}.c72", m, 64, 576), (f"ssh{l}.c73", m, 64, 576), (f"head{l}", m, 32, 256)]
     return L
 
 

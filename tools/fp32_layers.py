@@ -15,7 +15,7 @@ from conv_layers import face_plan  # noqa: E402
 def main(path, B=64, block=True, chain=2):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     # fp32 plan: layer1 bottlenecks fused (block32.hip) unless option block_fuse32=0
-    plan = face_plan(B, fused=True, block=block, chain={1: (0, 1, 2), 2: (0, 1, 2, 3, 4)} if chain == 1 else ({1: (0, 1, 2)} if chain == 2 else {}), ssh_fused=True, dual=(0,))
+    plan = face_plan(B, fused=True, block=block, chain={1: (0, 1, 2), 2: (0, 1, 2, 3, 4)} if chain == 1 else ({1: (0, 1, 2)} if chain == 2 else {}), ssh_fused=2, dual=(0,))
     # the face streams run the fused stem / layer1 kernels (with face_groups both group
     # streams do); the one with the latest launch is the context stream, which runs
     # bench.py's instrumented pass (face_groups = 1) last: its last len(plan) conv

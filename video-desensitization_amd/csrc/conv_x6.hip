@@ -1441,7 +1441,11 @@ hipError_t launch_stream_x6(const ConvArgs& a, hipStream_t s) {
 // C2f bottleneck's shortcut as a post-activation residual) -- and the space-to-depth
 // model.0 on its integer canvas (x_exact: one A plane). Returns false when not taken.
 static bool launch_taps_x6(const ConvArgs& a, hipStream_t s, hipError_t* err) {
-    if (!a.tune || !a.tune->x6_taps || (a.kh == 1 && a.kw == 1 && a.pad == 0 && a.stride == 1)) return false;
+    // plain 1x1 convs go to the streaming form unless their K is padded (model.2's cv2 over
+    // the 48-channel C2f concat: K 48 in a 64-wide k range)
+    if (!a.tune || !a.tune->x6_taps ||
+        (a.kh == 1 && a.kw == 1 && a.pad == 0 && a.stride == 1 && a.kpad == a.cin_pad))
+        return false;
     if (a.act != VD_ACT_SILU || (a.res_mode != VD_RES_NONE && a.res_mode != VD_RES_POST_ACT)) return false;
     if ((a.cin_pad & 7) || ((a.ldx | a.xcoff) & 3) || ((a.ldy | a.ycoff) & 7)) return false;
     if (a.res_mode != VD_RES_NONE && (a.res_up || ((a.res_ld | a.res_coff) & 7))) return false;
@@ -1464,6 +1468,7 @@ static bool launch_taps_x6(const ConvArgs& a, hipStream_t s, hipError_t* err) {
     // K <= 160 only: at K = 288 (model.3, the 32-channel bottlenecks at 80x48) the
     // two register sets of x need ~210 VGPRs, one workgroup per CU, and the form
     // measured 5-40 % slower than the GEMM / halo tiles
+    if (ks == 2 && co == 32) VD_TAPS(2, 2, 2);
     if (ks == 5 && co == 16) VD_TAPS(5, 1, 2);
     if (ks == 5 && co == 32) VD_TAPS(5, 2, 2);
 #undef VD_TAPS

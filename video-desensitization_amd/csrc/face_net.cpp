@@ -278,7 +278,46 @@ int vd_build_face(Ctx& c, const WMap& W) {
         const int t5c = c.convs[s51].cout;
         Act cat, t5, t7;
         int hoff = 0;   // channel offset of the concat [c3 | c5 | c7] in `cat`
-        if ((rc = c.act(t7, f.h, f.w, c.convs[s72].cout))) return rc;
+        const int t7c = c.convs[s72].cout;
+        if (!sleaky && ssh_fuse && c.tune.ssh_fuse >= 2) {
+            // conv5X5_2 and conv7X7_2 both read t5 with ReLU: one conv with Cout c5o + t7c
+            // too. cat = [t5 | c3 | c7 | c5 | t7]: the first fused conv writes [t5 | c3],
+            // the second [c5 | t7], conv7x7_3 reads t7 and writes c7, and the heads read
+            // [c3 | c7 | c5] with their input channels permuted to that order.
+            int s351, s5272;
+            if ((rc = c.make_conv_bn_cat(W, {{pre + ".conv5X5_1.0.weight", pre + ".conv5X5_1.1"},
+                                             {pre + ".conv3X3.0.weight", pre + ".conv3X3.1"}},
+                                         BN_EPS, 1, 1, VD_ACT_RELU, 0.f, &s351)))
+                return rc;
+            if ((rc = c.make_conv_bn_cat(W, {{pre + ".conv5X5_2.0.weight", pre + ".conv5X5_2.1"},
+                                             {pre + ".conv7X7_2.0.weight", pre + ".conv7X7_2.1"}},
+                                         BN_EPS, 1, 1, VD_ACT_RELU, 0.f, &s5272)))
+                return rc;
+            if ((rc = c.act(cat, f.h, f.w, t5c + c3o + c7o + c5o + t7c))) return rc;
+            const int o_c7 = t5c + c3o, o_c5 = o_c7 + c7o, o_t7 = o_c5 + c5o;
+            if ((rc = c.add_conv(F.net, s351, f, 0, cat, 0))) return rc;
+            if ((rc = c.add_conv(F.net, s5272, cat, 0, cat, o_c5))) return rc;
+            if ((rc = c.add_conv(F.net, s73, cat, o_t7, cat, o_c7))) return rc;
+            std::vector<int> perm(c3o + c5o + c7o);   // packed [c3 | c7 | c5] <- tensors' [c3 | c5 | c7]
+            for (int i = 0; i < c3o; ++i) perm[i] = i;
+            for (int i = 0; i < c7o; ++i) perm[c3o + i] = c3o + c5o + i;
+            for (int i = 0; i < c5o; ++i) perm[c3o + c7o + i] = c3o + i;
+            int hc;
+            const std::string L = std::to_string(l);
+            if ((rc = c.make_conv_cat(W,
+                                      {"BboxHead." + L + ".conv1x1.weight", "ClassHead." + L + ".conv1x1.weight",
+                                       "LandmarkHead." + L + ".conv1x1.weight"},
+                                      {"BboxHead." + L + ".conv1x1.bias", "ClassHead." + L + ".conv1x1.bias",
+                                       "LandmarkHead." + L + ".conv1x1.bias"},
+                                      VD_ACT_NONE, &hc, &perm)))
+                return rc;
+            if (c.convs[hc].cout != 32) return vd_set_error(VD_ERR_WEIGHTS, "heads of level %d: %d channels != 32", l, c.convs[hc].cout);
+            if ((rc = c.act(F.heads[l], f.h, f.w, 32, true))) return rc;
+            if ((rc = c.add_conv(F.net, hc, cat, t5c, F.heads[l], 0))) return rc;
+            ssh_e[l] = (int)F.net.ops.size();
+            continue;
+        }
+        if ((rc = c.act(t7, f.h, f.w, t7c))) return rc;
         if (!sleaky && ssh_fuse) {
             // conv5X5_1 and conv3X3 read the same input with the same activation
             // (ReLU: conv3X3's own, after the concat): one conv with Cout t5c + c3o

@@ -7,6 +7,7 @@
 #include <string>
 #include <unordered_map>
 #include <utility>
+#include <map>
 #include <vector>
 
 struct HT {   // host tensor from the VDW1 container
@@ -174,6 +175,7 @@ struct Ctx {
     std::vector<hipStream_t> group_streams;      // option face_groups: streams of frame groups 1..G-1
     std::vector<hipEvent_t> group_events;        //   and their completion events (joined by the context stream)
     std::vector<hipEvent_t> group_lag_events;    //   group g done with its first face_group_lag ops
+    std::map<int, unsigned*> amax_snaps;         // per conv: its input's range slots frozen (in-place concat)
     int fork_at = -1;                                // run_ops records ev_fork after this many face ops
     std::mutex mu;
     std::vector<void*> allocs;
@@ -228,7 +230,8 @@ struct Ctx {
     int make_conv_bn_cat(const WMap& W, const std::vector<std::pair<std::string, std::string>>& parts, float eps,
                          int stride, int pad, int act, float slope, int* out_idx);
     int make_conv_cat(const WMap& W, const std::vector<std::string>& wkeys, const std::vector<std::string>& bkeys,
-                      int act, int* out_idx);
+                      int act, int* out_idx,
+                      const std::vector<int>* cin_perm = nullptr);
     int add_conv_dual(Net& net, int ci, const Act& x, int c2, const Act& x2, Act& y);
     bool dual_ok(int ci, int c2, const Act& y) const;
     int add_conv(Net& net, int ci, const Act& x, int xcoff, Act& y, int ycoff, const Act* res = nullptr,

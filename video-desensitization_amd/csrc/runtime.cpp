@@ -329,8 +329,10 @@ int Ctx::add_dwconv(Net& net, int di, const Act& x, Act& y) {
 }
 
 // Several 1x1 conv heads with bias fused along Cout (retinaface.py:90-92,140-142).
+// cin_perm (1x1 heads): input channel i of the packed conv reads the tensors' channel
+// cin_perm[i] (a concat laid out in another block order)
 int Ctx::make_conv_cat(const WMap& W, const std::vector<std::string>& wkeys, const std::vector<std::string>& bkeys,
-                       int act, int* out_idx) {
+                       int act, int* out_idx, const std::vector<int>* cin_perm) {
     Conv cv{};
     std::vector<float> wall, sc, sh;
     for (size_t i = 0; i < wkeys.size(); ++i) {
@@ -344,6 +346,14 @@ int Ctx::make_conv_cat(const WMap& W, const std::vector<std::string>& wkeys, con
         wall.insert(wall.end(), w->data.begin(), w->data.end());
         for (int n = 0; n < w->shape[0]; ++n) { sc.push_back(1.f); sh.push_back(b ? b->data[n] : 0.f); }
         cv.cout += w->shape[0];
+    }
+    if (cin_perm) {
+        if ((int)cin_perm->size() != cv.cin || cv.kh != 1 || cv.kw != 1)
+            return vd_set_error(VD_ERR_STATE, "internal: head channel permutation");
+        std::vector<float> pw(wall.size());
+        for (int o = 0; o < cv.cout; ++o)
+            for (int i = 0; i < cv.cin; ++i) pw[(size_t)o * cv.cin + i] = wall[(size_t)o * cv.cin + (*cin_perm)[i]];
+        wall.swap(pw);
     }
     cv.stride = 1; cv.pad = cv.kh / 2; cv.act = act; cv.slope = 0.f;
     int rc = upload_conv(cv, wall, sc, sh);
@@ -451,6 +461,19 @@ int Ctx::run_conv_op(const Op& op, int f0, int n, int fam) {
     a.ymax = op.y.amax ? op.y.amax + f0 : nullptr;
     if (cv.split == 2 && !a.xmax && !(a.xbound > 0.f))
         return vd_set_error(VD_ERR_ARG, "internal: conv input without a range (fp16-pair plan)");
+    if (a.xmax && op.x.amax == op.y.amax) {
+        // input and output are channel slices of one buffer (the SSH concat): the kernel
+        // reads the input's per-frame range while its epilogue raises the same slots, so
+        // it reads a copy frozen before the launch (one array per conv: the frame groups
+        // run the same conv concurrently on disjoint frames)
+        unsigned*& snap = amax_snaps[op.conv];
+        if (!snap) {
+            int rc = dalloc((void**)&snap, (size_t)cfg.max_batch * 4);
+            if (rc) return rc;
+        }
+        VD_CHECK_HIP(hipMemcpyAsync(snap + f0, a.xmax, (size_t)n * 4, hipMemcpyDeviceToDevice, stream));
+        a.xmax = snap + f0;
+    }
     double flops = cv.flops_per_px * a.M;
     if (op.conv2 >= 0) {
         const Conv& c2 = convs[op.conv2];

@@ -67,7 +67,7 @@ struct VdTune {
     int chain = 2;            // plan: conv3 + next conv1 as one kernel (chain.hip; fp32: chain32.hip: 2 = layer2,
                               //   1 = layer2 + layer3 -- level on the grouped headline, slower per launch)
     int stem_pool = 1;        // plan: stem conv + maxpool (stem.hip)
-    int ssh_fuse = 1;         // plan: SSH conv3X3 + conv5X5_1 as one conv
+    int ssh_fuse = 2;         // plan: SSH conv3X3 + conv5X5_1 as one conv (2: and conv5X5_2 + conv7X7_2)
     int plate_s2d = 1;        // plan: YOLO space-to-depth stem input
     int jenc_gpu = 1;         // vd_jpeg_encode: Huffman coding on the device (0: host threads)
     int jdec_gpu = 1;         // vd_jpeg_decode: entropy decode on the device (0: host threads)
