@@ -295,3 +295,23 @@ def test_plate_raw_fp32_taps_matches_gemm(gpu, h, w):
     for b in range(3):   # same boxes; float corners within f32 rounding (observed 2e-7)
         np.testing.assert_array_equal(boxes[1][b][0], boxes[0][b][0])
         np.testing.assert_allclose(boxes[1][b][1], boxes[0][b][1], rtol=2e-6, atol=0)
+
+
+@pytest.mark.parametrize("h,w", [(1080, 1920), (480, 640)])
+def test_plate_raw_fp32_grouped_det_bit_identical(gpu, h, w):
+    """fp32 plan: the Detect heads' cv2.i.1 and cv3.i.1 (3x3, 64 -> 64 on the two halves
+    of det0.i's output) as one grouped conv on the halo tile (option det_group: each
+    64-wide N tile reads its group's 64 input channels). The same tile form and K order
+    as the two convs (det_group=0): raw outputs bit-identical."""
+    import vdmi
+    from vdmi import synth, weights
+    fr = synth.frames(2, h, w, seed=47)
+    out = {}
+    for g in (1, 0):
+        c = vdmi.Context(precision="fp32", max_batch=2, options={"det_group": g})
+        try:
+            c.load_weights(1, weights.yolov8n_state_dict(0))
+            out[g] = c.plate_raw(fr)
+        finally:
+            c.close()
+    np.testing.assert_array_equal(out[1], out[0])

@@ -809,12 +809,13 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
     const __amdgpu_buffer_rsrc_t rsrc_x = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, (int)xbytes, 0x00020000);
     int hoff[QI];                                    // element offset of the item's pixel + channels
     unsigned hexp = 0;                              // the items' frame scale exponents, a byte each
+    const int xg = a.grp_co ? (n0 / a.grp_co) * a.grp_ci : 0;   // grouped conv: this N tile's input group
 #pragma unroll
     for (int q = 0; q < QI; ++q) {
         const int it = tid + NT * q, hr = it >> 2, pr = it & 3;
         const int pix = m0 - W - 1 + hr;
         const bool ok = hr < HR && pix >= 0 && pix < a.M;
-        hoff[q] = ok ? pix * a.ldx + a.xcoff + pr * 8 : -1;
+        hoff[q] = ok ? pix * a.ldx + a.xcoff + xg + pr * 8 : -1;
         hexp |= (unsigned)((ok ? act_scale_exp(a, pix / HW) : 0) & 0xff) << (8 * q);
     }
     u32x4 hx[QI][2];
@@ -1785,6 +1786,12 @@ bool vd_conv1x1_x6_dual_ok(const ConvArgs& a) {
 hipError_t vd_launch_conv_x6(const ConvArgs& a0, hipStream_t s) {
     ConvArgs a = a0;
     a.dbg = a.tune ? a.tune->x6_dbg : 0;
+    if (a.grp_co) {   // grouped: the halo form only, one 64-wide N tile per group
+        if (a.grp_co != 64 || a.f32_split != 2 || !a.wx3 || !a.tune || !x6_halo_ok(a) || (a.ymax && a.B > kAmaxFrames))
+            return hipErrorInvalidValue;
+        a.scale = a.scale_x;
+        return launch_x6_halo<64>(a, s);
+    }
     if (a.x2) {
         if (!vd_conv1x1_x6_dual_ok(a) || (a.ymax && a.B > kAmaxFrames)) return hipErrorInvalidValue;
         return launch_dual_x6<2, 2, 8>(a, s);

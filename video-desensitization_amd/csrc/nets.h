@@ -42,6 +42,7 @@ struct Conv {
     float* scale = nullptr;
     float* shift = nullptr;
     double flops_per_px = 0;   // algorithmic FLOPs per output pixel (real Cin, no padding)
+    int grp_co = 0, grp_ci = 0; // grouped (conv_x6_halo only): rows [g grp_co, +grp_co) read input channels g grp_ci + [0, cin)
 };
 
 // One fused layer1 bottleneck (block.hip, block.cpp): the per-conv bf16 weights

@@ -134,6 +134,20 @@ int yconv_pair(Ctx& c, const WMap& W, const std::string& a, const std::string& b
     return VD_OK;
 }
 
+// The Detect head's cv2.i.1 and cv3.i.1 (3x3, 64 -> 64 each, on the two halves of det0.i's
+// output) as one grouped conv: output rows [0, 64) read input channels [0, 64), rows
+// [64, 128) channels [64, 128) (fp32 plan: conv_x6_halo_kernel, one 64-wide N tile per
+// group). Same products per output as the two convs: bit-identical.
+int yconv_group(Ctx& c, const WMap& W, const std::string& a, const std::string& b, const std::string& name) {
+    int rc = yconv_pair(c, W, a, b, name);
+    if (rc) return rc;
+    Conv& cv = c.convs[conv_of(c.plate, name)];
+    if (cv.cin != 64 || cv.cout != 128) return vd_set_error(VD_ERR_WEIGHTS, "unsupported Detect head widths");
+    cv.grp_co = 64;
+    cv.grp_ci = 64;
+    return VD_OK;
+}
+
 int yhead(Ctx& c, const WMap& W, const std::string& pre, const std::string& name) {
     int idx;
     int rc = c.make_conv_cat(W, {pre + ".weight"}, {pre + ".bias"}, VD_ACT_NONE, &idx);
@@ -244,8 +258,12 @@ int build_plan(Ctx& c, int ch, int cw, Net& net) {
         Act hd = P.head[i];
         hd.h = ch / (8 << i); hd.w = cw / (8 << i);
         p.conv("det0." + I, p.buf(lv[i]), 0, d0, 0);
-        p.conv("model.22.cv2." + I + ".1", d0, 0, d1, 0);
-        p.conv("model.22.cv3." + I + ".1", d0, 64, d1, 64);
+        if (conv_of(P, "det1." + I) >= 0 && hd.w <= 126 && c.tune.x6_halo) {   // the halo tile's width limit
+            p.conv("det1." + I, d0, 0, d1, 0);
+        } else {
+            p.conv("model.22.cv2." + I + ".1", d0, 0, d1, 0);
+            p.conv("model.22.cv3." + I + ".1", d0, 64, d1, 64);
+        }
         p.conv("box." + I, d1, 0, hd, 0);
         p.conv("cls." + I, d1, 64, hd, 64);
     }
@@ -286,6 +304,9 @@ int vd_build_plate(Ctx& c, const WMap& W) {
         if ((rc = yconv_pair(c, W, "model.22.cv2." + I + ".0", "model.22.cv3." + I + ".0", "det0." + I))) return rc;
         if ((rc = yconv(c, W, "model.22.cv2." + I + ".1", 1))) return rc;
         if ((rc = yconv(c, W, "model.22.cv3." + I + ".1", 1))) return rc;
+        if (c.f32 && c.tune.f32_split == 2 && c.tune.det_group &&
+            (rc = yconv_group(c, W, "model.22.cv2." + I + ".1", "model.22.cv3." + I + ".1", "det1." + I)))
+            return rc;
         if ((rc = yhead(c, W, "model.22.cv2." + I + ".2", "box." + I))) return rc;
         if ((rc = yhead(c, W, "model.22.cv3." + I + ".2", "cls." + I))) return rc;
         if (c.convs[conv_of(P, "box." + I)].cout != 64 || c.convs[conv_of(P, "det0." + I)].cout != 128)

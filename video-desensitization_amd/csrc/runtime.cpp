@@ -405,7 +405,8 @@ int Ctx::add_conv(Net& net, int ci, const Act& x, int xcoff, Act& y, int ycoff, 
     if (res) { op.r = *res; op.rcoff = rcoff; op.rmode = rmode; op.rup = rup; }
     const int oh = (x.h + 2 * cv.pad - cv.kh) / cv.stride + 1;
     const int ow = (x.w + 2 * cv.pad - cv.kw) / cv.stride + 1;
-    if (oh != y.h || ow != y.w || ycoff + cv.cout > y.c || xcoff + cv.cin_pad > x.c)
+    const int xspan = cv.grp_co ? (cv.cout / cv.grp_co - 1) * cv.grp_ci + cv.cin_pad : cv.cin_pad;
+    if (oh != y.h || ow != y.w || ycoff + cv.cout > y.c || xcoff + xspan > x.c)
         return vd_set_error(VD_ERR_ARG, "conv plan shape mismatch (%dx%d vs %dx%d)", oh, ow, y.h, y.w);
     net.ops.push_back(op);
     return VD_OK;
@@ -459,6 +460,7 @@ int Ctx::run_conv_op(const Op& op, int f0, int n, int fam) {
     a.xbound = op.x.bound;
     a.x_exact = (op.x.exact16 && cv.split == 2 && tune.x6_exact) ? 1 : 0;
     a.ymax = op.y.amax ? op.y.amax + f0 : nullptr;
+    a.grp_co = cv.grp_co; a.grp_ci = cv.grp_ci;
     if (cv.split == 2 && !a.xmax && !(a.xbound > 0.f))
         return vd_set_error(VD_ERR_ARG, "internal: conv input without a range (fp16-pair plan)");
     if (a.xmax && op.x.amax == op.y.amax) {
@@ -642,7 +644,7 @@ int Ctx::run_dwconv_op(const Op& op, int f0, int n) {
 
 // max-pool / upsample: the output's per-frame range is within the input's
 static hipError_t amax_follow_impl(const Op& op, int f0, int n, hipStream_t s) {
-    if (!op.y.amax) return hipSuccess;
+    if (!op.y.amax || op.y.amax == op.x.amax) return hipSuccess;   // in-place slices: already covered
     if (!op.x.amax) return op.x.bound > 0.f ? hipErrorInvalidValue : hipSuccess;
     return vd_launch_amax_merge(op.y.amax + f0, op.x.amax + f0, n, s);
 }
@@ -1140,7 +1142,7 @@ int vd_set_option(vd_ctx* h, const char* name, int value) {
         {"plate_s2d", &VdTune::plate_s2d}, {"f32_split", &VdTune::f32_split},
         {"x6_small_k", &VdTune::x6_small_k}, {"x6_small_tiles", &VdTune::x6_small_tiles},
         {"x6_stream", &VdTune::x6_stream}, {"x6_small_k2", &VdTune::x6_small_k2}, {"x6_bn256", &VdTune::x6_bn256},
-        {"x6_exact", &VdTune::x6_exact}, {"x6_mid", &VdTune::x6_mid}, {"block_fuse32", &VdTune::block_fuse32}, {"x6_mf32", &VdTune::x6_mf32}, {"x6_tail", &VdTune::x6_tail}, {"x6_stream_silu", &VdTune::x6_stream_silu}, {"x6_slots", &VdTune::x6_slots}, {"x6_halo", &VdTune::x6_halo}, {"x6_halo_narrow", &VdTune::x6_halo_narrow}, {"x6_adepth", &VdTune::x6_adepth}, {"x6_gemm1x1", &VdTune::x6_gemm1x1}, {"x6_taps", &VdTune::x6_taps}, {"x6_halo_tr", &VdTune::x6_halo_tr}, {"x6_stream256", &VdTune::x6_stream256}, {"plate_stage", &VdTune::plate_stage}, {"ssh_side", &VdTune::ssh_side}, {"face_groups", &VdTune::face_groups}, {"face_group_lag", &VdTune::face_group_lag}, {"plate_s2d32", &VdTune::plate_s2d32},
+        {"x6_exact", &VdTune::x6_exact}, {"x6_mid", &VdTune::x6_mid}, {"block_fuse32", &VdTune::block_fuse32}, {"x6_mf32", &VdTune::x6_mf32}, {"x6_tail", &VdTune::x6_tail}, {"x6_stream_silu", &VdTune::x6_stream_silu}, {"x6_slots", &VdTune::x6_slots}, {"x6_halo", &VdTune::x6_halo}, {"x6_halo_narrow", &VdTune::x6_halo_narrow}, {"x6_adepth", &VdTune::x6_adepth}, {"x6_gemm1x1", &VdTune::x6_gemm1x1}, {"x6_taps", &VdTune::x6_taps}, {"x6_halo_tr", &VdTune::x6_halo_tr}, {"x6_stream256", &VdTune::x6_stream256}, {"plate_stage", &VdTune::plate_stage}, {"ssh_side", &VdTune::ssh_side}, {"face_groups", &VdTune::face_groups}, {"face_group_lag", &VdTune::face_group_lag}, {"plate_s2d32", &VdTune::plate_s2d32}, {"det_group", &VdTune::det_group},
         {"jenc_gpu", &VdTune::jenc_gpu}, {"jdec_gpu", &VdTune::jdec_gpu}, {"jdec_chunk", &VdTune::jdec_chunk}, {"jdec_sync", &VdTune::jdec_sync}, {"jdec_group", &VdTune::jdec_group},
     };
     for (const Opt& o : opts)

@@ -77,6 +77,7 @@ struct VdTune {
     int ssh_side = 0;         // 1: face SSH levels 1-2 (+ heads) on a second stream beside FPN merge / level 0
                               //   (at weight load; measured -0.1 ms/step, but overlapping launches inflate
                               //   the per-launch durations behind `roofline`: off by default)
+    int det_group = 1;        // plan (fp32): the Detect heads' cv2.i.1 + cv3.i.1 as one grouped 3x3 conv
     int plate_s2d32 = 1;      // fp32 plan: the plate stem on the fp16 space-to-depth canvas (with plate_s2d)
     int face_groups = 2;      // face net as G frame groups on G streams (the tails of one group's launches
                               //   fill with the others'; bit-identical; 0 / 1: one launch over the batch)
@@ -153,6 +154,8 @@ struct ConvArgs {
     int x_exact;                                 // fp16 pairs: input values exact in fp16 (integer canvas)
     int mbase;                                   // conv_x6 tiles: first output row of the launch (tail split)
     int dbg;                                     // VdTune::x6_dbg (timing experiments; 0 in production)
+    int grp_co, grp_ci;                          // grouped conv (fp32 halo tiles): output channels n read input
+                                                 //   channels (n / grp_co) * grp_ci + [0, cin); 0: dense
 };
 
 // One fused layer1 bottleneck (block.hip): x [B][H][W][cin] -> y [B][H][W][256],
