@@ -361,8 +361,8 @@ def test_heads_fp32_fused_layer1_matches_unfused(gpu):
         np.testing.assert_array_equal(a, b)
 
 
-@pytest.mark.parametrize("chain", [2, 1])
-def test_heads_fp32_chain_matches_unfused(gpu, chain):
+@pytest.mark.parametrize("chain,gpw", [(2, 1), (1, 1), (2, 2)])
+def test_heads_fp32_chain_matches_unfused(gpu, chain, gpw):
     """fp32 plan, default: layer2's conv3 (+bn3 + identity + relu) and the next block's
     conv1 (+bn1 + relu) as one kernel (chain32.hip: the block output goes to HBM once
     and reaches conv1 from registers, split per (pixel, 64-channel chunk)); option
@@ -374,7 +374,7 @@ def test_heads_fp32_chain_matches_unfused(gpu, chain):
     fr = _frames(3, 1080, 1920, seed=37)
     heads, boxes = {}, {}
     for ch in (chain, 0):
-        ctx = vdmi.Context(precision="fp32", max_batch=3, options={"chain": ch})
+        ctx = vdmi.Context(precision="fp32", max_batch=3, options={"chain": ch, "chain_gpw": gpw})
         try:
             ctx.load_weights(0, face_weights("default"))
             heads[ch] = ctx.forward_heads(fr)

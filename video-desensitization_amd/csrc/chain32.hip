@@ -43,11 +43,13 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 // Shapes: layer2 (t2 128 -> y 512 -> t1' 128; weight chunks of 64 conv3 channels) and
 // layer3 (256 -> 1024 -> 256; chunks of 32). Either way a chunk is 32 KB of W3 rows and
 // 32 KB of W1 columns, and a wave runs 48 + 48 MFMAs on it.
-template <int CM_, int CO_, int NCH_, int GPW_> struct ChainShape {
+template <int CM_, int CO_, int NCH_, int GPW_, int WAVES_ = 8> struct ChainShape {
     static constexpr int CM = CM_, CO = CO_, NCH = NCH_;
-    static constexpr int GPW = GPW_;             // 16-pixel groups per wave (8 groups per super-group)
-    static constexpr int THREADS = 64 * 8 / GPW; // 8 or 4 waves
-    static constexpr int ND = 64 / (8 / GPW);    // weight DMA instructions per wave per chunk
+    static constexpr int GPW = GPW_;             // 16-pixel groups per wave
+    static constexpr int WAVES = WAVES_;
+    static constexpr int SGG = GPW * WAVES;      // groups per super-group (one pass of the weights)
+    static constexpr int THREADS = 64 * WAVES;
+    static constexpr int ND = 64 / WAVES;        // weight DMA instructions per wave per chunk
     static constexpr int KS3 = CM / 32;          // conv3 k-steps
     static constexpr int T3 = NCH / 16;          // conv3 tiles per chunk
     static constexpr int KC = NCH / 32;          // conv1' k-steps per chunk
@@ -59,7 +61,8 @@ template <int CM_, int CO_, int NCH_, int GPW_> struct ChainShape {
     static constexpr int LDS = 2 * STAGE + (2 * CO + 2 * CM) * 4;
     static_assert(W3B == 32768 && W1B == 32768, "64-KB stages");
 };
-using L2Shape = ChainShape<128, 512, 64, 1>;    // 8 waves, 2 per SIMD
+using L2Shape = ChainShape<128, 512, 64, 1>;    // 8 waves of 16 pixels: 128-pixel super-groups
+using L2Shape2 = ChainShape<128, 512, 64, 2>;   // option chain_gpw=2: 32 pixels per wave (~55 VGPRs spill)
 using L3Shape = ChainShape<256, 1024, 32, 1>;
 
 // s_waitcnt vmcnt(N), expcnt / lgkmcnt left alone (gfx9 encoding)
@@ -128,7 +131,8 @@ __global__ __launch_bounds__(S::THREADS, 1) void chain32_kernel(Chain32Args a) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int p = lane & 15, q = lane >> 4;
-    const int nsg = (a.M + 127) / 128;
+    constexpr int SGG = S::SGG;
+    const int nsg = (a.M + 16 * SGG - 1) / (16 * SGG);
     const int G = gridDim.x, sg0 = blockIdx.x;
     if (sg0 >= nsg) return;                                 // uniform over the workgroup
     const int nmine = (nsg - sg0 + G - 1) / G;
@@ -193,15 +197,20 @@ __global__ __launch_bounds__(S::THREADS, 1) void chain32_kernel(Chain32Args a) {
             r[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, (int)(base + 64u * j), 0, 0));
     };
 
-    // wave w takes groups GPW w .. +GPW of each super-group of 8 groups
-    int g0 = sg0 * 8 + GPW * w;
-    u32x4 xr[GPW][KS3][2], idt[2][GPW][T3];
+    // wave w takes groups GPW w .. +GPW of each super-group of SGG groups
+    int g0 = sg0 * SGG + GPW * w;
+    // IDB: the identity of chunk c + 1 loaded during chunk c (two register sets); with two
+    // groups per wave there is room for one set only, loaded at the top of its own chunk
+    constexpr bool IDB = GPW == 1;
+    u32x4 xr[GPW][KS3][2], idt[IDB ? 2 : 1][GPW][T3];
     dma(0, 0);
+    if constexpr (IDB) {
 #pragma unroll
-    for (int u = 0; u < GPW; ++u) load_idt(g0 + u, 0, idt[0][u]);
+        for (int u = 0; u < GPW; ++u) load_idt(g0 + u, 0, idt[0][u]);
+    }
 #pragma unroll 1
     for (int it = 0; it < nmine; ++it) {
-        const int gn = it + 1 < nmine ? (sg0 + (it + 1) * G) * 8 + GPW * w : g0;   // next super-group
+        const int gn = it + 1 < nmine ? (sg0 + (it + 1) * G) * SGG + GPW * w : g0;   // next super-group
         // x of this super-group (GPW = 1: loaded at the end of the previous one)
         if (GPW > 1 || it == 0) {
 #pragma unroll
@@ -243,13 +252,19 @@ __global__ __launch_bounds__(S::THREADS, 1) void chain32_kernel(Chain32Args a) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int c = 2 * cp + h, st = h;               // chunk c in stage c & 1
-            // chunk c landed (younger: identity(c), y(c-1))
-            if (c > 0) __builtin_amdgcn_s_waitcnt(vmcnt_imm(2 * GPW * T3));
+            // chunk c landed (younger: identity(c) when prefetched, y(c-1))
+            if (c > 0) __builtin_amdgcn_s_waitcnt(vmcnt_imm((IDB ? 2 : 1) * GPW * T3));
             lds_barrier();                                  // every wave's DMA of chunk c landed; stage st^1 free
             const int cn = c + 1 < NCHUNK ? c + 1 : 0;
-            dma(cn, st ^ 1);
+            if constexpr (!IDB) {
 #pragma unroll
-            for (int u = 0; u < GPW; ++u) load_idt((cn == 0 ? gn : g0) + u, cn, idt[h ^ 1][u]);
+                for (int u = 0; u < GPW; ++u) load_idt(g0 + u, c, idt[0][u]);
+            }
+            dma(cn, st ^ 1);
+            if constexpr (IDB) {
+#pragma unroll
+                for (int u = 0; u < GPW; ++u) load_idt((cn == 0 ? gn : g0) + u, cn, idt[h ^ 1][u]);
+            }
             const char* w3s = smem + st * STAGE;
             const char* w1s = w3s + W3B;
             // ---- conv3, channels NCH c .. +NCH of the wave's pixels ----
@@ -274,7 +289,8 @@ __global__ __launch_bounds__(S::THREADS, 1) void chain32_kernel(Chain32Args a) {
             }
             // ---- epilogue: bn3 + identity + relu, store y, split for conv1' ----
             // identity(c) (younger: y(c-1), DMA(c+1), identity(c+1))
-            __builtin_amdgcn_s_waitcnt(vmcnt_imm(ND + 2 * GPW * T3));
+            // IDB: younger than identity(c) are y(c-1), DMA(c+1), identity(c+1); else DMA(c+1)
+            __builtin_amdgcn_s_waitcnt(vmcnt_imm(IDB ? ND + 2 * GPW * T3 : ND));
             u32x4 yb[GPW][KC][2];
 #pragma unroll
             for (int u = 0; u < GPW; ++u) {
@@ -287,7 +303,7 @@ __global__ __launch_bounds__(S::THREADS, 1) void chain32_kernel(Chain32Args a) {
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
                         const float v = (acc3[u][j][e] * inv_sa[u]) * s_sc3[ch + e] + s_sh3[ch + e];
-                        float t = v + __uint_as_float(idt[h][u][j][e]);
+                        float t = v + __uint_as_float(idt[IDB ? h : 0][u][j][e]);
                         t = t > 0.f ? t : 0.f;
                         yv[j][e] = t;
                         cmax = fmaxf(cmax, t);
@@ -386,7 +402,7 @@ static hipError_t launch_chain32_t(const Chain32Args& a, hipStream_t s) {
         (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
         return n > 0 ? n : 256;
     }();
-    const int nsg = (a.M + 127) / 128;
+    const int nsg = (a.M + 16 * S::SGG - 1) / (16 * S::SGG);
     const int grid = nsg < cus ? nsg : cus;                 // persistent: one workgroup per CU
     hipLaunchKernelGGL(chain32_kernel<S>, dim3(grid), dim3(S::THREADS), S::LDS + 8 * a.B, s, a);
     return hipGetLastError();
@@ -395,7 +411,8 @@ static hipError_t launch_chain32_t(const Chain32Args& a, hipStream_t s) {
 hipError_t vd_launch_chain32(const Chain32Args& a, hipStream_t s) {
     if (a.M <= 0) return hipSuccess;
     if (a.B <= 0 || a.B > 1024 || a.hw <= 0) return hipErrorInvalidValue;
-    if (a.ld_t2 == 128 && a.ld_res == 512) return launch_chain32_t<L2Shape>(a, s);
+    if (a.ld_t2 == 128 && a.ld_res == 512)
+        return a.gpw == 2 ? launch_chain32_t<L2Shape2>(a, s) : launch_chain32_t<L2Shape>(a, s);
     if (a.ld_t2 == 256 && a.ld_res == 1024) return launch_chain32_t<L3Shape>(a, s);
     return hipErrorInvalidValue;
 }

@@ -77,6 +77,7 @@ struct VdTune {
     int ssh_side = 0;         // 1: face SSH levels 1-2 (+ heads) on a second stream beside FPN merge / level 0
                               //   (at weight load; measured -0.1 ms/step, but overlapping launches inflate
                               //   the per-launch durations behind `roofline`: off by default)
+    int chain_gpw = 1;        // chain32.hip layer2: 16-pixel groups per wave (2: 256-pixel super-groups)
     int det_group = 1;        // plan (fp32): the Detect heads' cv2.i.1 + cv3.i.1 as one grouped 3x3 conv
     int plate_s2d32 = 1;      // fp32 plan: the plate stem on the fp16 space-to-depth canvas (with plate_s2d)
     int face_groups = 2;      // face net as G frame groups on G streams (the tails of one group's launches
@@ -219,6 +220,7 @@ struct Chain32Args {
     int M, B, hw;                         // pixels, frames, pixels per frame
     const unsigned* xmax; float xbound;   // t2's per-frame max |x| slots (frame 0 of this call)
     unsigned* ymax; unsigned* y2max;      // y's / y2's slots (atomic max)
+    int gpw;                              // 16-pixel groups per wave (layer2: 1 or 2)
 };
 
 // Depthwise 3x3 conv (pad 1) + BN + activation, NHWC (dwconv.hip): MobileNetV1 conv_dw.
