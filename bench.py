@@ -461,7 +461,8 @@ def main():
                 "channel by powers of two and split into fp16 pairs, 3 products on v_mfma_f32_16x16x32_f16, f32 "
                 "accumulate; peak = 2500/3)" if precision == "fp32" else
                 "conv_igemm_kernel<float> launches (exact-f32 v_mfma_f32_16x16x4_f32)" if precision == "fp32_exact" else
-                "conv_igemm_kernel<_Float16> launches" if precision == "fp16" else
+                "stem_pool + bottleneck (fused layer1) + chain (layer2) + conv_big + conv_igemm + conv1x1_stream "
+                "launches on _Float16 operands" if precision == "fp16" else
                 "stem_pool + bottleneck (fused layer1) + chain (layer2) + conv_big + conv_igemm + conv1x1_stream")
         r["roofline"] = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
                          "frac": round(ach / peak, 4), "traffic": traffic,

@@ -361,6 +361,24 @@ def test_heads_fp32_fused_layer1_matches_unfused(gpu):
         np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.parametrize("xd", [3, 4])
+def test_heads_fp32_block32_depth_bit_identical(gpu, xd):
+    """block32.hip's stage-1 x register sets (option block32_xd) only move when the
+    loads are issued: heads bit-identical to the default depth."""
+    import vdmi
+    fr = _frames(2, 720, 1280, seed=31)
+    heads = {}
+    for d in (2, xd):
+        ctx = vdmi.Context(precision="fp32", max_batch=2, options={"block32_xd": d})
+        try:
+            ctx.load_weights(0, face_weights("default"))
+            heads[d] = ctx.forward_heads(fr)
+        finally:
+            ctx.close()
+    for a, b in zip(heads[xd], heads[2]):
+        np.testing.assert_array_equal(a, b)
+
+
 @pytest.mark.parametrize("chain,gpw", [(2, 1), (1, 1), (2, 2)])
 def test_heads_fp32_chain_matches_unfused(gpu, chain, gpw):
     """fp32 plan, default: layer2's conv3 (+bn3 + identity + relu) and the next block's

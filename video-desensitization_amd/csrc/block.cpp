@@ -288,6 +288,7 @@ int Ctx::run_block_op(const Op& op, int f0, int n, int fam) {
         a.w1 = bk.w1; a.w2 = bk.w2; a.w3 = bk.w3; a.wd = bk.wd; a.bn = bk.bn;
         a.xmax = op.x.amax + f0;
         a.ymax = op.y.amax + f0;
+        a.xdepth = tune.block32_xd;
         t_begin(fam, fpp * n * a.H * a.W);
         hipError_t e = vd_launch_block32(a, stream);
         t_end();

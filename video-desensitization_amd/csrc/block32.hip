@@ -116,9 +116,13 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
-template <int CIN, bool DS>
+template <int CIN, bool DS, int XD>
 __global__ __launch_bounds__(512, 1) void bottleneck32_kernel(Block32Args a) {
     constexpr int KS1 = CIN / 32;                         // stage-1 k-steps
+    // stage-1 x register sets: k-step s + XD - 1 is issued while s is split and
+    // multiplied (the loads are HBM latency bound: one k-step of MFMA work is a small
+    // fraction of a load's round trip)
+    static_assert(XD >= 2 && XD <= KS1, "stage-1 x depth");
     constexpr int W1PL = KS1 * 64 * 64;                   // one W1 plane
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* lw1 = smem;
@@ -226,14 +230,15 @@ __global__ __launch_bounds__(512, 1) void bottleneck32_kernel(Block32Args a) {
             for (int c = 0; c < 4; ++c) accA[c] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int c = 0; c < 2; ++c) accB[c] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-            u32x4 xa[2][2], xb[2][2];                    // [set][half]: k-step s in set s & 1
-            ldx(rx, offA, offB, 0, xa[0], xb[0]);
+            u32x4 xa[XD][2], xb[XD][2];                  // [set][half]: k-step s in set s % XD
+#pragma unroll
+            for (int s = 0; s + 1 < XD; ++s) ldx(rx, offA, offB, s, xa[s], xb[s]);
 #pragma unroll
             for (int s = 0; s < KS1; ++s) {
-                if (s + 1 < KS1) ldx(rx, offA, offB, s + 1, xa[(s + 1) & 1], xb[(s + 1) & 1]);
+                if (s + XD - 1 < KS1) ldx(rx, offA, offB, s + XD - 1, xa[(s + XD - 1) % XD], xb[(s + XD - 1) % XD]);
                 u32x4 pa[2], pb[2];
-                split8(xa[s & 1][0], xa[s & 1][1], sax, pa);
-                split8(xb[s & 1][0], xb[s & 1][1], sax, pb);
+                split8(xa[s % XD][0], xa[s % XD][1], sax, pa);
+                split8(xb[s % XD][0], xb[s % XD][1], sax, pb);
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
                     u32x4 wf[2];
@@ -487,11 +492,11 @@ __global__ __launch_bounds__(512, 1) void bottleneck32_kernel(Block32Args a) {
     if (ob >= 0 && lane == 0 && om > 0.f) atomicMax(a.ymax + ob, __float_as_uint(om));
 }
 
-template <int CIN, bool DS>
+template <int CIN, bool DS, int XD>
 hipError_t launch(const Block32Args& a, hipStream_t s) {
     constexpr size_t lds = (size_t)2 * (CIN / 32) * 4096 + 2 * T1PL + 2 * T2PL + (256 + 512 * (DS ? 2 : 1)) * 4 + 16;
     static const int cus = [] {
-        (void)hipFuncSetAttribute((const void*)bottleneck32_kernel<CIN, DS>,
+        (void)hipFuncSetAttribute((const void*)bottleneck32_kernel<CIN, DS, XD>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         int dev = 0, n = 256;
         (void)hipGetDevice(&dev);
@@ -500,7 +505,7 @@ hipError_t launch(const Block32Args& a, hipStream_t s) {
     }();
     const int tiles = a.B * a.tiles_x * a.tiles_y;
     const int grid = tiles < cus ? tiles : cus;            // persistent: one workgroup per CU
-    hipLaunchKernelGGL((bottleneck32_kernel<CIN, DS>), dim3(grid), dim3(512), lds, s, a);
+    hipLaunchKernelGGL((bottleneck32_kernel<CIN, DS, XD>), dim3(grid), dim3(512), lds, s, a);
     return hipGetLastError();
 }
 
@@ -514,7 +519,11 @@ bool vd_block32_ok(int cin, bool ds, int h, int w) {
 hipError_t vd_launch_block32(const Block32Args& a, hipStream_t s) {
     if (a.B <= 0) return hipSuccess;
     if (!a.xmax || !a.ymax) return hipErrorInvalidValue;
-    if (a.cin == 256 && !a.ds) return launch<256, false>(a, s);
-    if (a.cin == 64 && a.ds) return launch<64, true>(a, s);
+    if (a.cin == 256 && !a.ds) {
+        if (a.xdepth == 3) return launch<256, false, 3>(a, s);
+        if (a.xdepth == 4) return launch<256, false, 4>(a, s);
+        return launch<256, false, 2>(a, s);
+    }
+    if (a.cin == 64 && a.ds) return launch<64, true, 2>(a, s);
     return hipErrorInvalidValue;
 }

@@ -63,6 +63,7 @@ struct VdTune {
     int mosaic_cells = 32;    //   cell-table kernel: workgroups per frame
     int mosaic_copy = 0;      //   copy-first output: one plain copy pass, the cell kernel writes the box pixels (measured slower)
     int block_fuse = 1;       // plan: fused layer1 bottlenecks (block.hip)
+    int block32_xd = 2;       //   block32 stage-1 x loads in flight + 1 (register sets: 2, 3, 4)
     int block_fuse32 = 1;     // plan, fp32 (fp16 pairs): fused layer1 bottlenecks (block32.hip)
     int chain = 2;            // plan: conv3 + next conv1 as one kernel (chain.hip; fp32: chain32.hip: 2 = layer2,
                               //   1 = layer2 + layer3 -- level on the grouped headline, slower per launch)
@@ -189,6 +190,7 @@ struct Block32Args {
     const float* bn;             // s1 h1 s2 h2 (64 each), s3 h3 (256 each), sd hd (256 each, ds)
     const unsigned* xmax;        // x's per-frame max |x| slots (frame 0 of this call)
     unsigned* ymax;              // y's slots (atomic max)
+    int xdepth;                  // stage-1 x register sets (option block32_xd: 2, 3, 4)
 };
 
 // A bottleneck's conv3 (+ identity, ReLU) and the next bottleneck's conv1 in one
