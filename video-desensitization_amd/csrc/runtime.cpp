@@ -1087,6 +1087,8 @@ int vd_destroy(vd_ctx* h) {
     if (ctx->jpeg_ev) hipEventDestroy(ctx->jpeg_ev);
     for (auto& t : ctx->ev_pool) { hipEventDestroy(t.a); hipEventDestroy(t.b); }
     hipStreamSynchronize(ctx->stream2);
+    for (hipStream_t ps : ctx->stream2_prio)
+        if (ps) { hipStreamSynchronize(ps); hipStreamDestroy(ps); }
     if (ctx->stream_side) {
         hipStreamSynchronize(ctx->stream_side);
         hipStreamDestroy(ctx->stream_side);
@@ -1143,7 +1145,7 @@ int vd_set_option(vd_ctx* h, const char* name, int value) {
         {"plate_s2d", &VdTune::plate_s2d}, {"f32_split", &VdTune::f32_split},
         {"x6_small_k", &VdTune::x6_small_k}, {"x6_small_tiles", &VdTune::x6_small_tiles},
         {"x6_stream", &VdTune::x6_stream}, {"x6_small_k2", &VdTune::x6_small_k2}, {"x6_bn256", &VdTune::x6_bn256},
-        {"x6_exact", &VdTune::x6_exact}, {"x6_mid", &VdTune::x6_mid}, {"block_fuse32", &VdTune::block_fuse32}, {"x6_mf32", &VdTune::x6_mf32}, {"x6_tail", &VdTune::x6_tail}, {"x6_stream_silu", &VdTune::x6_stream_silu}, {"x6_slots", &VdTune::x6_slots}, {"x6_halo", &VdTune::x6_halo}, {"x6_halo_narrow", &VdTune::x6_halo_narrow}, {"x6_adepth", &VdTune::x6_adepth}, {"x6_gemm1x1", &VdTune::x6_gemm1x1}, {"x6_taps", &VdTune::x6_taps}, {"x6_halo_tr", &VdTune::x6_halo_tr}, {"x6_stream256", &VdTune::x6_stream256}, {"plate_stage", &VdTune::plate_stage}, {"ssh_side", &VdTune::ssh_side}, {"face_groups", &VdTune::face_groups}, {"face_group_lag", &VdTune::face_group_lag}, {"plate_s2d32", &VdTune::plate_s2d32}, {"det_group", &VdTune::det_group}, {"chain_gpw", &VdTune::chain_gpw}, {"block32_xd", &VdTune::block32_xd},
+        {"x6_exact", &VdTune::x6_exact}, {"x6_mid", &VdTune::x6_mid}, {"block_fuse32", &VdTune::block_fuse32}, {"x6_mf32", &VdTune::x6_mf32}, {"x6_tail", &VdTune::x6_tail}, {"x6_stream_silu", &VdTune::x6_stream_silu}, {"x6_slots", &VdTune::x6_slots}, {"x6_halo", &VdTune::x6_halo}, {"x6_halo_narrow", &VdTune::x6_halo_narrow}, {"x6_adepth", &VdTune::x6_adepth}, {"x6_gemm1x1", &VdTune::x6_gemm1x1}, {"x6_taps", &VdTune::x6_taps}, {"x6_halo_tr", &VdTune::x6_halo_tr}, {"x6_stream256", &VdTune::x6_stream256}, {"plate_stage", &VdTune::plate_stage}, {"ssh_side", &VdTune::ssh_side}, {"face_groups", &VdTune::face_groups}, {"face_group_lag", &VdTune::face_group_lag}, {"plate_s2d32", &VdTune::plate_s2d32}, {"det_group", &VdTune::det_group}, {"chain_gpw", &VdTune::chain_gpw}, {"block32_xd", &VdTune::block32_xd}, {"plate_prio", &VdTune::plate_prio},
         {"jenc_gpu", &VdTune::jenc_gpu}, {"jdec_gpu", &VdTune::jdec_gpu}, {"jdec_chunk", &VdTune::jdec_chunk}, {"jdec_sync", &VdTune::jdec_sync}, {"jdec_group", &VdTune::jdec_group},
     };
     for (const Opt& o : opts)
@@ -1285,6 +1287,17 @@ int vd_process(vd_ctx* h, const uint8_t* in, uint8_t* out, int n, int fh, int fw
     // Face and plate branches run concurrently (the reference submits them to two
     // threads, combine_detect.py:214-217): plates on stream2, forked/joined by events.
     const bool fork = do_faces && do_plates;
+    hipStream_t plate_stream = ctx->stream2;
+    if (fork && (ctx->tune.plate_prio == 1 || ctx->tune.plate_prio == 2)) {
+        hipStream_t& ps = ctx->stream2_prio[ctx->tune.plate_prio - 1];
+        if (!ps) {
+            int least = 0, greatest = 0;
+            VD_CHECK_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+            VD_CHECK_HIP(hipStreamCreateWithPriority(&ps, hipStreamNonBlocking,
+                                                     ctx->tune.plate_prio == 1 ? greatest : least));
+        }
+        plate_stream = ps;
+    }
     // Both canvases from one read of the frames where the geometry allows (pre.hip
     // letterbox_s2d_pair_kernel); the plate branch then forks after it.
     bool paired = false;
@@ -1311,27 +1324,27 @@ int vd_process(vd_ctx* h, const uint8_t* in, uint8_t* out, int n, int fh, int fw
     }
     if (fork && ctx->fork_at < 0) {
         VD_CHECK_HIP(hipEventRecord(ctx->ev_fork, ctx->stream));
-        VD_CHECK_HIP(hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
+        VD_CHECK_HIP(hipStreamWaitEvent(plate_stream, ctx->ev_fork, 0));
     }
     if (do_faces) {
         if (!paired && (rc = ctx->face_letterbox(d, n, fh, fw, pitch))) return rc;
         if ((rc = ctx->face_forward(n))) return rc;
         if (ctx->fork_at > 0) {
             ctx->fork_at = -1;
-            VD_CHECK_HIP(hipStreamWaitEvent(ctx->stream2, ctx->ev_fork, 0));
+            VD_CHECK_HIP(hipStreamWaitEvent(plate_stream, ctx->ev_fork, 0));
         }
         if ((rc = ctx->face_post(n, fh, fw, tf))) return rc;
     }
     if (do_plates) {
         hipStream_t main = ctx->stream;
-        if (fork) ctx->stream = ctx->stream2;
+        if (fork) ctx->stream = plate_stream;
         rc = vd_plate_forward(*ctx, d, n, fh, fw, pitch, paired);
         if (!rc) rc = vd_plate_post(*ctx, n, fh, fw, tp);
         ctx->stream = main;
         if (rc) return rc;
     }
     if (fork) {
-        VD_CHECK_HIP(hipEventRecord(ctx->ev_join, ctx->stream2));
+        VD_CHECK_HIP(hipEventRecord(ctx->ev_join, plate_stream));
         VD_CHECK_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
     }
     if (do_mosaic) {

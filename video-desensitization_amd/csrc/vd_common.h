@@ -84,6 +84,7 @@ struct VdTune {
     int face_groups = 2;      // face net as G frame groups on G streams (the tails of one group's launches
                               //   fill with the others'; bit-identical; 0 / 1: one launch over the batch)
     int face_group_lag = 0;   //   group g starts after group g - 1's first N ops (0: together)
+    int plate_prio = 0;       // plate branch stream priority (0: default, 1: high, 2: low)
     int plate_stage = 3;      // plate branch starts after face stage N (0: with the stem; 1-4: after
                               //   layerN; 5: after the whole face net). After layer3 its HBM-bound
                               //   convs overlap the MFMA-bound late face layers: 30.8 -> 30.0 ms/step
