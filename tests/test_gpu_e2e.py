@@ -361,6 +361,23 @@ def test_heads_fp32_fused_layer1_matches_unfused(gpu):
         np.testing.assert_array_equal(a, b)
 
 
+def test_heads_fp32_x6_one_bit_identical(gpu):
+    """conv_x6_kernel's 1x1 A loads at row offset + scalar K offset (option x6_one)
+    fetch the same values as the tap-stepping path: heads bit-identical."""
+    import vdmi
+    fr = _frames(2, 720, 1280, seed=41)
+    heads = {}
+    for v in (0, 1):
+        ctx = vdmi.Context(precision="fp32", max_batch=2, options={"x6_one": v})
+        try:
+            ctx.load_weights(0, face_weights("default"))
+            heads[v] = ctx.forward_heads(fr)
+        finally:
+            ctx.close()
+    for a, b in zip(heads[1], heads[0]):
+        np.testing.assert_array_equal(a, b)
+
+
 @pytest.mark.parametrize("xd", [3, 4])
 def test_heads_fp32_block32_depth_bit_identical(gpu, xd):
     """block32.hip's stage-1 x register sets (option block32_xd) only move when the

@@ -510,6 +510,17 @@ __global__ __launch_bounds__(NT, NT == 256 && BM == 256 ? 1 : 2) void conv_x6_ke
     // loaded value -- a select would force a wait right at the load
     const long xbytes = (long)a.B * a.xh * a.xw * a.ldx * 4;
     const __amdgpu_buffer_rsrc_t rsrc_x = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, (int)xbytes, 0x00020000);
+    // 1x1 convs without K padding (option x6_one): K tile kt of a row is bytes
+    // [128 kt, 128 kt + 128) past the row's pixel, so each load is the row's byte offset
+    // (rows past M: out of range) plus a scalar offset -- no per-tile tap stepping
+    const bool one = (a.dbg & 4) && a.kh == 1 && a.kw == 1 && a.pad == 0 &&
+                     a.kpad == a.cin_pad && a.cin_pad % KT == 0;
+    if (one) {
+#pragma unroll
+        for (int i = 0; i < AIT; ++i)
+            pix0[i] = m0 + arow + AROWS * i < a.M ? pix0[i] * 4 + apair * 32 : (int)0x80000000;
+    }
+    int lk = 0;                                     // K tiles loaded so far (one: the scalar offset)
 
     // two register sets of A (8 f32 of each of 2 rows): tile t lives in set t & 1,
     // loaded two iterations before it is split into LDS
@@ -527,6 +538,16 @@ __global__ __launch_bounds__(NT, NT == 256 && BM == 256 ? 1 : 2) void conv_x6_ke
         tdx[h] = t - tdy[h] * a.kw;
     }
     auto load_a = [&](u32x4 (&r)[AIT][2]) {
+        if (one) {
+            const int so = lk * (KT * 4);
+#pragma unroll
+            for (int i = 0; i < AIT; ++i) {
+                r[i][0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc_x, pix0[i], so, 0));
+                r[i][1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc_x, pix0[i] + 16, so, 0));
+            }
+            ++lk;
+            return;
+        }
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             // a chunk past the last tap (K padding) is pushed off the image rows, so
@@ -1785,7 +1806,7 @@ bool vd_conv1x1_x6_dual_ok(const ConvArgs& a) {
 
 hipError_t vd_launch_conv_x6(const ConvArgs& a0, hipStream_t s) {
     ConvArgs a = a0;
-    a.dbg = a.tune ? a.tune->x6_dbg : 0;
+    a.dbg = a.tune ? (a.tune->x6_dbg & 3) | (a.tune->x6_one ? 4 : 0) : 0;
     if (a.grp_co) {   // grouped: the halo form only, one 64-wide N tile per group
         if (a.grp_co != 64 || a.f32_split != 2 || !a.wx3 || !a.tune || !x6_halo_ok(a) || (a.ymax && a.B > kAmaxFrames))
             return hipErrorInvalidValue;

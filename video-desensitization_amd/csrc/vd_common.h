@@ -111,6 +111,7 @@ struct VdTune {
     int x6_slots = 0;         //   workgroup slots of one round (0: the CU count; tests force small values)
     int x6_halo_tr = 2;       // fp32 plan: halo 3x3 tiles with D^T accumulators and the register epilogue
                               //   (1: the 128-256-wide tiles, 2: all; bit-identical)
+    int x6_one = 1;           // fp16 pairs, GEMM tiles: 1x1 convs load A at row offset + scalar K offset (no tap stepping)
     int x6_taps = 1;          // fp32 plan: narrow KxK YOLO layers (K <= 288) on the streaming TAPS form
     int x6_gemm1x1 = 1;       // fp16 pairs: GEMM 1x1 convs on the TR tiles (D^T accumulators, register epilogue;
                               //   2: also the streaming form's K <= 256 layers, 0: off)
@@ -156,7 +157,8 @@ struct ConvArgs {
     const unsigned* x2max; float x2bound;
     int x_exact;                                 // fp16 pairs: input values exact in fp16 (integer canvas)
     int mbase;                                   // conv_x6 tiles: first output row of the launch (tail split)
-    int dbg;                                     // VdTune::x6_dbg (timing experiments; 0 in production)
+    int dbg;                                     // VdTune::x6_dbg (bits 0-1, timing experiments; 0 in production),
+                                                 // bit 2: VdTune::x6_one
     int grp_co, grp_ci;                          // grouped conv (fp32 halo tiles): output channels n read input
                                                  //   channels (n / grp_co) * grp_ci + [0, cin); 0: dense
 };
