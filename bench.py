@@ -80,6 +80,9 @@ def parse(argv=None):
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP event timing")
+    ap.add_argument("--inflight", type=int, default=1,
+                    help="64-frame batches in flight: N contexts (own weights, streams, output and box buffers) take "
+                         "consecutive steps round-robin, so one batch's letterbox / post / mosaic overlap another's convs")
     ap.add_argument("--microbatch", type=int, default=0, help="frames per depth-first backbone micro-batch (0: off)")
     ap.add_argument("--microbatch-stage", type=int, default=2, help="micro-batch the backbone through layer<N>")
     ap.add_argument("--faces", type=int, default=1, help="0: plates only, no mosaic (profiling the plate net)")
@@ -230,12 +233,60 @@ class Mode:
         self.flags = _lib.VD_PROC_FACES | _lib.VD_PROC_MOSAIC | (_lib.VD_PROC_PLATES if plates else 0)
         if not a.faces:
             self.flags = _lib.VD_PROC_PLATES
+        # --inflight N: slots 1..N-1 = further contexts, each on its own stream with its own
+        # output frames and box lists; step i runs on slot i mod N (slot 0 = this context on
+        # the caller's stream). `inflight` is how many take steps (the instrumented pass and
+        # the host / JPEG legs use slot 0 alone).
+        import torch
+        self.torch = torch
+        self.slots = []
+        for _ in range(max(1, a.inflight) - 1):
+            c = vdmi.Context(device=dev.index or 0, precision=precision.split("_")[0],
+                             max_batch=a.batch, options=opts, microbatch=a.microbatch,
+                             microbatch_stage=a.microbatch_stage)
+            c.load_weights(_lib.VD_NET_RETINAFACE, sd)
+            if plates:
+                c.load_weights(_lib.VD_NET_YOLOV8N, weights.yolov8n_state_dict(0))
+            st = torch.cuda.Stream(dev)
+            c.set_stream(st.cuda_stream)
+            self.slots.append((c, st, vdmi.DeviceBoxes(a.batch, 256, dev),
+                               vdmi.DeviceBoxes(a.batch, 256, dev) if plates else None))
+        self.inflight = 1 + len(self.slots)
+        self.ready = [False] * len(self.slots)
+        self.outs = {}
+        self.step = 0
+        self.cur = 0
+
+    def next_slot(self, main):
+        """The slot of the next step -> its torch stream (slot 0: `main`, this context's)."""
+        k = self.step % self.inflight
+        self.step += 1
+        self.cur = k
+        if k == 0:
+            return main
+        st = self.slots[k - 1][1]
+        if not self.ready[k - 1]:                 # once: the frames uploaded on `main` are visible
+            st.wait_stream(main)
+            self.ready[k - 1] = True
+        return st
 
     def process(self, frames, out):
-        self.ctx.process(frames, out, faces=self.faces, plates=self.pboxes, flags=self.flags)
+        """One batch on the current slot (on its stream); returns the face boxes it writes."""
+        if self.cur == 0:
+            self.ctx.process(frames, out, faces=self.faces, plates=self.pboxes, flags=self.flags)
+            return self.faces
+        c, st, fb, pb = self.slots[self.cur - 1]
+        key = (self.cur, out.data_ptr(), tuple(out.shape))
+        if key not in self.outs:
+            with self.torch.cuda.stream(st):
+                self.outs[key] = self.torch.empty_like(out)
+        c.process(frames, self.outs[key], faces=fb, plates=pb, flags=self.flags)
+        return fb
 
     def close(self):
         self.ctx.close()
+        for c, *_ in self.slots:
+            c.close()
 
 
 def main():
@@ -252,7 +303,10 @@ def main():
     if world != a.gpus:
         sys.exit(f"bench.py: WORLD_SIZE={world} but --gpus {a.gpus}")
     if a.launch_probe:
-        print(json.dumps({"rank": rank, "world": world, "local_rank": local}), flush=True)
+        # one write(2) per line: the ranks share the parent's stdout pipe, and a line split
+        # over two writes could interleave with another rank's
+        sys.stdout.flush()
+        os.write(1, (json.dumps({"rank": rank, "world": world, "local_rank": local}) + "\n").encode())
         return
     import torch
     import torch.distributed as dist
@@ -296,25 +350,26 @@ def main():
 
     def run(mode, timed_steps, sync=True):
         for _ in range(timed_steps):
-            recs = []
-            for s, n in batches:
-                fr, o = (frames, out) if n == B else (frames[:n], out[:n])
-                mode.process(fr, o)
-                if dist_on or a.records_out:
-                    recs.append(pack_records(mode.faces.count[:n], mode.faces.xyxy[:n], rec_cap,
-                                             mode.faces.score[:n], mode.faces.label[:n],
-                                             torch.arange(f0 + s, f0 + s + n, dtype=torch.int32, device=dev)))
-            if dist_on:     # per-frame box records -> every rank (RCCL all-gather over xGMI)
-                rec = torch.cat(recs) if recs else torch.zeros((0, 2 + 6 * rec_cap), dtype=torch.int32, device=dev)
-                if rec.shape[0] < per_rank:                       # uneven shards: padding rows (frame = -1)
-                    pad = torch.zeros((per_rank - rec.shape[0], rec.shape[1]), dtype=torch.int32, device=dev)
-                    pad[:, 0] = -1
-                    rec = torch.cat([rec, pad])
-                got = all_gather_records(rec)
-                if mode.precision == a.precision:
-                    gathered["rec"] = got
-            elif recs and mode.precision == a.precision:
-                gathered["rec"] = torch.cat(recs)
+            with torch.cuda.stream(mode.next_slot(stream)):   # --inflight: this step's slot
+                recs = []
+                for s, n in batches:
+                    fr, o = (frames, out) if n == B else (frames[:n], out[:n])
+                    fb = mode.process(fr, o)
+                    if dist_on or a.records_out:
+                        recs.append(pack_records(fb.count[:n], fb.xyxy[:n], rec_cap,
+                                                 fb.score[:n], fb.label[:n],
+                                                 torch.arange(f0 + s, f0 + s + n, dtype=torch.int32, device=dev)))
+                if dist_on:     # per-frame box records -> every rank (RCCL all-gather over xGMI)
+                    rec = torch.cat(recs) if recs else torch.zeros((0, 2 + 6 * rec_cap), dtype=torch.int32, device=dev)
+                    if rec.shape[0] < per_rank:                       # uneven shards: padding rows (frame = -1)
+                        pad = torch.zeros((per_rank - rec.shape[0], rec.shape[1]), dtype=torch.int32, device=dev)
+                        pad[:, 0] = -1
+                        rec = torch.cat([rec, pad])
+                    got = all_gather_records(rec)
+                    if mode.precision == a.precision:
+                        gathered["rec"] = got
+                elif recs and mode.precision == a.precision:
+                    gathered["rec"] = torch.cat(recs)
 
     def timed(mode):
         torch.cuda.synchronize(dev)
@@ -440,7 +495,9 @@ def main():
         ctx.set_option("face_groups", 1)
         ctx.timing(True)
         ctx.timing_reset()
+        nin, mode.inflight, mode.step = mode.inflight, 1, 0   # slot 0 alone
         dt_ev = timed(mode)
+        mode.inflight = nin
         ctx.set_option("face_groups", mode.face_groups)
         r = {"instrumented_ms_per_step": round(dt_ev / a.steps * 1e3, 3)}
         cms, cn, cflop = ctx.timing_read(_lib.FAM_CONV)
@@ -508,7 +565,7 @@ def main():
                    "global_batch": total, "frame": f"{W}x{H}", "net_input": "640x640",
                    "parallelism": f"frame-sharded x{world}" + (
                        f", {'RCCL' if a.backend == 'nccl' else 'gloo'} all-gather of box records" if dist_on else ""),
-                   "plates": plates},
+                   "plates": plates, "batches_in_flight": max(1, a.inflight)},
     }
     for k in ("roofline", "blur_roofline", "faces_per_frame", "instrumented_ms_per_step", "plate_conv",
               "ms_breakdown_per_step", "host_pipeline", "jpeg_pipeline", "jpeg_pipeline_structured"):

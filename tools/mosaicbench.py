@@ -24,6 +24,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--option", action="append", default=[], help="name=value (vd_set_option)")
     a = ap.parse_args()
     import vdmi
     from vdmi import _lib, synth, weights
@@ -31,6 +32,9 @@ def main():
     dev = torch.device("cuda:0")
     ctx = vdmi.Context(device=0, precision="bf16", max_batch=B)
     ctx.load_weights(0, weights.retinaface_state_dict(0))
+    for o in a.option:
+        k, v = o.split("=", 1)
+        ctx.set_option(k, int(v))
     frames = torch.from_numpy(synth.frames(B, H, W, seed=0)).to(dev)
     out = torch.empty_like(frames)
     stream = torch.cuda.current_stream(dev)
