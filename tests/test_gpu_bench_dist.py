@@ -74,3 +74,21 @@ def test_bench_rccl_world1_equals_no_dist(gpu, tmp_path):
     r1, r2 = unpack_records(np.load(one)), unpack_records(np.load(rc))
     assert list(r2) == list(range(6)) and sum(v[3] for v in r1.values()) > 0
     assert r2 == r1
+
+
+@pytest.mark.parametrize("dist", [False, True])
+def test_bench_inflight_records_equal_single_slot(gpu, tmp_path, dist):
+    """bench.py --inflight 2 (two contexts taking consecutive steps on their own streams;
+    the records of a step are packed, and with --force-dist all-gathered over RCCL, on
+    that step's stream): the last step's records (slot 1's) equal a one-slot run's."""
+    from vdmi.dist import unpack_records
+    one = str(tmp_path / "one.npy")
+    two = str(tmp_path / "two.npy")
+    common = [c if c != "1" or i != COMMON.index("--steps") + 1 else "2" for i, c in enumerate(COMMON)]
+    extra = ["--gpus", "1", "--force-dist", "--backend", "nccl"] if dist else []
+    _run([sys.executable, "bench.py"] + extra + common, one)
+    out = _run([sys.executable, "bench.py", "--inflight", "2"] + extra + common, two)
+    assert '"batches_in_flight": 2' in out
+    r1, r2 = unpack_records(np.load(one)), unpack_records(np.load(two))
+    assert list(r2) == list(range(6)) and sum(v[3] for v in r1.values()) > 0
+    assert r2 == r1

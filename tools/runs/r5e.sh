@@ -5,6 +5,8 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 OUT=gpurun_out/r5e
 mkdir -p $OUT
 export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_gpu_bench_dist.py -x -q --timeout 200 --timeout-method thread -k inflight > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
+tail -1 $OUT/tests.log
 B=(python bench.py --steps 20 --warmup 3 --compare "" --no-cpu-baseline --host-pipeline 0)
 for r in 1 2; do
   for n in 1 2 3; do
