@@ -467,7 +467,8 @@ def main():
             src = frames[:B]
         jp = ctx.jpeg_encode(src, quality=95, subsampling=2)
         steps = max(1, min(a.steps, 8))
-        st = GpuJpegStages(ctx, B, mode.flags, quality=95, subsampling=2)
+        copts = {k: int(v) for k, v in (o.split("=", 1) for o in a.option) if k.startswith(("jdec_", "jenc_"))}
+        st = GpuJpegStages(ctx, B, mode.flags, quality=95, subsampling=2, codec_options=copts)
         outj = []
         done = lambda key, res, nf, npl: outj.__setitem__(slice(None), res[0][1])
         try:

@@ -221,7 +221,7 @@ class GpuJpegStages:
     combine_detect.py:204-262 is the loop this replaces (cv2.imread -> detect ->
     mosaic -> cv2.imwrite per batch)."""
 
-    def __init__(self, ctx, max_batch, flags, quality=95, subsampling=2, depth=3, cap=256):
+    def __init__(self, ctx, max_batch, flags, quality=95, subsampling=2, depth=3, cap=256, codec_options=None):
         import torch
         from .context import Context, DeviceBoxes
         self.torch = torch
@@ -231,8 +231,9 @@ class GpuJpegStages:
         self.quality, self.subsampling = int(quality), int(subsampling)
         self.depth = max(2, int(depth))
         dev = self.dev = torch.device(f"cuda:{ctx.device}")
-        self.dctx = Context(device=ctx.device, precision="fp32", max_batch=self.B)
-        self.ectx = Context(device=ctx.device, precision="fp32", max_batch=self.B)
+        # codec_options: vd_set_option switches of both codec contexts (jdec_* / jenc_*)
+        self.dctx = Context(device=ctx.device, precision="fp32", max_batch=self.B, options=codec_options)
+        self.ectx = Context(device=ctx.device, precision="fp32", max_batch=self.B, options=codec_options)
         # the codec contexts run on high-priority streams: their small, latency-bound
         # kernels (entropy-decode passes between host convergence checks) are dispatched
         # ahead of the queued workgroups of the process context's convs
