@@ -476,6 +476,7 @@ def main():
             torch.cuda.synchronize(dev)
             for k in st.stats:
                 st.stats[k] = 0.0
+            st.serial_jobs = 0
             t0 = time.perf_counter()
             st.run(((s, lambda: jp, None) for s in range(steps)), done)
             d = time.perf_counter() - t0
@@ -486,6 +487,7 @@ def main():
         stg = {k: round(v / steps * 1e3, 2) for k, v in st.stats.items()}
         return {"value": round(B * steps / d, 2), "unit": "frames/s", "ms_per_step": round(d / steps * 1e3, 3),
                 "frames": what, "stage_ms_per_step": stg, "decode_sync_passes": passes, "steps": steps,
+                "serial_decode_jobs": st.serial_jobs,
                 "jpeg_bytes_in_per_frame": int(np.mean([len(j) for j in jp])),
                 "jpeg_bytes_out_per_frame": int(np.mean([len(j) for j in outj])),
                 "what": "in-memory q95 4:2:0 JPEG frames -> GPU decode (device entropy decode + HIP IDCT, second "

@@ -208,3 +208,37 @@ def test_batch_process_images_load_failure_aborts(gpu, tmp_path):
                              saver=lambda img, p: saved.__setitem__(os.path.basename(p), img))
     listed = [f for f in os.listdir(tmp_path) if f.endswith(".png")]
     assert len(saved) == listed.index("x5.png")      # every batch listed before the bad frame
+
+
+def test_gpu_jpeg_stages_serial_decode_equals_overlapped(gpu):
+    """GpuJpegStages with decode(i + 1) held back until process(i) has finished
+    (decode_overlap=False; "auto" picks it after a decode with many resynchronisation
+    passes) writes the same JPEG bytes, face counts and job order as the overlapped
+    schedule."""
+    import vdmi
+    from vdmi import _lib, synth, weights
+    from vdmi.pipeline import GpuJpegStages
+    ctx = vdmi.Context(device=0, precision="fp32", max_batch=4)
+    ctx.load_weights(_lib.VD_NET_RETINAFACE, weights.retinaface_state_dict(0))
+    frames = [np.stack([np.repeat(np.repeat(synth.frame(180, 320, 4 * j + k, seed=5), 2, 0), 2, 1) for k in range(4)])
+              for j in range(4)]
+    frames[1] = synth.frames(4, 360, 640, seed=9)                      # noise: many passes
+    import torch
+    blobs = [[bytes(b) for b in ctx.jpeg_encode(torch.from_numpy(f).cuda(), quality=95, subsampling=2)]
+             for f in frames]
+    flags = _lib.VD_PROC_FACES | _lib.VD_PROC_MOSAIC
+    got = {}
+    for mode in (True, False, "auto"):
+        st = GpuJpegStages(ctx, 4, flags, quality=95, subsampling=2, decode_overlap=mode)
+        out = []
+        try:
+            st.run(((j, (lambda j=j: blobs[j]), None) for j in range(len(blobs))),
+                   lambda key, res, nf, npl: out.append((key, nf, [bytes(b) for _, jp in res for b in jp])))
+        finally:
+            st.close()
+        if mode is False:
+            assert st.serial_jobs == len(blobs) - 1
+        got[mode] = out
+    ctx.close()
+    assert [k for k, _, _ in got[True]] == list(range(len(blobs)))
+    assert got[False] == got[True] and got["auto"] == got[True]

@@ -22,8 +22,10 @@ reference's two-thread path unchanged.
 File I/O uses cv2 when importable (combine_detect.py:167-180: imread + BGR->RGB,
 imwrite of RGB->BGR) and Pillow otherwise; ``loader`` / ``saver`` override both.
 """
+import collections
 import logging
 import os
+import threading
 from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
@@ -221,8 +223,22 @@ class GpuJpegStages:
     combine_detect.py:204-262 is the loop this replaces (cv2.imread -> detect ->
     mosaic -> cv2.imwrite per batch)."""
 
-    def __init__(self, ctx, max_batch, flags, quality=95, subsampling=2, depth=3, cap=256, codec_options=None):
+    SERIAL_PASSES = 6
+
+    def __init__(self, ctx, max_batch, flags, quality=95, subsampling=2, depth=3, cap=256, codec_options=None,
+                 decode_overlap=True):
         import torch
+        # decode_overlap: True (default) = decode(i + 1) runs beside process(i); False =
+        # decode(i + 1) starts once process(i) has finished (device order decode, process,
+        # decode, ...; encode still overlaps); "auto" = serial after a decode that needed
+        # more than SERIAL_PASSES resynchronisation passes (noise-like entropy data), else
+        # overlapped. Serial measured level on 2.4-MB noise frames (792-809 vs 800-825
+        # frames/s): the decode stage costs ~50 ms per 64 such frames even with the GPU
+        # to itself, ~70 ms beside process
+        self.decode_overlap = decode_overlap
+        self.last_passes = 0
+        self.proc_queued = {}                           # job i -> Event: process(i) is queued (main thread creates)
+        self.serial_jobs = 0
         from .context import Context, DeviceBoxes
         self.torch = torch
         self.ctx = ctx
@@ -274,6 +290,13 @@ class GpuJpegStages:
             groups.setdefault(key, []).append(k)
         if wait_ev is not None:
             self.s_dec.wait_event(wait_ev)              # process(i - depth) is done with the slot
+        serial = self.decode_overlap is False or (self.decode_overlap == "auto" and
+                                                  self.last_passes > self.SERIAL_PASSES)
+        ev = self.proc_queued.get(i - 1) if i > 0 else None
+        if serial and ev is not None:
+            ev.wait()                                   # process(i - 1) queued (or the run ended)
+            self.s_dec.wait_event(self.ev_proc[(i - 1) % self.depth])
+            self.serial_jobs += 1
         slot = i % self.depth
         out = []
         for (h, w), idx in groups.items():
@@ -288,6 +311,7 @@ class GpuJpegStages:
                     din.copy_(self.torch.from_numpy(host))
             out.append((idx, h, w))
         self.ev_dec[slot].record(self.s_dec)
+        self.last_passes = self.dctx.jdec_passes()
         self.stats["decode"] += time.perf_counter() - t0
         return out
 
@@ -332,6 +356,8 @@ class GpuJpegStages:
             key, fetch, fallback = job
             i = nxt[0]
             nxt[0] += 1
+            self.proc_queued.setdefault(i, threading.Event())
+            self.proc_queued.pop(i - D - 1, None)         # long done
             wait_ev = self.ev_proc[i % D] if i >= D else None
             dec.append((i, key, self.dpool.submit(self._decode, i, fetch, fallback, wait_ev)))
 
@@ -370,14 +396,23 @@ class GpuJpegStages:
                         on_error(key, e)
                         ok.append((None, h, w))
                 self.ev_proc[slot].record(self.torch.cuda.ExternalStream(self.ctx.stream(), device=self.dev))
+                self.proc_queued[i].set()
                 self.stats["queue"] += time.perf_counter() - t2
                 enc.append((i, key, self.epool.submit(self._encode, i, ok)))
                 submit_decode()
         finally:
             for _, _, fut in dec:                        # decodes queued behind a failure: not processed
                 fut.cancel()
+            for ev in list(self.proc_queued.values()):   # release a decode waiting on a job never processed
+                ev.set()
             while enc:
                 finish_one()
+            for _, _, fut in dec:
+                try:
+                    fut.exception()                      # cancelled or finished: nothing left on the thread
+                except Exception:
+                    pass
+            self.proc_queued.clear()
 
     def close(self):
         self.dpool.shutdown()
