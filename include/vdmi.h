@@ -67,8 +67,10 @@ extern "C" {
                               * the f16 matrix cores, f32 accumulate; option
                               * f32_split=1: exact 3-term bf16 split (6 products),
                               * 0: exact-f32 MFMA */
-#define VD_PREC_FP16 2       /* fp16 operands, f32 accumulate (implicit GEMM on   *
-                              * v_mfma_f32_16x16x32_f16; no bf16-only fusions)    */
+#define VD_PREC_FP16 2       /* fp16 operands, f32 accumulate on                  *
+                              * v_mfma_f32_16x16x32_f16; the bf16 plan's fused     *
+                              * kernels (stem + pool, layer1 blocks, layer2        *
+                              * chains, phased 256x256) templated on the 16-bit type */
 
 #define VD_NET_RETINAFACE 0  /* detect_face/retinaface.py, cfg_re50 */
 #define VD_NET_YOLOV8N    1  /* ultralytics YOLOv8n plate detector [ext] */
@@ -156,9 +158,12 @@ int vd_process(vd_ctx* ctx, const uint8_t* in, uint8_t* out, int n, int h, int w
  * libjpeg-turbo's default decode (ISLOW IDCT, fancy upsampling, table YCbCr->RGB),
  * bit-identical. data[i] / sizes[i]: n host JPEG buffers, all h x w with one
  * component layout (1 or 3 components, 1x1 / 2x1 / 2x2 sampling; no progressive /
- * arithmetic coding). Entropy decode on host threads; dequantize + IDCT + upsample +
- * colour in HIP kernels writing `out` (VD_DEVICE: queued on the context stream, the
- * frames feed vd_process directly; VD_HOST: returns when `out` is filled). */
+ * arithmetic coding). Headers parsed and scan segments staged on host threads; the
+ * entropy decode runs on the device (chunked speculative Huffman decode with
+ * resynchronisation passes; option jdec_gpu=0: host Huffman threads, same pixels),
+ * then dequantize + IDCT + upsample + colour in HIP kernels writing `out`
+ * (VD_DEVICE: queued on the context stream, the frames feed vd_process directly;
+ * VD_HOST: returns when `out` is filled). */
 int vd_jpeg_decode(vd_ctx* ctx, const uint8_t* const* data, const size_t* sizes, int n, uint8_t* out,
                    int h, int w, size_t pitch, int where);
 int vd_jpeg_info(const uint8_t* data, size_t size, int* h, int* w, int* comps);
@@ -238,7 +243,9 @@ int vdt_plate_raw(vd_ctx* ctx, const uint8_t* frames, int n, int h, int w, size_
  * recordDeal.read_record2h265_all, combine_detect.py:839).
  * vd_record_repack_h265: the same records rewritten into out_dir with each
  * extracted message's data replaced by the matching access unit of
- * <videos_dir>/<camera>.h265 (or .hevc, processed_<camera>.h265); everything else
+ * <videos_dir>/<camera>_processed.h265 (or _processed.hevc, processed_<camera>.h265:
+ * the desensitised stream, named as combine_detect.py:658 names it; the un-suffixed
+ * <camera>.h265 is the extract step's ORIGINAL stream and is refused); everything else
  * carried over, positions and sizes recomputed (replaces
  * recordDeal.write_allH265_record_all, combine_detect.py:958). Uncompressed
  * records only. */

@@ -25,6 +25,35 @@ def softmax2(conf_logits):
     return np.stack([e0 / s, e1 / s], -1).astype(F32)
 
 
+def softmax2_torch(conf_logits, form="divide"):
+    """retinaface.py:147 with torch's own exp instead of the shared ``vd_expf``
+    restatement -- measurement only (tools/exp_substitution.py). form "divide": the
+    softmax2 formula (max, exp, e_k / sum: the form of torch's CUDA softmax for short
+    rows, which is where the reference runs it -- its CPU path raises at
+    utils_bbox.py's unconditional .cuda()) with ``torch.exp`` (CPU, SLEEF); form
+    "torch": ``torch.softmax`` on the CPU as-is (it multiplies by 1 / sum)."""
+    import torch
+    c = torch.from_numpy(np.ascontiguousarray(conf_logits, F32))
+    if form == "torch":
+        return torch.softmax(c, dim=-1).numpy()
+    m = torch.maximum(c[..., 0], c[..., 1])
+    e0, e1 = torch.exp(c[..., 0] - m), torch.exp(c[..., 1] - m)
+    s = e0 + e1
+    return torch.stack([e0 / s, e1 / s], -1).numpy()
+
+
+def decode_torch(loc, priors, variances=(0.1, 0.2)):
+    """utils_bbox.py:49-59 as the reference writes it, in torch-CPU ops (``torch.exp``):
+    cat(p_xy + loc_xy * v0 * p_wh, p_wh * exp(loc_wh * v1)); xy1 -= wh / 2; xy2 += xy1."""
+    import torch
+    lo = torch.from_numpy(np.ascontiguousarray(loc, F32))
+    p = torch.from_numpy(np.ascontiguousarray(priors, F32))
+    b = torch.cat((p[:, :2] + lo[:, :2] * variances[0] * p[:, 2:], p[:, 2:] * torch.exp(lo[:, 2:] * variances[1])), 1)
+    b[:, :2] -= b[:, 2:] / 2
+    b[:, 2:] += b[:, :2]
+    return b.numpy()
+
+
 def decode(loc, priors, variances=(0.1, 0.2)):
     """utils_bbox.py:49-59. Python-float variances act as float32 scalars.
     cx = p_cx + (l*0.1)*p_w ; w = p_w*exp(l*0.2) ; x1 = cx - w/2 ; x2 = w + x1."""
@@ -87,12 +116,20 @@ def nms_torchvision(boxes, scores, iou_threshold):
     return np.asarray(keep, np.int64)
 
 
-def postprocess_frame(loc, conf_logits, anchors, conf_thres=0.5, nms_iou=0.4):
+def scores_boxes(loc, conf_logits, anchors, torch_exp=None):
+    """(face score [A], decoded boxes [A,4]) of one frame. torch_exp None: vd_expf
+    (the restatement the device twins); "divide" / "torch": torch's exp (decode_torch,
+    softmax2_torch(form)) -- measurement only."""
+    if torch_exp:
+        return softmax2_torch(conf_logits, torch_exp)[:, 1], decode_torch(loc, anchors)
+    return softmax2(conf_logits)[:, 1], decode(loc, anchors)
+
+
+def postprocess_frame(loc, conf_logits, anchors, conf_thres=0.5, nms_iou=0.4, torch_exp=None):
     """One image of face.py:93-115 up to (not including) box correction.
     Returns (anchor_idx [M] int64 in output order, boxes [M,4] float32 normalised,
-    scores [M] float32)."""
-    boxes = decode(loc, anchors)
-    score = softmax2(conf_logits)[:, 1]
+    scores [M] float32). torch_exp: see scores_boxes (measurement only)."""
+    score, boxes = scores_boxes(loc, conf_logits, anchors, torch_exp)
     cand = np.nonzero(score >= F32(conf_thres))[0]      # utils_bbox.py:115-116 (>=, inclusive)
     if cand.size == 0:
         return np.zeros((0,), np.int64), np.zeros((0, 4), F32), np.zeros((0,), F32)

@@ -56,22 +56,25 @@ def nms_log(boxes, score, thr=0.5, iou=0.4):
     return order, by
 
 
-def frame_result(loc, conf, pri, h, w):
-    idx, boxes, _ = obbox.postprocess_frame(loc, conf, pri, 0.5, 0.4)
+def frame_result(loc, conf, pri, h, w, torch_exp=None):
+    idx, boxes, _ = obbox.postprocess_frame(loc, conf, pri, 0.5, 0.4, torch_exp=torch_exp)
     fb = obbox.correct_and_scale(boxes, h, w)
     return idx, obbox.truncate_boxes(fb), fb
 
 
-def explain(oloc, oconf, gloc, gconf, pri, h, w):
+def explain(oloc, oconf, gloc, gconf, pri, h, w, exp_o=None, exp_g=None):
     """First differing decision between oracle heads (o) and GPU heads (g) of one
     frame, or None if keep lists and int boxes agree. Returns a dict with the kind,
-    the anchor(s), both sides' values and |value - threshold| on each side."""
-    io, xo, fo = frame_result(oloc, oconf, pri, h, w)
-    ig, xg, fg = frame_result(gloc, gconf, pri, h, w)
+    the anchor(s), both sides' values and |value - threshold| on each side.
+    exp_o / exp_g: each side's exp (None = vd_expf; "divide" / "torch" = torch's,
+    oracle/bbox.py scores_boxes) -- with the same heads on both sides this explains
+    what the exp substitution alone changes."""
+    io, xo, fo = frame_result(oloc, oconf, pri, h, w, exp_o)
+    ig, xg, fg = frame_result(gloc, gconf, pri, h, w, exp_g)
     if np.array_equal(io, ig) and np.array_equal(xo, xg):
         return None
-    so, sg = obbox.softmax2(oconf)[:, 1], obbox.softmax2(gconf)[:, 1]
-    bo, bg = obbox.decode(oloc, pri), obbox.decode(gloc, pri)
+    so, bo = obbox.scores_boxes(oloc, oconf, pri, exp_o)
+    sg, bg = obbox.scores_boxes(gloc, gconf, pri, exp_g)
     co, cg = set(np.nonzero(so >= F32(0.5))[0].tolist()), set(np.nonzero(sg >= F32(0.5))[0].tolist())
     flips = sorted(co ^ cg)
     if flips:

@@ -242,3 +242,51 @@ def test_gpu_jpeg_stages_serial_decode_equals_overlapped(gpu):
     ctx.close()
     assert [k for k, _, _ in got[True]] == list(range(len(blobs)))
     assert got[False] == got[True] and got["auto"] == got[True]
+
+
+def test_gpu_jpeg_stages_mixed_sizes_counts(gpu):
+    """A job whose frames have two sizes: each size group is processed into its own
+    rows of the slot's box lists, so the job's face / plate totals equal the sum of
+    per-frame vd_process counts (a shared row range would count the last group twice
+    and drop the first), and every frame's JPEG bytes equal the encode of its own
+    processed frame."""
+    import torch
+    import vdmi
+    from vdmi import _lib, synth, weights
+    from vdmi.pipeline import GpuJpegStages
+    ctx = vdmi.Context(device=0, precision="fp32", max_batch=4)
+    ctx.load_weights(_lib.VD_NET_RETINAFACE, weights.retinaface_state_dict(0))
+    ctx.load_weights(_lib.VD_NET_YOLOV8N, weights.yolov8n_state_dict(0))
+    flags = _lib.VD_PROC_FACES | _lib.VD_PROC_PLATES | _lib.VD_PROC_MOSAIC | _lib.VD_PROC_MOSAIC_PLATES
+    jobs = []
+    for j in range(3):
+        fr = []
+        for k in range(4):
+            h, w = ((360, 640), (720, 1280))[(j + k) % 2 if k < 3 else 1]
+            fr.append(np.repeat(np.repeat(synth.frame(h // 2, w // 2, 4 * j + k, seed=21), 2, 0), 2, 1))
+        jobs.append(fr)
+    blobs = [[bytes(ctx.jpeg_encode(torch.from_numpy(f[None]).cuda(), quality=95, subsampling=2)[0]) for f in fr]
+             for fr in jobs]
+    got = []
+    st = GpuJpegStages(ctx, 4, flags, quality=95, subsampling=2)
+    try:
+        st.run(((j, (lambda j=j: blobs[j]), None) for j in range(len(blobs))),
+               lambda key, res, nf, npl: got.append((key, nf, npl, {k: bytes(b) for idx, jp in res
+                                                                     for k, b in zip(idx, jp)})))
+    finally:
+        st.close()
+    assert [g[0] for g in got] == list(range(len(blobs)))
+    tf = tp = 0
+    for (j, nf, npl, jpegs), fr in zip(got, jobs):
+        ef = ep = 0
+        for k, b in enumerate(blobs[j]):
+            dec = torch.from_numpy(ctx.jpeg_decode([b])).cuda()
+            out, faces, plates = ctx.process(dec, flags=flags)
+            ef += int(faces.count.sum())
+            ep += int(plates.count.sum())
+            assert jpegs[k] == bytes(ctx.jpeg_encode(out, quality=95, subsampling=2)[0]), (j, k)
+        assert (nf, npl) == (ef, ep), j
+        tf += ef
+        tp += ep
+    ctx.close()
+    assert tf > 0

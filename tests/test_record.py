@@ -89,7 +89,11 @@ def test_repack_with_own_streams_is_byte_identical(rec):
     from vdmi import record
     tmp, src, blobs, names = rec
     record.read_record2h265_all(str(src), str(tmp / "h265"))
-    n = record.write_allH265_record_all(str(src), str(tmp / "h265" / "hevcs"), str(tmp / "out"))
+    vids = tmp / "videos"
+    vids.mkdir()
+    for f in (tmp / "h265" / "hevcs").iterdir():        # the extracted streams under the processed name
+        (vids / (f.stem + "_processed.h265")).write_bytes(f.read_bytes())
+    n = record.write_allH265_record_all(str(src), str(vids), str(tmp / "out"))
     assert n == len(names)
     for name, data in zip(names, blobs):
         assert (tmp / "out" / name).read_bytes() == data
@@ -118,7 +122,7 @@ def test_repack_replaces_camera_data_and_relayouts(rec):
         first = next(i for i, u in enumerate(units) if orec.is_key_frame(u))
         repl = [au(rng, orec.is_key_frame(u), n=int(rng.integers(5, 400))) for u in units[first:]]
         new_aus[cam] = (first, repl)
-        (vids / f"{cam}.h265").write_bytes(b"".join(repl))
+        (vids / f"{cam}_processed.h265").write_bytes(b"".join(repl))
     record.write_allH265_record_all(str(src), str(vids), str(tmp / "out"))
     seen = {cam: 0 for cam in orig}
     for name, data in zip(names, blobs):
@@ -186,6 +190,19 @@ def test_repack_reference_output_names(rec):
         got = [orec.get(orec.parse(c), 4) for d in names for ch, _, c in orec.messages((tmp / "out" / d).read_bytes())
                if ch == topic]
         assert got[first:] == repl
+
+
+def test_repack_from_extract_dir_is_an_error(rec):
+    """The extract step writes the ORIGINAL streams as hevcs/<camera>.h265: a repack
+    pointed at that directory must refuse (it would write the original frames back),
+    and nothing is written."""
+    import vdmi
+    from vdmi import record
+    tmp, src, blobs, names = rec
+    record.read_record2h265_all(str(src), str(tmp / "h265"))
+    with pytest.raises(vdmi.VdError, match="no desensitised stream"):
+        record.write_allH265_record_all(str(src), str(tmp / "h265" / "hevcs"), str(tmp / "out"))
+    assert not any((tmp / "out" / n).exists() for n in names)
 
 
 def test_repack_short_stream_is_an_error(rec):

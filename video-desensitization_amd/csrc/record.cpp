@@ -506,8 +506,10 @@ extern "C" int vd_record_repack_h265(const char* record_dir, const char* videos_
     std::vector<int> have(kNumTopics, 0);
     for (int t = 0; t < kNumTopics; ++t) {
         if (!count[t]) continue;
-        for (const char* pat : {"%s/%s_processed.h265", "%s/%s_processed.hevc", "%s/%s.h265", "%s/%s.hevc",
-                                "%s/processed_%s.h265"}) {
+        // only the desensitised names: <camera>.h265 is what vd_record_extract_h265 writes
+        // for the ORIGINAL stream (hevcs/<camera>.h265), so accepting it would let a repack
+        // pointed at the extract directory put the original frames back
+        for (const char* pat : {"%s/%s_processed.h265", "%s/%s_processed.hevc", "%s/processed_%s.h265"}) {
             char p[4096];
             std::snprintf(p, sizeof p, pat, videos_dir, camera_of(t).c_str());
             struct stat st;
@@ -523,8 +525,9 @@ extern "C" int vd_record_repack_h265(const char* record_dir, const char* videos_
         }
         if (!have[t])
             return vd_set_error(VD_ERR_ARG, "record: no desensitised stream for camera %s in %s (looked for "
-                                "%s_processed.h265 / .hevc, %s.h265 / .hevc)", camera_of(t).c_str(), videos_dir,
-                                camera_of(t).c_str(), camera_of(t).c_str());
+                                "%s_processed.h265 / .hevc, processed_%s.h265; the un-suffixed %s.h265 is the extracted "
+                                "original and is never used)", camera_of(t).c_str(), videos_dir,
+                                camera_of(t).c_str(), camera_of(t).c_str(), camera_of(t).c_str());
     }
     make_dirs(out_dir);
     std::vector<size_t> next(kNumTopics, 0);

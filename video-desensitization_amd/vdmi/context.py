@@ -60,6 +60,17 @@ class DeviceBoxes:
         return _lib.vd_boxes(self.cap, _lib.VD_DEVICE, self.count.data_ptr(), self.xyxy.data_ptr(),
                              self.xyxy_f.data_ptr(), self.score.data_ptr(), self.label.data_ptr())
 
+    def view(self, start, n):
+        """Frames [start, start + n) as a DeviceBoxes sharing this one's storage (a call
+        writing it fills exactly those rows)."""
+        if start < 0 or n < 0 or start + n > self.n:
+            raise ValueError(f"rows [{start}, {start + n}) outside [0, {self.n})")
+        v = DeviceBoxes.__new__(DeviceBoxes)
+        v.n, v.cap = n, self.cap
+        for k in ("count", "xyxy", "xyxy_f", "score", "label"):
+            setattr(v, k, getattr(self, k)[start:start + n])
+        return v
+
 
 class Context:
     """vd_create/vd_destroy with the reference-facing knobs as keyword args."""

@@ -322,16 +322,16 @@ class GpuJpegStages:
         slot = i % self.depth
         self.s_enc.wait_event(self.ev_proc[slot])
         res, nf, npl = [], 0, 0
-        for idx, h, w in groups:
+        for idx, h, w, off in groups:
             if idx is None:
                 continue
             jp = self.ectx.jpeg_encode(self._buffers(h, w)[1][slot][:len(idx)], quality=self.quality,
                                        subsampling=self.subsampling, copy=False)
             res.append((idx, jp))
-        for idx, h, w in groups:                        # the encode synchronised: process(i) is complete
-            if idx is not None:
-                nf += int(self.faces[slot].count[:len(idx)].sum().item())
-                npl += int(self.plates[slot].count[:len(idx)].sum().item())
+        for idx, h, w, off in groups:                   # the encode synchronised: process(i) is complete
+            if idx is not None:                         # each size group's own rows of the slot's lists
+                nf += int(self.faces[slot].count[off:off + len(idx)].sum().item())
+                npl += int(self.plates[slot].count[off:off + len(idx)].sum().item())
         self.stats["encode"] += time.perf_counter() - t0
         return res, nf, npl
 
@@ -383,18 +383,20 @@ class GpuJpegStages:
                 slot = i % D
                 self.ctx.stream_wait_event(self.ev_dec[slot])
                 ok = []
+                off = 0                                 # size groups write their own box-list rows
                 for idx, h, w in groups:
                     din, dout = self._buffers(h, w)
                     n = len(idx)
                     try:
-                        self.ctx.process(din[slot][:n], dout[slot][:n], faces=self.faces[slot],
-                                         plates=self.plates[slot], flags=self.flags)
-                        ok.append((idx, h, w))
+                        self.ctx.process(din[slot][:n], dout[slot][:n], faces=self.faces[slot].view(off, n),
+                                         plates=self.plates[slot].view(off, n), flags=self.flags)
+                        ok.append((idx, h, w, off))
                     except Exception as e:              # combine_detect.py:226-228: the batch is dropped
                         if on_error is None:
                             raise
                         on_error(key, e)
-                        ok.append((None, h, w))
+                        ok.append((None, h, w, off))
+                    off += n
                 self.ev_proc[slot].record(self.torch.cuda.ExternalStream(self.ctx.stream(), device=self.dev))
                 self.proc_queued[i].set()
                 self.stats["queue"] += time.perf_counter() - t2

@@ -9,8 +9,11 @@ vd_record_repack_h265 in include/vdmi.h).
         its first key frame on); returns the number of camera streams written.
     write_allH265_record_all(record_dir, videos_dir, record_output_dir)
         the same segments rewritten into record_output_dir with the extracted
-        messages' data replaced by the access units of videos_dir/<camera>.h265;
-        returns the number of record files written.
+        messages' data replaced by the access units of the desensitised stream
+        videos_dir/<camera>_processed.h265 (or .hevc, or processed_<camera>.h265;
+        the name combine_detect.py:658 gives it); the extract step's un-suffixed
+        <camera>.h265 holds the ORIGINAL frames and is refused. Returns the number
+        of record files written.
 
 Errors (missing directory, not a CyberRT record, a compressed record) raise
 VdError, as the reference's RecordException surfaces them. Only uncompressed
