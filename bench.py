@@ -277,18 +277,16 @@ class Mode:
             self.ready[k - 1] = True
         return st
 
-    def process(self, frames, out):
-        """One batch on the current slot (on its stream); returns the face boxes it writes."""
+    def current(self, out):
+        """(context, output frames, face boxes, plate boxes) of the current slot."""
         if self.cur == 0:
-            self.ctx.process(frames, out, faces=self.faces, plates=self.pboxes, flags=self.flags)
-            return self.faces
+            return self.ctx, out, self.faces, self.pboxes
         c, st, fb, pb = self.slots[self.cur - 1]
         key = (self.cur, out.data_ptr(), tuple(out.shape))
         if key not in self.outs:
             with self.torch.cuda.stream(st):
                 self.outs[key] = self.torch.empty_like(out)
-        c.process(frames, self.outs[key], faces=fb, plates=pb, flags=self.flags)
-        return fb
+        return c, self.outs[key], fb, pb
 
     def close(self):
         self.ctx.close()
@@ -318,7 +316,7 @@ def main():
     import torch
     import torch.distributed as dist
     from vdmi import _lib, synth, weights
-    from vdmi.dist import all_gather_records, pack_records, shard_range
+    from vdmi.dist import RecordSink, process_frames, shard_range
 
     if a.same_device:
         local = 0
@@ -344,12 +342,18 @@ def main():
         total = world * B
         f0, nloc, per_rank = rank * B, B, B
     batches = [(s, min(B, nloc - s)) for s in range(0, nloc, B)]
-    nhost = min(B, max(nloc, 1))                          # one batch of distinct frames, reused
+    # weak: this rank's own B distinct frames (hash frames f0 ..); strong: one list whose
+    # frame g shows hash frame g mod B, whichever rank holds it (B distinct frames made
+    # on the host once, the rank's whole shard gathered from them in HBM)
+    start = f0 if a.scaling == "weak" else 0
+    nhost = max(1, min(B, nloc if a.scaling == "weak" else total))
     if a.frames_src == "up2":
-        host = np.repeat(np.repeat(synth.frames(nhost, H // 2, W // 2, seed=0, start=f0), 2, axis=1), 2, axis=2)
+        host = np.repeat(np.repeat(synth.frames(nhost, H // 2, W // 2, seed=0, start=start), 2, axis=1), 2, axis=2)
     else:
-        host = synth.frames(nhost, H, W, seed=0, start=f0)
+        host = synth.frames(nhost, H, W, seed=0, start=start)
     frames = torch.from_numpy(host).to(dev)
+    if a.scaling == "strong":
+        frames = frames[torch.arange(f0, f0 + nloc, device=dev) % nhost].contiguous()
     out = torch.empty_like(frames)
     stream = torch.cuda.current_stream(dev)
     rec_cap = 64                      # box record: frame, count, 64 x (box, score, anchor)
@@ -358,25 +362,17 @@ def main():
     def run(mode, timed_steps, sync=True):
         for _ in range(timed_steps):
             with torch.cuda.stream(mode.next_slot(stream)):   # --inflight: this step's slot
-                recs = []
-                for s, n in batches:
-                    fr, o = (frames, out) if n == B else (frames[:n], out[:n])
-                    fb = mode.process(fr, o)
-                    if dist_on or a.records_out:
-                        recs.append(pack_records(fb.count[:n], fb.xyxy[:n], rec_cap,
-                                                 fb.score[:n], fb.label[:n],
-                                                 torch.arange(f0 + s, f0 + s + n, dtype=torch.int32, device=dev)))
-                if dist_on:     # per-frame box records -> every rank (RCCL all-gather over xGMI)
-                    rec = torch.cat(recs) if recs else torch.zeros((0, 2 + 6 * rec_cap), dtype=torch.int32, device=dev)
-                    if rec.shape[0] < per_rank:                       # uneven shards: padding rows (frame = -1)
-                        pad = torch.zeros((per_rank - rec.shape[0], rec.shape[1]), dtype=torch.int32, device=dev)
-                        pad[:, 0] = -1
-                        rec = torch.cat([rec, pad])
-                    got = all_gather_records(rec)
+                ctx, o, fb, pb = mode.current(out)
+                # the product's shard loop (vdmi.dist.process_frames): one vd_process per batch,
+                # each batch's box records packed on the context stream behind it
+                sink = RecordSink(per_rank, cap=rec_cap, device=dev) if (dist_on or a.records_out) else None
+                process_frames(ctx, frames, o, B, f0, sink, mode.flags, fb, pb)
+                if dist_on:     # per-frame box records -> every rank (ONE RCCL all-gather over xGMI)
+                    got = sink.gather()
                     if mode.precision == a.precision:
                         gathered["rec"] = got
-                elif recs and mode.precision == a.precision:
-                    gathered["rec"] = torch.cat(recs)
+                elif sink is not None and mode.precision == a.precision:
+                    gathered["rec"] = sink.rec
 
     def timed(mode):
         torch.cuda.synchronize(dev)
@@ -540,16 +536,21 @@ def main():
                          "traffic_source": tsrc,
                          "measured_with": "face_groups=1 (one launch per layer over the batch, face stream)",
                          "flop_per_step": round(cflop / max(a.steps, 1))}
-        # blur: the output pass (mosaic_out_kernel) dominates; algorithmic bytes per launch =
-        # 2*W*H*3 per frame (out-of-place, reference new-array semantics); the family adds
-        # the cell-table kernel (box prep + walked cell colours)
+        # blur: algorithmic bytes per launch = 2*W*H*3 per frame (out-of-place, reference
+        # new-array semantics). Default (option mosaic_fused=1): ONE launch, the output pass
+        # computes its bands' cell colours itself, so kernel == family; with mosaic_fused=0
+        # the family adds the cell-table kernel (box prep + walked cell colours)
         bach = mbytes / (mms * 1e-3) / 1e9 if mms > 0 else 0.0
         fach = mbytes / ((mms + cms6) * 1e-3) / 1e9 if mms > 0 else 0.0
+        fused = cms6 == 0
         r["blur_roofline"] = {"bound": "hbm", "achieved": round(bach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                               "frac": round(bach / PEAK_HBM_GBS, 4), "avg_launch_ms": round(mms / max(mn, 1), 4),
-                              "bytes_per_launch": round(mbytes / max(mn, 1)), "kernel": "mosaic_out_kernel",
+                              "bytes_per_launch": round(mbytes / max(mn, 1)),
+                              "kernel": "mosaic_out_kernel<FUSED>" if fused else "mosaic_out_kernel<false>",
                               "traffic": blur_traffic, "traffic_source": tsrc,
-                              "family": {"kernels": "mosaic_cell_kernel + mosaic_out_kernel",
+                              "family": {"kernels": "mosaic_out_kernel<FUSED> (one launch: band cells walked in "
+                                                    "its prelude)" if fused else
+                                                    "mosaic_cell_kernel + mosaic_out_kernel<false>",
                                          "achieved": round(fach, 1), "frac": round(fach / PEAK_HBM_GBS, 4),
                                          "avg_ms_per_step": round((mms + cms6) / max(mn, 1), 4)}}
         steps = max(a.steps, 1)

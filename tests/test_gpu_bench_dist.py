@@ -33,17 +33,23 @@ def _run(cmd, out):
     return r.stdout
 
 
-def test_bench_two_ranks_strong_equals_single_rank(gpu, tmp_path):
+@pytest.mark.parametrize("frames,batch", [(6, 6), (13, 4)])
+def test_bench_two_ranks_strong_equals_single_rank(gpu, tmp_path, frames, batch):
+    """(13, 4): shards of 7 / 6 frames in batches of 4 through vdmi.dist.process_frames
+    (a short last batch on each rank, records padded to 7 rows)."""
     from vdmi.dist import unpack_records
     one = str(tmp_path / "one.npy")
     two = str(tmp_path / "two.npy")
-    _run([sys.executable, "bench.py"] + COMMON, one)
+    common = list(COMMON)
+    common[common.index("--frames") + 1] = str(frames)
+    common[common.index("--batch") + 1] = str(batch)
+    _run([sys.executable, "bench.py"] + common, one)
     out = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
                 "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
-                "--backend", "gloo", "--same-device"] + COMMON, two)
+                "--backend", "gloo", "--same-device"] + common, two)
     assert '"n_gpus": 2' in out
     r1, r2 = unpack_records(np.load(one)), unpack_records(np.load(two))
-    assert list(r1) == list(range(6)) and list(r2) == list(range(6))
+    assert list(r1) == list(range(frames)) and list(r2) == list(range(frames))
     assert sum(v[3] for v in r1.values()) > 0
     assert r2 == r1
 

@@ -508,7 +508,7 @@ def test_conv_tr_tiles_bit_identical(gpu, face_ctx_factory, case):
 
 @pytest.mark.parametrize("copy", [0, 1])
 def test_mosaic_output_forms_match_oracle(gpu, copy):
-    """Option mosaic_copy: 1 (default) = copy-first (one plain copy pass, the cell
+    """Option mosaic_copy: 0 (default) = the band output pass; 1 = copy-first (one plain copy pass, the cell
     kernel writes each box cell's owned pixel runs, the band output pass only for
     frames without a cell table); 0 = the band output pass writes every byte. Both
     exact against the oracle on overlapping / nested boxes, > 256 boxes (no cell
@@ -527,5 +527,33 @@ def test_mosaic_output_forms_match_oracle(gpu, copy):
             got = mosaic_frames(frames, boxes, level, ctx=ctx)
             for i in range(4):
                 np.testing.assert_array_equal(got[i], omosaic.mosaic_frame(frames[i], boxes[i], level))
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("fused", [0, 1])
+def test_mosaic_fused_and_two_launch_paths_match_oracle(gpu, fused):
+    """Option mosaic_fused: 1 (default) = one launch, the output pass walks and gathers
+    its bands' cells itself; 0 = cell-table kernel + output pass. Both exact on random
+    boxes (incl. degenerate / off-frame ones), nested chains, a level-2 band whose cells
+    exceed the LDS slice, > MAPBOX boxes in a band and > BOX_FAST boxes in a frame."""
+    import vdmi
+    from vdmi import mosaic_frames, synth
+    ctx = vdmi.Context(precision="bf16", max_batch=4, options={"mosaic_fused": fused})
+    try:
+        rng = np.random.default_rng(17 + fused)
+        frames = synth.frames(3, 1080, 1920, seed=21)
+        cases = [(_rand_boxes(rng, 3, 1080, 1920, 40), 8)]
+        cases.append(([[(10 + 3 * i, 5 + 9 * i, 1900 - 2 * i, 1070 - i) for i in range(25)],
+                       [(100, 200, 1100, 600), (900, 500, 1500, 900)],
+                       [(40 * i, 300 + i, 40 * i + 60, 360 + 2 * i) for i in range(45)]], 2))
+        many = [tuple(int(v) for v in (x, y, x + rng.integers(4, 90), y + rng.integers(4, 90)))
+                for x, y in zip(rng.integers(-20, 1920, 300), rng.integers(-20, 1080, 300))]
+        cases.append(([many, many[:200], []], 8))
+        for boxes, level in cases:
+            got = mosaic_frames(frames, boxes, level, ctx=ctx)
+            for i in range(3):
+                np.testing.assert_array_equal(got[i], omosaic.mosaic_frame(frames[i], boxes[i], level),
+                                              err_msg=f"frame {i} level {level}")
     finally:
         ctx.close()

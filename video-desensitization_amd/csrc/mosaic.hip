@@ -99,6 +99,40 @@ __device__ __forceinline__ bool inside(const MBox& m, int y, int x) {
     return x >= m.x1 && x < m.x2 && y >= m.y1 && y < m.y2;
 }
 
+// ---- the fused output pass's box form: the clipped rectangle (empty when the box
+// is, so neither a band nor a point ever meets it) and sw | sh << 16; resizeNN
+// factors are derived where a map is applied, with prep_box's exact operations.
+__device__ __forceinline__ int4 clip_rect(const MosaicArgs& a, int f, int k, int n0, uint32_t& sz) {
+    const int* src = k < n0 ? a.xy0 + ((size_t)f * a.cap0 + k) * 4 : a.xy1 + ((size_t)f * a.cap1 + (k - n0)) * 4;
+    const int x1 = max(0, src[0]), y1 = max(0, src[1]), x2 = min(a.w, src[2]), y2 = min(a.h, src[3]);
+    if (!(x2 > x1 && y2 > y1)) { sz = 1u | (1u << 16); return make_int4(0, 0, 0, 0); }   // :150-151
+    sz = (uint32_t)max(1, (x2 - x1) / a.level) | ((uint32_t)max(1, (y2 - y1) / a.level) << 16);   // :153-154
+    return make_int4(x1, y1, x2, y2);
+}
+
+__device__ __forceinline__ bool in_rect(const int4 q, int y, int x) {
+    return x >= q.x && x < q.z && y >= q.y && y < q.w;
+}
+
+__device__ __forceinline__ double up_factor(int len, int s) {      // resizeNN up:   dst = len, src = s
+    return __ddiv_rn(1.0, __ddiv_rn((double)len, (double)s));
+}
+__device__ __forceinline__ double down_factor(int len, int s) {    // resizeNN down: dst = s, src = len
+    return __ddiv_rn(1.0, __ddiv_rn((double)s, (double)len));
+}
+
+// apply() of a box given as (rect, sw | sh << 16): bit-identical to prep_box + apply
+__device__ __forceinline__ void apply_rect(const int4 q, uint32_t sz, int& y, int& x) {
+    const int sw = (int)(sz & 0xFFFFu), sh = (int)(sz >> 16);
+    const int bw = q.z - q.x, bh = q.w - q.y;
+    const int ux = min((int)floor(VD_DMUL((double)(x - q.x), up_factor(bw, sw))), sw - 1);
+    const int dx = min((int)floor(VD_DMUL((double)ux, down_factor(bw, sw))), bw - 1);
+    const int uy = min((int)floor(VD_DMUL((double)(y - q.y), up_factor(bh, sh))), sh - 1);
+    const int dy = min((int)floor(VD_DMUL((double)uy, down_factor(bh, sh))), bh - 1);
+    x = q.x + dx;
+    y = q.y + dy;
+}
+
 
 // Highest set bit index < lim in a 256-bit mask, or -1.
 __device__ __forceinline__ int top_below(const uint64_t* m, int lim) {
@@ -394,7 +428,23 @@ __device__ __forceinline__ unsigned byte_mask32(unsigned m4) {
 // Generic path (otherwise): 16-B chunks no band box touches are copied, the
 // rest take each pixel's owner cell from the global table, or walk when the
 // frame has no cell table or the band overflows TB_CAP.
+//
+// FUSED (option mosaic_fused, default 1): one launch per call, no cell kernel and no
+// global cell table. Every workgroup clips its frame's boxes into LDS itself
+// (s_box / s_bsz: a few hundred bytes of L2 reads), and the fast path's prelude
+// computes the band's cell colours in place of the copy from the cell table: per
+// cell of a band box, the down-mapped point, the backward walk over the earlier
+// boxes of the frame (the first earlier box containing the point, then from it,
+// ...: a box containing a point of box k meets box k, so this is the overlap-graph
+// walk of mosaic_cell_kernel), and the 3-byte gather. Bands the fast path does not
+// take (more than MAPBOX boxes, cells past the LDS slice, unaligned rows) and frames
+// of more than BOX_FAST boxes walk per pixel (the whole box list, from the last box).
+template <bool FUSED>
 __global__ __launch_bounds__(256) void mosaic_out_kernel(MosaicArgs a) {
+    __shared__ int4 s_box[FUSED ? BOX_FAST : 1];       // FUSED: the frame's clipped boxes
+    __shared__ uint32_t s_bsz[FUSED ? BOX_FAST : 1];   //        sw | sh << 16
+    __shared__ double s_fdx[FUSED ? MAPBOX : 1];       //        down factors of the band boxes
+    __shared__ double s_fdy[FUSED ? MAPBOX : 1];
     __shared__ int s_idx[TB_CAP];           // table index of each band box (call order)
     __shared__ int4 s_rect[TB_CAP];         // x1, y1, x2, y2 of each band box
     __shared__ int s_rb[MAPBOX][ROWS];      // LDS cell-slice index of (band box, row)'s cell row
@@ -421,17 +471,39 @@ __global__ __launch_bounds__(256) void mosaic_out_kernel(MosaicArgs a) {
     const int nb = frame_boxes(a, f, n0);
     const MBox* table = a.table + (size_t)f * a.tcap;
     const int* cpref = a.cpref + (size_t)f * (BOX_FAST + 1);
-    const bool use_cells = nb <= BOX_FAST && cpref[nb] <= CELL_CAP;
-    if ((a.map_on & 8) && a.vec_ok && use_cells) return;   // copy-first: copy + cell kernel wrote the frame
+    // FUSED: the frame's boxes fit the LDS table (else per-pixel walks over the raw list)
+    const bool use_cells = FUSED ? nb <= BOX_FAST : (nb <= BOX_FAST && cpref[nb] <= CELL_CAP);
+    if (!FUSED && (a.map_on & 8) && a.vec_ok && use_cells) return;   // copy-first: copy + cell kernel wrote the frame
+    if constexpr (FUSED) {
+        if (use_cells)
+            for (int k = tid; k < nb; k += 256) {
+                uint32_t sz;
+                s_box[k] = clip_rect(a, f, k, n0, sz);
+                s_bsz[k] = sz;
+            }
+    }
     if (tid == 0) s_n = 0;
     __syncthreads();
+    // box k of the frame as (rect, sw | sh << 16); invalid boxes have an empty rect
+    auto box_rect = [&](int k, uint32_t& sz) -> int4 {
+        if constexpr (FUSED) {
+            if (use_cells) { sz = s_bsz[k]; return s_box[k]; }
+            return clip_rect(a, f, k, n0, sz);
+        } else {
+            const MBox& m = table[k];
+            sz = (uint32_t)m.sw | ((uint32_t)m.sh << 16);
+            return m.valid ? make_int4(m.x1, m.y1, m.x2, m.y2) : make_int4(0, 0, 0, 0);
+        }
+    };
     // ordered compaction of the boxes intersecting rows [y0, y0+ROWS)
     for (int base = 0; base < nb; base += 256) {
         const int k = base + tid;
         bool hit = false;
+        int4 q = make_int4(0, 0, 0, 0);
         if (k < nb) {
-            const MBox& m = table[k];
-            hit = m.valid && m.y1 < y0 + ROWS && m.y2 > y0;
+            uint32_t sz;
+            q = box_rect(k, sz);
+            hit = q.z > q.x && q.y < y0 + ROWS && q.w > y0;
         }
         const uint64_t bal = __ballot(hit);
         const int wpre = __popcll(bal & ((1ULL << lane) - 1ULL));
@@ -440,9 +512,8 @@ __global__ __launch_bounds__(256) void mosaic_out_kernel(MosaicArgs a) {
         int off = s_n;
         for (int i = 0; i < wid; ++i) off += s_wsum[i];
         if (hit && off + wpre < TB_CAP) {
-            const MBox& m = table[k];
             s_idx[off + wpre] = k;
-            s_rect[off + wpre] = make_int4(m.x1, m.y1, m.x2, m.y2);
+            s_rect[off + wpre] = q;
         }
         __syncthreads();
         if (tid == 0) s_n += s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
@@ -464,18 +535,34 @@ __global__ __launch_bounds__(256) void mosaic_out_kernel(MosaicArgs a) {
         if (wid == 0) {
             int t = lane, nc = 0, bad = 0;
             if (t < nt) {
-                const MBox& m = table[s_idx[t]];
-                const int ya = max(y0, m.y1), yb = min(y0 + rows, m.y2) - 1;
-                const int ulo = min((int)floor(VD_DMUL((double)(ya - m.y1), m.fuy)), m.sh - 1);
-                const int uhi = min((int)floor(VD_DMUL((double)(yb - m.y1), m.fuy)), m.sh - 1);
-                nc = (uhi - ulo + 1) * m.sw;
-                bad = m.sw > 2047;
+                int sw, sh, y1, y2;
+                double fux, fuy;
+                if constexpr (FUSED) {
+                    const int4 q = s_rect[t];
+                    const uint32_t sz = s_bsz[s_idx[t]];
+                    sw = (int)(sz & 0xFFFFu);
+                    sh = (int)(sz >> 16);
+                    y1 = q.y;
+                    y2 = q.w;
+                    fux = up_factor(q.z - q.x, sw);
+                    fuy = up_factor(q.w - q.y, sh);
+                    s_fdx[t] = down_factor(q.z - q.x, sw);
+                    s_fdy[t] = down_factor(q.w - q.y, sh);
+                } else {
+                    const MBox& m = table[s_idx[t]];
+                    sw = m.sw; sh = m.sh; y1 = m.y1; y2 = m.y2; fux = m.fux; fuy = m.fuy;
+                    s_cb[t] = cpref[m.idx];
+                }
+                const int ya = max(y0, y1), yb = min(y0 + rows, y2) - 1;
+                const int ulo = min((int)floor(VD_DMUL((double)(ya - y1), fuy)), sh - 1);
+                const int uhi = min((int)floor(VD_DMUL((double)(yb - y1), fuy)), sh - 1);
+                nc = (uhi - ulo + 1) * sw;
+                bad = sw > 2047;
                 s_uylo[t] = ulo;
-                s_fux[t] = m.fux;
-                s_fuy[t] = m.fuy;
-                s_sw[t] = m.sw;
-                s_sh[t] = m.sh;
-                s_cb[t] = cpref[m.idx];
+                s_fux[t] = fux;
+                s_fuy[t] = fuy;
+                s_sw[t] = sw;
+                s_sh[t] = sh;
             }
             int v = nc;
 #pragma unroll
@@ -510,12 +597,12 @@ __global__ __launch_bounds__(256) void mosaic_out_kernel(MosaicArgs a) {
         }
         if (tid < 64) s_pxb[tid] = px_to_bytes(tid);
         __syncthreads();
-        fast = !s_bad;
+        fast = !s_bad && (!FUSED || s_ltot <= LCELL);   // FUSED: no global cell table to fall back on
     }
 
     if (!fast) {
         const int nchunk = (row_bytes + 15) >> 4;
-        const bool cell_owner = use_cells && !overflow;
+        const bool cell_owner = !FUSED && use_cells && !overflow;
         for (int i = tid; i < rows * nchunk; i += 256) {
             const int r = i / nchunk, c = i - r * nchunk;
             const int y = y0 + r;
@@ -543,7 +630,8 @@ __global__ __launch_bounds__(256) void mosaic_out_kernel(MosaicArgs a) {
                 const int x = bb / 3, ch = bb - 3 * x;
                 if (x != lastx) {
                     lastx = x;
-                    if (cell_owner) {
+                    if (FUSED) {
+                    } else if (cell_owner) {
                         int t = nt - 1;
                         for (; t >= 0; --t) {
                             const int4 q = s_rect[t];
@@ -559,6 +647,16 @@ __global__ __launch_bounds__(256) void mosaic_out_kernel(MosaicArgs a) {
                         }
                     } else {
                         cv = walk_pixel(s_idx, nt - 1, overflow, table, nb, y0, src, a.pitch, y, x);
+                    }
+                    if constexpr (FUSED) {     // the whole list, last box first (box_rect: LDS or raw)
+                        int yy = y, xx = x;
+                        for (int k = nb - 1; k >= 0; --k) {
+                            uint32_t sz;
+                            const int4 q = box_rect(k, sz);
+                            if (in_rect(q, yy, xx)) apply_rect(q, sz, yy, xx);
+                        }
+                        const uint8_t* sp = src + (size_t)yy * a.pitch + xx * 3;
+                        cv = (uint32_t)sp[0] | ((uint32_t)sp[1] << 8) | ((uint32_t)sp[2] << 16);
                     }
                 }
                 drow[bb] = (uint8_t)(cv >> (8 * ch));
@@ -581,12 +679,28 @@ __global__ __launch_bounds__(256) void mosaic_out_kernel(MosaicArgs a) {
         }
         s_rb[t][r] = v;
     }
-    // the band's cell rows of every box: contiguous in the global cell table
+    // the band's cell rows of every box: contiguous in the global cell table, or
+    // (FUSED) walked and gathered here, one thread per cell
     if (lcell_ok)
         for (int i = tid; i < s_ltot; i += 256) {
             int t = 0;
             while (t + 1 < nt && s_lb[t + 1] <= i) ++t;
-            s_lcell[i] = cells[s_cb[t] + s_uylo[t] * s_sw[t] + (i - s_lb[t])];
+            if constexpr (FUSED) {
+                const int c = i - s_lb[t], sw = s_sw[t];
+                const int cr = c / sw, ux = c - cr * sw, uy = s_uylo[t] + cr;
+                const int4 q = s_rect[t];
+                // any pixel of cell (ux, uy) maps to this point under box t
+                int x = q.x + min((int)floor(VD_DMUL((double)ux, s_fdx[t])), q.z - q.x - 1);
+                int y = q.y + min((int)floor(VD_DMUL((double)uy, s_fdy[t])), q.w - q.y - 1);
+                for (int j = s_idx[t] - 1; j >= 0; --j) {
+                    const int4 r = s_box[j];
+                    if (in_rect(r, y, x)) apply_rect(r, s_bsz[j], y, x);
+                }
+                const uint8_t* sp = src + (size_t)y * a.pitch + x * 3;
+                s_lcell[i] = (uint32_t)sp[0] | ((uint32_t)sp[1] << 8) | ((uint32_t)sp[2] << 16);
+            } else {
+                s_lcell[i] = cells[s_cb[t] + s_uylo[t] * s_sw[t] + (i - s_lb[t])];
+            }
         }
     // vector maps of the first dmax row classes (rows of later classes scan per vector):
     // one descriptor per 16-B vector = pixels p0..p0+5 of the row
@@ -844,6 +958,7 @@ hipError_t vd_launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w
         hipLaunchKernelGGL(mosaic_copy_kernel, dim3((h + ROWS - 1) / ROWS, n), dim3(256), 0, s, a);
     }
     if (stages & 1) hipLaunchKernelGGL(mosaic_cell_kernel, dim3(cell_blocks, n), dim3(256), 0, s, a);
-    if (stages & 2) hipLaunchKernelGGL(mosaic_out_kernel, dim3((h + ROWS - 1) / ROWS, n), dim3(256), 0, s, a);
+    if (stages & 2) hipLaunchKernelGGL(mosaic_out_kernel<false>, dim3((h + ROWS - 1) / ROWS, n), dim3(256), 0, s, a);
+    if (stages & 8) hipLaunchKernelGGL(mosaic_out_kernel<true>, dim3((h + ROWS - 1) / ROWS, n), dim3(256), 0, s, a);
     return hipGetLastError();
 }

@@ -957,15 +957,21 @@ int Ctx::launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w, siz
     const int tcap = (cnt0 ? cap0 : 0) + (cnt1 ? cap1 : 0);
     int rc = ensure_staging(&mosaic_table, &mosaic_table_bytes, vd_mosaic_table_bytes(n, tcap) + 64);
     if (rc) return rc;
-    const int map_on = tune.mosaic_map | (tune.mosaic_nt << 1) | (tune.mosaic_copy ? 8 : 0);
-    const bool copy_first = tune.mosaic_copy && (pitch % 16 == 0) && ((uintptr_t)in % 16 == 0) &&
+    const int map_on = tune.mosaic_map | (tune.mosaic_nt << 1) | (tune.mosaic_copy && in != out ? 8 : 0);
+    // copy-first gathers source colours while it writes output pixels: never in place
+    const bool copy_first = tune.mosaic_copy && in != out && (pitch % 16 == 0) && ((uintptr_t)in % 16 == 0) &&
                             ((uintptr_t)out % 16 == 0);
     auto launch = [&](int stages) {
         return vd_launch_mosaic(in, out, n, h, w, pitch, cnt0, xy0, cap0, cnt1, xy1, cap1, level, mosaic_table, stages,
                                 map_on, tune.mosaic_cells, stream);
     };
     hipError_t e = hipSuccess;
-    if (copy_first) {
+    if (tune.mosaic_fused && !copy_first) {
+        // one launch: the output pass walks and gathers its bands' cells itself (family 1)
+        t_begin(1, 2.0 * n * (double)h * w * 3);
+        e = launch(8);
+        t_end();
+    } else if (copy_first) {
         // every byte once by the copy (family 1, the output pass), then the cell kernel's
         // box pixels and the frames without a cell table (family 6)
         t_begin(1, 2.0 * n * (double)h * w * 3);
@@ -1140,7 +1146,7 @@ int vd_set_option(vd_ctx* h, const char* name, int value) {
         {"conv_dual", &VdTune::conv_dual}, {"conv_taps", &VdTune::conv_taps}, {"conv_n192", &VdTune::conv_n192},
         {"conv_small", &VdTune::conv_small}, {"conv_big", &VdTune::conv_big},
         {"conv_big_kmin", &VdTune::conv_big_kmin}, {"stream_ntt", &VdTune::stream_ntt},
-        {"lb_pair", &VdTune::lb_pair}, {"mosaic_map", &VdTune::mosaic_map}, {"mosaic_nt", &VdTune::mosaic_nt}, {"mosaic_cells", &VdTune::mosaic_cells}, {"mosaic_copy", &VdTune::mosaic_copy}, {"block_fuse", &VdTune::block_fuse},
+        {"lb_pair", &VdTune::lb_pair}, {"mosaic_map", &VdTune::mosaic_map}, {"mosaic_nt", &VdTune::mosaic_nt}, {"mosaic_cells", &VdTune::mosaic_cells}, {"mosaic_copy", &VdTune::mosaic_copy}, {"mosaic_fused", &VdTune::mosaic_fused}, {"block_fuse", &VdTune::block_fuse},
         {"chain", &VdTune::chain}, {"stem_pool", &VdTune::stem_pool}, {"ssh_fuse", &VdTune::ssh_fuse},
         {"plate_s2d", &VdTune::plate_s2d}, {"f32_split", &VdTune::f32_split},
         {"x6_small_k", &VdTune::x6_small_k}, {"x6_small_tiles", &VdTune::x6_small_tiles},

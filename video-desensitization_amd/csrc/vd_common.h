@@ -62,6 +62,7 @@ struct VdTune {
     int mosaic_nt = 0;        //   non-temporal output stores (1), and source loads (3)
     int mosaic_cells = 32;    //   cell-table kernel: workgroups per frame
     int mosaic_copy = 0;      //   copy-first output: one plain copy pass, the cell kernel writes the box pixels (measured slower)
+    int mosaic_fused = 1;     //   one launch: the output pass computes its bands' cell colours itself (0: cell kernel + output pass)
     int block_fuse = 1;       // plan: fused layer1 bottlenecks (block.hip)
     int block32_xd = 2;       //   block32 stage-1 x loads in flight + 1 (register sets: 2, 3, 4)
     int block_fuse32 = 1;     // plan, fp32 (fp16 pairs): fused layer1 bottlenecks (block32.hip)

@@ -20,8 +20,16 @@ Differences, all deliberate:
   conv on scaled fp16 pairs -- three f16 MFMA products, f32 accumulation, heads
   within 6e-6 of the torch-CPU fp32 forward; option ``f32_split=0`` runs exact-f32
   MFMA instead; "bf16" / "fp16" trade box parity for 2-3x throughput, see
-  INTEGRATION.md), ``max_batch``, ``device_index``, ``seed``, ``weights``
-  (a state_dict, or "random"), ``options`` (kernel-selection switches).
+  INTEGRATION.md), ``max_batch``, ``device_ids`` / ``device_index``, ``seed``,
+  ``weights`` (a state_dict, or "random"), ``options`` (kernel-selection switches).
+* Devices (face.py:55-56 wraps the net in ``nn.DataParallel``: every forward is
+  split over ALL visible GPUs, the weights re-broadcast each time): one context per
+  device, weights uploaded once each; ``detect_images`` cuts the image list into
+  contiguous shards, one per device, each driven by its own host thread (the C
+  calls release the GIL). Default devices: ``device_ids`` if given ("all" = every
+  visible GPU), else ``[device_index]`` if given, else ``[LOCAL_RANK]`` inside a
+  torchrun rank (one GPU per process: vdmi.dist), else every visible GPU -- what
+  DataParallel uses.
 """
 import os
 
@@ -30,6 +38,37 @@ import numpy as np
 from . import _lib
 from .context import Context
 from .weights import load_reference_checkpoint, retinaface_mnet_state_dict, retinaface_state_dict
+
+
+def resolve_devices(device_ids=None, device_index=None):
+    """The GPUs a drop-in detector spreads over (see the module docstring)."""
+    def visible():
+        try:
+            import torch
+            return max(1, torch.cuda.device_count())
+        except Exception:
+            return 1
+    if device_ids is not None:
+        ids = list(range(visible())) if device_ids == "all" else [int(d) for d in device_ids]
+        if not ids:
+            raise ValueError("device_ids is empty")
+        return ids
+    if device_index is not None:
+        return [int(device_index)]
+    if os.environ.get("LOCAL_RANK") not in (None, ""):
+        return [int(os.environ["LOCAL_RANK"])]
+    return list(range(visible()))
+
+
+def split_run(ctxs, items, fn):
+    """fn(ctx, sub_list) -> list per item, with `items` cut into contiguous shards,
+    one per context, each on its own thread; results in item order."""
+    from .dist import run_on_devices, shard_range
+    if len(ctxs) == 1 or len(items) <= 1:
+        return fn(ctxs[0], items)
+    spans = [shard_range(len(items), len(ctxs), i) for i in range(len(ctxs))]
+    parts = run_on_devices(lambda i, sp: fn(ctxs[i], items[sp[0]:sp[1]]) if sp[1] > sp[0] else [], spans)
+    return [r for p in parts for r in p]
 
 
 class Retinaface(object):
@@ -44,7 +83,8 @@ class Retinaface(object):
         # vdmi extras
         "precision": "fp32",
         "max_batch": 64,
-        "device_index": 0,
+        "device_index": None,
+        "device_ids": None,
         "seed": 0,
         "weights": None,
         "max_boxes": 256,
@@ -64,14 +104,18 @@ class Retinaface(object):
             raise ValueError("Batch inference requires letterbox_image=True for shape alignment.")  # face.py:80
         if not self.cuda:
             raise RuntimeError("vdmi.Retinaface runs on the GPU only (no CPU fallback)")
+        self.device_ids = resolve_devices(self.device_ids, self.device_index)
+        self.device_index = self.device_ids[0]
         try:
             import torch
             self.device = torch.device(f"cuda:{self.device_index}")
         except Exception:  # torch is optional plumbing
             self.device = f"cuda:{self.device_index}"
-        self.ctx = Context(device=self.device_index, precision=self.precision, max_batch=self.max_batch,
-                           input_shape=self.input_shape[:2], confidence=self.confidence, nms_iou=self.nms_iou,
-                           max_boxes=self.max_boxes)
+        self.options = getattr(self, "options", None)
+        self.ctxs = [Context(device=d, precision=self.precision, max_batch=self.max_batch,
+                             input_shape=self.input_shape[:2], confidence=self.confidence, nms_iou=self.nms_iou,
+                             max_boxes=self.max_boxes, options=self.options) for d in self.device_ids]
+        self.ctx = self.ctxs[0]
         self.generate()
 
     def generate(self):
@@ -86,12 +130,17 @@ class Retinaface(object):
             raise FileNotFoundError(f"RetinaFace checkpoint {self.model_path!r} not found (pass model_path=, "
                                     "weights=<state_dict>, or weights='random' for seeded test weights)")
         self.state_dict = sd           # kept for a fused face+plate context (vdmi.pipeline)
-        self.ctx.load_weights(_lib.VD_NET_RETINAFACE, sd)
+        for c in self.ctxs:            # once per device (DataParallel re-broadcasts every forward)
+            c.load_weights(_lib.VD_NET_RETINAFACE, sd)
 
     def detect_boxes(self, images):
-        """Per image: (float32 boxes [M,4], int boxes [M,4], scores [M]) in NMS order."""
+        """Per image: (float32 boxes [M,4], int boxes [M,4], scores [M]) in NMS order;
+        the list is split over the detector's devices (one thread each)."""
         if not isinstance(images, list):
             images = [images]
+        return split_run(self.ctxs, images, self._detect_on)
+
+    def _detect_on(self, ctx, images):
         out = [None] * len(images)
         groups = {}
         for i, img in enumerate(images):
@@ -100,7 +149,7 @@ class Retinaface(object):
             for s in range(0, len(idx), self.max_batch):
                 chunk = idx[s:s + self.max_batch]
                 batch = np.stack([images[i] for i in chunk]) if len(chunk) > 1 else images[chunk[0]][None]
-                boxes = self.ctx.detect(np.ascontiguousarray(batch, np.uint8))
+                boxes = ctx.detect(np.ascontiguousarray(batch, np.uint8))
                 for j, i in enumerate(chunk):
                     xi, xf, sc, _ = boxes.frame(j)
                     out[i] = (xf.copy(), xi.copy(), sc.copy())

@@ -173,6 +173,13 @@ class FramePipeline:
         self.seq += 1
         return (k, n)
 
+    def record(self, ticket, sink, rows, frame_ids):
+        """Pack a submitted batch's box records into `sink` (vdmi.dist.RecordSink) on the
+        compute stream, right behind its vd_process (no host wait)."""
+        k, n = ticket
+        sink.add(rows, frame_ids, self.d_faces[k].view(0, n),
+                 self.d_plates[k].view(0, n) if self.plates else None, stream=self.s_comp)
+
     def collect(self, ticket):
         """Wait for a submitted batch: (out uint8 [n,h,w,3], face_counts [n], face_boxes,
         plate_counts, plate_boxes). `out` and the boxes are views of pinned buffers,
@@ -335,12 +342,16 @@ class GpuJpegStages:
         self.stats["encode"] += time.perf_counter() - t0
         return res, nf, npl
 
-    def run(self, jobs, done, on_error=None):
+    def run(self, jobs, done, on_error=None, on_processed=None):
         """jobs: iterable of (key, fetch, fallback): fetch() -> list of JPEG bytes;
         fallback(k) -> host-decoded RGB frame k or None. done(key, [(frame indices,
         JPEG views)], faces, plates) is called in order on the caller thread. A fetch /
         decode error propagates after every job already processed has been encoded
-        and handed to done; a process error drops that job (on_error(key, exc))."""
+        and handed to done; a process error drops that job (on_error(key, exc)).
+        on_processed(key, frame indices, faces, plates, stream): called on the caller
+        thread right after each size group's vd_process is queued, with DeviceBoxes
+        views holding exactly that group's frames and the context stream they are
+        written on (record packing, vdmi.dist.RecordSink.add)."""
         import collections
         import time
         jobs = iter(jobs)
@@ -388,8 +399,10 @@ class GpuJpegStages:
                     din, dout = self._buffers(h, w)
                     n = len(idx)
                     try:
-                        self.ctx.process(din[slot][:n], dout[slot][:n], faces=self.faces[slot].view(off, n),
-                                         plates=self.plates[slot].view(off, n), flags=self.flags)
+                        fv, pv = self.faces[slot].view(off, n), self.plates[slot].view(off, n)
+                        self.ctx.process(din[slot][:n], dout[slot][:n], faces=fv, plates=pv, flags=self.flags)
+                        if on_processed is not None:
+                            on_processed(key, idx, fv, pv, self.ctx.stream())
                         ok.append((idx, h, w, off))
                     except Exception as e:              # combine_detect.py:226-228: the batch is dropped
                         if on_error is None:
@@ -424,23 +437,25 @@ class GpuJpegStages:
         self.ectx.close()
 
 
-def fused_context(face_detector, plate_detector, batch_size):
-    """One context holding both drop-ins' weights and the face detector's knobs
-    (cached on the face detector)."""
+def fused_context(face_detector, plate_detector, batch_size, device=None):
+    """One context on `device` (default: the face detector's first device) holding both
+    drop-ins' weights and the face detector's knobs (cached on the face detector, one
+    per device)."""
     from .context import Context
-    key = (id(plate_detector), int(batch_size))
-    cache = getattr(face_detector, "_fused", None)
-    if cache and cache[0] == key:
-        return cache[1]
     fd, pd = face_detector, plate_detector
-    ctx = Context(device=fd.device_index, precision=fd.precision, max_batch=max(int(batch_size), 1),
+    dev = fd.device_ids[0] if device is None else int(device)
+    key = (id(plate_detector), int(batch_size), dev)
+    cache = fd.__dict__.setdefault("_fused_ctx", {})
+    if key in cache:
+        return cache[key]
+    ctx = Context(device=dev, precision=fd.precision, max_batch=max(int(batch_size), 1),
                   input_shape=fd.input_shape[:2], confidence=fd.confidence, nms_iou=fd.nms_iou,
                   max_boxes=fd.max_boxes, plate_nc=pd.nc, plate_conf=pd.ctx.cfg.plate_conf,
                   plate_iou=pd.ctx.cfg.plate_iou, plate_max_det=pd.ctx.cfg.plate_max_det,
-                  plate_imgsz=pd.ctx.cfg.plate_imgsz)
+                  plate_imgsz=pd.ctx.cfg.plate_imgsz, options=getattr(fd, "options", None))
     ctx.load_weights(_lib.VD_NET_RETINAFACE, fd.state_dict)
     ctx.load_weights(_lib.VD_NET_YOLOV8N, pd.state_dict)
-    face_detector._fused = (key, ctx)
+    cache[key] = ctx
     return ctx
 
 
@@ -450,16 +465,58 @@ def _is_vdmi_pair(face_detector, plate_detector):
     return isinstance(face_detector, Retinaface) and isinstance(plate_detector, YOLO)
 
 
+def _shard_mode(shard, face_detector, group, fused):
+    """"ranks" (one shard per rank of an initialised process group), "devices" (one
+    shard per device of the vdmi face detector, one thread each) or "none"."""
+    from .dist import world_info
+    if shard in (None, False, "none"):
+        return "none"
+    _, world = world_info(group)
+    if shard == "ranks":
+        return "ranks"
+    if shard == "devices":
+        if not fused:
+            raise ValueError("shard='devices' needs the vdmi Retinaface / YOLO drop-ins")
+        return "devices"
+    if shard != "auto":
+        raise ValueError(f"shard must be 'auto', 'ranks', 'devices' or None, got {shard!r}")
+    if world > 1:
+        return "ranks"
+    if fused and len(getattr(face_detector, "device_ids", [0])) > 1:
+        return "devices"
+    return "none"
+
+
 def batch_process_images(input_dir, output_dir, face_detector, plate_detector, batch_size=16,
                          loader=None, saver=None, mosaic_plates=False, mosaic_level=8, num_workers=6,
-                         gpu_codec="auto", jpeg_quality=95):
+                         gpu_codec="auto", jpeg_quality=95, shard="auto", group=None, records=None):
     """combine_detect.py:183-277. Returns (total_processed, total_faces, total_plates).
 
     gpu_codec ("auto" | True | False): with vdmi detectors, no custom loader/saver and
     only .jpg/.jpeg frames (what the reference's ffmpeg split writes), the frames are
     read as bytes, decoded on the GPU (vd_jpeg_decode), processed and encoded on the
     GPU (vd_jpeg_encode, cv2.imwrite's quality 95 / 4:2:0), so pixels never cross
-    PCIe; the bytes written equal libjpeg-turbo's encode of the processed frames."""
+    PCIe; the bytes written equal libjpeg-turbo's encode of the processed frames.
+
+    shard: how the frames use several GPUs (the reference's nn.DataParallel,
+    face.py:55-56, splits every forward over all of them):
+      "auto"    "ranks" inside an initialised torch.distributed group of more than one
+                rank (torchrun), else "devices" when the vdmi face detector holds more
+                than one device (Retinaface(device_ids=...); by default every visible
+                GPU outside torchrun), else one device;
+      "ranks"   the frame list (sorted: every rank sees the same order) is cut into
+                contiguous shards, rank r processes vdmi.dist.shard_range(n, world, r)
+                on its own GPU and writes those frames, and the ranks exchange the
+                per-frame box records with one RCCL all-gather over xGMI (pixels never
+                leave their GPU); the returned totals cover the WHOLE list, identical
+                on every rank; a failure on any rank raises on every rank;
+      "devices" one process, one context and one host thread per device, each device
+                taking a contiguous shard of the frame list; totals summed;
+      None      one device.
+    records: an optional dict, filled with every frame's boxes as
+    {file name: {"faces": (int boxes, scores, anchors, count), "plates": ... or None}}
+    (vdmi.dist.unpack_sink; the gathered records in "ranks" mode, so every rank gets
+    the whole list's)."""
     logger = logging.getLogger("VideoProcessor.batch_process_images")
     custom_io = loader is not None or saver is not None
     if gpu_codec is True and custom_io:
@@ -468,24 +525,121 @@ def batch_process_images(input_dir, output_dir, face_detector, plate_detector, b
     saver = saver or save_output_image
     image_paths = [os.path.join(input_dir, f) for f in os.listdir(input_dir) if f.lower().endswith(IMAGE_EXT)]
     os.makedirs(output_dir, exist_ok=True)
-    batches = [image_paths[i:i + batch_size] for i in range(0, len(image_paths), batch_size)]
-    io = ThreadPoolExecutor(max_workers=num_workers)
-    try:
-        fused = _is_vdmi_pair(face_detector, plate_detector) and mosaic_level == face_detector.ctx.cfg.mosaic_level
-        all_jpeg = all(p.lower().endswith((".jpg", ".jpeg")) for p in image_paths)
-        if fused and gpu_codec and (gpu_codec is True or (not custom_io and all_jpeg)):
-            res = _gpu_codec_batches(batches, output_dir, face_detector, plate_detector, batch_size, mosaic_plates,
-                                     io, logger, jpeg_quality)
-        elif fused:
-            res = _fused_batches(batches, output_dir, face_detector, plate_detector, batch_size, loader, saver,
-                                 mosaic_plates, io, logger)
-        else:
-            res = _threaded_batches(batches, output_dir, face_detector, plate_detector, loader, saver,
-                                    mosaic_plates, mosaic_level, io, logger)
-    finally:
-        io.shutdown(wait=True)
+    fused = _is_vdmi_pair(face_detector, plate_detector) and mosaic_level == face_detector.ctx.cfg.mosaic_level
+    all_jpeg = all(p.lower().endswith((".jpg", ".jpeg")) for p in image_paths)
+    codec = fused and gpu_codec and (gpu_codec is True or (not custom_io and all_jpeg))
+    mode = _shard_mode(shard, face_detector, group, fused)
+    run = dict(output_dir=output_dir, face_detector=face_detector, plate_detector=plate_detector,
+               batch_size=batch_size, loader=loader, saver=saver, mosaic_plates=mosaic_plates,
+               mosaic_level=mosaic_level, num_workers=num_workers, fused=fused, codec=codec,
+               jpeg_quality=jpeg_quality, logger=logger)
+    want_rec = records is not None or mode == "ranks"
+    if mode == "ranks":
+        res, rec = _rank_shard(sorted(image_paths), group, run)
+    elif mode == "devices":
+        devs = list(face_detector.device_ids)
+        from .dist import run_on_devices, shard_range
+        spans = [shard_range(len(image_paths), len(devs), i) for i in range(len(devs))]
+
+        def one(i, span):
+            b, e = span
+            return _local(image_paths[b:e], b, devs[i], want_rec, run)
+        outs = run_on_devices(one, spans)
+        res = tuple(sum(o[0][k] for o in outs) for k in range(3))
+        rec = _concat_records([o[1] for o in outs]) if want_rec else None
+    else:
+        res, rec = _local(image_paths, 0, None, want_rec, run)
+    if records is not None and rec is not None:
+        from .dist import unpack_sink
+        order = sorted(image_paths) if mode == "ranks" else image_paths   # what the frame ids index
+        for f, v in unpack_sink(rec, _REC_CAP, True).items():
+            records[os.path.basename(order[f])] = v
     logger.info(f"processed {res[0]} images: {res[1]} faces, {res[2]} plates")
     return res
+
+
+_REC_CAP = 64          # boxes per frame carried in a record (vdmi.dist; counts stay complete)
+
+
+def _concat_records(recs):
+    import torch
+    return torch.cat([r.cpu() for r in recs if r is not None]) if any(r is not None for r in recs) else None
+
+
+def _local(paths, first, device, want_rec, run):
+    """One device over `paths` (global frame ids first, first + 1, ...): the fused /
+    GPU-codec / generic loop. Returns ((processed, faces, plates), records or None)."""
+    from .dist import RecordSink
+    fd = run["face_detector"]
+    io = ThreadPoolExecutor(max_workers=run["num_workers"])
+    sink = None
+    if want_rec:
+        dev = None
+        if run["fused"]:
+            dev = f"cuda:{fd.device_ids[0] if device is None else device}"
+        sink = RecordSink(len(paths), cap=_REC_CAP, device=dev, plates=True)
+    ids = {p: (k, first + k) for k, p in enumerate(paths)}
+    bs = run["batch_size"]
+    batches = [paths[i:i + bs] for i in range(0, len(paths), bs)]
+    try:
+        if run["fused"] and run["codec"]:
+            res = _gpu_codec_batches(batches, run["output_dir"], fd, run["plate_detector"], bs,
+                                     run["mosaic_plates"], io, run["logger"], run["jpeg_quality"], device, sink, ids)
+        elif run["fused"]:
+            res = _fused_batches(batches, run["output_dir"], fd, run["plate_detector"], bs, run["loader"],
+                                 run["saver"], run["mosaic_plates"], io, run["logger"], device, sink, ids)
+        else:
+            res = _threaded_batches(batches, run["output_dir"], fd, run["plate_detector"], run["loader"],
+                                    run["saver"], run["mosaic_plates"], run["mosaic_level"], io, run["logger"],
+                                    sink, ids)
+    finally:
+        io.shutdown(wait=True)
+    if sink is not None and sink.device.type == "cuda":
+        import torch
+        torch.cuda.synchronize(sink.device)
+    return res, (sink.rec if sink is not None else None)
+
+
+def _rank_shard(paths, group, run):
+    """This rank's contiguous shard of the (sorted) list through _local, then ONE
+    all-gather of the box records of every rank (RCCL for device records). Totals and
+    records cover the whole list on every rank. Every rank reaches the all-gather,
+    also after a failure of its own (status row), so no rank is left waiting in the
+    collective; then every rank raises."""
+    from .dist import RecordSink, shard_range, world_info
+    rank, world = world_info(group)
+    n = len(paths)
+    b, e = shard_range(n, world, rank)
+    per = -(-n // world) if n else 0
+    fd = run["face_detector"]
+    err, res, rec = None, (0, 0, 0), None
+    try:
+        res, rec = _local(paths[b:e], b, None, True, run)
+    except Exception as ex:      # noqa: BLE001 -- re-raised after the collective
+        err = ex
+    dev = f"cuda:{fd.device_ids[0]}" if run["fused"] else None
+    if dev is None:
+        import torch.distributed as dist
+        if dist.get_backend(group) == "nccl":     # RCCL gathers device tensors only
+            from .dist import local_device
+            dev = f"cuda:{local_device()}"
+    sink = RecordSink(per, cap=_REC_CAP, device=dev, plates=True)
+    if rec is not None and rec.shape[0]:
+        sink.rec[:rec.shape[0]] = rec.to(sink.device)
+    got = sink.gather(group, status=0 if err is None else 1)
+    status = sink.statuses(got)
+    if err is not None:
+        raise err
+    bad = [r for r, v in enumerate(status) if v]
+    if bad:
+        raise RuntimeError(f"batch_process_images: rank(s) {bad} failed; their shards are incomplete")
+    got = got.cpu()
+    w = got.shape[1] // 2
+    ok = got[:, 0] >= 0
+    total = int(ok.sum())
+    faces = int(got[ok, 1].sum())
+    plates = int(got[ok, w + 1].clamp(min=0).sum()) if run["mosaic_plates"] else 0
+    return (total, faces, plates), got
 
 
 def _save_all(futs, logger):
@@ -497,15 +651,16 @@ def _save_all(futs, logger):
 
 
 def _fused_batches(batches, output_dir, face_detector, plate_detector, batch_size, loader, saver, mosaic_plates,
-                   io, logger):
+                   io, logger, device=None, sink=None, ids=None):
     """The vdmi path, streaming: decode batch b+1 (threads) while batch b is on the
     GPU (FramePipeline: one vd_process per batch), collect batch b-1 and hand its
     frames to the encoder threads. Frames of another size get their own pipeline;
     a batch whose inference fails is dropped (combine_detect.py:226-228), a load
-    failure aborts the call (:209-211)."""
+    failure aborts the call (:209-211). sink / ids: box records packed per batch on
+    the compute stream (vdmi.dist.RecordSink; ids: path -> (row, frame id))."""
     totals = [0, 0, 0]
     save_futs = []
-    ctx = fused_context(face_detector, plate_detector, batch_size)
+    ctx = fused_context(face_detector, plate_detector, batch_size, device)
     pipes = {}
     load = lambda files: list(io.map(loader, files))
 
@@ -530,7 +685,8 @@ def _fused_batches(batches, output_dir, face_detector, plate_detector, batch_siz
         for bi, files in enumerate(batches):
             imgs = fut.result()          # a load failure propagates (combine_detect.py:209-211)
             fut = io.submit(load, batches[bi + 1]) if bi + 1 < len(batches) else None
-            pending = _submit_groups(files, imgs, pipes, ctx, batch_size, mosaic_plates, pending, finish, logger)
+            pending = _submit_groups(files, imgs, pipes, ctx, batch_size, mosaic_plates, pending, finish, logger,
+                                     sink, ids)
     finally:
         if fut is not None:
             fut.cancel()
@@ -542,7 +698,7 @@ def _fused_batches(batches, output_dir, face_detector, plate_detector, batch_siz
     return tuple(totals)
 
 
-def _submit_groups(files, imgs, pipes, ctx, batch_size, mosaic_plates, pending, finish, logger):
+def _submit_groups(files, imgs, pipes, ctx, batch_size, mosaic_plates, pending, finish, logger, sink=None, ids=None):
     """Submit one loaded batch (one pipeline per frame size), finishing the previous
     submission behind it; returns the new pending submission."""
     groups = {}
@@ -553,8 +709,11 @@ def _submit_groups(files, imgs, pipes, ctx, batch_size, mosaic_plates, pending, 
             pipes[shape] = FramePipeline(ctx, shape[0], shape[1], max_batch=batch_size, plates=True,
                                          mosaic_plates=mosaic_plates)
         try:
-            cur = (pipes[shape], pipes[shape].submit(np.stack([im for _, im in items])),
-                   [f for f, _ in items])
+            pipe = pipes[shape]
+            ticket = pipe.submit(np.stack([im for _, im in items]))
+            if sink is not None:
+                pipe.record(ticket, sink, [ids[f][0] for f, _ in items], [ids[f][1] for f, _ in items])
+            cur = (pipe, ticket, [f for f, _ in items])
         except Exception as e:       # combine_detect.py:226-228: the batch is dropped
             logger.error(f"parallel inference failed: {e}")
             cur = None
@@ -575,7 +734,7 @@ def _write_bytes(data, path):
 
 
 def _gpu_codec_batches(batches, output_dir, face_detector, plate_detector, batch_size, mosaic_plates, io, logger,
-                       quality):
+                       quality, device=None, sink=None, ids=None):
     """Frame I/O on the GPU (GpuJpegStages): file bytes (reader threads) ->
     vd_jpeg_decode into device frames -> one vd_process (faces | plates | mosaic) ->
     vd_jpeg_encode from device memory -> writer threads, the three stages of
@@ -583,7 +742,7 @@ def _gpu_codec_batches(batches, output_dir, face_detector, plate_detector, batch
     decoder does not take (progressive, other layout) is decoded by the host loader;
     a batch whose inference fails is dropped (combine_detect.py:226-228); a read
     failure aborts the call after the batches before it are written (:209-211)."""
-    ctx = fused_context(face_detector, plate_detector, batch_size)
+    ctx = fused_context(face_detector, plate_detector, batch_size, device)
     flags = _lib.VD_PROC_FACES | _lib.VD_PROC_MOSAIC | _lib.VD_PROC_PLATES
     if mosaic_plates:
         flags |= _lib.VD_PROC_MOSAIC_PLATES
@@ -603,10 +762,14 @@ def _gpu_codec_batches(batches, output_dir, face_detector, plate_detector, batch
         if mosaic_plates:                # the reference's tuple check discards plate boxes otherwise
             totals[2] += npl
 
+    def processed(files, idx, faces, plates, stream):
+        sink.add([ids[files[k]][0] for k in idx], [ids[files[k]][1] for k in idx], faces, plates, stream=stream)
+
     stages = GpuJpegStages(ctx, max(int(batch_size), 1), flags, quality=quality, subsampling=2)
     try:
         stages.run((job(files) for files in batches), done,
-                   on_error=lambda files, e: logger.error(f"parallel inference failed: {e}"))
+                   on_error=lambda files, e: logger.error(f"parallel inference failed: {e}"),
+                   on_processed=processed if sink is not None else None)
     finally:
         stages.close()
         _save_all(save_futs, logger)
@@ -614,7 +777,7 @@ def _gpu_codec_batches(batches, output_dir, face_detector, plate_detector, batch
 
 
 def _threaded_batches(batches, output_dir, face_detector, plate_detector, loader, saver, mosaic_plates,
-                      mosaic_level, io, logger):
+                      mosaic_level, io, logger, sink=None, ids=None):
     """Generic detectors: the reference's two-thread face || plate submission, then
     one batched mosaic launch per same-size group."""
     total = faces = plates = 0
@@ -631,6 +794,7 @@ def _threaded_batches(batches, output_dir, face_detector, plate_detector, loader
                 logger.error(f"parallel inference failed: {e}")
                 continue
         per_frame = []
+        fl, pl = [], []
         for j in range(len(batch_images)):
             face_boxes = _boxes_of(face_results[j])
             if mosaic_plates and not isinstance(plate_results[j], tuple):
@@ -640,8 +804,12 @@ def _threaded_batches(batches, output_dir, face_detector, plate_detector, loader
             boxes = [(int(x1), int(y1), int(x2), int(y2)) for x1, y1, x2, y2 in face_boxes]
             boxes += [(int(x1), int(y1), int(x2), int(y2)) for x1, y1, x2, y2 in plate_boxes]
             per_frame.append(boxes)
+            fl.append(face_boxes)
+            pl.append(plate_boxes)
             faces += len(face_boxes)
             plates += len(plate_boxes)
+        if sink is not None:
+            sink.add_lists([ids[f][0] for f in files], [ids[f][1] for f in files], fl, pl)
         processed = _mosaic_grouped(batch_images, per_frame, mosaic_level)
         for path, img in zip(files, processed):
             out = os.path.join(output_dir, f"processed_{os.path.basename(path)}")

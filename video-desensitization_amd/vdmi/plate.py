@@ -88,21 +88,27 @@ def load_plate_weights(path):
 class YOLO:
     """ultralytics-style plate detector on libvdmi."""
 
-    def __init__(self, model="best.pt", nc=1, weights=None, precision="fp32", max_batch=64, device_index=0,
-                 seed=0, imgsz=640, iou=0.7, max_det=300, names=None):
+    def __init__(self, model="best.pt", nc=1, weights=None, precision="fp32", max_batch=64, device_index=None,
+                 seed=0, imgsz=640, iou=0.7, max_det=300, names=None, device_ids=None):
+        from .face import resolve_devices
         self.nc = nc
         self.names = names or {i: f"plate{i}" if nc > 1 else "plate" for i in range(nc)}
-        self.device_index = device_index
+        # devices as vdmi.Retinaface resolves them (one context each; a call's image list
+        # is split over them, one thread per device)
+        self.device_ids = resolve_devices(device_ids, device_index)
+        self.device_index = self.device_ids[0]
         self.max_batch = max_batch
-        self.ctx = Context(device=device_index, precision=precision, max_batch=max_batch, plate_nc=nc,
-                           plate_iou=iou, plate_max_det=max_det, plate_imgsz=imgsz)
+        self.ctxs = [Context(device=d, precision=precision, max_batch=max_batch, plate_nc=nc, plate_iou=iou,
+                             plate_max_det=max_det, plate_imgsz=imgsz) for d in self.device_ids]
+        self.ctx = self.ctxs[0]
         if isinstance(weights, str) and weights == "random":   # explicit opt-in (tests, bench)
             weights = yolov8n_state_dict(seed, nc)
         elif weights is None:
             weights = load_plate_weights(model)
         self.state_dict = weights      # kept for a fused face+plate context (vdmi.pipeline)
-        self.ctx.load_weights(_lib.VD_NET_YOLOV8N, weights)
-        self.model = _ModelProxy(f"cuda:{device_index}")
+        for c in self.ctxs:
+            c.load_weights(_lib.VD_NET_YOLOV8N, weights)
+        self.model = _ModelProxy(f"cuda:{self.device_index}")
         self._conf = 0.5
 
     def cuda(self):
@@ -112,9 +118,13 @@ class YOLO:
         return self(source, conf=conf, verbose=verbose)
 
     def __call__(self, source, verbose=False, conf=0.5, **_):
+        from .face import split_run
         imgs = source if isinstance(source, list) else [source]
         if abs(conf - self.ctx.cfg.plate_conf) > 1e-12:
             raise ValueError(f"conf={conf} differs from the context's plate_conf={self.ctx.cfg.plate_conf}")
+        return split_run(self.ctxs, imgs, self._detect_on)
+
+    def _detect_on(self, ctx, imgs):
         out = [None] * len(imgs)
         groups = {}
         for i, im in enumerate(imgs):
@@ -123,7 +133,7 @@ class YOLO:
             for s in range(0, len(idx), self.max_batch):
                 chunk = idx[s:s + self.max_batch]
                 batch = np.stack([imgs[i] for i in chunk]) if len(chunk) > 1 else imgs[chunk[0]][None]
-                bx = self.ctx.detect_plates(np.ascontiguousarray(batch, np.uint8))
+                bx = ctx.detect_plates(np.ascontiguousarray(batch, np.uint8))
                 for j, i in enumerate(chunk):
                     _, xf, sc, lab = bx.frame(j)
                     out[i] = Results(imgs[i], Boxes(xf.copy(), sc.copy(), lab.astype(np.float32)), self.names)
