@@ -404,10 +404,19 @@ def main():
             rf = res["roofline"]
             # the timed steps' face-conv FLOPs over their whole wall time (every other
             # kernel of the step, the plate net included, counted against them)
+            # is the headline figure: `achieved` / `frac` describe the timed
+            # steps themselves; the per-launch figure of the face_groups=1 instrumented pass
+            # (HIP events per launch, what the committed rocprof summaries check) is kept
+            # under `per_launch`
             sa = rf["flop_per_step"] / (res["ms_per_step"] * 1e-3) / 1e12
-            rf["step"] = {"achieved": round(sa, 2), "frac": round(sa / rf["peak"], 4),
-                          "face_groups": mode.face_groups,
-                          "what": "face-conv FLOP per step / ms_per_step of the timed steps"}
+            rf["per_launch"] = {k: rf[k] for k in ("achieved", "frac", "avg_launch_ms", "launches",
+                                                   "flop_per_launch", "measured_with")}
+            for k in ("avg_launch_ms", "launches", "flop_per_launch", "measured_with"):
+                del rf[k]
+            rf["achieved"], rf["frac"] = round(sa, 2), round(sa / rf["peak"], 4)
+            rf["measured_with"] = (f"face-conv FLOP per step / ms_per_step of the timed steps (face_groups="
+                                   f"{mode.face_groups}: every other kernel of the step, the plate net included, "
+                                   "counted against the convs)")
         res["faces_per_frame"] = round(float(mode.faces.count.float().mean().item()), 2)
         lists = frame_lists(mode.ctx, batches[-1][1]) if batches and a.faces else []
         if world == 1 and precision == a.precision and a.host_pipeline:
@@ -596,7 +605,7 @@ def main():
                                           "faces_per_frame") if k in m}
             if "roofline" in modes[p]:
                 modes[p]["roofline"] = {k: modes[p]["roofline"][k] for k in ("achieved", "peak", "frac",
-                                                                             "avg_launch_ms")}
+                                                                             "per_launch")}
         if modes:
             res["modes"] = modes
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

@@ -255,13 +255,14 @@ def test_heads_16bit_chain_matches_unfused(gpu, prec):
 @pytest.mark.parametrize("prec", ["bf16", "fp16"])
 def test_heads_16bit_ssh_fused_matches_unfused(gpu, prec):
     """ReLU-SSH plans (cfg_re50) run conv5X5_1 and conv3X3 as one conv with Cout
-    64 + 128 on a 192-wide tile, writing [t5 | c3] of one concat buffer;
+    64 + 128 on a 192-wide tile, writing [t5 | c3] of one concat buffer (ssh_fuse=1);
     option ssh_fuse=0 keeps the two convs. Every output channel sees the same K order
-    and the same rounding: the heads are identical."""
+    and the same rounding: the heads are identical. ssh_fuse=2 (default) fuses
+    conv5X5_2 + conv7X7_2 too: heads within accumulation rounding."""
     import vdmi
     fr = _frames(2, 1080, 1920, seed=13)
     out = {}
-    for fuse in ("1", "0"):
+    for fuse in ("2", "1", "0"):     # 2 (default): conv5X5_2 + conv7X7_2 fused too ([t5|c3|c7|c5|t7])
         ctx = vdmi.Context(precision=prec, max_batch=2, options={"ssh_fuse": int(fuse)})
         try:
             ctx.load_weights(0, face_weights("default"))
@@ -270,6 +271,36 @@ def test_heads_16bit_ssh_fused_matches_unfused(gpu, prec):
             ctx.close()
     for a, b in zip(out["1"], out["0"]):
         np.testing.assert_array_equal(a, b)
+    # ssh_fuse=2 also runs conv5X5_2 + conv7X7_2 as one 128-wide conv: another tile form
+    # (another in-tile K order) than the two 64-wide convs -- within f32 accumulation
+    # rounding of the 16-bit plan, not bit-identical (measured max |diff| ~1e-6)
+    for a, b in zip(out["2"], out["0"]):
+        assert _rel(a, b) < 1e-4, _rel(a, b)
+
+
+def test_heads_fp32_ssh_fuse_levels(gpu):
+    """fp32 pair plan: ssh_fuse=2 (default; conv5X5_2 + conv7X7_2 as one conv, so
+    conv7x7_3 splits t7 with the concat buffer's per-frame scale) against 1 and 0:
+    heads within the f32 head bound of each other, identical keep lists and int boxes."""
+    import vdmi
+    fr = _frames(3, 1080, 1920, seed=31)
+    heads, boxes = {}, {}
+    for fuse in (2, 1, 0):
+        ctx = vdmi.Context(precision="fp32", max_batch=3, options={"ssh_fuse": fuse})
+        try:
+            ctx.load_weights(0, face_weights("default"))
+            heads[fuse] = ctx.forward_heads(fr)
+            r = ctx.detect(fr)
+            boxes[fuse] = [(r.frame(b)[3].copy(), r.frame(b)[0].copy()) for b in range(3)]
+        finally:
+            ctx.close()
+    assert sum(len(x[0]) for x in boxes[0]) > 0
+    for f in (2, 1):
+        for a, b in zip(heads[f], heads[0]):
+            assert np.abs(a - b).max() <= 6e-6 * (np.abs(b).max() + 1e-6), (f, np.abs(a - b).max())
+        for (ka, xa), (kb, xb) in zip(boxes[f], boxes[0]):
+            np.testing.assert_array_equal(ka, kb)
+            np.testing.assert_array_equal(xa, xb)
 
 
 def test_heads_fp32_dual_downsample_bit_identical(gpu):
@@ -359,6 +390,32 @@ def test_heads_fp32_fused_layer1_matches_unfused(gpu):
     assert sum(len(x) for x in boxes[0]) > 0
     for a, b in zip(boxes[1], boxes[0]):
         np.testing.assert_array_equal(a, b)
+
+
+def test_heads_fp32_block32_pipe_matches_one_group(gpu):
+    """layer1.1 / layer1.2 on the producer / consumer block (option block32_pipe=1,
+    default: stage 1 + 3 on waves 0-3, stage 2 on waves 4-7, f32 t1 / t2 split by the
+    consumer) against the one-group block (0): the same products and operand scales,
+    stage 2 summed in one accumulator instead of two K halves -- heads within f32
+    rounding, identical keep lists and int boxes."""
+    import vdmi
+    fr = _frames(4, 1080, 1920, seed=37)
+    heads, boxes = {}, {}
+    for pipe in (1, 0):
+        ctx = vdmi.Context(precision="fp32", max_batch=4, options={"block32_pipe": pipe})
+        try:
+            ctx.load_weights(0, face_weights("default"))
+            heads[pipe] = ctx.forward_heads(fr)
+            r = ctx.detect(fr)
+            boxes[pipe] = [(r.frame(b)[3].copy(), r.frame(b)[0].copy()) for b in range(4)]
+        finally:
+            ctx.close()
+    for a, b in zip(heads[1], heads[0]):
+        assert np.abs(a - b).max() <= 6e-6 * (np.abs(b).max() + 1e-6), np.abs(a - b).max() / np.abs(b).max()
+    assert sum(len(x[0]) for x in boxes[0]) > 0
+    for (ka, xa), (kb, xb) in zip(boxes[1], boxes[0]):
+        np.testing.assert_array_equal(ka, kb)
+        np.testing.assert_array_equal(xa, xb)
 
 
 def test_heads_fp32_x6_one_bit_identical(gpu):

@@ -336,6 +336,7 @@ BLOCK_CASES = [
     (2, 16, 32, 256, False),     # whole 8x16 tiles
     (1, 21, 37, 256, False),     # ragged tiles on both axes
     (2, 13, 18, 64, True),       # layer1.0: cin 64 + downsample branch
+    (8, 96, 160, 256, False),    # 960 tiles: several per persistent workgroup (block32_pipe's buffers cycle)
     (1, 8, 5, 64, True),         # narrower than one tile
     (1, 40, 40, 256, False),     # 3x3 halo across interior tile seams
 ]

@@ -289,6 +289,8 @@ int Ctx::run_block_op(const Op& op, int f0, int n, int fam) {
         a.xmax = op.x.amax + f0;
         a.ymax = op.y.amax + f0;
         a.xdepth = tune.block32_xd;
+        a.pipe = tune.block32_pipe;
+        a.dbg = tune.block32_dbg;
         t_begin(fam, fpp * n * a.H * a.W);
         hipError_t e = vd_launch_block32(a, stream);
         t_end();

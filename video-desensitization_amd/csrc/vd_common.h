@@ -65,6 +65,8 @@ struct VdTune {
     int mosaic_fused = 1;     //   one launch: the output pass computes its bands' cell colours itself (0: cell kernel + output pass)
     int block_fuse = 1;       // plan: fused layer1 bottlenecks (block.hip)
     int block32_xd = 2;       //   block32 stage-1 x loads in flight + 1 (register sets: 2, 3, 4)
+    int block32_dbg = 0;      //   timing-only: skip block32 stages (bits: 1 S1, 2 S2, 4 S3 math, 8 S3 stores, 16 S3 identity)
+    int block32_pipe = 1;     //   block32 (CIN 256): producer / consumer wave groups on consecutive tiles (0: one group)
     int block_fuse32 = 1;     // plan, fp32 (fp16 pairs): fused layer1 bottlenecks (block32.hip)
     int chain = 2;            // plan: conv3 + next conv1 as one kernel (chain.hip; fp32: chain32.hip: 2 = layer2,
                               //   1 = layer2 + layer3 -- level on the grouped headline, slower per launch)
@@ -195,6 +197,8 @@ struct Block32Args {
     const unsigned* xmax;        // x's per-frame max |x| slots (frame 0 of this call)
     unsigned* ymax;              // y's slots (atomic max)
     int xdepth;                  // stage-1 x register sets (option block32_xd: 2, 3, 4)
+    int pipe;                    // producer / consumer wave groups on consecutive tiles (option block32_pipe)
+    int dbg;                     // timing-only stage skips of the one-group kernel (option block32_dbg; wrong results)
 };
 
 // A bottleneck's conv3 (+ identity, ReLU) and the next bottleneck's conv1 in one
