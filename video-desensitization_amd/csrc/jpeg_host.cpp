@@ -103,7 +103,9 @@ int build_huff(Huff& hf, const uint8_t* counts, const uint8_t* syms, int nsym) {
 
 inline int u16be(const uint8_t* p) { return (p[0] << 8) | p[1]; }
 
-int parse(const uint8_t* d, size_t n, Info& j) {
+// header_only: stop at the scan header (frame size / layout known, the entropy-coded
+// segment neither delimited nor checked): what vd_jpeg_info needs
+int parse(const uint8_t* d, size_t n, Info& j, bool header_only = false) {
     if (n < 4 || d[0] != 0xFF || d[1] != 0xD8) return vd_set_error(VD_ERR_ARG, "jpeg: no SOI marker");
     size_t o = 2;
     bool sof = false;
@@ -188,8 +190,18 @@ int parse(const uint8_t* d, size_t n, Info& j) {
             }
             o += len;
             j.scan = d + o;
+            if (header_only) return VD_OK;
+            // the segment ends at the first marker that is neither a stuffed 0xFF00 nor RSTn:
+            // memchr to each 0xFF instead of a byte loop
             size_t e = o;
-            while (e + 1 < n && !(d[e] == 0xFF && d[e + 1] != 0x00 && !(d[e + 1] >= 0xD0 && d[e + 1] <= 0xD7))) ++e;
+            while (e + 1 < n) {
+                const void* ff = memchr(d + e, 0xFF, n - 1 - e);
+                if (!ff) { e = n - 1; break; }
+                e = (size_t)((const uint8_t*)ff - d);
+                const uint8_t nx = d[e + 1];
+                if (nx != 0x00 && !(nx >= 0xD0 && nx <= 0xD7)) break;
+                ++e;
+            }
             j.scan_len = e - o;
             o = e;
             continue;
@@ -585,7 +597,7 @@ int device_entropy(Ctx* ctx, const std::vector<Info>& info, int n, JpegArgs& a, 
 extern "C" int vd_jpeg_info(const uint8_t* data, size_t size, int* h, int* w, int* comps) {
     if (!data) return vd_set_error(VD_ERR_ARG, "null data");
     Info j;
-    int rc = parse(data, size, j);
+    int rc = parse(data, size, j, true);
     if (rc) return rc;
     if (h) *h = j.h;
     if (w) *w = j.w;

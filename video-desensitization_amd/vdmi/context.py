@@ -36,11 +36,18 @@ def _frames_arg(frames):
 
 
 def jpeg_info(data):
-    """(h, w, components) of a baseline JPEG (host-only parse, no GPU)."""
+    """(h, w, components) of a baseline JPEG (host-only parse, no GPU). A bytes object is
+    parsed in place (its own buffer: no copy -- a 2.4-MB frame copied under the GIL for every
+    frame of a batch stalled the decode / process / encode threads of GpuJpegStages)."""
     lib = _lib.load()
     h, w, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-    buf = ctypes.create_string_buffer(bytes(data), len(data))
+    if isinstance(data, bytes):
+        keep = ctypes.c_char_p(data)
+        buf = ctypes.cast(keep, ctypes.c_void_p)
+    else:
+        buf = keep = ctypes.create_string_buffer(bytes(data), len(data))
     check(lib.vd_jpeg_info(buf, len(data), ctypes.byref(h), ctypes.byref(w), ctypes.byref(c)))
+    del keep
     return h.value, w.value, c.value
 
 

@@ -271,7 +271,8 @@ class GpuJpegStages:
         self.ev_proc = [torch.cuda.Event() for _ in range(self.depth)]
         self.buf = {}                                   # (h, w) -> ([d_in] * depth, [d_out] * depth)
         self.dpool, self.epool = ThreadPoolExecutor(1), ThreadPoolExecutor(1)
-        self.stats = {"decode_wait": 0.0, "encode_wait": 0.0, "queue": 0.0, "decode": 0.0, "encode": 0.0}
+        self.stats = {"decode_wait": 0.0, "encode_wait": 0.0, "queue": 0.0, "decode": 0.0, "encode": 0.0,
+                      "decode_fetch": 0.0, "decode_call": 0.0}
 
     def _buffers(self, h, w):
         if (h, w) not in self.buf:
@@ -286,6 +287,7 @@ class GpuJpegStages:
         from .context import jpeg_info
         t0 = time.perf_counter()
         blobs = fetch()
+        t_f = time.perf_counter()
         groups = {}
         for k, b in enumerate(blobs):
             try:
@@ -306,6 +308,7 @@ class GpuJpegStages:
             self.serial_jobs += 1
         slot = i % self.depth
         out = []
+        t_c = time.perf_counter()
         for (h, w), idx in groups.items():
             din = self._buffers(h, w)[0][slot][:len(idx)]
             try:
@@ -319,7 +322,10 @@ class GpuJpegStages:
             out.append((idx, h, w))
         self.ev_dec[slot].record(self.s_dec)
         self.last_passes = self.dctx.jdec_passes()
-        self.stats["decode"] += time.perf_counter() - t0
+        t1 = time.perf_counter()
+        self.stats["decode"] += t1 - t0
+        self.stats["decode_fetch"] += t_f - t0            # reading the files (the caller's fetch)
+        self.stats["decode_call"] += t1 - t_c             # vd_jpeg_decode (host parse, staging, passes)
         return out
 
     def _encode(self, i, groups):
