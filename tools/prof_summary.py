@@ -19,7 +19,8 @@ import os
 import sys
 
 FAMILIES = [("conv", ("conv_igemm_kernel", "conv1x1_stream_kernel", "conv_big_kernel", "bottleneck_kernel",
-                       "bottleneck32_kernel", "stem_pool_kernel", "stem_pool32_kernel", "chain_kernel", "dwconv", "conv_x6_kernel", "conv_x6_halo_kernel",
+                       "bottleneck32_kernel", "bottleneck32p_kernel", "stem_pool_kernel", "stem_pool32_kernel", "chain_kernel",
+                       "chain32_kernel", "dwconv", "conv_x6_kernel", "conv_x6_halo_kernel",
                        "conv1x1_x6_kernel")),
             ("mosaic", ("mosaic_",)), ("letterbox", ("letterbox_kernel", "letterbox_s2d")),
             ("post", ("candidates_kernel", "nms_kernel")), ("other", ("maxpool", "upsample")),
@@ -90,7 +91,8 @@ def main(path, out=None, bench=None):
         last = 0
         if bench:
             line = [x for x in open(bench).read().splitlines() if x.startswith("{")][-1]
-            last = int(json.loads(line)["roofline"]["launches"])
+            roof = json.loads(line)["roofline"]
+            last = int(roof.get("per_launch", roof).get("launches", 0))
         (fc, ft), (oc, ot), (lc, lt) = face_stream_convs(trace, last)
         lines.append("")
         lines.append("| conv launches by stream | calls | total ms | avg us per launch |")

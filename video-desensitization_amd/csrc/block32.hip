@@ -501,26 +501,28 @@ __global__ __launch_bounds__(512, 1) void bottleneck32_kernel(Block32Args a) {
 }
 
 // ---------------------------------------------------------------------------------
-// Pipelined form (option block32_pipe, default 1; layer1.1 / layer1.2, CIN = 256):
-// the same three stages, tiles and products, with the eight waves split into a
-// producer group and a consumer group that work on DIFFERENT tiles at once, so the
-// x stream from HBM does not stop at a workgroup barrier:
-//   P (waves 0-3): stage 1 of tile j (wave w: halo pixel tiles 3w..3w+2, all 64 t1
-//                  channels, W1 planes from LDS, x in flight two k-steps deep and the
-//                  next tile's first k-step already issued before stage 3), then stage 3
-//                  of tile j-1 (wave w: output channels 64w.., two 32-channel groups);
-//   C (waves 4-7): stage 2 of tile j (W2 stationary in VGPRs: the wave owns t2 channels
-//                  16jn.. over the full K = 9 taps x 64) while P runs stage 3 of j-1 and
-//                  stage 1 of j+1.
-// t1 and t2 cross between the groups through single LDS buffers as f32 (45 KB + 32 KB;
-// each producer holds its values in registers until the buffer is free) and are split
-// into their per-tile-scaled fp16 pairs by the CONSUMER as it reads them, so the tile
-// max needs no group barrier: producers fold their wave max into the tile's slot and bump
-// a counter, the consumer waits for the counter (LDS spin with s_sleep) and reads the
-// slot. Four monotonic counters order the two buffers (t1 ready / free, t2 ready / free);
-// no s_barrier after the prologue. Products and operand scales are those of the
-// one-group kernel above; stage 2 sums each output's 18 k-steps in one accumulator
-// instead of two K halves (f32 rounding; tests/test_gpu_e2e.py, test_gpu_kernels.py).
+// Pipelined form (option block32_pipe, default 1; layer1.1 / layer1.2, CIN = 256): the
+// same three stages, tiles, products and operand scales, on twelve waves in three groups
+// of four that work on CONSECUTIVE tiles at once, so neither the x stream from HBM nor
+// the output stores stop at a workgroup barrier:
+//   P (waves 0-3):  stage 1 of tile j+1 -- wave w: halo pixel tiles 3w..3w+2, all 64 t1
+//                   channels, W1 planes from LDS, x two k-steps deep and the next tile's
+//                   first k-step issued before the t1 hand-over;
+//   C (waves 4-7):  stage 2 of tile j -- the wave owns t2 channels 16jn.. over the full
+//                   K = 9 taps x 64; its W2 taps re-read from L2 as the previous K half's
+//                   taps fall dead;
+//   Q (waves 8-11): stage 3 of tile j-1 -- the wave owns output channels 64jn.., two
+//                   32-channel groups one after the other, W3 per group from L2 and the
+//                   group's eight identity rows issued before its stores (CDNA4's vmcnt
+//                   retires loads and stores in issue order: a load issued behind a store
+//                   waits for it).
+// t1 and t2 cross between the groups through single LDS plane buffers, split once by
+// their producer (each holds its values in registers until the buffer is free); the
+// per-tile max is a counter barrier among the four producing waves. Six monotonic LDS
+// counters (t1 ready / free, t2 ready / free, P max, C max; waits spin with s_sleep)
+// replace the workgroup barriers. Stage 2 sums each output's 18 k-steps in one
+// accumulator instead of two K halves (f32 rounding; tests/test_gpu_e2e.py,
+// test_gpu_kernels.py).
 
 __device__ __forceinline__ int lds_load_flag(int* f) {
     return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -725,8 +727,8 @@ __global__ __launch_bounds__(768, 1) void bottleneck32p_kernel(Block32Args a) {
         // ================= C: stage 2 of tile j =================
         const int jn = w - 4;
         const __amdgpu_buffer_rsrc_t rw2 = __builtin_amdgcn_make_buffer_rsrc((void*)a.w2, 0, 0x7fffffff, 0x00020000);
-        // W2 fragments of K half hf (9 taps x 2 planes), re-read per tile from L2 (stationary
-        // they would leave stage 3 too few registers)
+        // W2 fragments of K half hf (9 taps x 2 planes), re-read per tile from L2 (all of W2
+        // stationary is 144 VGPRs: past the 168 of three waves per SIMD)
         // (taps tp0 .. tp0 + nt - 1 of half hf into f)
         auto ldw2 = [&](int hf, int tp0, int nt, u32x4 (&f)[9][2]) {
             unsigned lo = lo16;
