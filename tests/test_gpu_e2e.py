@@ -435,27 +435,6 @@ def test_heads_fp32_x6_one_bit_identical(gpu):
         np.testing.assert_array_equal(a, b)
 
 
-@pytest.mark.parametrize("opt,tr2", [("x6_tr2", 1), ("x6_tr2", 2), ("x6_tr2p", 1), ("x6_tr2p", 2)])
-def test_heads_fp32_x6_tr2_bit_identical(gpu, opt, tr2):
-    """The two-per-CU 1x1 tiles (option x6_tr2) and the persistent two-group form (option
-    x6_tr2p, on every eligible layer however few tiles); 2: also the streaming form's
-    K <= 256 layers, compared with those layers on the TR tiles (x6_gemm1x1 = 2). Both
-    compute the TR tiles' products in the same order: heads bit-identical."""
-    import vdmi
-    fr = _frames(2, 720, 1280, seed=43)
-    heads = {}
-    for v in (0, tr2):
-        ctx = vdmi.Context(precision="fp32", max_batch=2,
-                           options={opt: v, "x6_tr2p_min": 0, "x6_gemm1x1": 2 if tr2 == 2 else 1})
-        try:
-            ctx.load_weights(0, face_weights("default"))
-            heads[v] = ctx.forward_heads(fr)
-        finally:
-            ctx.close()
-    for a, b in zip(heads[tr2], heads[0]):
-        np.testing.assert_array_equal(a, b)
-
-
 @pytest.mark.parametrize("xd", [3, 4])
 def test_heads_fp32_block32_depth_bit_identical(gpu, xd):
     """block32.hip's stage-1 x register sets (option block32_xd) only move when the

@@ -507,49 +507,6 @@ def test_conv_tr_tiles_bit_identical(gpu, face_ctx_factory, case):
     test_conv_matches_torch(gpu, face_ctx_factory, "fp32", case, options=dict(x6_gemm1x1=1, x6_stream=0))
 
 
-TR2_CASES = TR_CASES + [
-    # K <= 256 (the streaming form's layers; option x6_tr2 = 2), one K tile, odd tile counts
-    (2, 29, 31, 256, 1024, 1, 1, 0, 1, 1),
-    (1, 40, 40, 128, 512, 1, 1, 0, 1, 1),
-    (3, 17, 16, 64, 256, 1, 2, 0, 0, 0),
-    (1, 9, 7, 32, 128, 1, 1, 0, 1, 2),
-    (2, 23, 21, 64, 384, 1, 1, 0, 1, 1),
-]
-
-
-TR2_FORMS = {
-    # two workgroups per CU (option x6_tr2)
-    "tr2": (("x6_tr2", 2),),
-    # persistent two-group form (option x6_tr2p) on every eligible layer however few tiles
-    # (x6_tr2p_min = 0), and with one workgroup slot so each group runs many tiles
-    "tr2p": (("x6_tr2p", 2), ("x6_tr2p_min", 0)),
-    "tr2p-1slot": (("x6_slots", 1), ("x6_tr2p", 2), ("x6_tr2p_min", 0)),
-}
-
-
-@pytest.mark.parametrize("form", sorted(TR2_FORMS))
-@pytest.mark.parametrize("case", TR2_CASES)
-def test_conv_tr2_bit_identical(gpu, face_ctx_factory, case, form):
-    """conv1x1_tr2_kernel (two workgroups per CU, A straight to registers, option x6_tr2)
-    and conv1x1_tr2p_kernel (one persistent workgroup per CU of two wave groups out of
-    step, option x6_tr2p) against the TR tiles: bit-identical outputs and per-frame max
-    slots, and within the fp32 tolerance of torch."""
-    n, h, w, cin, cout, k, s, p, act, res_mode = case
-    rng = np.random.default_rng(cin + 5 * cout + h)
-    x = np.maximum(rng.standard_normal((n, h, w, cin)), 0).astype(F32)
-    wt = (rng.standard_normal((cout, cin, k, k)) * np.sqrt(2.0 / cin)).astype(F32)
-    scale = rng.uniform(0.5, 1.5, cout).astype(F32)
-    shift = rng.standard_normal(cout).astype(F32) * F32(0.1)
-    oh, ow = (h - 1) // s + 1, (w - 1) // s + 1
-    res = rng.standard_normal((n, oh, ow, cout)).astype(F32) if res_mode else None
-    outs = []
-    for opts in ((), TR2_FORMS[form]):
-        ctx = face_ctx_factory("fp32", 8, options=(("x6_gemm1x1", 2),) + opts)
-        outs.append(ctx.conv2d(x, wt, s, p, scale, shift, act, 0.1, res, res_mode))
-    assert np.array_equal(outs[0], outs[1])
-    test_conv_matches_torch(gpu, face_ctx_factory, "fp32", case, options=dict(TR2_FORMS[form]))
-
-
 @pytest.mark.parametrize("copy", [0, 1])
 def test_mosaic_output_forms_match_oracle(gpu, copy):
     """Option mosaic_copy: 0 (default) = the band output pass; 1 = copy-first (one plain copy pass, the cell

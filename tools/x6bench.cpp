@@ -46,7 +46,7 @@ static const TuneField kTune[] = {
     {"x6_mid", &VdTune::x6_mid},         {"x6_mf32", &VdTune::x6_mf32},           {"x6_tail", &VdTune::x6_tail},
     {"x6_halo", &VdTune::x6_halo},       {"x6_adepth", &VdTune::x6_adepth},       {"x6_small_k", &VdTune::x6_small_k},
     {"x6_small_tiles", &VdTune::x6_small_tiles}, {"x6_gemm1x1", &VdTune::x6_gemm1x1}, {"x6_dbg", &VdTune::x6_dbg},
-    {"x6_halo_tr", &VdTune::x6_halo_tr}, {"x6_one", &VdTune::x6_one}, {"x6_tr2", &VdTune::x6_tr2}, {"x6_tr2p", &VdTune::x6_tr2p}, {"x6_tr2p_min", &VdTune::x6_tr2p_min},
+    {"x6_halo_tr", &VdTune::x6_halo_tr}, {"x6_one", &VdTune::x6_one},
 };
 
 static float frand(uint32_t& st) {
@@ -97,7 +97,7 @@ static double run(const Layer& L, int B, int reps, const VdTune& tune, bool chec
     a.M = B * oh * ow; a.act = VD_ACT_RELU; a.slope = 0.f; a.out_f32 = 1;
     a.tune = &tune;
     a.wx3 = dw; a.scale_x = dsc; a.f32_split = 2;
-    a.xmax = dxm; a.ymax = getenv("X6_NOYMAX") ? nullptr : dym;
+    a.xmax = dxm; a.ymax = dym;
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
     for (int i = 0; i < 2; ++i) CK(vd_launch_conv(a, true, 0));

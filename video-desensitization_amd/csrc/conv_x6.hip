@@ -380,9 +380,7 @@ __device__ __forceinline__ void x6_epilogue(const ConvArgs& a, AccT (&acc)[S::TM
 // the 8 consecutive channels 32 jp + 8 q .. +7 of pixel 16 i + p: BN + residual +
 // activation on 8 values, two 16-B stores, no LDS staging and no workgroup barrier
 // (only the per-frame max goes through LDS). Same arithmetic as x6_epilogue.
-// LDS_ONLY: the per-frame max into the LDS slots only, no workgroup barrier and no flush
-// (conv1x1_tr2p_kernel's wave groups run out of step; the group flushes them itself)
-template <class S, bool LDS_ONLY = false>
+template <class S>
 __device__ __forceinline__ void x6_epilogue_tr(const ConvArgs& a, f32x4_t (&acc)[S::TM][S::TN], int m0, int n0,
                                                int wm, int wn, int lane, unsigned* s_amax) {
     constexpr int TM = S::TM, TN = S::TN;
@@ -447,7 +445,6 @@ __device__ __forceinline__ void x6_epilogue_tr(const ConvArgs& a, f32x4_t (&acc)
     if (a.ymax) {
 #pragma unroll
         for (int i = 0; i < TM; ++i) amax_lds_add(s_amax, fbs[i], vmax[i]);
-        if constexpr (LDS_ONLY) return;
         __syncthreads();
         amax_lds_flush(s_amax, a.ymax, a.B);
     }
@@ -781,359 +778,6 @@ __global__ __launch_bounds__(NT, NT == 256 && BM == 256 ? 1 : 2) void conv_x6_ke
     } else {
         __syncthreads();
         x6_epilogue<S, MF>(a, acc, m0, n0, wm, wn, tid, lane, smem, S::LDS);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// 1x1 GEMM convs at TWO workgroups per CU (option x6_tr2): the 256 x 256 TR tile runs one
-// workgroup per CU, so its epilogue (BN + residual + activation + the f32 stores: 8 B of HBM
-// traffic per output, ~25 us per tile when every CU is in it) never overlaps a main loop --
-// x6bench, B = 64: layer4 conv3 286 us of which 117 epilogue, layer3.0 downsample 448 / 136,
-// FPN output1 489 / 116. Here a workgroup is 4 waves with a 256 x 128 tile (wave w: pixel
-// rows 64 w .. 64 w + 63 x all 128 channels, the TR accumulators of the big tile, 128
-// VGPRs), and two of them share a CU (48 KB of LDS each), so one's epilogue runs beside the
-// other's MFMAs. No wave shares its pixel rows, so A needs no LDS image: each lane loads its
-// own fragment rows straight into registers (pixel 16 i + l % 16, channels 8 (l / 16) .. +7
-// of the K tile = 32 contiguous bytes; two K tiles in flight) and splits them in place into
-// the fp16 pair. B (the split weights, rows permuted by x6_tr_row) arrives by LDS-DMA into
-// three stages, one barrier per K tile. Same products in the same order as conv_x6_kernel's
-// TR tiles and the same register epilogue (x6_epilogue_tr): bit-identical results.
-struct Tr2Shape { static constexpr int TM = 4, TN = 8, WTM = 64, WTN = 128; };
-
-__global__ __launch_bounds__(256, 2) void conv1x1_tr2_kernel(ConvArgs a) {
-    constexpr int BM = 256, BN = 128, TM = 4, TN = 8, NSB = 3;
-    constexpr int PL_B = BN * 64, STAGE = 2 * PL_B;        // 8 KB per plane, two planes per stage
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-
-    // XCD-aware bijective remap (blocks b, b+8, ... share an XCD), N tiles of an M panel adjacent
-    const int nwg = gridDim.x, bid = blockIdx.x;
-    const int q8 = nwg >> 3, r8 = nwg & 7, xcd = bid & 7;
-    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-    const int tn = wg % a.ntiles_n, tm = wg / a.ntiles_n;
-    const int m0 = tm * BM, n0 = tn * BN;
-    const int pl = lane & 15, ql = lane >> 4;
-
-    // this lane's A rows: pixel m0 + 64 wid + 16 i + pl, bytes [32 ql, 32 ql + 32) of each K tile
-    const int ohw = a.yh * a.yw;
-    int voff[TM];
-    float sa[TM];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-        const int m = m0 + 64 * wid + 16 * i + pl;
-        sa[i] = 1.f;
-        voff[i] = (int)0x80000000;                          // past num_records: loads return zeros
-        if (m < a.M) {
-            const int b = m / ohw, rem = m - b * ohw;
-            const int oy = rem / a.yw, ox = rem - oy * a.yw;
-            const int pix = ((b * a.xh + oy * a.stride) * a.xw + ox * a.stride) * a.ldx + a.xcoff;
-            voff[i] = pix * 4 + ql * 32;
-            sa[i] = __builtin_ldexpf(1.f, act_scale_exp(a, b));
-        }
-    }
-    const long xbytes = (long)a.B * a.xh * a.xw * a.ldx * 4;
-    const __amdgpu_buffer_rsrc_t rsrc_x = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, (int)xbytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rsrc_w = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7fffffff, 0x00020000);
-    const int nk = a.kpad / KT;
-
-    auto load_a = [&](u32x4 (&r)[TM][2], int kt) {
-        const int so = kt * (KT * 4);
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-            r[i][0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc_x, voff[i], so, 0));
-            r[i][1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc_x, voff[i] + 16, so, 0));
-        }
-    };
-    // B: 16 DMA instructions of 1 KB (16 rows of one plane) per K tile, 4 per wave
-    auto dma_b = [&](int kt, int st) {
-        char* Bs = smem + st * STAGE;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int j = wid + 4 * q;
-            const int p = j >> 3, r0 = (j & 7) * 16;
-            const int row = r0 + (lane >> 2), slot = lane & 3;
-            const int chunk = slot ^ (((row >> 3) & 1) * 3);
-            const unsigned off = (unsigned)((((long)(n0 + x6_tr_row(row)) * nk + kt) * 2 + p) * 64 + chunk * 16);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_w, (lds_void_t*)(Bs + p * PL_B + r0 * 64), 16, off, 0, 0, 0);
-        }
-    };
-
-    f32x4_t acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{};
-    unsigned* s_amax = (unsigned*)(smem + NSB * STAGE);
-    if (a.ymax)   // ordered before use by the main loop's barriers
-        for (int f = tid; f < a.B; f += 256) s_amax[f] = 0u;
-
-    auto compute = [&](int st, const u32x4 (&r)[TM][2]) {
-        u32x4 af[TM][3];
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-            float e[8];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                e[j] = __uint_as_float(r[i][0][j]);
-                e[4 + j] = __uint_as_float(r[i][1][j]);
-            }
-            split_pair8(e, sa[i], af[i][0], af[i][1]);
-        }
-        const char* Bs = smem + st * STAGE;
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            u32x4 bf[3];
-            bf[0] = *(const u32x4*)(Bs + swz(j * 16 + pl, ql));
-            bf[1] = *(const u32x4*)(Bs + PL_B + swz(j * 16 + pl, ql));
-#pragma unroll
-            for (int i = 0; i < TM; ++i) acc[i][j] = mfma_pair_tr(af[i], bf, acc[i][j]);
-        }
-    };
-
-    // Per thread VMEM issue order: iteration u issues B(u+2) (4 DMAs) after its barrier and
-    // A(u+2) (8 loads) after its MFMAs; the prologue issues B(0), A(0), B(1), A(1). At the top
-    // of iteration t the ops younger than A(t) are iteration t-1's B(t+1) and A(t+1), so
-    // vmcnt(12) retires A(t) and the older B(t) (vmcnt(0) on the last tile).
-    u32x4 ra[2][TM][2];
-    dma_b(0, 0);
-    load_a(ra[0], 0);
-    if (nk > 1) {
-        dma_b(1, 1);
-        load_a(ra[1], 1);
-    }
-    auto iter = [&](int kt, u32x4 (&r)[TM][2]) {
-        if (kt + 1 < nk) wait_vm_k<12>();
-        else wait_vm_k<0>();
-        __builtin_amdgcn_s_barrier();                        // B(kt) landed for every wave; stage (kt+2) % 3 free
-        asm volatile("" ::: "memory");
-        if (kt + 2 < nk) dma_b(kt + 2, (kt + 2) % NSB);
-        compute(kt % NSB, r);
-        if (kt + 2 < nk) load_a(r, kt + 2);
-    };
-    for (int kt = 0; kt < nk; kt += 2) {
-        iter(kt, ra[0]);
-        if (kt + 1 < nk) iter(kt + 1, ra[1]);
-    }
-    if (a.dbg & 1) {                                         // timing experiment: main loop only
-        if (acc[0][0][0] == 1234.5f) ((float*)a.y)[tid] = 1.f;
-        return;
-    }
-    x6_epilogue_tr<Tr2Shape>(a, acc, m0, n0, wid, 0, lane, s_amax);
-}
-
-// LDS counters of conv1x1_tr2p_kernel's wave groups (monotonic; waits spin with s_sleep)
-__device__ __forceinline__ void grp_wait(int* f, int v) {
-    while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < v)
-        __builtin_amdgcn_s_sleep(1);
-    asm volatile("" ::: "memory");
-}
-__device__ __forceinline__ void grp_post(int* f, int lane) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_fetch_add(f, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    asm volatile("" ::: "memory");
-}
-
-// The two-per-CU tiles above measured level with the one-per-CU TR tile: every workgroup
-// of a launch starts together and runs the same work, so the two on a CU reach their
-// epilogues at the same time and nothing overlaps (x6bench: layer4 conv3 292 us either
-// way). This form makes the offset explicit: ONE persistent workgroup per CU of two
-// 4-wave groups, each the 256 x 128 tile of conv1x1_tr2_kernel with its own three B
-// stages, running the workgroup's tiles alternately (group g: tiles w + (2 j + g) G of
-// the remapped index w). Group 1 starts when group 0 has finished half of its first
-// tile's K loop, so from then on one group's epilogue (and the other stalls of its
-// loads) falls into the other's MFMA phase. A group synchronises its four waves through
-// one LDS counter (a wave bumps it after its own B DMAs of K tile u have landed and its
-// reads of tile u - 1 are done; all four bumps = stage u readable and stage u - 1 free)
-// instead of s_barrier, which would couple the groups. K tiles run back to back across
-// a group's tiles (the next tile's first A / B loads are issued under the current
-// tile's last K tiles and its epilogue). Per-frame max merged per group in LDS, flushed by its last wave.
-// Same products, same order, same epilogue arithmetic: bit-identical to the TR tiles.
-__global__ __launch_bounds__(512, 1) void conv1x1_tr2p_kernel(ConvArgs a, int ntiles) {
-    constexpr int TM = 4, TN = 8, NSB = 3;
-    constexpr int PL_B = 128 * 64, STAGE = 2 * PL_B, GLDS = NSB * STAGE;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int grp = wid >> 2, gw = wid & 3;
-    char* gs = smem + grp * GLDS;
-    int* flg = (int*)(smem + 2 * GLDS);                     // ready[2], epilogue arrivals[2]
-    unsigned* s_amax = (unsigned*)(flg + 4) + grp * kAmaxFrames;   // the group's per-frame max slots
-    if (tid < 4) flg[tid] = 0;
-    if (a.ymax)
-        for (int f = tid; f < 2 * kAmaxFrames; f += 512) ((unsigned*)(flg + 4))[f] = 0u;
-    __syncthreads();
-    int* ready = flg + grp;
-    int* earr = flg + 2 + grp;
-
-    const int G = gridDim.x, bid = blockIdx.x;
-    const int q8 = G >> 3, r8 = G & 7, xcd = bid & 7;
-    const int w = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-    const int first = w + grp * G;
-    const int ntl = first < ntiles ? (ntiles - 1 - first) / (2 * G) + 1 : 0;
-    const int nk = a.kpad / KT;
-    const int U = ntl * nk;                                  // this group's K tiles, all its tiles
-    const int pl = lane & 15, ql = lane >> 4;
-    const int ohw = a.yh * a.yw;
-    const long xbytes = (long)a.B * a.xh * a.xw * a.ldx * 4;
-    const __amdgpu_buffer_rsrc_t rsrc_x = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, (int)xbytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rsrc_w = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7fffffff, 0x00020000);
-
-    auto tile_mn = [&](int j, int& m0, int& n0) {
-        const int t = first + 2 * G * j;
-        m0 = (t / a.ntiles_n) * 256;
-        n0 = (t % a.ntiles_n) * 128;
-    };
-    auto row_of = [&](int m0, int i) { return m0 + 64 * gw + 16 * i + pl; };
-    // load position (the K tile u + 2 of the main loop): tile lj, K tile lkt, its rows' offsets
-    int lj = 0, lkt = 0, lm0 = 0, ln0 = 0;
-    int voff[TM];
-    auto set_rows = [&]() {
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-            const int m = row_of(lm0, i);
-            voff[i] = (int)0x80000000;
-            if (m < a.M) {
-                const int b = m / ohw, rem = m - b * ohw;
-                const int oy = rem / a.yw, ox = rem - oy * a.yw;
-                voff[i] = (((b * a.xh + oy * a.stride) * a.xw + ox * a.stride) * a.ldx + a.xcoff) * 4 + ql * 32;
-            }
-        }
-    };
-    auto dma_b = [&](int st) {                               // B of the load position into stage st
-        char* Bs = gs + st * STAGE;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int j = gw + 4 * q;
-            const int p = j >> 3, r0 = (j & 7) * 16;
-            const int row = r0 + (lane >> 2), slot = lane & 3;
-            const int chunk = slot ^ (((row >> 3) & 1) * 3);
-            const unsigned off = (unsigned)((((long)(ln0 + x6_tr_row(row)) * nk + lkt) * 2 + p) * 64 + chunk * 16);
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_w, (lds_void_t*)(Bs + p * PL_B + r0 * 64), 16, off, 0, 0, 0);
-        }
-    };
-    auto load_a = [&](u32x4 (&r)[TM][2]) {                  // A of the load position, then advance it
-        const int so = lkt * (KT * 4);
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-            r[i][0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc_x, voff[i], so, 0));
-            r[i][1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc_x, voff[i] + 16, so, 0));
-        }
-        if (++lkt == nk) {
-            lkt = 0;
-            if (++lj < ntl) {
-                tile_mn(lj, lm0, ln0);
-                set_rows();
-            }
-        }
-    };
-
-    f32x4_t acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{};
-    // compute position: the tile's first row / channel and its frame scales
-    int cm0 = 0, cn0 = 0;
-    float sa[TM];
-    auto set_scales = [&]() {
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-            const int m = row_of(cm0, i);
-            sa[i] = m < a.M ? __builtin_ldexpf(1.f, act_scale_exp(a, m / ohw)) : 1.f;
-        }
-    };
-    auto compute = [&](int st, const u32x4 (&r)[TM][2]) {
-        u32x4 af[TM][3];
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-            float e[8];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                e[j] = __uint_as_float(r[i][0][j]);
-                e[4 + j] = __uint_as_float(r[i][1][j]);
-            }
-            split_pair8(e, sa[i], af[i][0], af[i][1]);
-        }
-        const char* Bs = gs + st * STAGE;
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            u32x4 bf[3];
-            bf[0] = *(const u32x4*)(Bs + swz(j * 16 + pl, ql));
-            bf[1] = *(const u32x4*)(Bs + PL_B + swz(j * 16 + pl, ql));
-#pragma unroll
-            for (int i = 0; i < TM; ++i) acc[i][j] = mfma_pair_tr(af[i], bf, acc[i][j]);
-        }
-    };
-
-    if (U > 0) {
-        tile_mn(0, lm0, ln0);
-        set_rows();
-        cm0 = lm0;
-        cn0 = ln0;
-        set_scales();
-    }
-    // Per wave VMEM issue order: iteration u issues B(u+2) (4 DMAs) after its counter wait
-    // and A(u+2) (8 loads) after its MFMAs, then (last K tile of a tile) the epilogue's
-    // loads and stores; the prologue issues B(0), A(0), B(1), A(1). At the top of iteration
-    // u the ops younger than A(u) are iteration u-1's B(u+1) and A(u+1): vmcnt(12), or 0
-    // after an epilogue (its stores are younger still) and on the last K tile.
-    u32x4 ra[2][TM][2];
-    bool epi = false;
-    if (U > 0) { dma_b(0); load_a(ra[0]); }
-    if (U > 1) { dma_b(1); load_a(ra[1]); }
-    // group 1 starts half a tile behind group 0 (its first loads already in flight)
-    if (grp == 1 && U > 0) {
-        const int ntl0 = w < ntiles ? (ntiles - 1 - w) / (2 * G) + 1 : 0;
-        grp_wait(flg, 4 * (ntl0 > 0 ? nk / 2 + 1 : 0));
-    }
-    auto iter = [&](int u, u32x4 (&r)[TM][2]) {
-        if (u + 1 < U && !epi) wait_vm_k<12>();
-        else wait_vm_k<0>();
-        epi = false;
-        grp_post(ready, lane);                               // B(u) landed (mine), stage (u-1) % 3 read (mine)
-        grp_wait(ready, 4 * (u + 1));
-        if (u + 2 < U) dma_b((u + 2) % NSB);
-        compute(u % NSB, r);
-        if (u + 2 < U) load_a(r);
-    };
-    // nk is even (x6_tr2p_ok): K tile kt of every tile uses register set kt & 1
-    int u = 0;
-    for (int j = 0; j < ntl; ++j) {
-        if (j) {
-            tile_mn(j, cm0, cn0);
-            set_scales();
-        }
-        for (int kt = 0; kt < nk; kt += 2, u += 2) {
-            iter(u, ra[0]);
-            iter(u + 1, ra[1]);
-        }
-        if (!(a.dbg & 1)) {
-            x6_epilogue_tr<Tr2Shape, true>(a, acc, cm0, cn0, gw, 0, lane, s_amax);
-            if (a.ymax) {   // the group's last wave to arrive moves the tile's frames' slots to global
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                int old = 0;
-                if (lane == 0) old = __hip_atomic_fetch_add(earr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                old = __builtin_amdgcn_readfirstlane(old);
-                if (old == 4 * j + 3) {
-                    const int f0 = cm0 / ohw, f1 = min(cm0 + 255, a.M - 1) / ohw;
-                    for (int f = f0 + lane; f <= f1; f += 64) {
-                        const unsigned v = __hip_atomic_load(s_amax + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        if (v) {
-                            atomicMax(a.ymax + f, v);
-                            s_amax[f] = 0u;
-                        }
-                    }
-                }
-            }
-        } else if (acc[0][0][0] == 1234.5f) {
-            ((float*)a.y)[tid] = 1.f;                        // timing experiment: no epilogue
-        }
-        epi = true;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int jj = 0; jj < TN; ++jj) acc[i][jj] = f32x4_t{};
     }
 }
 
@@ -2035,50 +1679,7 @@ static bool x6_tr_ok(const ConvArgs& a) {
     return a.res_mode == VD_RES_NONE || !((a.res_ld | a.res_coff) & 7);
 }
 
-// conv1x1_tr2_kernel: 1x1, no padding, K in whole 32-channel tiles, Cout % 128, 16-B A rows
-static bool x6_tr2_ok(const ConvArgs& a) {
-    if (!x6_tr_ok(a) || a.kpad != a.cin_pad || a.cin_pad % KT || ((a.ldx | a.xcoff) & 3)) return false;
-    return (long)a.B * a.xh * a.xw * a.ldx * 4 < (1L << 31);
-}
-
-static hipError_t launch_tr2(const ConvArgs& a0, hipStream_t s) {
-    ConvArgs a = a0;
-    a.w = a.wx3;
-    a.ntiles_n = a.cout / 128;
-    a.mbase = 0;
-    const int mt = (a.M + 255) / 256;
-    const int lds = 3 * 2 * 128 * 64 + (a.ymax ? 4 * a.B : 0);
-    hipLaunchKernelGGL(conv1x1_tr2_kernel, dim3(mt * a.ntiles_n), dim3(256), lds, s, a);
-    return hipGetLastError();
-}
-
-// persistent two-group form: one workgroup per CU, at least two tiles per group pair
-static hipError_t launch_tr2p(const ConvArgs& a0, hipStream_t s) {
-    ConvArgs a = a0;
-    a.w = a.wx3;
-    a.ntiles_n = a.cout / 128;
-    a.mbase = 0;
-    const int ntiles = (a.M + 255) / 256 * a.ntiles_n;
-    const int G = std::min(device_cus(), (ntiles + 1) / 2);
-    constexpr int lds = 2 * 3 * 2 * 128 * 64 + 16 + 2 * 4 * kAmaxFrames;
-    static const bool attr = [] {
-        (void)hipFuncSetAttribute((const void*)conv1x1_tr2p_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        return true;
-    }();
-    (void)attr;
-    hipLaunchKernelGGL(conv1x1_tr2p_kernel, dim3(G), dim3(512), lds, s, a, ntiles);
-    return hipGetLastError();
-}
-
-static bool x6_tr2p_ok(const ConvArgs& a) {
-    const int slots = a.tune->x6_slots > 0 ? a.tune->x6_slots : device_cus();
-    return x6_tr2_ok(a) && (a.kpad / KT) % 2 == 0 &&
-           (long)(a.M + 255) / 256 * (a.cout / 128) >= (long)a.tune->x6_tr2p_min * slots;
-}
-
 static hipError_t launch_tr(const ConvArgs& a, hipStream_t s) {
-    if (a.tune->x6_tr2p && x6_tr2p_ok(a)) return launch_tr2p(a, s);
-    if (a.tune->x6_tr2 && x6_tr2_ok(a)) return launch_tr2(a, s);
     const long t256 = (long)((a.M + 255) / 256) * (a.cout / 256);
     if (a.cout % 256 == 0 && t256 >= 192) return launch_x6<256, 256, 512, 2, 2, 16, 2, true>(a, s);
     if (a.cout == 128 && a.tune->x6_mid && a.kpad <= a.tune->x6_mid) return launch_x6<128, 128, 256, 2, 2, 16, 2, true>(a, s);
@@ -2118,9 +1719,6 @@ static hipError_t launch_terms(const ConvArgs& a0, hipStream_t s) {
         // option x6_gemm1x1 = 2 (experiments): the K <= 256 layers of the streaming form on the
         // TR tiles as well (measured 20-35 % slower than the streaming form)
         if (a.tune && a.tune->x6_gemm1x1 == 2 && x6_tr_ok(a)) return launch_tr(a, s);
-        // option x6_tr2 = 2: the streaming form's K <= 256 layers on the two-per-CU tiles too
-        if (a.tune && a.tune->x6_tr2p >= 2 && x6_tr2p_ok(a)) return launch_tr2p(a, s);
-        if (a.tune && a.tune->x6_tr2 >= 2 && x6_tr2_ok(a)) return launch_tr2(a, s);
     }
     if (const int nch = stream_x6_nch(a, TERMS)) {
         if constexpr (TERMS == 2) {   // 256-channel slices: each pixel read by half as many workgroups

@@ -118,13 +118,6 @@ struct VdTune {
     int x6_taps = 1;          // fp32 plan: narrow KxK YOLO layers (K <= 288) on the streaming TAPS form
     int x6_gemm1x1 = 1;       // fp16 pairs: GEMM 1x1 convs on the TR tiles (D^T accumulators, register epilogue;
                               //   2: also the streaming form's K <= 256 layers, 0: off)
-    int x6_tr2 = 0;           // fp16 pairs: the TR GEMM 1x1 convs at two workgroups per CU (256 x 128 tiles,
-                              //   A straight to registers, epilogue beside the other's main loop;
-                              //   bit-identical; 2: also the streaming form's K <= 256 layers)
-    int x6_tr2p = 0;          // fp16 pairs: the TR GEMM 1x1 convs with at least x6_tr2p_min x CUs 256 x 128 tiles
-                              //   on the persistent two-group form (conv1x1_tr2p_kernel; bit-identical;
-                              //   2: also the streaming form's K <= 256 layers)
-    int x6_tr2p_min = 2;
     int x6_dbg = 0;           // experiments (tools/x6bench): 1 = no epilogue (WRONG results), 2 = runtime vmcnt waits
     int f32_split = 2;        // plan (fp32, at weight load): 2 = operands scaled by powers of two
                               //   and split into fp16 pairs, 3 products on the f16 matrix cores;
