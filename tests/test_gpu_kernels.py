@@ -475,6 +475,44 @@ def test_postprocess_ties_and_capacity(gpu, face_ctx_factory):
     np.testing.assert_array_equal(full.frame(0)[0], e[2])
 
 
+S2_CASES = [
+    # fp32 stride-2 3x3 convs on the phase halos (option x6_halo_s2): odd input dims (the odd
+    # row / column past the input), several frames per tile, N = 64 / 128 / 256-wide tiles,
+    # residual, the widest phase halo (Wo = 254)
+    (3, 17, 15, 32, 64, 3, 2, 1, 1, 0),
+    (2, 16, 16, 64, 128, 3, 2, 1, 1, 1),
+    (1, 5, 507, 32, 128, 3, 2, 1, 2, 0),
+    (1, 9, 8, 256, 512, 3, 2, 1, 1, 0),
+    (4, 224, 224, 32, 256, 3, 2, 1, 1, 0),    # >= 192 256-wide tiles: the 256 x 256 halo tile
+]
+
+
+@pytest.mark.parametrize("case", S2_CASES)
+def test_conv_halo_s2_matches_torch_and_batch_invariant(gpu, face_ctx_factory, case):
+    """Phase-halo stride-2 convs (conv_x6_halo_kernel<..., S2>) within the fp32 tolerance of
+    torch, like the tap-major tiles they replace (x6_halo_s2 = 0); every output's K order
+    is fixed, so a frame's outputs do not depend on the batch around it (bit-identical
+    to the frame run alone)."""
+    for s2 in (1, 0):
+        test_conv_matches_torch(gpu, face_ctx_factory, "fp32", case, options=dict(x6_halo_s2=s2))
+    n, h, w, cin, cout, k, s, p, act, res_mode = case
+    if n == 1:
+        return
+    ctx = face_ctx_factory("fp32", 8, options=(("x6_halo_s2", 1),))
+    rng = np.random.default_rng(cin + cout)
+    x = np.maximum(rng.standard_normal((n, h, w, cin)), 0).astype(F32)
+    wt = (rng.standard_normal((cout, cin, k, k)) * np.sqrt(2.0 / (9 * cin))).astype(F32)
+    scale = rng.uniform(0.5, 1.5, cout).astype(F32)
+    shift = rng.standard_normal(cout).astype(F32) * F32(0.1)
+    oh, ow = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    res = rng.standard_normal((n, oh, ow, cout)).astype(F32) if res_mode else None
+    full = ctx.conv2d(x, wt, s, p, scale, shift, act, 0.1, res, res_mode)
+    for b in range(n):
+        one = ctx.conv2d(x[b:b + 1], wt, s, p, scale, shift, act, 0.1,
+                         None if res is None else res[b:b + 1], res_mode)
+        assert np.array_equal(one[0], full[b]), b
+
+
 TR_CASES = [
     # 1x1 convs on the TR tiles (option x6_gemm1x1): 256 x 256 (Cout % 256, >= 192 tiles), 256 x 128,
     # 128 x 128 (Cout 128, K <= 512); M tails, stride 2, residual before / after the activation

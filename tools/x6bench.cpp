@@ -44,7 +44,7 @@ struct TuneField { const char* name; int VdTune::*f; };
 static const TuneField kTune[] = {
     {"x6_stream", &VdTune::x6_stream},   {"x6_stream256", &VdTune::x6_stream256}, {"x6_bn256", &VdTune::x6_bn256},
     {"x6_mid", &VdTune::x6_mid},         {"x6_mf32", &VdTune::x6_mf32},           {"x6_tail", &VdTune::x6_tail},
-    {"x6_halo", &VdTune::x6_halo},       {"x6_adepth", &VdTune::x6_adepth},       {"x6_small_k", &VdTune::x6_small_k},
+    {"x6_halo", &VdTune::x6_halo},       {"x6_halo_s2", &VdTune::x6_halo_s2}, {"x6_adepth", &VdTune::x6_adepth},       {"x6_small_k", &VdTune::x6_small_k},
     {"x6_small_tiles", &VdTune::x6_small_tiles}, {"x6_gemm1x1", &VdTune::x6_gemm1x1}, {"x6_dbg", &VdTune::x6_dbg},
     {"x6_halo_tr", &VdTune::x6_halo_tr}, {"x6_one", &VdTune::x6_one},
 };

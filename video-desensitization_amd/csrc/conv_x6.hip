@@ -806,7 +806,28 @@ __device__ __forceinline__ int swzh(int row, int chunk) { return row * 64 + ((ch
 // TR (round 4, option x6_halo_tr): the MFMA operands exchanged as on the TR GEMM tiles
 // (weight rows permuted by x6_tr_row in the DMA, D^T accumulators), so the epilogue runs
 // from registers (x6_epilogue_tr) with no LDS staging passes: bit-identical.
-template <int BN, int NSB, bool TR = false>
+//
+// S2 (round 5, option x6_halo_s2): 3x3 / stride 2 / pad 1 by phase decomposition. Input
+// pixel (2 yo + dy, 2 xo + dx) of output (yo, xo) lies in phase image (py, px) = (dy != 0,
+// dx != 0) -- input rows / columns of one parity, an Ho x Wo image indexed like the
+// output -- at phase pixel (yo - (dy < 0), xo - (dx < 0)). So each tap reads its phase
+// image at a shift of 0 or -1 row / column, the stride-1 halo trick with the halo rows
+// m0 - Wo - 1 .. m0 + 255 of one phase image at a time. Per 32-channel chunk the four
+// phase halos are split and staged in turn -- phase (1,1) with taps (+-1, +-1), (1,0)
+// with (+-1, 0), (0,1) with (0, +-1), (0,0) with (0, 0) -- each loaded into registers
+// under the previous phase's taps. A shift-0 tap never crosses a frame (the phase
+// pixel is the output pixel's own), a shift of -1 needs yo > 0 / xo > 0, and an odd
+// row / column past an odd-sized input is a zero load. conv_x6_kernel splits every
+// input element of a stride-2 3x3 conv ~2.25 times per chunk (once per tap that reads
+// it); here ~1.3 (the phase halos' overlap). K runs chunk-major in phase order: a
+// fixed order for every output (batch invariance), another f32 summation order than
+// the tap-major GEMM.
+__host__ __device__ constexpr int s2_tap(int j) {   // step j of a chunk -> weight tap (dy + 1) * 3 + dx + 1
+    return j == 0 ? 8 : j == 1 ? 6 : j == 2 ? 2 : j == 3 ? 0 : j == 4 ? 7 : j == 5 ? 1 : j == 6 ? 5 : j == 7 ? 3 : 4;
+}
+__host__ __device__ constexpr bool s2_last(int j) { return j == 3 || j == 5 || j == 7 || j == 8; }   // a phase ends
+
+template <int BN, int NSB, bool TR = false, bool S2 = false>
 __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(ConvArgs a) {
     using S = X6Shape<256, BN, 512, 2, 2>;
     constexpr int BM = 256, NT = 512, TM = S::TM, TN = S::TN, WAVES = S::WAVES, PL_B = S::PL_B;
@@ -819,31 +840,45 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
     const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
     const int tn = wg % a.ntiles_n, tm = wg / a.ntiles_n;
     const int m0 = a.mbase + tm * BM, n0 = tn * BN;
+    static_assert(!S2 || (NSB == 3 && S::NDMA % WAVES == 0), "stride-2 halo: three B stages, whole DMA rounds");
     const int W = a.yw, H = a.yh, HW = H * W;
-    const int HR = BM + 2 * W + 2, HP = HR + 1;     // halo rows + one zero row (index HR)
+    const int HR = S2 ? BM + W + 1 : BM + 2 * W + 2, HP = HR + 1;   // halo rows + one zero row (index HR)
     const int PL_H = HP * 64;
     char* Ah = smem + NSB * 2 * PL_B;               // after the B stages
     const int CH = a.cin_pad / 32, nsteps = 9 * CH, nk = a.kpad / KT;
+    const int nhalo = S2 ? 4 * CH : CH;             // halos per tile (S2: four phase images per chunk)
 
     // ---- halo staging: item i = tid + NT q: row hr = i >> 2, 8 channels pr = i & 3
     const long xbytes = (long)a.B * a.xh * a.xw * a.ldx * 4;
     const __amdgpu_buffer_rsrc_t rsrc_x = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, (int)xbytes, 0x00020000);
     int hoff[QI];                                    // element offset of the item's pixel + channels
     unsigned hexp = 0;                              // the items' frame scale exponents, a byte each
+    unsigned hodd = 0;                              // S2: item q's odd input row (bit 2q) / column (2q+1) exists
     const int xg = a.grp_co ? (n0 / a.grp_co) * a.grp_ci : 0;   // grouped conv: this N tile's input group
 #pragma unroll
     for (int q = 0; q < QI; ++q) {
         const int it = tid + NT * q, hr = it >> 2, pr = it & 3;
         const int pix = m0 - W - 1 + hr;
         const bool ok = hr < HR && pix >= 0 && pix < a.M;
-        hoff[q] = ok ? pix * a.ldx + a.xcoff + xg + pr * 8 : -1;
+        if constexpr (S2) {   // phase pixel pix = (b, yo, xo): phase (0, 0) input pixel (b, 2 yo, 2 xo)
+            const int b = pix / HW, rem = pix - b * HW, yo = rem / W, xo = rem - yo * W;
+            hoff[q] = ok ? ((b * a.xh + 2 * yo) * a.xw + 2 * xo) * a.ldx + a.xcoff + xg + pr * 8 : -1;
+            hodd |= (unsigned)((2 * yo + 1 < a.xh ? 1 : 0) | (2 * xo + 1 < a.xw ? 2 : 0)) << (2 * q);
+        } else {
+            hoff[q] = ok ? pix * a.ldx + a.xcoff + xg + pr * 8 : -1;
+        }
         hexp |= (unsigned)((ok ? act_scale_exp(a, pix / HW) : 0) & 0xff) << (8 * q);
     }
     u32x4 hx[QI][2];
-    auto load_halo = [&](int c) {
+    // halo h: chunk h (stride 1); chunk h / 4, phase (py, px) = (1,1) (1,0) (0,1) (0,0) for h % 4 (S2)
+    auto load_halo = [&](int h) {
+        const int c = S2 ? h >> 2 : h, ph = S2 ? 3 - (h & 3) : 0, py = ph >> 1, px = ph & 1;
+        const int dph = (py * a.xw + px) * a.ldx;
+        const unsigned need = (unsigned)(py | (px << 1));
 #pragma unroll
         for (int q = 0; q < QI; ++q) {
-            const unsigned off = hoff[q] >= 0 ? (unsigned)(hoff[q] + c * KT) * 4u : 0x80000000u;
+            const bool v = hoff[q] >= 0 && (!S2 || ((hodd >> (2 * q)) & need) == need);
+            const unsigned off = v ? (unsigned)(hoff[q] + dph + c * KT) * 4u : 0x80000000u;
             hx[q][0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc_x, (int)off, 0, 0));
             hx[q][1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc_x, (int)off, 16, 0));
         }
@@ -873,7 +908,7 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
     const int my_dma = NDMA / WAVES + (wid < NDMA % WAVES ? 1 : 0);
     const __amdgpu_buffer_rsrc_t rsrc_w = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7fffffff, 0x00020000);
     auto dma_b = [&](int s, int st) {
-        const int c = s / 9, kt = (s - 9 * c) * CH + c;
+        const int c = s / 9, j = s - 9 * c, kt = (S2 ? s2_tap(j) : j) * CH + c;
         char* Bs = smem + st * 2 * PL_B;
 #pragma unroll
         for (int q = 0; q < (NDMA + WAVES - 1) / WAVES; ++q) {
@@ -914,8 +949,11 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
     auto compute = [&](int st, int dy, int dx) {
         const char* Bs = smem + st * 2 * PL_B;
         const int ch = lane >> 4;
-        const int need = (dy < 0 ? 1 : 0) | (dy > 0 ? 2 : 0) | (dx < 0 ? 4 : 0) | (dx > 0 ? 8 : 0) | 16;
-        const int shift = dy * W + dx;
+        // S2: taps with d = +1 read the phase pixel itself (its own frame; odd rows / columns
+        // past the input were loaded as zeros), d = -1 the previous phase row / column
+        const int need = S2 ? (dy < 0 ? 1 : 0) | (dx < 0 ? 4 : 0) | 16
+                            : (dy < 0 ? 1 : 0) | (dy > 0 ? 2 : 0) | (dx < 0 ? 4 : 0) | (dx > 0 ? 8 : 0) | 16;
+        const int shift = S2 ? (dy < 0 ? -W : 0) + (dx < 0 ? -1 : 0) : dy * W + dx;
         if constexpr (TN < TM) {   // narrow N: B fragments resident, A streamed (VGPRs at 4 waves / SIMD)
             u32x4 bf[TN][3];
 #pragma unroll
@@ -966,7 +1004,7 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
     if (tid < 8) *(u32x4*)(Ah + (tid >> 2) * PL_H + swzh(HR, tid & 3)) = u32x4{0u, 0u, 0u, 0u};
     dma_b(0, 0);
     if (nsteps > 1) dma_b(1, 1);
-    if (CH > 1) load_halo(1);
+    if (nhalo > 1) load_halo(1);
     // Per thread VMEM issue order: ... [halo loads of chunk c+2 at the end of step
     // 9c+8], B(s+2) at the end of step s. At the top of step s, younger than B(s):
     // B(s+1) (if issued) and the halo loads issued at the end of step s-1 or (s = 1)
@@ -977,11 +1015,13 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
         // switch costs a tree of scalar branches per step). (Unrolling the nine taps of a
         // chunk as well measured no better and spills on the 192 / 256-wide tiles.)
         constexpr int MYD = S::NDMA % WAVES == 0 ? S::NDMA / WAVES : 0;
+        int hcur = 0;                                    // the halo in LDS
         for (int s = 0; s < nsteps; ++s) {
-            const int c = s / 9, tap = s - 9 * c;
-            // halo loads younger than B(s): chunk c+1's, issued at the end of step s-1
-            // (tap 0, c >= 1) or in the prologue after B(1) (s = 0, 1)
-            const bool halo_prev = tap == 0 ? c + 1 < CH : (s == 1 && CH > 1);
+            const int tap = s % 9;
+            // halo loads younger than B(s): halo hcur+1's, issued at the end of step s-1 when
+            // that step ended a halo, or in the prologue after B(1) (s = 0, 1)
+            const bool ended = s >= 1 && (S2 ? s2_last(tap == 0 ? 8 : tap - 1) : tap == 0);
+            const bool halo_prev = ended ? hcur + 1 < nhalo : (s <= 1 && nhalo > 1);
             if (halo_prev) {
                 if (s + 1 < nsteps) wait_vm_k<MYD + 2 * QI>();
                 else wait_vm_k<2 * QI>();
@@ -992,16 +1032,18 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();                // B(s) visible; stage (s + 2) % 3 free
             asm volatile("" ::: "memory");
-            const bool rehalo = tap == 8 && c + 1 < CH;
+            const bool rehalo = (S2 ? s2_last(tap) : tap == 8) && hcur + 1 < nhalo;
             if (!rehalo && s + 2 < nsteps) dma_b(s + 2, (s + 2) % 3);
-            const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
+            const int wt = S2 ? s2_tap(tap) : tap;
+            const int dy = wt / 3 - 1, dx = wt - (wt / 3) * 3 - 1;
             compute(s % 3, dy, dx);
             if (rehalo) {
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                __builtin_amdgcn_s_barrier();            // every wave is done with chunk c's halo
+                __builtin_amdgcn_s_barrier();            // every wave is done with halo hcur
                 asm volatile("" ::: "memory");
                 store_halo();
-                if (c + 2 < CH) load_halo(c + 2);
+                ++hcur;
+                if (hcur + 1 < nhalo) load_halo(hcur + 1);
                 if (s + 2 < nsteps) dma_b(s + 2, (s + 2) % 3);
             }
         }
@@ -1593,18 +1635,18 @@ static hipError_t launch_x6_big(const ConvArgs& a, hipStream_t s) {
 template <int BN, int NSB>
 static int x6_halo_lds(const ConvArgs& a) {
     using S = X6Shape<256, BN, 512, 2, 2>;
-    const int HP = 256 + 2 * a.yw + 3;
+    const int HP = a.stride == 2 ? 256 + a.yw + 2 : 256 + 2 * a.yw + 3;
     return std::max(NSB * 2 * S::PL_B + 2 * HP * 64, S::EPR * S::EPLD * 4) + (a.ymax ? 4 * a.B : 0);
 }
 
-template <int BN, int NSB, bool TR = false>
+template <int BN, int NSB, bool TR = false, bool S2 = false>
 static hipError_t launch_x6_halo_t(const ConvArgs& a0, hipStream_t s) {
     ConvArgs a = a0;
     a.w = a.wx3;
     a.ntiles_n = (a.cout + BN - 1) / BN;
     a.mbase = 0;
     static const bool attr = [] {
-        (void)hipFuncSetAttribute((const void*)conv_x6_halo_kernel<BN, NSB, TR>,
+        (void)hipFuncSetAttribute((const void*)conv_x6_halo_kernel<BN, NSB, TR, S2>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         return true;
     }();
@@ -1612,7 +1654,7 @@ static hipError_t launch_x6_halo_t(const ConvArgs& a0, hipStream_t s) {
     const int lds = x6_halo_lds<BN, NSB>(a);
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     const int mt = (a.M + 255) / 256;
-    hipLaunchKernelGGL((conv_x6_halo_kernel<BN, NSB, TR>), dim3(mt * a.ntiles_n), dim3(512), lds, s, a);
+    hipLaunchKernelGGL((conv_x6_halo_kernel<BN, NSB, TR, S2>), dim3(mt * a.ntiles_n), dim3(512), lds, s, a);
     return hipGetLastError();
 }
 
@@ -1622,6 +1664,10 @@ template <int BN, int NSB>
 static hipError_t launch_x6_halo_n(const ConvArgs& a, hipStream_t s) {
     const bool tr = a.tune && a.tune->x6_halo_tr >= (BN >= 128 ? 1 : 2) && !((a.ldy | a.ycoff) & 7) &&
                     (a.res_mode == VD_RES_NONE || !((a.res_ld | a.res_coff) & 7));
+    if constexpr (NSB == 3 && BN >= 64) {   // stride 2: the phase halos (x6_halo_ok)
+        if (a.stride == 2) return tr ? launch_x6_halo_t<BN, 3, true, true>(a, s) : launch_x6_halo_t<BN, 3, false, true>(a, s);
+    }
+    if (a.stride != 1) return hipErrorInvalidValue;
     if (tr) return launch_x6_halo_t<BN, NSB, true>(a, s);
     return launch_x6_halo_t<BN, NSB, false>(a, s);
 }
@@ -1629,16 +1675,24 @@ static hipError_t launch_x6_halo_n(const ConvArgs& a, hipStream_t s) {
 // option x6_halo: 1 two B stages, 2 three where they fit LDS beside the halo
 template <int BN>
 static hipError_t launch_x6_halo(const ConvArgs& a, hipStream_t s) {
-    if (a.tune->x6_halo >= 2 && x6_halo_lds<BN, 3>(a) <= 160 * 1024) return launch_x6_halo_n<BN, 3>(a, s);
+    if ((a.tune->x6_halo >= 2 || a.stride == 2) && x6_halo_lds<BN, 3>(a) <= 160 * 1024) return launch_x6_halo_n<BN, 3>(a, s);
     return launch_x6_halo_n<BN, 2>(a, s);
 }
 
 // 3x3 / stride 1 / pad 1, same-size in and out, K = 9 x Cin in whole 32-channel chunks,
-// halo of at most 512 rows (W <= 126) that fits LDS beside the B stages
+// halo of at most 512 rows (W <= 126) that fits LDS beside the B stages; stride 2 (option
+// x6_halo_s2): the phase halos of at most 512 rows (Wo <= 254), N tiles of >= 64 (Cout > 32,
+// whole DMA rounds), three B stages, dense
 static bool x6_halo_ok(const ConvArgs& a) {
-    if (!a.tune || !a.tune->x6_halo || a.kh != 3 || a.kw != 3 || a.stride != 1 || a.pad != 1) return false;
-    if (a.xh != a.yh || a.xw != a.yw || a.cin_pad % 32 || a.kpad != 9 * a.cin_pad) return false;
-    if (256 + 2 * a.yw + 2 > 512 || (a.ymax && a.B > kAmaxFrames)) return false;
+    if (!a.tune || !a.tune->x6_halo || a.kh != 3 || a.kw != 3 || a.pad != 1) return false;
+    if (a.cin_pad % 32 || a.kpad != 9 * a.cin_pad || (a.ymax && a.B > kAmaxFrames)) return false;
+    if (a.stride == 2) {
+        if (!a.tune->x6_halo_s2 || a.cout <= 32 || a.grp_co) return false;
+        if (a.yh != (a.xh - 1) / 2 + 1 || a.yw != (a.xw - 1) / 2 + 1 || 256 + a.yw + 2 > 512) return false;
+        return (3 * 2 * 256 * 64 + 2 * (256 + a.yw + 2) * 64 + (a.ymax ? 4 * a.B : 0)) <= 160 * 1024;
+    }
+    if (a.stride != 1 || a.xh != a.yh || a.xw != a.yw) return false;
+    if (256 + 2 * a.yw + 2 > 512) return false;
     return true;
 }
 

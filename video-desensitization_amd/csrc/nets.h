@@ -168,7 +168,8 @@ struct Ctx {
     VdTune tune;                                  // kernel-selection switches (vd_set_option)
     hipStream_t stream = nullptr, own_stream = nullptr;
     hipStream_t stream2 = nullptr;               // plate branch runs beside the face branch
-    hipStream_t stream2_prio[2] = {nullptr, nullptr};   // option plate_prio 1 / 2: plate stream at high / low priority
+    hipStream_t stream2_prio[3] = {nullptr, nullptr, nullptr};   // option plate_prio 1 / 2 / 3: plate stream at high /
+                                                                 //   low priority / on plate_cus CUs
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     hipStream_t stream_side = nullptr;           // the face net's second lane (SSH levels 1-2 beside level 0)
     std::vector<hipEvent_t> lane_ev;             // per face op: completion event for the other lane

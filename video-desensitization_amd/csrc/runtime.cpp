@@ -1151,7 +1151,7 @@ int vd_set_option(vd_ctx* h, const char* name, int value) {
         {"plate_s2d", &VdTune::plate_s2d}, {"f32_split", &VdTune::f32_split},
         {"x6_small_k", &VdTune::x6_small_k}, {"x6_small_tiles", &VdTune::x6_small_tiles},
         {"x6_stream", &VdTune::x6_stream}, {"x6_small_k2", &VdTune::x6_small_k2}, {"x6_bn256", &VdTune::x6_bn256},
-        {"x6_exact", &VdTune::x6_exact}, {"x6_mid", &VdTune::x6_mid}, {"block_fuse32", &VdTune::block_fuse32}, {"x6_mf32", &VdTune::x6_mf32}, {"x6_tail", &VdTune::x6_tail}, {"x6_stream_silu", &VdTune::x6_stream_silu}, {"x6_slots", &VdTune::x6_slots}, {"x6_halo", &VdTune::x6_halo}, {"x6_halo_narrow", &VdTune::x6_halo_narrow}, {"x6_adepth", &VdTune::x6_adepth}, {"x6_gemm1x1", &VdTune::x6_gemm1x1}, {"x6_taps", &VdTune::x6_taps}, {"x6_halo_tr", &VdTune::x6_halo_tr}, {"x6_stream256", &VdTune::x6_stream256}, {"plate_stage", &VdTune::plate_stage}, {"ssh_side", &VdTune::ssh_side}, {"face_groups", &VdTune::face_groups}, {"face_group_lag", &VdTune::face_group_lag}, {"plate_s2d32", &VdTune::plate_s2d32}, {"det_group", &VdTune::det_group}, {"chain_gpw", &VdTune::chain_gpw}, {"block32_xd", &VdTune::block32_xd}, {"block32_pipe", &VdTune::block32_pipe}, {"block32_dbg", &VdTune::block32_dbg}, {"plate_prio", &VdTune::plate_prio}, {"x6_one", &VdTune::x6_one},
+        {"x6_exact", &VdTune::x6_exact}, {"x6_mid", &VdTune::x6_mid}, {"block_fuse32", &VdTune::block_fuse32}, {"x6_mf32", &VdTune::x6_mf32}, {"x6_tail", &VdTune::x6_tail}, {"x6_stream_silu", &VdTune::x6_stream_silu}, {"x6_slots", &VdTune::x6_slots}, {"x6_halo", &VdTune::x6_halo}, {"x6_halo_narrow", &VdTune::x6_halo_narrow}, {"x6_halo_s2", &VdTune::x6_halo_s2}, {"x6_adepth", &VdTune::x6_adepth}, {"x6_gemm1x1", &VdTune::x6_gemm1x1}, {"x6_taps", &VdTune::x6_taps}, {"x6_halo_tr", &VdTune::x6_halo_tr}, {"x6_stream256", &VdTune::x6_stream256}, {"plate_stage", &VdTune::plate_stage}, {"ssh_side", &VdTune::ssh_side}, {"face_groups", &VdTune::face_groups}, {"face_group_lag", &VdTune::face_group_lag}, {"plate_s2d32", &VdTune::plate_s2d32}, {"det_group", &VdTune::det_group}, {"chain_gpw", &VdTune::chain_gpw}, {"block32_xd", &VdTune::block32_xd}, {"block32_pipe", &VdTune::block32_pipe}, {"block32_dbg", &VdTune::block32_dbg}, {"plate_prio", &VdTune::plate_prio}, {"plate_cus", &VdTune::plate_cus}, {"x6_one", &VdTune::x6_one},
         {"jenc_gpu", &VdTune::jenc_gpu}, {"jdec_gpu", &VdTune::jdec_gpu}, {"jdec_chunk", &VdTune::jdec_chunk}, {"jdec_sync", &VdTune::jdec_sync}, {"jdec_group", &VdTune::jdec_group},
     };
     for (const Opt& o : opts)
@@ -1294,6 +1294,19 @@ int vd_process(vd_ctx* h, const uint8_t* in, uint8_t* out, int n, int fh, int fw
     // threads, combine_detect.py:214-217): plates on stream2, forked/joined by events.
     const bool fork = do_faces && do_plates;
     hipStream_t plate_stream = ctx->stream2;
+    if (fork && ctx->tune.plate_prio == 3) {
+        hipStream_t& ps = ctx->stream2_prio[2];
+        if (!ps) {   // every (CUs / plate_cus)-th CU: an even share of each XCD
+            int dev = 0, cus = 256;
+            VD_CHECK_HIP(hipGetDevice(&dev));
+            VD_CHECK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+            const int want = std::max(1, std::min(cus, ctx->tune.plate_cus)), step = std::max(1, cus / want);
+            std::vector<uint32_t> mask((cus + 31) / 32, 0u);
+            for (int c = 0, k = 0; c < cus && k < want; c += step, ++k) mask[c / 32] |= 1u << (c % 32);
+            VD_CHECK_HIP(hipExtStreamCreateWithCUMask(&ps, (uint32_t)mask.size(), mask.data()));
+        }
+        plate_stream = ps;
+    }
     if (fork && (ctx->tune.plate_prio == 1 || ctx->tune.plate_prio == 2)) {
         hipStream_t& ps = ctx->stream2_prio[ctx->tune.plate_prio - 1];
         if (!ps) {

@@ -87,7 +87,8 @@ struct VdTune {
     int face_groups = 2;      // face net as G frame groups on G streams (the tails of one group's launches
                               //   fill with the others'; bit-identical; 0 / 1: one launch over the batch)
     int face_group_lag = 0;   //   group g starts after group g - 1's first N ops (0: together)
-    int plate_prio = 0;       // plate branch stream priority (0: default, 1: high, 2: low)
+    int plate_prio = 0;       // plate branch stream priority (0: default, 1: high, 2: low, 3: CU-masked to
+    int plate_cus = 64;       //   plate_cus CUs spread over the XCDs)
     int plate_stage = 3;      // plate branch starts after face stage N (0: with the stem; 1-4: after
                               //   layerN; 5: after the whole face net). After layer3 its HBM-bound
                               //   convs overlap the MFMA-bound late face layers: 30.8 -> 30.0 ms/step
@@ -110,6 +111,7 @@ struct VdTune {
     int x6_halo = 2;          // fp16 pairs, 3x3 stride-1 convs: input split once per 32-channel chunk
                               //   over the tile's linear halo (conv_x6_halo_kernel); 2: three B stages, 1: two
     int x6_halo_narrow = 1;   // ... also for Cout <= 64 (N tiles of 32 / 64)
+    int x6_halo_s2 = 1;       // ... also 3x3 stride-2 convs (phase halos; Cout > 32)
     int x6_adepth = 2;        // A register sets of the 256 x {128, 64, 32} fp16-pair tiles (2 or 4; 4 measured level)
     int x6_slots = 0;         //   workgroup slots of one round (0: the CU count; tests force small values)
     int x6_halo_tr = 2;       // fp32 plan: halo 3x3 tiles with D^T accumulators and the register epilogue
