@@ -528,7 +528,8 @@ def main():
         peak = PEAK_TFLOPS[precision]
         kern = ("conv_x6_kernel<..., 3> launches (f32 operands split exactly into 3 bf16 terms, 6 products on "
                 "v_mfma_f32_16x16x32_bf16, f32 accumulate; peak = 2500/6)" if precision == "fp32_x6" else
-                "stem_pool32_kernel + bottleneck32_kernel + conv_x6_kernel<..., 2> / conv_x6_halo_kernel / conv1x1_x6_kernel<..., 2> "
+                "stem_pool32_kernel + bottleneck32_kernel / bottleneck32p_kernel + chain32_kernel + conv_x6_kernel<..., 2> / "
+                "conv_x6_halo_kernel / conv1x1_x6_kernel<..., 2> "
                 "launches (f32 operands scaled per frame / per "
                 "channel by powers of two and split into fp16 pairs, 3 products on v_mfma_f32_16x16x32_f16, f32 "
                 "accumulate; peak = 2500/3)" if precision == "fp32" else
