@@ -137,7 +137,9 @@ __device__ __forceinline__ void lb_src_rows(const LetterboxArgs& a, int y, int* 
     if (a.mode == LB_AREA2) { *r0 = 2 * ry; *r1 = 2 * ry + 1; return; }
     *ty = linear_tap(ry, a.ih, a.scale_y);
     *r0 = ty->s0;
-    *r1 = ty->s1;
+    // a zero-weight second row (an exact gather: 1080p -> 640 samples rows 3y + 1 with weights
+    // (1, 0)) adds exact zeros, so it is not staged: the pixel reads row r0 twice instead
+    *r1 = ty->a1 ? ty->s1 : -1;
 }
 
 __device__ __forceinline__ void lb_px_lds(const LetterboxArgs& a, const uint8_t* L0, const uint8_t* L1, const Tap& ty,
@@ -209,7 +211,7 @@ __global__ __launch_bounds__(256) void letterbox_s2d_lds_kernel(LetterboxArgs a)
             float v[3] = {0.f, 0.f, 0.f};   // conv zero padding outside the canvas
             const int y = 2 * Y + h - 1;
             if ((unsigned)y < (unsigned)a.oh && (unsigned)x < (unsigned)a.ow)
-                lb_px_lds(a, lrow + (2 * h) * RS, lrow + (2 * h + 1) * RS, ty[h], x, rin[h], v);
+                lb_px_lds(a, lrow + (2 * h) * RS, lrow + (2 * h + (rows[2 * h + 1] >= 0 ? 1 : 0)) * RS, ty[h], x, rin[h], v);
             t[4 * s + 0] = v[0]; t[4 * s + 1] = v[1]; t[4 * s + 2] = v[2];
             t[4 * s + 3] = 0.f;
         }
@@ -245,6 +247,7 @@ __global__ __launch_bounds__(256) void letterbox_s2d_pair_kernel(LetterboxArgs a
     const int rbytes = a.iw * 3;
     const int nch = (rbytes + 15) / 16;
     const int RS = nch * 16;
+    const bool st1[2] = {ra[1] >= 0 || rb[1] >= 0, ra[3] >= 0 || rb[3] >= 0};   // second rows staged
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int row = ra[k] >= 0 ? ra[k] : rb[k];   // the same source row when both canvases need one
@@ -277,7 +280,7 @@ __global__ __launch_bounds__(256) void letterbox_s2d_pair_kernel(LetterboxArgs a
                 float v[3] = {0.f, 0.f, 0.f};
                 const int y = 2 * YY + h - 1;
                 if ((unsigned)y < (unsigned)c.oh && (unsigned)x < (unsigned)c.ow)
-                    lb_px_lds(c, lrow + (2 * h) * RS, lrow + (2 * h + 1) * RS, ty[h], x, rin[h], v);
+                    lb_px_lds(c, lrow + (2 * h) * RS, lrow + (2 * h + (st1[h] ? 1 : 0)) * RS, ty[h], x, rin[h], v);
                 t[4 * s + 0] = v[0]; t[4 * s + 1] = v[1]; t[4 * s + 2] = v[2];
                 t[4 * s + 3] = 0.f;
             }
