@@ -15,6 +15,7 @@
 #include "vd_math.h"
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 
 namespace {
@@ -155,6 +156,12 @@ __device__ __forceinline__ void lb_px_lds(const LetterboxArgs& a, const uint8_t*
 #pragma unroll
             for (int c = 0; c < 3; ++c)
                 p3[c] = (L0[6 * rx + c] + L0[6 * rx + c + 3] + L1[6 * rx + c] + L1[6 * rx + c + 3] + 2) >> 2;
+        } else if (a.gx_k > 0 && ty.a1 == 0) {
+            // exact gather both ways (weights (1, 0): the bilinear sum below reduces to the
+            // source byte exactly, ((4 p + 2) >> 2) = p), e.g. 1080p -> 640: column 3 rx + 1
+            const int sx = a.gx_k * rx + a.gx_c;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) p3[c] = L0[sx * 3 + c];
         } else {
             const Tap tx = linear_tap(rx, a.iw, a.scale_x);
 #pragma unroll
@@ -384,7 +391,40 @@ bool vd_letterbox_pair_ok(const LetterboxArgs& a, const LetterboxArgs& b) {
            ((a.top - b.top) & 1) == 0 && ((a.left - b.left) & 1) == 0;
 }
 
-hipError_t vd_launch_letterbox_pair(const LetterboxArgs& a, const LetterboxArgs& b, hipStream_t s) {
+// linear_tap on the host (the same IEEE round-to-nearest operations as the device): source
+// column s0 and second weight a1 of resized column d
+static void lb_tap_host(int d, int ssize, double scale, int* s0, int* a1) {
+    float f = (float)((((double)d + 0.5) * scale) - 0.5);
+    int s = (int)std::floor(f);
+    f = f - (float)s;
+    if (s < 0) { f = 0.f; s = 0; }
+    if (s >= ssize - 1) { f = 0.f; s = ssize - 1; }
+    *s0 = s;
+    *a1 = (int)std::nearbyint(f * 2048.0f);
+}
+
+// LB_LINEAR columns that are an exact affine gather (every a1 = 0, s0 = k d + c): the kernels'
+// gather fast path (checked over every resized column, so it is exact by construction)
+static void lb_set_gather(LetterboxArgs& a) {
+    a.gx_k = a.gx_c = 0;
+    if (a.mode != LB_LINEAR || a.nw < 2) return;
+    int s0, s1, a1;
+    lb_tap_host(0, a.iw, a.scale_x, &s0, &a1);
+    lb_tap_host(1, a.iw, a.scale_x, &s1, &a1);
+    const int k = s1 - s0, c = s0;
+    if (k <= 0) return;
+    for (int d = 0; d < a.nw; ++d) {
+        lb_tap_host(d, a.iw, a.scale_x, &s0, &a1);
+        if (a1 != 0 || s0 != k * d + c) return;
+    }
+    a.gx_k = k;
+    a.gx_c = c;
+}
+
+hipError_t vd_launch_letterbox_pair(const LetterboxArgs& a0, const LetterboxArgs& b0, hipStream_t s) {
+    LetterboxArgs a = a0, b = b0;
+    lb_set_gather(a);
+    lb_set_gather(b);
     if (!vd_letterbox_pair_ok(a, b)) return hipErrorInvalidValue;
     static const bool attr = [] {
         (void)hipFuncSetAttribute((const void*)letterbox_s2d_pair_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -400,7 +440,9 @@ hipError_t vd_launch_letterbox_pair(const LetterboxArgs& a, const LetterboxArgs&
     return hipGetLastError();
 }
 
-hipError_t vd_launch_letterbox(const LetterboxArgs& a, hipStream_t s) {
+hipError_t vd_launch_letterbox(const LetterboxArgs& a0, hipStream_t s) {
+    LetterboxArgs a = a0;
+    lb_set_gather(a);
     if (a.s2d && a.iw * 3 <= LB_LDS_MAX) {
         static const bool attr = [] {
             (void)hipFuncSetAttribute((const void*)letterbox_s2d_lds_kernel,

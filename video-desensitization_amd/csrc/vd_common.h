@@ -318,6 +318,8 @@ struct LetterboxArgs {
     int s2d;               // 1: space-to-depth canvas for the stride-2 stem (bf16, 16 channels):
                            //    out[Y][X][(py*2+px)*4 + c] = canvas[2Y+py-1][2X+px-1][c], 0 off-canvas,
                            //    Y in [0, oh/2], X in [0, ow/2]
+    int gx_k, gx_c;        // set by the launcher (pre.hip): gx_k > 0 when the LB_LINEAR column taps are
+                           //    an exact gather, source column gx_k * rx + gx_c with weights (1, 0)
 };
 
 // One batch of JPEG frames (jpeg_host.cpp -> jpeg.hip): sparse coefficients per
