@@ -77,6 +77,8 @@ def parse(argv=None):
     ap.add_argument("--records-out", default="", help="rank 0 saves the gathered box records of the last step (.npy)")
     ap.add_argument("--frames", type=int, default=0, help="strong scaling: total frames per step (default 64*8)")
     ap.add_argument("--option", action="append", default=[], help="name=value kernel-selection switch (vd_set_option)")
+    ap.add_argument("--debug", action="append", default=[],
+                    help="name=value timing-only experiment switch (vdt_set_debug; WRONG results while set)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="skip per-kernel HIP event timing")
@@ -128,17 +130,48 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
-def cpu_baseline(frames, sd, seconds, plates=True):
+def _oracle_pass(frames, m, ym, pri, bs, seconds):
+    """Frames through the oracle `bs` at a time (one letterbox + forward per chunk, the
+    per-frame post-processing and mosaic after it) until `seconds` have passed."""
+    import torch
+    from oracle import bbox, letterbox, mosaic
+    from oracle.yolov8 import postprocess as yolo_post, raw_heads
+    done, ref = 0, []
+    t0 = time.perf_counter()
+    while done < len(frames):
+        chunk = list(frames[done:done + bs])
+        x, _ = letterbox.preprocess(chunk)
+        with torch.no_grad():
+            loc, cls, _ = m.forward_raw(torch.from_numpy(x))
+        if ym is not None:       # plate forward + NMS (boxes discarded like the reference)
+            yx = letterbox.yolo_preprocess(chunk)
+            with torch.no_grad():
+                lv = ym(torch.from_numpy(yx))
+            yolo_post(raw_heads(lv), [tuple(t.shape[2:]) for t in lv], yx.shape[2:], chunk[0].shape[:2])
+        for i, img in enumerate(chunk):
+            idx, boxes, _ = bbox.postprocess_frame(loc[i].numpy(), cls[i].numpy(), pri, 0.5, 0.4)
+            ib = bbox.truncate_boxes(bbox.correct_and_scale(boxes, img.shape[0], img.shape[1]))
+            mosaic.mosaic_frame(img, [tuple(int(v) for v in r) for r in ib], 8)
+            ref.append((np.asarray(idx, np.int64), np.asarray(ib, np.int64).reshape(-1, 4)))
+        done += len(chunk)
+        if time.perf_counter() - t0 > seconds:
+            break
+    return done, time.perf_counter() - t0, ref
+
+
+def cpu_baseline(frames, sd, seconds, plates=True, batch=8):
     """The CPU oracle on a bounded sample of the same synthetic frames, on this host's
     cores, doing what the headline step does per frame: torch-CPU fp32 RetinaFace +
     numpy decode/NMS/correction, the YOLOv8n plate forward + NMS beside it (when the
     headline runs plates; the reference discards plate boxes, combine_detect.py:239),
-    and the sequential mosaic. Returns the timing record and the oracle's per-frame
-    (keep list, int boxes) for the parity block."""
+    and the sequential mosaic. Frames are forwarded `batch` at a time, as the
+    reference batches its forwards (combine_detect.py:204,216; config.ini batch 64);
+    the one-frame-at-a-time rate is kept as detail (`per_frame`). Returns the timing
+    record and the oracle's per-frame (keep list, int boxes) for the parity block."""
     import torch
-    from oracle import anchors, bbox, letterbox, mosaic
+    from oracle import anchors
     from oracle.retinaface import build_oracle_model
-    from oracle.yolov8 import build_oracle_yolo, postprocess as yolo_post, raw_heads
+    from oracle.yolov8 import build_oracle_yolo
     from vdmi import weights
     # the GPU box shares its host: use the per-GPU CPU share (OMP_NUM_THREADS, 16 there)
     cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
@@ -146,32 +179,16 @@ def cpu_baseline(frames, sd, seconds, plates=True):
     m = build_oracle_model(sd)
     ym = build_oracle_yolo(weights.yolov8n_state_dict(0)) if plates else None
     pri = anchors.get_anchors((640, 640))
-    done = 0
-    ref = []
-    t0 = time.perf_counter()
-    while done < len(frames):
-        img = frames[done]
-        x, _ = letterbox.preprocess([img])
-        with torch.no_grad():
-            loc, cls, _ = m.forward_raw(torch.from_numpy(x))
-        idx, boxes, _ = bbox.postprocess_frame(loc[0].numpy(), cls[0].numpy(), pri, 0.5, 0.4)
-        ib = bbox.truncate_boxes(bbox.correct_and_scale(boxes, img.shape[0], img.shape[1]))
-        if ym is not None:       # plate forward + NMS (boxes discarded like the reference)
-            yx = letterbox.yolo_preprocess([img])
-            with torch.no_grad():
-                lv = ym(torch.from_numpy(yx))
-            yolo_post(raw_heads(lv), [tuple(t.shape[2:]) for t in lv], yx.shape[2:], img.shape[:2])
-        mosaic.mosaic_frame(img, [tuple(int(v) for v in r) for r in ib], 8)
-        ref.append((np.asarray(idx, np.int64), np.asarray(ib, np.int64).reshape(-1, 4)))
-        done += 1
-        if time.perf_counter() - t0 > seconds:
-            break
-    dt = time.perf_counter() - t0
+    done, dt, ref = _oracle_pass(frames, m, ym, pri, batch, seconds)
+    d1, t1, _ = _oracle_pass(frames[:8], m, ym, pri, 1, max(2.0, seconds / 4))
+    what = (f"torch-CPU fp32 RetinaFace-R50 + numpy decode/NMS/mosaic"
+            f"{' + YOLOv8n plate forward/NMS' if plates else ''}")
     rec = {"value": done / dt, "unit": "frames/s", "cores": cores, "kind": "port", "cpu_model": cpu_model(),
-           "sample": f"{done} x {frames.shape[2]}x{frames.shape[1]} synthetic frames through the oracle "
-                     f"(torch-CPU fp32 RetinaFace-R50 + numpy decode/NMS/mosaic"
-                     f"{' + YOLOv8n plate forward/NMS' if plates else ''}; one frame at a time, where the reference "
-                     f"forwards 64-frame batches, combine_detect.py:204,216), {dt:.1f} s"}
+           "batch": batch,
+           "sample": f"{done} x {frames.shape[2]}x{frames.shape[1]} synthetic frames through the oracle ({what}; "
+                     f"{batch} frames per forward, as the reference batches, combine_detect.py:204,216), {dt:.1f} s",
+           "per_frame": {"value": d1 / t1, "frames": d1, "seconds": round(t1, 2),
+                         "sample": "the same frames one at a time"}}
     return rec, ref
 
 
@@ -223,6 +240,8 @@ class Mode:
         self.ctx = vdmi.Context(device=dev.index or 0, precision=precision.split("_")[0],
                                 max_batch=a.batch, options=opts, microbatch=a.microbatch,
                                 microbatch_stage=a.microbatch_stage)
+        for k, v in (o.split("=", 1) for o in a.debug):
+            self.ctx.set_debug(k, int(v))
         self.ctx.load_weights(_lib.VD_NET_RETINAFACE, sd)
         if plates:
             self.ctx.load_weights(_lib.VD_NET_YOLOV8N, weights.yolov8n_state_dict(0))

@@ -137,9 +137,14 @@ int   vd_set_stream(vd_ctx* ctx, void* hip_stream);   /* NULL -> library-owned s
  * rest to the next launch. Names: conv_stream conv_stream512 conv_dual conv_taps
  * conv_n192 conv_small conv_big conv_big_kmin stream_ntt lb_pair mosaic_map
  * block_fuse chain stem_pool ssh_fuse plate_s2d f32_split x6_small_k x6_small_tiles x6_stream
- * x6_small_k2 x6_bn256 x6_exact x6_stream256 plate_stage jenc_gpu.
+ * x6_small_k2 x6_bn256 x6_exact x6_stream256 plate_stage jenc_gpu (the full list:
+ * runtime.cpp vd_set_option).
  * VD_ERR_ARG for unknown names. */
 int   vd_set_option(vd_ctx* ctx, const char* name, int value);
+/* Test / profiling only: timing experiments that skip work and give WRONG results
+ * while set ("x6_dbg": conv epilogues, "block32_dbg": layer1 block stages). They are
+ * not vd_set_option names (that call refuses them). VD_ERR_ARG for unknown names. */
+int   vdt_set_debug(vd_ctx* ctx, const char* name, int value);
 void* vd_get_stream(vd_ctx* ctx);
 int   vd_sync(vd_ctx* ctx);
 
@@ -148,7 +153,13 @@ int vd_detect(vd_ctx* ctx, const uint8_t* frames, int n, int h, int w, size_t pi
 int vd_detect_plates(vd_ctx* ctx, const uint8_t* frames, int n, int h, int w, size_t pitch,
                      int where, vd_boxes* plates);
 /* Mosaic of caller box lists; host lists with count[f] > cap are refused
- * (VD_ERR_CAPACITY: boxes the caller does not hold would go unblurred). */
+ * (VD_ERR_CAPACITY: boxes the caller does not hold would go unblurred).
+ * Out of place only, as the reference blurs a copy (combine_detect.py:142):
+ * `out` equal to `in`, or (VD_DEVICE) any overlap of the two n*h*pitch ranges, is
+ * VD_ERR_ARG. vd_process with VD_PROC_MOSAIC and VD_DEVICE frames refuses
+ * overlapping `in` / `out` the same way (its one-launch output pass gathers cell
+ * colours from `in` while other workgroups write `out`); VD_HOST frames are staged
+ * in separate device buffers, so host in == out is allowed there. */
 int vd_mosaic(vd_ctx* ctx, const uint8_t* in, uint8_t* out, int n, int h, int w, size_t pitch,
               int where, const vd_boxes* boxes, int level, int mode);
 int vd_process(vd_ctx* ctx, const uint8_t* in, uint8_t* out, int n, int h, int w, size_t pitch,

@@ -200,3 +200,21 @@ def test_rank_shard_totals_and_failure_two_ranks_gloo(fail_rank):
         assert list(got) == list(range(N_LIST))
         for f in range(N_LIST):
             assert (got[f]["faces"][0], got[f]["faces"][3]) == _expect(f)
+
+
+def test_shard_ranks_without_group_is_a_clear_error(tmp_path):
+    """shard="ranks" needs an initialised process group: without one, batch_process_images
+    raises a ValueError naming the fix instead of failing inside torch.distributed."""
+    from vdmi.pipeline import _shard_mode
+    with pytest.raises(ValueError, match="process group"):
+        _shard_mode("ranks", object(), None, False)
+    assert _shard_mode(None, object(), None, False) == "none"
+
+
+def test_run_on_devices_binds_devices_only_when_given():
+    """run_on_devices(devices=...) checks the device list against the shards; without a
+    GPU the device scope is a no-op, so the CPU path runs the same."""
+    from vdmi.dist import run_on_devices
+    assert run_on_devices(lambda i, sh: i * 10 + sh, [1, 2], devices=[0, 0]) == [1, 12]
+    with pytest.raises(ValueError):
+        run_on_devices(lambda i, sh: sh, [1, 2], devices=[0])

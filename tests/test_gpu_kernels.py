@@ -545,16 +545,15 @@ def test_conv_tr_tiles_bit_identical(gpu, face_ctx_factory, case):
     test_conv_matches_torch(gpu, face_ctx_factory, "fp32", case, options=dict(x6_gemm1x1=1, x6_stream=0))
 
 
-@pytest.mark.parametrize("copy", [0, 1])
-def test_mosaic_output_forms_match_oracle(gpu, copy):
-    """Option mosaic_copy: 0 (default) = the band output pass; 1 = copy-first (one plain copy pass, the cell
-    kernel writes each box cell's owned pixel runs, the band output pass only for
-    frames without a cell table); 0 = the band output pass writes every byte. Both
-    exact against the oracle on overlapping / nested boxes, > 256 boxes (no cell
-    table), a cell-table overflow and frames with no boxes."""
+@pytest.mark.parametrize("mapon", [0, 1])
+def test_mosaic_output_forms_match_oracle(gpu, mapon):
+    """Option mosaic_map: 1 (default) = the band output pass with per-band vector maps;
+    0 = the generic per-pixel path. Both exact against the oracle on overlapping /
+    nested boxes, > 256 boxes (no cell table), a cell-table overflow and frames with
+    no boxes."""
     import vdmi
     from vdmi import mosaic_frames, synth
-    ctx = vdmi.Context(precision="bf16", max_batch=4, options={"mosaic_copy": copy})
+    ctx = vdmi.Context(precision="bf16", max_batch=4, options={"mosaic_map": mapon})
     try:
         rng = np.random.default_rng(21)
         frames = synth.frames(4, 480, 720, seed=21)

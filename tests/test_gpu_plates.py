@@ -208,34 +208,6 @@ def test_process_plate_release_point(gpu, stage):
         np.testing.assert_array_equal(res[stage][2][b], res[3][2][b])
 
 
-@pytest.mark.parametrize("prio,cus", [(1, 64), (2, 64), (3, 32), (3, 1)])
-def test_process_plate_stream_placement(gpu, prio, cus):
-    """Option plate_prio puts the plate branch on a high / low priority stream (1 / 2) or
-    on a stream CU-masked to plate_cus CUs (3; runtime.cpp, hipExtStreamCreateWithCUMask).
-    Placement only: boxes and mosaicked frames equal the default stream's."""
-    import vdmi
-    from vdmi import _lib, synth, weights
-    fr = synth.frames(3, 1080, 1920, seed=24)
-    flags = _lib.VD_PROC_FACES | _lib.VD_PROC_PLATES | _lib.VD_PROC_MOSAIC | _lib.VD_PROC_MOSAIC_PLATES
-    res = {}
-    for key, opts in (("alt", {"plate_prio": prio, "plate_cus": cus}), ("base", {})):
-        c = vdmi.Context(precision="fp32", max_batch=3, options=opts)
-        try:
-            c.load_weights(0, weights.retinaface_state_dict(0))
-            c.load_weights(1, weights.yolov8n_state_dict(0))
-            for _ in range(2):                                     # the second call reuses the stream
-                out, faces, plates = c.process(fr, flags=flags)
-            res[key] = (out.copy(), [faces.frame(b)[0].copy() for b in range(3)],
-                        [plates.frame(b)[0].copy() for b in range(3)])
-        finally:
-            c.close()
-    np.testing.assert_array_equal(res["alt"][0], res["base"][0])
-    assert sum(len(x) for x in res["base"][1] + res["base"][2]) > 0
-    for b in range(3):
-        np.testing.assert_array_equal(res["alt"][1][b], res["base"][1][b])
-        np.testing.assert_array_equal(res["alt"][2][b], res["base"][2][b])
-
-
 @pytest.mark.parametrize("prec,plates,groups", [("fp32", True, 2), ("fp32", False, 2), ("bf16", True, 2),
                                                ("fp32", True, 3), ("fp16", False, 4)])
 def test_process_face_groups_bit_identical(gpu, prec, plates, groups):

@@ -76,8 +76,11 @@ def test_batch_process_images_devices_equal_single(gpu, tmp_path, codec):
     src = _jpeg_dir(tmp_path / "in")
     kw = {} if codec else {"loader": lambda p: _frame(int(os.path.basename(p)[1:4]))}
     runs = {}
-    for name, ids, shard in (("one", [0], None), ("two", [0, 0], "devices")):
-        face, plate = _detectors(ids)
+    dets = {"one": _detectors([0]), "two": _detectors([0, 0])}
+    # "two" runs twice on the same detectors: the second call finds its fused contexts
+    # cached, and each shard must still get its OWN context (ids repeat: [0, 0])
+    for name, det, shard in (("one", "one", None), ("two", "two", "devices"), ("two_again", "two", "devices")):
+        face, plate = dets[det]
         saved, rec = {}, {}
         if not codec:
             kw["saver"] = lambda img, p, saved=saved: saved.__setitem__(os.path.basename(p), img.copy())
@@ -85,16 +88,20 @@ def test_batch_process_images_devices_equal_single(gpu, tmp_path, codec):
         tot = batch_process_images(str(src), str(out), face, plate, batch_size=4, shard=shard, records=rec,
                                    mosaic_plates=True, **kw)
         runs[name] = (tot, rec, _files(out) if codec else saved)
-    (t1, r1, o1), (t2, r2, o2) = runs["one"], runs["two"]
-    assert t1[0] == N and t1[1] > 0 and t2 == t1
+    ctxs = list(dets["two"][0].__dict__["_fused_ctx"].values())
+    assert len(ctxs) == 2 and ctxs[0] is not ctxs[1]
+    (t1, r1, o1) = runs["one"]
+    assert t1[0] == N and t1[1] > 0
     assert sorted(r1) == sorted(o1 if codec else [f"f{i:03d}.jpg" for i in range(N)]) or len(r1) == N
-    assert r2 == r1
-    assert sorted(o1) == sorted(o2) and len(o1) == N
-    for k in o1:
-        if codec:
-            assert o1[k] == o2[k], k
-        else:
-            np.testing.assert_array_equal(o1[k], o2[k], err_msg=k)
+    for name in ("two", "two_again"):
+        t2, r2, o2 = runs[name]
+        assert t2 == t1 and r2 == r1, name
+        assert sorted(o1) == sorted(o2) and len(o1) == N
+        for k in o1:
+            if codec:
+                assert o1[k] == o2[k], (name, k)
+            else:
+                np.testing.assert_array_equal(o1[k], o2[k], err_msg=f"{name} {k}")
 
 
 def _free_port():

@@ -87,3 +87,71 @@ def test_host_boxes_struct():
     assert s.cap == 5 and s.where == _lib.VD_HOST and s.count == hb.count.ctypes.data
     hb.count[:] = [2, 0, 9]
     assert hb.frame(0)[0].shape == (2, 4) and hb.frame(2)[0].shape == (5, 4)
+
+
+# ---- boundary hardening (GPU: a context needs a device) -------------------------
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["x6_dbg", "block32_dbg", "mosaic_copy", "face_group_lag", "plate_prio",
+                                  "plate_cus"])
+def test_set_option_refuses_debug_and_removed_switches(gpu, name):
+    """The timing-only switches that skip work (wrong results) are not vd_set_option
+    names -- only the test entry vdt_set_debug takes them -- and the dead experiment
+    switches are gone."""
+    import vdmi
+    from vdmi import _lib
+    ctx = vdmi.Context(precision="fp32", max_batch=1)
+    try:
+        with pytest.raises(_lib.VdError, match="unknown option"):
+            ctx.set_option(name, 1)
+        if name.endswith("_dbg"):
+            ctx.set_debug(name, 0)
+        else:
+            with pytest.raises(_lib.VdError, match="unknown debug switch"):
+                ctx.set_debug(name, 0)
+        ctx.set_option("face_groups", 2)              # a production switch still takes
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
+def test_process_refuses_overlapping_mosaic_output(gpu):
+    """vd_process with VD_PROC_MOSAIC on device frames is out of place
+    (combine_detect.py:142 blurs a copy, :247-249 reads each previous box's output):
+    out == in, or out overlapping in by part of a frame, is VD_ERR_ARG -- the fused
+    output pass would gather cell colours from pixels other workgroups already
+    rewrote. vd_mosaic refuses the same. A separate output buffer works."""
+    import torch
+    import vdmi
+    from vdmi import _lib, synth, weights
+    fr = torch.from_numpy(synth.frames(2, 120, 160, seed=3)).cuda()
+    ctx = vdmi.Context(precision="fp32", max_batch=2)
+    try:
+        ctx.load_weights(0, weights.retinaface_state_dict(0))
+        with pytest.raises(_lib.VdError, match="out-of-place"):
+            ctx.process(fr, out=fr)
+        big = torch.zeros((3, 120, 160, 3), dtype=torch.uint8, device="cuda")
+        big[:2] = fr
+        with pytest.raises(_lib.VdError, match="out-of-place"):
+            ctx.process(big[:2], out=big[1:])                # shifted by one frame: overlaps
+        faces = _lib.HostBoxes(2, 4)
+        faces.count[:] = [1, 0]
+        faces.xyxy[0, 0] = [10, 10, 60, 50]
+        with pytest.raises(_lib.VdError, match="out-of-place"):
+            _mosaic_call(ctx, big[:2], big[1:], faces)
+        _mosaic_call(ctx, big[:2], torch.empty_like(fr), faces)          # separate output: fine
+        out, _, _ = ctx.process(fr)                          # out of place: fine
+        assert out.shape == fr.shape
+        torch.cuda.synchronize()
+    finally:
+        ctx.close()
+
+
+def _mosaic_call(ctx, src, dst, boxes):
+    """vd_mosaic on device frames through the raw ABI (src / dst torch uint8 [n,h,w,3])."""
+    import ctypes
+    from vdmi import _lib
+    n, h, w, _ = src.shape
+    s = boxes.struct()
+    _lib.check(ctx._lib.vd_mosaic(ctx._h, ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(dst.data_ptr()), n, h, w,
+                                  w * 3, _lib.VD_DEVICE, ctypes.byref(s), 8, _lib.VD_MOSAIC_OUT_OF_PLACE))

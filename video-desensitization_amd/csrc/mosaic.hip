@@ -166,47 +166,8 @@ __device__ __forceinline__ void walk_back(const MBox* tab, const uint64_t (*ovl)
     }
 }
 
-// First offset d in [0, len) of box-axis cell u: the smallest d whose resizeNN
-// up-map min(floor(d * f), s - 1) reaches u (the map is monotone in d); len for u = s
-__device__ __forceinline__ int cell_start(int u, int len, int s, double f) {
-    if (u <= 0) return 0;
-    if (u >= s) return len;
-    auto map = [&](int d) { return min((int)floor(VD_DMUL((double)d, f)), s - 1); };
-    int d = min(len, (int)(((double)u * len) / s));
-    while (d > 0 && map(d - 1) >= u) --d;
-    while (d < len && map(d) < u) ++d;
-    return d;
-}
-
-// bytes [3 x0, 3 x1) of an RGB row <- colour c (packed R | G << 8 | B << 16): head
-// bytes up to 4-B alignment, 4-B words of the 3-byte pattern at their phase, tail bytes.
-// Only bytes inside the range are written (cells sharing a word write disjoint bytes).
-__device__ __forceinline__ void fill_rgb(uint8_t* row, int x0, int x1, uint32_t c) {
-    int bo = 3 * x0;
-    const int be = 3 * x1, b0 = 3 * x0;
-    const uint8_t col[3] = {(uint8_t)(c & 255u), (uint8_t)((c >> 8) & 255u), (uint8_t)((c >> 16) & 255u)};
-    while (bo < be && ((uintptr_t)(row + bo) & 3)) { row[bo] = col[(bo - b0) % 3]; ++bo; }
-    if (bo + 4 <= be) {
-        uint32_t wv[3];
-#pragma unroll
-        for (int p = 0; p < 3; ++p)
-            wv[p] = (uint32_t)col[p] | ((uint32_t)col[(p + 1) % 3] << 8) | ((uint32_t)col[(p + 2) % 3] << 16) |
-                    ((uint32_t)col[p] << 24);
-        int ph = (bo - b0) % 3;
-        for (; bo + 4 <= be; bo += 4) {
-            *(uint32_t*)(row + bo) = wv[ph];
-            ph = ph == 2 ? 0 : ph + 1;
-        }
-    }
-    for (; bo < be; ++bo) row[bo] = col[(bo - b0) % 3];
-}
-
 // One thread per mosaic cell of every box of a fast-path frame (flat over the
-// frame's cells): map, walk, gather the colour into the cell table. With the
-// copy-first output (map_on & 8, after mosaic_copy_kernel), the thread also writes
-// the cell's pixels that no LATER box covers (the last box containing a pixel owns
-// it, combine_detect.py:246-249): whole rows when no later box meets the cell,
-// else owned runs per row.
+// frame's cells): map, walk, gather the colour into the cell table.
 __global__ __launch_bounds__(256) void mosaic_cell_kernel(MosaicArgs a) {
     __shared__ MBox s_tab[BOX_FAST];
     __shared__ uint64_t s_ovl[BOX_FAST][4];
@@ -282,91 +243,8 @@ __global__ __launch_bounds__(256) void mosaic_cell_kernel(MosaicArgs a) {
         const uint8_t* sp = src + (size_t)y * a.pitch + x * 3;
         const uint32_t colour = (uint32_t)sp[0] | ((uint32_t)sp[1] << 8) | ((uint32_t)sp[2] << 16);
         cells[t] = colour;
-        if (!(a.map_on & 8)) continue;
-        // the cell's pixel rectangle and the later boxes that meet it
-        const int bw = bk.x2 - bk.x1, bh = bk.y2 - bk.y1;
-        const int cx0 = bk.x1 + cell_start(ux, bw, bk.sw, bk.fux), cx1 = bk.x1 + cell_start(ux + 1, bw, bk.sw, bk.fux);
-        const int cy0 = bk.y1 + cell_start(uy, bh, bk.sh, bk.fuy), cy1 = bk.y1 + cell_start(uy + 1, bh, bk.sh, bk.fuy);
-        uint64_t later[4];
-        bool any = false;
-#pragma unroll
-        for (int wq = 0; wq < 4; ++wq) {
-            uint64_t m = s_ovl[k][wq];
-            const int lo = k + 1 - 64 * wq;              // bits >= lo of this word are boxes > k
-            m = lo <= 0 ? m : (lo >= 64 ? 0ULL : m & ~((1ULL << lo) - 1ULL));
-            uint64_t keep = 0;
-            while (m) {
-                const int bit = __ffsll((long long)m) - 1;
-                m &= m - 1;
-                const MBox& bj = s_tab[64 * wq + bit];
-                if (bj.x1 < cx1 && cx0 < bj.x2 && bj.y1 < cy1 && cy0 < bj.y2) keep |= 1ULL << bit;
-            }
-            later[wq] = keep;
-            any |= keep != 0;
-        }
-        uint8_t* dst = a.out + (size_t)f * a.h * a.pitch;
-        for (int py = cy0; py < cy1; ++py) {
-            uint8_t* row = dst + (size_t)py * a.pitch;
-            if (!any) {
-                fill_rgb(row, cx0, cx1, colour);
-                continue;
-            }
-            int run = -1;                                 // owned runs: pixels no later box covers
-            for (int px = cx0; px <= cx1; ++px) {
-                bool owned = px < cx1;
-                if (owned) {
-#pragma unroll
-                    for (int wq = 0; wq < 4 && owned; ++wq) {
-                        uint64_t m = later[wq];
-                        while (m && owned) {
-                            const int bit = __ffsll((long long)m) - 1;
-                            m &= m - 1;
-                            if (inside(s_tab[64 * wq + bit], py, px)) owned = false;
-                        }
-                    }
-                }
-                if (owned && run < 0) run = px;
-                if (!owned && run >= 0) {
-                    fill_rgb(row, run, px, colour);
-                    run = -1;
-                }
-            }
-        }
     }
 }
-
-// Copy-first output (option mosaic_map & 8 with 16-B aligned rows): every frame copied
-// to the output in one pass, 16-row bands, each wave moving contiguous 1-KB spans with
-// the next four vectors loaded before this four are stored; the cell kernel then
-// writes the box pixels (their owned runs) and mosaic_out_kernel only the frames
-// without a cell table (> BOX_FAST boxes or cell-table overflow).
-__global__ __launch_bounds__(256) void mosaic_copy_kernel(MosaicArgs a) {
-    const int f = blockIdx.y, y0 = blockIdx.x * ROWS;
-    const int rows = min(ROWS, a.h - y0);
-    const size_t base = ((size_t)f * a.h + y0) * a.pitch;
-    const int nv = (int)((size_t)rows * a.pitch / 16);
-    const uint4* s4 = (const uint4*)(a.in + base);
-    uint4* d4 = (uint4*)(a.out + base);
-    int i = threadIdx.x;
-    uint4 v0{}, v1{}, v2{}, v3{};
-    auto load4 = [&](int j, uint4& x0, uint4& x1, uint4& x2, uint4& x3) {
-        if (j < nv) x0 = s4[j];
-        if (j + 256 < nv) x1 = s4[j + 256];
-        if (j + 512 < nv) x2 = s4[j + 512];
-        if (j + 768 < nv) x3 = s4[j + 768];
-    };
-    load4(i, v0, v1, v2, v3);
-    for (; i < nv; i += 1024) {
-        uint4 n0{}, n1{}, n2{}, n3{};
-        load4(i + 1024, n0, n1, n2, n3);
-        d4[i] = v0;
-        if (i + 256 < nv) d4[i + 256] = v1;
-        if (i + 512 < nv) d4[i + 512] = v2;
-        if (i + 768 < nv) d4[i + 768] = v3;
-        v0 = n0; v1 = n1; v2 = n2; v3 = n3;
-    }
-}
-
 
 // Backward walk of (y, x) from band entry t (or, on band overflow, over the whole
 // table); returns the packed source colour. Out of line: the rare path (cell
@@ -473,7 +351,6 @@ __global__ __launch_bounds__(256) void mosaic_out_kernel(MosaicArgs a) {
     const int* cpref = a.cpref + (size_t)f * (BOX_FAST + 1);
     // FUSED: the frame's boxes fit the LDS table (else per-pixel walks over the raw list)
     const bool use_cells = FUSED ? nb <= BOX_FAST : (nb <= BOX_FAST && cpref[nb] <= CELL_CAP);
-    if (!FUSED && (a.map_on & 8) && a.vec_ok && use_cells) return;   // copy-first: copy + cell kernel wrote the frame
     if constexpr (FUSED) {
         if (use_cells)
             for (int k = tid; k < nb; k += 256) {
@@ -952,11 +829,6 @@ hipError_t vd_launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w
     MosaicArgs a{in, out, n, h, w, pitch, cnt0, xy0, cap0, cnt1, xy1, cap1, level, vec_ok, (MBox*)table, tcap,
                  (int*)cpre, (uint32_t*)cel, 1};
     a.map_on = map_on;
-    if (!vec_ok) a.map_on &= ~8;                     // copy-first needs 16-B aligned rows
-    if (stages & 4) {
-        if (!(a.map_on & 8)) return hipSuccess;
-        hipLaunchKernelGGL(mosaic_copy_kernel, dim3((h + ROWS - 1) / ROWS, n), dim3(256), 0, s, a);
-    }
     if (stages & 1) hipLaunchKernelGGL(mosaic_cell_kernel, dim3(cell_blocks, n), dim3(256), 0, s, a);
     if (stages & 2) hipLaunchKernelGGL(mosaic_out_kernel<false>, dim3((h + ROWS - 1) / ROWS, n), dim3(256), 0, s, a);
     if (stages & 8) hipLaunchKernelGGL(mosaic_out_kernel<true>, dim3((h + ROWS - 1) / ROWS, n), dim3(256), 0, s, a);

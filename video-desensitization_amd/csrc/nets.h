@@ -168,8 +168,6 @@ struct Ctx {
     VdTune tune;                                  // kernel-selection switches (vd_set_option)
     hipStream_t stream = nullptr, own_stream = nullptr;
     hipStream_t stream2 = nullptr;               // plate branch runs beside the face branch
-    hipStream_t stream2_prio[3] = {nullptr, nullptr, nullptr};   // option plate_prio 1 / 2 / 3: plate stream at high /
-                                                                 //   low priority / on plate_cus CUs
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     hipStream_t stream_side = nullptr;           // the face net's second lane (SSH levels 1-2 beside level 0)
     std::vector<hipEvent_t> lane_ev;             // per face op: completion event for the other lane
@@ -177,7 +175,6 @@ struct Ctx {
     hipEvent_t ev_half = nullptr;                // option face_groups: fork of the frame groups
     std::vector<hipStream_t> group_streams;      // option face_groups: streams of frame groups 1..G-1
     std::vector<hipEvent_t> group_events;        //   and their completion events (joined by the context stream)
-    std::vector<hipEvent_t> group_lag_events;    //   group g done with its first face_group_lag ops
     std::map<int, unsigned*> amax_snaps;         // per conv: its input's range slots frozen (in-place concat)
     int fork_at = -1;                                // run_ops records ev_fork after this many face ops
     std::mutex mu;

@@ -23,6 +23,12 @@
 
 static thread_local std::string g_err;
 
+// [a, a + bytes) and [b, b + bytes) share a byte (device frame batches of one geometry)
+static bool vd_ranges_overlap(const void* a, const void* b, size_t bytes) {
+    const uintptr_t x = (uintptr_t)a, y = (uintptr_t)b;
+    return bytes && x < y + bytes && y < x + bytes;
+}
+
 int vd_set_error(int code, const char* fmt, ...) {
     char buf[1024];
     va_list ap;
@@ -887,24 +893,13 @@ int Ctx::face_forward(int n) {
         if (!ev_half) VD_CHECK_HIP(hipEventCreateWithFlags(&ev_half, hipEventDisableTiming));
         if (net.amax) VD_CHECK_HIP(hipMemsetAsync(net.amax, 0, net.amax_bytes, stream));
         VD_CHECK_HIP(hipEventRecord(ev_half, stream));
-        // option face_group_lag = L: group g starts once group g - 1 has finished its
-        // first L ops (0: all groups start together)
         const int ne = (int)net.ops.size();
-        const int lag = std::min(std::max(tune.face_group_lag, 0), ne);
-        while ((int)group_lag_events.size() < G - 1) {
-            hipEvent_t ev;
-            VD_CHECK_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-            group_lag_events.push_back(ev);
-        }
         hipStream_t main = stream;
         for (int g = 0; g < G; ++g) {
             const int f0 = (int)((long)n * g / G), f1 = (int)((long)n * (g + 1) / G);
             stream = g ? group_streams[g - 1] : main;
-            if (g) VD_CHECK_HIP(hipStreamWaitEvent(stream, lag ? group_lag_events[g - 1] : ev_half, 0));
-            int rc = run_ops(net, 0, lag, f0, f1 - f0);
-            if (!rc && lag && g + 1 < G && hipEventRecord(group_lag_events[g], stream) != hipSuccess)
-                rc = vd_set_error(VD_ERR_HIP, "group lag event");
-            if (!rc) rc = run_ops(net, lag, ne, f0, f1 - f0);
+            if (g) VD_CHECK_HIP(hipStreamWaitEvent(stream, ev_half, 0));
+            int rc = run_ops(net, 0, ne, f0, f1 - f0);
             if (!rc && g && hipEventRecord(group_events[g - 1], stream) != hipSuccess)
                 rc = vd_set_error(VD_ERR_HIP, "group event");
             stream = main;
@@ -957,31 +952,17 @@ int Ctx::launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w, siz
     const int tcap = (cnt0 ? cap0 : 0) + (cnt1 ? cap1 : 0);
     int rc = ensure_staging(&mosaic_table, &mosaic_table_bytes, vd_mosaic_table_bytes(n, tcap) + 64);
     if (rc) return rc;
-    const int map_on = tune.mosaic_map | (tune.mosaic_nt << 1) | (tune.mosaic_copy && in != out ? 8 : 0);
-    // copy-first gathers source colours while it writes output pixels: never in place
-    const bool copy_first = tune.mosaic_copy && in != out && (pitch % 16 == 0) && ((uintptr_t)in % 16 == 0) &&
-                            ((uintptr_t)out % 16 == 0);
+    const int map_on = tune.mosaic_map | (tune.mosaic_nt << 1);
     auto launch = [&](int stages) {
         return vd_launch_mosaic(in, out, n, h, w, pitch, cnt0, xy0, cap0, cnt1, xy1, cap1, level, mosaic_table, stages,
                                 map_on, tune.mosaic_cells, stream);
     };
     hipError_t e = hipSuccess;
-    if (tune.mosaic_fused && !copy_first) {
+    if (tune.mosaic_fused) {
         // one launch: the output pass walks and gathers its bands' cells itself (family 1)
         t_begin(1, 2.0 * n * (double)h * w * 3);
         e = launch(8);
         t_end();
-    } else if (copy_first) {
-        // every byte once by the copy (family 1, the output pass), then the cell kernel's
-        // box pixels and the frames without a cell table (family 6)
-        t_begin(1, 2.0 * n * (double)h * w * 3);
-        e = launch(4);
-        t_end();
-        if (e == hipSuccess) {
-            t_begin(6, 0);
-            e = launch(1 | 2);
-            t_end();
-        }
     } else {
         t_begin(6, 0);
         e = launch(1);
@@ -1093,8 +1074,6 @@ int vd_destroy(vd_ctx* h) {
     if (ctx->jpeg_ev) hipEventDestroy(ctx->jpeg_ev);
     for (auto& t : ctx->ev_pool) { hipEventDestroy(t.a); hipEventDestroy(t.b); }
     hipStreamSynchronize(ctx->stream2);
-    for (hipStream_t ps : ctx->stream2_prio)
-        if (ps) { hipStreamSynchronize(ps); hipStreamDestroy(ps); }
     if (ctx->stream_side) {
         hipStreamSynchronize(ctx->stream_side);
         hipStreamDestroy(ctx->stream_side);
@@ -1110,7 +1089,6 @@ int vd_destroy(vd_ctx* h) {
         hipStreamDestroy(ctx->group_streams[g]);
         hipEventDestroy(ctx->group_events[g]);
     }
-    for (hipEvent_t ev : ctx->group_lag_events) hipEventDestroy(ev);
     hipStreamDestroy(ctx->stream2);
     hipStreamDestroy(ctx->own_stream);
     delete ctx;
@@ -1146,12 +1124,12 @@ int vd_set_option(vd_ctx* h, const char* name, int value) {
         {"conv_dual", &VdTune::conv_dual}, {"conv_taps", &VdTune::conv_taps}, {"conv_n192", &VdTune::conv_n192},
         {"conv_small", &VdTune::conv_small}, {"conv_big", &VdTune::conv_big},
         {"conv_big_kmin", &VdTune::conv_big_kmin}, {"stream_ntt", &VdTune::stream_ntt},
-        {"lb_pair", &VdTune::lb_pair}, {"mosaic_map", &VdTune::mosaic_map}, {"mosaic_nt", &VdTune::mosaic_nt}, {"mosaic_cells", &VdTune::mosaic_cells}, {"mosaic_copy", &VdTune::mosaic_copy}, {"mosaic_fused", &VdTune::mosaic_fused}, {"block_fuse", &VdTune::block_fuse},
+        {"lb_pair", &VdTune::lb_pair}, {"mosaic_map", &VdTune::mosaic_map}, {"mosaic_nt", &VdTune::mosaic_nt}, {"mosaic_cells", &VdTune::mosaic_cells}, {"mosaic_fused", &VdTune::mosaic_fused}, {"block_fuse", &VdTune::block_fuse},
         {"chain", &VdTune::chain}, {"stem_pool", &VdTune::stem_pool}, {"ssh_fuse", &VdTune::ssh_fuse},
         {"plate_s2d", &VdTune::plate_s2d}, {"f32_split", &VdTune::f32_split},
         {"x6_small_k", &VdTune::x6_small_k}, {"x6_small_tiles", &VdTune::x6_small_tiles},
         {"x6_stream", &VdTune::x6_stream}, {"x6_small_k2", &VdTune::x6_small_k2}, {"x6_bn256", &VdTune::x6_bn256},
-        {"x6_exact", &VdTune::x6_exact}, {"x6_mid", &VdTune::x6_mid}, {"block_fuse32", &VdTune::block_fuse32}, {"x6_mf32", &VdTune::x6_mf32}, {"x6_tail", &VdTune::x6_tail}, {"x6_stream_silu", &VdTune::x6_stream_silu}, {"x6_slots", &VdTune::x6_slots}, {"x6_halo", &VdTune::x6_halo}, {"x6_halo_narrow", &VdTune::x6_halo_narrow}, {"x6_halo_s2", &VdTune::x6_halo_s2}, {"x6_adepth", &VdTune::x6_adepth}, {"x6_gemm1x1", &VdTune::x6_gemm1x1}, {"x6_taps", &VdTune::x6_taps}, {"x6_halo_tr", &VdTune::x6_halo_tr}, {"x6_stream256", &VdTune::x6_stream256}, {"plate_stage", &VdTune::plate_stage}, {"ssh_side", &VdTune::ssh_side}, {"face_groups", &VdTune::face_groups}, {"face_group_lag", &VdTune::face_group_lag}, {"plate_s2d32", &VdTune::plate_s2d32}, {"det_group", &VdTune::det_group}, {"chain_gpw", &VdTune::chain_gpw}, {"block32_xd", &VdTune::block32_xd}, {"block32_pipe", &VdTune::block32_pipe}, {"block32_dbg", &VdTune::block32_dbg}, {"plate_prio", &VdTune::plate_prio}, {"plate_cus", &VdTune::plate_cus}, {"x6_one", &VdTune::x6_one},
+        {"x6_exact", &VdTune::x6_exact}, {"x6_mid", &VdTune::x6_mid}, {"block_fuse32", &VdTune::block_fuse32}, {"x6_mf32", &VdTune::x6_mf32}, {"x6_tail", &VdTune::x6_tail}, {"x6_stream_silu", &VdTune::x6_stream_silu}, {"x6_slots", &VdTune::x6_slots}, {"x6_halo", &VdTune::x6_halo}, {"x6_halo_narrow", &VdTune::x6_halo_narrow}, {"x6_halo_s2", &VdTune::x6_halo_s2}, {"x6_adepth", &VdTune::x6_adepth}, {"x6_gemm1x1", &VdTune::x6_gemm1x1}, {"x6_taps", &VdTune::x6_taps}, {"x6_halo_tr", &VdTune::x6_halo_tr}, {"x6_stream256", &VdTune::x6_stream256}, {"plate_stage", &VdTune::plate_stage}, {"ssh_side", &VdTune::ssh_side}, {"face_groups", &VdTune::face_groups}, {"plate_s2d32", &VdTune::plate_s2d32}, {"det_group", &VdTune::det_group}, {"chain_gpw", &VdTune::chain_gpw}, {"block32_xd", &VdTune::block32_xd}, {"block32_pipe", &VdTune::block32_pipe}, {"x6_one", &VdTune::x6_one},
         {"jenc_gpu", &VdTune::jenc_gpu}, {"jdec_gpu", &VdTune::jdec_gpu}, {"jdec_chunk", &VdTune::jdec_chunk}, {"jdec_sync", &VdTune::jdec_sync}, {"jdec_group", &VdTune::jdec_group},
     };
     for (const Opt& o : opts)
@@ -1162,6 +1140,16 @@ int vd_set_option(vd_ctx* h, const char* name, int value) {
             return VD_OK;
         }
     return vd_set_error(VD_ERR_ARG, "unknown option '%s'", name);
+}
+
+int vdt_set_debug(vd_ctx* h, const char* name, int value) {
+    Ctx* ctx = (Ctx*)h;
+    VD_ENTRY(ctx);
+    if (!name) return vd_set_error(VD_ERR_ARG, "null debug switch name");
+    // timing-only stage skips: results are WRONG while set (tools/x6bench, tools/runs)
+    if (!strcmp(name, "x6_dbg")) { ctx->tune.x6_dbg = value; return VD_OK; }
+    if (!strcmp(name, "block32_dbg")) { ctx->tune.block32_dbg = value; return VD_OK; }
+    return vd_set_error(VD_ERR_ARG, "unknown debug switch '%s'", name);
 }
 
 int vd_set_stream(vd_ctx* h, void* s) {
@@ -1221,10 +1209,11 @@ int vd_mosaic(vd_ctx* h, const uint8_t* in, uint8_t* out, int n, int fh, int fw,
     if (mode != VD_MOSAIC_OUT_OF_PLACE) return vd_set_error(VD_ERR_ARG, "unsupported mosaic mode %d", mode);
     if (!in || !out || !boxes || !boxes->count || !boxes->xyxy || boxes->cap <= 0)
         return vd_set_error(VD_ERR_ARG, "vd_mosaic: null argument");
-    if ((const void*)in == (const void*)out)
-        return vd_set_error(VD_ERR_ARG, "vd_mosaic: out-of-place only (out must not alias in)");
     if (n <= 0 || fh <= 0 || fw <= 0 || pitch < (size_t)fw * 3 || level <= 0)
         return vd_set_error(VD_ERR_ARG, "vd_mosaic: bad geometry");
+    if ((const void*)in == (const void*)out ||
+        (where == VD_DEVICE && vd_ranges_overlap(in, out, (size_t)n * fh * pitch)))
+        return vd_set_error(VD_ERR_ARG, "vd_mosaic: out-of-place only (out must not overlap in)");
     int rc = VD_OK;
     const uint8_t* din = in;
     uint8_t* dout = out;
@@ -1276,6 +1265,12 @@ int vd_process(vd_ctx* h, const uint8_t* in, uint8_t* out, int n, int fh, int fw
     if (do_mosaic && !out) return vd_set_error(VD_ERR_ARG, "MOSAIC needs an output buffer");
     int rc = ctx->check_frames(n, fh, fw, pitch);
     if (rc) return rc;
+    // the mosaic is out of place (combine_detect.py:142 blurs a copy; each box reads the
+    // previous box's output, :247-249): its one-launch output pass gathers cell colours
+    // from `in` anywhere in the frame while other workgroups write `out`, so device
+    // frames that overlap would race (host frames are staged in separate buffers)
+    if (do_mosaic && where == VD_DEVICE && vd_ranges_overlap(in, out, (size_t)n * fh * pitch))
+        return vd_set_error(VD_ERR_ARG, "vd_process: MOSAIC is out-of-place (out must not overlap in)");
     BoxTargets tf{}, tp{};
     if (do_faces && (rc = ctx->box_targets(faces, n, tf))) return rc;
     if (do_plates && plates) {   // plate box staging must not alias the face staging
@@ -1294,29 +1289,6 @@ int vd_process(vd_ctx* h, const uint8_t* in, uint8_t* out, int n, int fh, int fw
     // threads, combine_detect.py:214-217): plates on stream2, forked/joined by events.
     const bool fork = do_faces && do_plates;
     hipStream_t plate_stream = ctx->stream2;
-    if (fork && ctx->tune.plate_prio == 3) {
-        hipStream_t& ps = ctx->stream2_prio[2];
-        if (!ps) {   // every (CUs / plate_cus)-th CU: an even share of each XCD
-            int dev = 0, cus = 256;
-            VD_CHECK_HIP(hipGetDevice(&dev));
-            VD_CHECK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-            const int want = std::max(1, std::min(cus, ctx->tune.plate_cus)), step = std::max(1, cus / want);
-            std::vector<uint32_t> mask((cus + 31) / 32, 0u);
-            for (int c = 0, k = 0; c < cus && k < want; c += step, ++k) mask[c / 32] |= 1u << (c % 32);
-            VD_CHECK_HIP(hipExtStreamCreateWithCUMask(&ps, (uint32_t)mask.size(), mask.data()));
-        }
-        plate_stream = ps;
-    }
-    if (fork && (ctx->tune.plate_prio == 1 || ctx->tune.plate_prio == 2)) {
-        hipStream_t& ps = ctx->stream2_prio[ctx->tune.plate_prio - 1];
-        if (!ps) {
-            int least = 0, greatest = 0;
-            VD_CHECK_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
-            VD_CHECK_HIP(hipStreamCreateWithPriority(&ps, hipStreamNonBlocking,
-                                                     ctx->tune.plate_prio == 1 ? greatest : least));
-        }
-        plate_stream = ps;
-    }
     // Both canvases from one read of the frames where the geometry allows (pre.hip
     // letterbox_s2d_pair_kernel); the plate branch then forks after it.
     bool paired = false;

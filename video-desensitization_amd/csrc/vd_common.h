@@ -61,11 +61,10 @@ struct VdTune {
     int mosaic_map = 1;       // mosaic output pass: per-band vector maps (0: generic path)
     int mosaic_nt = 0;        //   non-temporal output stores (1), and source loads (3)
     int mosaic_cells = 32;    //   cell-table kernel: workgroups per frame
-    int mosaic_copy = 0;      //   copy-first output: one plain copy pass, the cell kernel writes the box pixels (measured slower)
     int mosaic_fused = 1;     //   one launch: the output pass computes its bands' cell colours itself (0: cell kernel + output pass)
     int block_fuse = 1;       // plan: fused layer1 bottlenecks (block.hip)
     int block32_xd = 2;       //   block32 stage-1 x loads in flight + 1 (register sets: 2, 3, 4)
-    int block32_dbg = 0;      //   timing-only: skip block32 stages (bits: 1 S1, 2 S2, 4 S3 math, 8 S3 stores, 16 S3 identity)
+    int block32_dbg = 0;      //   timing-only (vdt_set_debug, never vd_set_option): skip block32 stages (bits: 1 S1, 2 S2, 4 S3 math, 8 S3 stores, 16 S3 identity)
     int block32_pipe = 1;     //   block32 (CIN 256): producer / consumer wave groups on consecutive tiles (0: one group)
     int block_fuse32 = 1;     // plan, fp32 (fp16 pairs): fused layer1 bottlenecks (block32.hip)
     int chain = 2;            // plan: conv3 + next conv1 as one kernel (chain.hip; fp32: chain32.hip: 2 = layer2,
@@ -86,9 +85,6 @@ struct VdTune {
     int plate_s2d32 = 1;      // fp32 plan: the plate stem on the fp16 space-to-depth canvas (with plate_s2d)
     int face_groups = 2;      // face net as G frame groups on G streams (the tails of one group's launches
                               //   fill with the others'; bit-identical; 0 / 1: one launch over the batch)
-    int face_group_lag = 0;   //   group g starts after group g - 1's first N ops (0: together)
-    int plate_prio = 0;       // plate branch stream priority (0: default, 1: high, 2: low, 3: CU-masked to
-    int plate_cus = 64;       //   plate_cus CUs spread over the XCDs)
     int plate_stage = 3;      // plate branch starts after face stage N (0: with the stem; 1-4: after
                               //   layerN; 5: after the whole face net). After layer3 its HBM-bound
                               //   convs overlap the MFMA-bound late face layers: 30.8 -> 30.0 ms/step
@@ -120,7 +116,7 @@ struct VdTune {
     int x6_taps = 1;          // fp32 plan: narrow KxK YOLO layers (K <= 288) on the streaming TAPS form
     int x6_gemm1x1 = 1;       // fp16 pairs: GEMM 1x1 convs on the TR tiles (D^T accumulators, register epilogue;
                               //   2: also the streaming form's K <= 256 layers, 0: off)
-    int x6_dbg = 0;           // experiments (tools/x6bench): 1 = no epilogue (WRONG results), 2 = runtime vmcnt waits
+    int x6_dbg = 0;           // experiments (vdt_set_debug / tools/x6bench): 1 = no epilogue (WRONG results), 2 = runtime vmcnt waits
     int f32_split = 2;        // plan (fp32, at weight load): 2 = operands scaled by powers of two
                               //   and split into fp16 pairs, 3 products on the f16 matrix cores;
                               //   1 = exact 3-term bf16 split, 6 products (conv_x6.hip);

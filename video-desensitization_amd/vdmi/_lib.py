@@ -91,6 +91,7 @@ SIGNATURES = [
     ("vdt_plate_raw", _I, [_P, _P, _I, _I, _I, _SZ, _I, _P, ctypes.POINTER(_I)]),
     ("vdt_jpeg_coefficients", _I, [_P, _SZ, _P, _SZ, ctypes.POINTER(_I)]),
     ("vdt_jdec_stats", _I, [_P, ctypes.POINTER(_I)]),
+    ("vdt_set_debug", _I, [_P, ctypes.c_char_p, _I]),
     ("vd_record_extract_h265", _I, [ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(_I)]),
     ("vd_record_repack_h265", _I, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(_I)]),
 ]

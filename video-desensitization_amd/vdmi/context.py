@@ -140,6 +140,11 @@ class Context:
     def set_option(self, name, value):
         check(self._lib.vd_set_option(self._h, str(name).encode(), int(value)))
 
+    def set_debug(self, name, value):
+        """Timing-only experiment switches (vdt_set_debug: "x6_dbg", "block32_dbg"); the
+        results are WRONG while they are set. Never a production knob."""
+        check(self._lib.vdt_set_debug(self._h, str(name).encode(), int(value)))
+
     def set_stream(self, stream_ptr):
         check(self._lib.vd_set_stream(self._h, stream_ptr))
 

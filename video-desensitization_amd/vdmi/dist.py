@@ -173,6 +173,12 @@ class RecordSink:
         self.rec[:, 0] = -1
         if plates:
             self.rec[:, self.w] = -1
+        # the fill above runs on this thread's current stream; add() packs on the stream
+        # that produced the boxes, which must not overtake it (an event orders the two)
+        self._init_ev = None
+        if self.device.type == "cuda":
+            self._init_ev = torch.cuda.Event()
+            self._init_ev.record(torch.cuda.current_stream(self.device))
         self.lock = threading.Lock()
 
     def _stream_ctx(self, stream):
@@ -205,6 +211,8 @@ class RecordSink:
             return
         with self._stream_ctx(stream):
             dev = self.device
+            if self._init_ev is not None:
+                torch.cuda.current_stream(dev).wait_event(self._init_ev)
             t = lambda a, dt: (a if isinstance(a, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(a))
                                ).to(device=dev, dtype=dt, non_blocking=False)
             ids = self._index(frame_ids, torch.int32)
@@ -294,17 +302,37 @@ def process_frames(ctx, frames, out, batch, first_frame, sink, flags, faces, pla
     return n_all
 
 
-def run_on_devices(fn, shards):
+def _device_scope(dev):
+    """torch.cuda.device(dev) when a GPU is usable (so a tensor, stream or event a
+    shard's code creates without naming a device lands on ITS device, not on the
+    thread's default cuda:0), else nothing."""
+    import contextlib
+    if dev is None:
+        return contextlib.nullcontext()
+    try:
+        import torch
+        if torch.cuda.is_available():
+            return torch.cuda.device(int(dev))
+    except Exception:
+        pass
+    return contextlib.nullcontext()
+
+
+def run_on_devices(fn, shards, devices=None):
     """Run fn(i, shard) for every shard on its own thread (one per device: each
-    drives its own context, whose C calls release the GIL) and wait for all. Returns
-    the results in shard order; re-raises the first shard's exception (in shard
-    order) after every thread has finished."""
+    drives its own context, whose C calls release the GIL) and wait for all.
+    devices[i] (optional): the GPU of shard i; its thread runs fn inside
+    torch.cuda.device(devices[i]). Returns the results in shard order; re-raises the
+    first shard's exception (in shard order) after every thread has finished."""
     res = [None] * len(shards)
     err = [None] * len(shards)
+    if devices is not None and len(devices) != len(shards):
+        raise ValueError(f"run_on_devices: {len(devices)} devices for {len(shards)} shards")
 
     def work(i):
         try:
-            res[i] = fn(i, shards[i])
+            with _device_scope(devices[i] if devices is not None else None):
+                res[i] = fn(i, shards[i])
         except BaseException as e:           # noqa: B902 -- re-raised below
             err[i] = e
 

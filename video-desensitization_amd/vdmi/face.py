@@ -67,7 +67,8 @@ def split_run(ctxs, items, fn):
     if len(ctxs) == 1 or len(items) <= 1:
         return fn(ctxs[0], items)
     spans = [shard_range(len(items), len(ctxs), i) for i in range(len(ctxs))]
-    parts = run_on_devices(lambda i, sp: fn(ctxs[i], items[sp[0]:sp[1]]) if sp[1] > sp[0] else [], spans)
+    parts = run_on_devices(lambda i, sp: fn(ctxs[i], items[sp[0]:sp[1]]) if sp[1] > sp[0] else [], spans,
+                           devices=[c.device for c in ctxs])
     return [r for p in parts for r in p]
 
 

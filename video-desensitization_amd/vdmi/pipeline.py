@@ -443,17 +443,30 @@ class GpuJpegStages:
         self.ectx.close()
 
 
-def fused_context(face_detector, plate_detector, batch_size, device=None):
+_FUSED_LOCK = threading.Lock()
+
+
+def fused_context(face_detector, plate_detector, batch_size, device=None, slot=0):
     """One context on `device` (default: the face detector's first device) holding both
-    drop-ins' weights and the face detector's knobs (cached on the face detector, one
-    per device)."""
+    drop-ins' weights and the face detector's knobs, cached on the face detector per
+    (plate detector, batch size, device, slot). `slot` is the shard index in
+    shard="devices" mode: two shards never share a context (its stream and staging are
+    per call sequence), also when device ids repeat (device_ids=[0, 0])."""
     from .context import Context
     fd, pd = face_detector, plate_detector
     dev = fd.device_ids[0] if device is None else int(device)
-    key = (id(plate_detector), int(batch_size), dev)
-    cache = fd.__dict__.setdefault("_fused_ctx", {})
-    if key in cache:
-        return cache[key]
+    key = (id(plate_detector), int(batch_size), dev, int(slot))
+    with _FUSED_LOCK:
+        cache = fd.__dict__.setdefault("_fused_ctx", {})
+        if key in cache:
+            return cache[key]
+        ctx = _new_fused_context(fd, pd, batch_size, dev)
+        cache[key] = ctx
+        return ctx
+
+
+def _new_fused_context(fd, pd, batch_size, dev):
+    from .context import Context
     ctx = Context(device=dev, precision=fd.precision, max_batch=max(int(batch_size), 1),
                   input_shape=fd.input_shape[:2], confidence=fd.confidence, nms_iou=fd.nms_iou,
                   max_boxes=fd.max_boxes, plate_nc=pd.nc, plate_conf=pd.ctx.cfg.plate_conf,
@@ -461,7 +474,6 @@ def fused_context(face_detector, plate_detector, batch_size, device=None):
                   plate_imgsz=pd.ctx.cfg.plate_imgsz, options=getattr(fd, "options", None))
     ctx.load_weights(_lib.VD_NET_RETINAFACE, fd.state_dict)
     ctx.load_weights(_lib.VD_NET_YOLOV8N, pd.state_dict)
-    cache[key] = ctx
     return ctx
 
 
@@ -479,6 +491,10 @@ def _shard_mode(shard, face_detector, group, fused):
         return "none"
     _, world = world_info(group)
     if shard == "ranks":
+        from .dist import _group_on
+        if not _group_on():
+            raise ValueError("shard='ranks' needs an initialised torch.distributed process group "
+                             "(vdmi.dist.init_from_env under torchrun)")
         return "ranks"
     if shard == "devices":
         if not fused:
@@ -549,8 +565,8 @@ def batch_process_images(input_dir, output_dir, face_detector, plate_detector, b
 
         def one(i, span):
             b, e = span
-            return _local(image_paths[b:e], b, devs[i], want_rec, run)
-        outs = run_on_devices(one, spans)
+            return _local(image_paths[b:e], b, devs[i], want_rec, run, slot=i)
+        outs = run_on_devices(one, spans, devices=devs)
         res = tuple(sum(o[0][k] for o in outs) for k in range(3))
         rec = _concat_records([o[1] for o in outs]) if want_rec else None
     else:
@@ -572,9 +588,10 @@ def _concat_records(recs):
     return torch.cat([r.cpu() for r in recs if r is not None]) if any(r is not None for r in recs) else None
 
 
-def _local(paths, first, device, want_rec, run):
+def _local(paths, first, device, want_rec, run, slot=0):
     """One device over `paths` (global frame ids first, first + 1, ...): the fused /
-    GPU-codec / generic loop. Returns ((processed, faces, plates), records or None)."""
+    GPU-codec / generic loop; `slot`: the shard's own fused context (devices mode).
+    Returns ((processed, faces, plates), records or None)."""
     from .dist import RecordSink
     fd = run["face_detector"]
     io = ThreadPoolExecutor(max_workers=run["num_workers"])
@@ -590,10 +607,11 @@ def _local(paths, first, device, want_rec, run):
     try:
         if run["fused"] and run["codec"]:
             res = _gpu_codec_batches(batches, run["output_dir"], fd, run["plate_detector"], bs,
-                                     run["mosaic_plates"], io, run["logger"], run["jpeg_quality"], device, sink, ids)
+                                     run["mosaic_plates"], io, run["logger"], run["jpeg_quality"], device, sink, ids,
+                                     slot)
         elif run["fused"]:
             res = _fused_batches(batches, run["output_dir"], fd, run["plate_detector"], bs, run["loader"],
-                                 run["saver"], run["mosaic_plates"], io, run["logger"], device, sink, ids)
+                                 run["saver"], run["mosaic_plates"], io, run["logger"], device, sink, ids, slot)
         else:
             res = _threaded_batches(batches, run["output_dir"], fd, run["plate_detector"], run["loader"],
                                     run["saver"], run["mosaic_plates"], run["mosaic_level"], io, run["logger"],
@@ -657,7 +675,7 @@ def _save_all(futs, logger):
 
 
 def _fused_batches(batches, output_dir, face_detector, plate_detector, batch_size, loader, saver, mosaic_plates,
-                   io, logger, device=None, sink=None, ids=None):
+                   io, logger, device=None, sink=None, ids=None, slot=0):
     """The vdmi path, streaming: decode batch b+1 (threads) while batch b is on the
     GPU (FramePipeline: one vd_process per batch), collect batch b-1 and hand its
     frames to the encoder threads. Frames of another size get their own pipeline;
@@ -666,7 +684,7 @@ def _fused_batches(batches, output_dir, face_detector, plate_detector, batch_siz
     the compute stream (vdmi.dist.RecordSink; ids: path -> (row, frame id))."""
     totals = [0, 0, 0]
     save_futs = []
-    ctx = fused_context(face_detector, plate_detector, batch_size, device)
+    ctx = fused_context(face_detector, plate_detector, batch_size, device, slot)
     pipes = {}
     load = lambda files: list(io.map(loader, files))
 
@@ -740,7 +758,7 @@ def _write_bytes(data, path):
 
 
 def _gpu_codec_batches(batches, output_dir, face_detector, plate_detector, batch_size, mosaic_plates, io, logger,
-                       quality, device=None, sink=None, ids=None):
+                       quality, device=None, sink=None, ids=None, slot=0):
     """Frame I/O on the GPU (GpuJpegStages): file bytes (reader threads) ->
     vd_jpeg_decode into device frames -> one vd_process (faces | plates | mosaic) ->
     vd_jpeg_encode from device memory -> writer threads, the three stages of
@@ -748,7 +766,7 @@ def _gpu_codec_batches(batches, output_dir, face_detector, plate_detector, batch
     decoder does not take (progressive, other layout) is decoded by the host loader;
     a batch whose inference fails is dropped (combine_detect.py:226-228); a read
     failure aborts the call after the batches before it are written (:209-211)."""
-    ctx = fused_context(face_detector, plate_detector, batch_size, device)
+    ctx = fused_context(face_detector, plate_detector, batch_size, device, slot)
     flags = _lib.VD_PROC_FACES | _lib.VD_PROC_MOSAIC | _lib.VD_PROC_PLATES
     if mosaic_plates:
         flags |= _lib.VD_PROC_MOSAIC_PLATES
