@@ -179,16 +179,24 @@ def cpu_baseline(frames, sd, seconds, plates=True, batch=8):
     m = build_oracle_model(sd)
     ym = build_oracle_yolo(weights.yolov8n_state_dict(0)) if plates else None
     pri = anchors.get_anchors((640, 640))
+    _oracle_pass(frames[:batch], m, ym, pri, batch, 0.0)          # untimed: oneDNN primitive set-up
+    _oracle_pass(frames[:1], m, ym, pri, 1, 0.0)
     done, dt, ref = _oracle_pass(frames, m, ym, pri, batch, seconds)
-    d1, t1, _ = _oracle_pass(frames[:8], m, ym, pri, 1, max(2.0, seconds / 4))
+    d1, t1, _ = _oracle_pass(frames, m, ym, pri, 1, max(3.0, seconds / 3))
     what = (f"torch-CPU fp32 RetinaFace-R50 + numpy decode/NMS/mosaic"
             f"{' + YOLOv8n plate forward/NMS' if plates else ''}")
-    rec = {"value": done / dt, "unit": "frames/s", "cores": cores, "kind": "port", "cpu_model": cpu_model(),
-           "batch": batch,
-           "sample": f"{done} x {frames.shape[2]}x{frames.shape[1]} synthetic frames through the oracle ({what}; "
-                     f"{batch} frames per forward, as the reference batches, combine_detect.py:204,216), {dt:.1f} s",
-           "per_frame": {"value": d1 / t1, "frames": d1, "seconds": round(t1, 2),
-                         "sample": "the same frames one at a time"}}
+    rb, r1 = done / dt, d1 / t1
+    # the baseline is the FASTER of the two forms (on 16 host cores one frame at a time
+    # can beat 8-frame batches: the batch's activations leave the caches)
+    best_b = rb >= r1
+    form = (f"{batch} frames per forward (the reference batches its forwards, combine_detect.py:204,216)"
+            if best_b else f"one frame per forward (faster here than {batch}-frame batches)")
+    rec = {"value": max(rb, r1), "unit": "frames/s", "cores": cores, "kind": "port", "cpu_model": cpu_model(),
+           "batch": batch if best_b else 1,
+           "sample": f"{done if best_b else d1} x {frames.shape[2]}x{frames.shape[1]} synthetic frames through the "
+                     f"oracle ({what}), {form}, {(dt if best_b else t1):.1f} s; the faster of the two forms",
+           "batched": {"value": rb, "batch": batch, "frames": done, "seconds": round(dt, 2)},
+           "per_frame": {"value": r1, "batch": 1, "frames": d1, "seconds": round(t1, 2)}}
     return rec, ref
 
 
