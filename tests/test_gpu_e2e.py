@@ -521,6 +521,28 @@ def test_heads_fp32_halo_tr_bit_identical(gpu):
             np.testing.assert_array_equal(a, b)
 
 
+def test_heads_fp32_pipelined_b_reads_bit_identical(gpu):
+    """fp32 plan, round 6: the halo and wide GEMM tiles read the B fragments of column
+    block j + 1 before block j's MFMAs (options x6_halo_pf / x6_gemm_pf, default 1) and
+    issue the DMA two K steps ahead between MFMA groups (x6_halo_dma: 0 after the
+    barrier, 1 after the MFMAs, 2 between groups, default). Schedule only: the same
+    products in the same order, heads bit-identical to the round-5 schedule."""
+    import vdmi
+    fr = _frames(2, 1080, 1920, seed=43)
+    heads = {}
+    for key, opts in (("r5", {"x6_halo_pf": 0, "x6_gemm_pf": 0, "x6_halo_dma": 0}), ("pf", {}),
+                      ("d1", {"x6_halo_dma": 1})):
+        ctx = vdmi.Context(precision="fp32", max_batch=2, options=opts)
+        try:
+            ctx.load_weights(0, face_weights("default"))
+            heads[key] = ctx.forward_heads(fr)
+        finally:
+            ctx.close()
+    for k in ("pf", "d1"):
+        for a, b in zip(heads[k], heads["r5"]):
+            np.testing.assert_array_equal(a, b)
+
+
 def test_heads_fp32_halo_conv(gpu):
     """fp32 plan: the 3x3 stride-1 convs with W <= 126 (layer2-4 conv2, FPN merges, SSH
     conv5X5_1 + conv3X3 at levels 0-2) run on conv_x6_halo_kernel (input split once per

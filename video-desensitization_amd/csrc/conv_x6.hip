@@ -458,7 +458,7 @@ __device__ __forceinline__ int x6_tr_row(int row) {
     return (row & ~31) + 8 * (i >> 2) + 4 * j + (i & 3);
 }
 
-template <int BM, int BN, int NT, int NST, int TERMS, int MF, int NA, bool TR = false>
+template <int BM, int BN, int NT, int NST, int TERMS, int MF, int NA, bool TR = false, bool PF = false>
 // NA: A register sets (K tiles of A loads in flight: NA - 1 besides the one being split)
 // 8 waves: two workgroups' worth of waves per SIMD pair (256 VGPRs each); 4 waves (one
 // per SIMD, 128 x 128 wave tiles): the whole 512-register file per wave, the
@@ -651,6 +651,36 @@ __global__ __launch_bounds__(NT, NT == 256 && BM == 256 ? 1 : 2) void conv_x6_ke
                         if (split_next && sk == q * 2 / AIT && j == (q * 2 % AIT) * TN / AIT) store_item(st_next, rn, q);
                 }
             }
+        } else if constexpr (TN > TM && PF) {
+            // PF (option x6_gemm_pf): B fragments of column block j + 1 read before the MFMAs
+            // of block j (two buffers), pinned by scheduling groups (as the halo tiles)
+            u32x4 af[TM][3], bq[2][3];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int p = 0; p < S::TA; ++p)
+                    af[i][p] = *(const u32x4*)(A + p * PL_A + swz(wm * S::WTM + i * 16 + (lane & 15), ch));
+#pragma unroll
+            for (int p = 0; p < S::TB; ++p) bq[0][p] = *(const u32x4*)(Bs + p * PL_B + swz(wn * S::WTN + (lane & 15), ch));
+            __builtin_amdgcn_sched_group_barrier(0x0100, TM * S::TA + S::TB, 0);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                if (j + 1 < TN) {
+#pragma unroll
+                    for (int p = 0; p < S::TB; ++p)
+                        bq[(j + 1) & 1][p] = *(const u32x4*)(Bs + p * PL_B + swz(wn * S::WTN + (j + 1) * 16 + (lane & 15), ch));
+                    __builtin_amdgcn_sched_group_barrier(0x0100, S::TB, 0);
+                }
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    if constexpr (TR) acc[i][j] = mfma_pair_tr(af[i], bq[j & 1], acc[i][j]);
+                    else acc[i][j] = mfma_terms<TERMS>(af[i], bq[j & 1], acc[i][j]);
+                }
+                __builtin_amdgcn_sched_group_barrier(0x0008, (TERMS == 3 ? 6 : TERMS == 2 ? 3 : 2) * TM, 0);
+#pragma unroll
+                for (int q = 0; q < AIT; ++q)
+                    if (split_next && j == q * TN / AIT) store_item(st_next, rn, q);
+            }
         } else if constexpr (TN > TM) {   // wide wave tile: all A fragments resident, B fragments streamed
             u32x4 af[TM][3];
 #pragma unroll
@@ -827,7 +857,7 @@ __host__ __device__ constexpr int s2_tap(int j) {   // step j of a chunk -> weig
 }
 __host__ __device__ constexpr bool s2_last(int j) { return j == 3 || j == 5 || j == 7 || j == 8; }   // a phase ends
 
-template <int BN, int NSB, bool TR = false, bool S2 = false>
+template <int BN, int NSB, bool TR = false, bool S2 = false, bool PF = false>
 __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(ConvArgs a) {
     using S = X6Shape<256, BN, 512, 2, 2>;
     constexpr int BM = 256, NT = 512, TM = S::TM, TN = S::TN, WAVES = S::WAVES, PL_B = S::PL_B;
@@ -907,23 +937,29 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
     constexpr int RB = BN / 16, NDMA = S::NDMA;
     const int my_dma = NDMA / WAVES + (wid < NDMA % WAVES ? 1 : 0);
     const __amdgpu_buffer_rsrc_t rsrc_w = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7fffffff, 0x00020000);
-    auto dma_b = [&](int s, int st) {
+    // piece q of this wave's DMA share of step s's K tile into stage st
+    auto dma_piece = [&](int s, int st, int q) {
         const int c = s / 9, j = s - 9 * c, kt = (S2 ? s2_tap(j) : j) * CH + c;
         char* Bs = smem + st * 2 * PL_B;
-#pragma unroll
-        for (int q = 0; q < (NDMA + WAVES - 1) / WAVES; ++q) {
-            const int j = wid + WAVES * q;
-            if (j < NDMA) {
-                const int p = j / RB, r0 = (j % RB) * 16;
-                const int row = r0 + (lane >> 2), slot = lane & 3;
-                const int chunk = slot ^ (((row >> 3) & 1) * 3);
-                const int wrow = TR ? x6_tr_row(row) : row;
-                const unsigned off = (unsigned)((((long)(n0 + wrow) * nk + kt) * 2 + p) * 64 + chunk * 16);
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_w, (lds_void_t*)(Bs + p * PL_B + r0 * 64), 16, off, 0,
-                                                         0, 0);
-            }
+        const int jd = wid + WAVES * q;
+        if (jd < NDMA) {
+            const int p = jd / RB, r0 = (jd % RB) * 16;
+            const int row = r0 + (lane >> 2), slot = lane & 3;
+            const int chunk = slot ^ (((row >> 3) & 1) * 3);
+            const int wrow = TR ? x6_tr_row(row) : row;
+            const unsigned off = (unsigned)((((long)(n0 + wrow) * nk + kt) * 2 + p) * 64 + chunk * 16);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_w, (lds_void_t*)(Bs + p * PL_B + r0 * 64), 16, off, 0,
+                                                     0, 0);
         }
     };
+    auto dma_b = [&](int s, int st) {
+#pragma unroll
+        for (int q = 0; q < (NDMA + WAVES - 1) / WAVES; ++q) dma_piece(s, st, q);
+    };
+    // where a step issues the DMA of step s + 2 (option x6_halo_dma, whole DMA rounds only):
+    // 0 right after the step's barrier, 1 after its MFMAs, 2 one piece between MFMA groups
+    constexpr int MYD = S::NDMA % WAVES == 0 ? S::NDMA / WAVES : 0;
+    const int hdma = MYD ? (a.dbg >> 3) & 3 : 0;
 
     // ---- per-lane A rows: this lane's output row of each fragment i, its halo row for
     // tap (0, 0) and which neighbours exist (bit 0 y-1, 1 y+1, 2 x-1, 3 x+1, 4 row < M)
@@ -946,7 +982,7 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
     if (a.ymax)
         for (int f = tid; f < a.B; f += NT) ((unsigned*)(smem + amax_off))[f] = 0u;
 
-    auto compute = [&](int st, int dy, int dx) {
+    auto compute = [&](int st, int dy, int dx, int dstep) {
         const char* Bs = smem + st * 2 * PL_B;
         const int ch = lane >> 4;
         // S2: taps with d = +1 read the phase pixel itself (its own frame; odd rows / columns
@@ -974,6 +1010,38 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
                     else acc[i][j] = mfma_terms<2>(af, bf[j], acc[i][j]);
                 }
             }
+        } else if constexpr (PF) {
+            // PF (option x6_halo_pf): the B fragments of column block j + 1 are read before
+            // the MFMAs of block j (two buffers: the registers of the compiler's paired reads),
+            // pinned by scheduling groups, so an LDS read's latency hides behind 3 TM MFMAs
+            u32x4 af[TM][3], bq[2][3];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int hr = (aflg[i] & need) == need ? arow[i] + shift : HR;
+                const int o = swzh(hr, ch);
+                af[i][0] = *(const u32x4*)(Ah + o);
+                af[i][1] = *(const u32x4*)(Ah + PL_H + o);
+            }
+            bq[0][0] = *(const u32x4*)(Bs + swz(wn * S::WTN + (lane & 15), ch));
+            bq[0][1] = *(const u32x4*)(Bs + PL_B + swz(wn * S::WTN + (lane & 15), ch));
+            __builtin_amdgcn_sched_group_barrier(0x0100, 2 * TM + 2, 0);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                if (j + 1 < TN) {
+                    bq[(j + 1) & 1][0] = *(const u32x4*)(Bs + swz(wn * S::WTN + (j + 1) * 16 + (lane & 15), ch));
+                    bq[(j + 1) & 1][1] = *(const u32x4*)(Bs + PL_B + swz(wn * S::WTN + (j + 1) * 16 + (lane & 15), ch));
+                    __builtin_amdgcn_sched_group_barrier(0x0100, 2, 0);
+                }
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    if constexpr (TR) acc[i][j] = mfma_pair_tr(af[i], bq[j & 1], acc[i][j]);
+                    else acc[i][j] = mfma_terms<2>(af[i], bq[j & 1], acc[i][j]);
+                }
+                __builtin_amdgcn_sched_group_barrier(0x0008, 3 * TM, 0);
+                if constexpr (MYD > 0 && TN % MYD == 0) {   // x6_halo_dma = 2: a DMA piece per group
+                    if (dstep >= 0 && j % (TN / MYD) == 0) dma_piece(dstep, dstep % 3, j / (TN / MYD));
+                }
+            }
         } else {
             u32x4 af[TM][3];
 #pragma unroll
@@ -992,6 +1060,9 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
                 for (int i = 0; i < TM; ++i) {
                     if constexpr (TR) acc[i][j] = mfma_pair_tr(af[i], bf, acc[i][j]);
                     else acc[i][j] = mfma_terms<2>(af[i], bf, acc[i][j]);
+                }
+                if constexpr (MYD > 0 && TN % MYD == 0) {   // x6_halo_dma = 2: a DMA piece per group
+                    if (dstep >= 0 && j % (TN / MYD) == 0) dma_piece(dstep, dstep % 3, j / (TN / MYD));
                 }
             }
         }
@@ -1014,7 +1085,6 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
         // is one of four immediates chosen by two uniform branches (the runtime wait_vm
         // switch costs a tree of scalar branches per step). (Unrolling the nine taps of a
         // chunk as well measured no better and spills on the 192 / 256-wide tiles.)
-        constexpr int MYD = S::NDMA % WAVES == 0 ? S::NDMA / WAVES : 0;
         int hcur = 0;                                    // the halo in LDS
         for (int s = 0; s < nsteps; ++s) {
             const int tap = s % 9;
@@ -1033,10 +1103,13 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
             __builtin_amdgcn_s_barrier();                // B(s) visible; stage (s + 2) % 3 free
             asm volatile("" ::: "memory");
             const bool rehalo = (S2 ? s2_last(tap) : tap == 8) && hcur + 1 < nhalo;
-            if (!rehalo && s + 2 < nsteps) dma_b(s + 2, (s + 2) % 3);
+            const bool dnext = !rehalo && s + 2 < nsteps;
+            const int hd = (TN % (MYD ? MYD : 1) == 0 && TN >= TM) ? hdma : (hdma ? 1 : 0);
+            if (dnext && hd == 0) dma_b(s + 2, (s + 2) % 3);
             const int wt = S2 ? s2_tap(tap) : tap;
             const int dy = wt / 3 - 1, dx = wt - (wt / 3) * 3 - 1;
-            compute(s % 3, dy, dx);
+            compute(s % 3, dy, dx, dnext && hd == 2 ? s + 2 : -1);
+            if (dnext && hd == 1) dma_b(s + 2, (s + 2) % 3);
             if (rehalo) {
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 __builtin_amdgcn_s_barrier();            // every wave is done with halo hcur
@@ -1064,7 +1137,7 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
             const bool rehalo = tap == 8 && c + 1 < CH;
             if (!rehalo && s + 2 < nsteps) dma_b(s + 2, (s + 2) % 3);
             const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
-            compute(s % 3, dy, dx);
+            compute(s % 3, dy, dx, -1);
             if (rehalo) {
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 __builtin_amdgcn_s_barrier();            // every wave is done with chunk c's halo
@@ -1086,7 +1159,7 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
-        compute(s & 1, dy, dx);
+        compute(s & 1, dy, dx, -1);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();                    // stage s & 1 (and, at tap 8, the halo) are free
         asm volatile("" ::: "memory");
@@ -1572,16 +1645,20 @@ bool vd_conv_x6_ok(const ConvArgs& a) {
 }
 
 // rows [mbase, M) of the conv (mbase a multiple of the caller's tile rows)
-template <int BM, int BN, int NT, int NST, int TERMS, int MF = 16, int NA = 2, bool TR = false>
+template <int BM, int BN, int NT, int NST, int TERMS, int MF = 16, int NA = 2, bool TR = false, bool PF = false>
 static hipError_t launch_x6(const ConvArgs& a0, hipStream_t s, int mbase = 0, int mtiles = -1) {
-    if constexpr (NA == 2 && BM == 256 && BN <= 128 && NST == 2 && TERMS == 2 && MF == 16 && !TR) {
+    if constexpr (NA == 2 && BM == 256 && BN <= 128 && NST == 2 && TERMS == 2 && MF == 16 && !TR && !PF) {
         // option x6_adepth: four A register sets (three K tiles of A loads in flight) on
         // the 256 x {128, 64, 32} tiles, whose accumulators leave the registers for them
         if (a0.tune && a0.tune->x6_adepth >= 4) return launch_x6<BM, BN, NT, NST, TERMS, MF, 4>(a0, s, mbase, mtiles);
     }
+    if constexpr (!PF && MF == 16 && NST == 2 && X6Shape<BM, BN, NT, NST, TERMS, MF>::TN > X6Shape<BM, BN, NT, NST, TERMS, MF>::TM) {
+        // option x6_gemm_pf: the wide-wave tiles with pipelined B-fragment reads
+        if (a0.tune && a0.tune->x6_gemm_pf) return launch_x6<BM, BN, NT, NST, TERMS, MF, NA, TR, true>(a0, s, mbase, mtiles);
+    }
     using S = X6Shape<BM, BN, NT, NST, TERMS, MF>;
     static const bool attr = [] {
-        (void)hipFuncSetAttribute((const void*)conv_x6_kernel<BM, BN, NT, NST, TERMS, MF, NA, TR>,
+        (void)hipFuncSetAttribute((const void*)conv_x6_kernel<BM, BN, NT, NST, TERMS, MF, NA, TR, PF>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS + 4 * kAmaxFrames);
         return true;
     }();
@@ -1592,7 +1669,7 @@ static hipError_t launch_x6(const ConvArgs& a0, hipStream_t s, int mbase = 0, in
     a.mbase = mbase;
     const int mt = mtiles >= 0 ? mtiles : (a.M - mbase + BM - 1) / BM;
     const int lds = S::LDS + (a.ymax ? 4 * a.B : 0);
-    hipLaunchKernelGGL((conv_x6_kernel<BM, BN, NT, NST, TERMS, MF, NA, TR>), dim3(mt * a.ntiles_n), dim3(NT), lds, s, a);
+    hipLaunchKernelGGL((conv_x6_kernel<BM, BN, NT, NST, TERMS, MF, NA, TR, PF>), dim3(mt * a.ntiles_n), dim3(NT), lds, s, a);
     return hipGetLastError();
 }
 
@@ -1639,14 +1716,14 @@ static int x6_halo_lds(const ConvArgs& a) {
     return std::max(NSB * 2 * S::PL_B + 2 * HP * 64, S::EPR * S::EPLD * 4) + (a.ymax ? 4 * a.B : 0);
 }
 
-template <int BN, int NSB, bool TR = false, bool S2 = false>
-static hipError_t launch_x6_halo_t(const ConvArgs& a0, hipStream_t s) {
+template <int BN, int NSB, bool TR, bool S2, bool PF>
+static hipError_t launch_x6_halo_pf(const ConvArgs& a0, hipStream_t s) {
     ConvArgs a = a0;
     a.w = a.wx3;
     a.ntiles_n = (a.cout + BN - 1) / BN;
     a.mbase = 0;
     static const bool attr = [] {
-        (void)hipFuncSetAttribute((const void*)conv_x6_halo_kernel<BN, NSB, TR, S2>,
+        (void)hipFuncSetAttribute((const void*)conv_x6_halo_kernel<BN, NSB, TR, S2, PF>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         return true;
     }();
@@ -1654,8 +1731,17 @@ static hipError_t launch_x6_halo_t(const ConvArgs& a0, hipStream_t s) {
     const int lds = x6_halo_lds<BN, NSB>(a);
     if (lds > 160 * 1024) return hipErrorInvalidValue;
     const int mt = (a.M + 255) / 256;
-    hipLaunchKernelGGL((conv_x6_halo_kernel<BN, NSB, TR, S2>), dim3(mt * a.ntiles_n), dim3(512), lds, s, a);
+    hipLaunchKernelGGL((conv_x6_halo_kernel<BN, NSB, TR, S2, PF>), dim3(mt * a.ntiles_n), dim3(512), lds, s, a);
     return hipGetLastError();
+}
+
+// option x6_halo_pf: the pipelined B-fragment reads on the 128-256-wide tiles
+template <int BN, int NSB, bool TR = false, bool S2 = false>
+static hipError_t launch_x6_halo_t(const ConvArgs& a, hipStream_t s) {
+    if constexpr (BN >= 128) {
+        if (a.tune && a.tune->x6_halo_pf) return launch_x6_halo_pf<BN, NSB, TR, S2, true>(a, s);
+    }
+    return launch_x6_halo_pf<BN, NSB, TR, S2, false>(a, s);
 }
 
 // TR form where the output (and residual) rows take 8-channel 16-B vectors (option
@@ -1860,7 +1946,7 @@ bool vd_conv1x1_x6_dual_ok(const ConvArgs& a) {
 
 hipError_t vd_launch_conv_x6(const ConvArgs& a0, hipStream_t s) {
     ConvArgs a = a0;
-    a.dbg = a.tune ? (a.tune->x6_dbg & 3) | (a.tune->x6_one ? 4 : 0) : 0;
+    a.dbg = a.tune ? (a.tune->x6_dbg & 3) | (a.tune->x6_one ? 4 : 0) | ((a.tune->x6_halo_dma & 3) << 3) : 0;
     if (a.grp_co) {   // grouped: the halo form only, one 64-wide N tile per group
         if (a.grp_co != 64 || a.f32_split != 2 || !a.wx3 || !a.tune || !x6_halo_ok(a) || (a.ymax && a.B > kAmaxFrames))
             return hipErrorInvalidValue;

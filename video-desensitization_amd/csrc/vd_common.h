@@ -110,6 +110,10 @@ struct VdTune {
     int x6_halo_s2 = 1;       // ... also 3x3 stride-2 convs (phase halos; Cout > 32)
     int x6_adepth = 2;        // A register sets of the 256 x {128, 64, 32} fp16-pair tiles (2 or 4; 4 measured level)
     int x6_slots = 0;         //   workgroup slots of one round (0: the CU count; tests force small values)
+    int x6_gemm_pf = 1;       // GEMM tiles with wide wave tiles (TN > TM): the same pipelined B-fragment reads
+    int x6_halo_pf = 1;       //   halo tiles (128-256 wide): B fragments of block j + 1 read before block j's MFMAs
+    int x6_halo_dma = 2;      //   halo tiles: where a K step issues the B DMA two steps ahead (0 after the
+                              //   barrier, 1 after the step's MFMAs, 2 one piece between MFMA groups)
     int x6_halo_tr = 2;       // fp32 plan: halo 3x3 tiles with D^T accumulators and the register epilogue
                               //   (1: the 128-256-wide tiles, 2: all; bit-identical)
     int x6_one = 1;           // fp16 pairs, GEMM tiles: 1x1 convs load A at row offset + scalar K offset (no tap stepping)
@@ -159,7 +163,7 @@ struct ConvArgs {
     int x_exact;                                 // fp16 pairs: input values exact in fp16 (integer canvas)
     int mbase;                                   // conv_x6 tiles: first output row of the launch (tail split)
     int dbg;                                     // VdTune::x6_dbg (bits 0-1, timing experiments; 0 in production),
-                                                 // bit 2: VdTune::x6_one
+                                                 // bit 2: VdTune::x6_one, bits 3-4: VdTune::x6_halo_dma
     int grp_co, grp_ci;                          // grouped conv (fp32 halo tiles): output channels n read input
                                                  //   channels (n / grp_co) * grp_ci + [0, cin); 0: dense
 };
