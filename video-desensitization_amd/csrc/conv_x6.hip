@@ -960,6 +960,9 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
     // 0 right after the step's barrier, 1 after its MFMAs, 2 one piece between MFMA groups
     constexpr int MYD = S::NDMA % WAVES == 0 ? S::NDMA / WAVES : 0;
     const int hdma = MYD ? (a.dbg >> 3) & 3 : 0;
+    // timing-only skips (x6_dbg bits 2-5 via vdt_set_debug / x6bench; WRONG results): 1 no B DMA
+    // past the prologue, 2 no halo reload, 8 no main-loop barriers
+    const int hdbg = (a.dbg >> 5) & 15;
 
     // ---- per-lane A rows: this lane's output row of each fragment i, its halo row for
     // tap (0, 0) and which neighbours exist (bit 0 y-1, 1 y+1, 2 x-1, 3 x+1, 4 row < M)
@@ -1100,10 +1103,10 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
                 else wait_vm_k<0>();
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();                // B(s) visible; stage (s + 2) % 3 free
+            if (!(hdbg & 8)) __builtin_amdgcn_s_barrier();   // B(s) visible; stage (s + 2) % 3 free
             asm volatile("" ::: "memory");
             const bool rehalo = (S2 ? s2_last(tap) : tap == 8) && hcur + 1 < nhalo;
-            const bool dnext = !rehalo && s + 2 < nsteps;
+            const bool dnext = !rehalo && s + 2 < nsteps && !(hdbg & 1);
             const int hd = (TN % (MYD ? MYD : 1) == 0 && TN >= TM) ? hdma : (hdma ? 1 : 0);
             if (dnext && hd == 0) dma_b(s + 2, (s + 2) % 3);
             const int wt = S2 ? s2_tap(tap) : tap;
@@ -1112,12 +1115,12 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
             if (dnext && hd == 1) dma_b(s + 2, (s + 2) % 3);
             if (rehalo) {
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                __builtin_amdgcn_s_barrier();            // every wave is done with halo hcur
+                if (!(hdbg & 8)) __builtin_amdgcn_s_barrier();   // every wave is done with halo hcur
                 asm volatile("" ::: "memory");
-                store_halo();
+                if (!(hdbg & 2)) store_halo();
                 ++hcur;
-                if (hcur + 1 < nhalo) load_halo(hcur + 1);
-                if (s + 2 < nsteps) dma_b(s + 2, (s + 2) % 3);
+                if (hcur + 1 < nhalo && !(hdbg & 2)) load_halo(hcur + 1);
+                if (s + 2 < nsteps && !(hdbg & 1)) dma_b(s + 2, (s + 2) % 3);
             }
         }
     } else if constexpr (NSB == 3) {
@@ -1946,7 +1949,8 @@ bool vd_conv1x1_x6_dual_ok(const ConvArgs& a) {
 
 hipError_t vd_launch_conv_x6(const ConvArgs& a0, hipStream_t s) {
     ConvArgs a = a0;
-    a.dbg = a.tune ? (a.tune->x6_dbg & 3) | (a.tune->x6_one ? 4 : 0) | ((a.tune->x6_halo_dma & 3) << 3) : 0;
+    a.dbg = a.tune ? (a.tune->x6_dbg & 3) | (a.tune->x6_one ? 4 : 0) | ((a.tune->x6_halo_dma & 3) << 3) |
+                     (((a.tune->x6_dbg >> 2) & 15) << 5) : 0;
     if (a.grp_co) {   // grouped: the halo form only, one 64-wide N tile per group
         if (a.grp_co != 64 || a.f32_split != 2 || !a.wx3 || !a.tune || !x6_halo_ok(a) || (a.ymax && a.B > kAmaxFrames))
             return hipErrorInvalidValue;

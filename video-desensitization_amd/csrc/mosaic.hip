@@ -317,8 +317,12 @@ __device__ __forceinline__ unsigned byte_mask32(unsigned m4) {
 // walk of mosaic_cell_kernel), and the 3-byte gather. Bands the fast path does not
 // take (more than MAPBOX boxes, cells past the LDS slice, unaligned rows) and frames
 // of more than BOX_FAST boxes walk per pixel (the whole box list, from the last box).
-template <bool FUSED>
+// R: rows per band (ROWS, or 24 / 32 with the fused pass: fewer, longer bands for
+// batches whose 16-row bands overfill one round of workgroup slots by a little, e.g.
+// 32 frames of 720p = 1440 bands on 1280 slots); the LDS cell slice scales with R
+template <bool FUSED, int R = ROWS>
 __global__ __launch_bounds__(256) void mosaic_out_kernel(MosaicArgs a) {
+    constexpr int ROWS = R, LCELL = R < 16 ? 2048 : 128 * R;
     __shared__ int4 s_box[FUSED ? BOX_FAST : 1];       // FUSED: the frame's clipped boxes
     __shared__ uint32_t s_bsz[FUSED ? BOX_FAST : 1];   //        sw | sh << 16
     __shared__ double s_fdx[FUSED ? MAPBOX : 1];       //        down factors of the band boxes
@@ -558,7 +562,40 @@ __global__ __launch_bounds__(256) void mosaic_out_kernel(MosaicArgs a) {
     }
     // the band's cell rows of every box: contiguous in the global cell table, or
     // (FUSED) walked and gathered here, one thread per cell
-    if (lcell_ok)
+    if (FUSED && lcell_ok && (a.map_on & 16)) {
+        // option mosaic_gather: a thread's cells walked first (LDS only), then all their
+        // source-pixel loads issued together -- one global latency per pass, not one per cell
+        constexpr int G = 8;
+        for (int i0 = tid; i0 < s_ltot; i0 += 256 * G) {
+            const uint8_t* sp[G];
+#pragma unroll
+            for (int u = 0; u < G; ++u) {
+                const int i = i0 + 256 * u;
+                sp[u] = nullptr;
+                if (i < s_ltot) {
+                    int t = 0;
+                    while (t + 1 < nt && s_lb[t + 1] <= i) ++t;
+                    const int c = i - s_lb[t], sw = s_sw[t];
+                    const int cr = c / sw, ux = c - cr * sw, uy = s_uylo[t] + cr;
+                    const int4 q = s_rect[t];
+                    int x = q.x + min((int)floor(VD_DMUL((double)ux, s_fdx[t])), q.z - q.x - 1);
+                    int y = q.y + min((int)floor(VD_DMUL((double)uy, s_fdy[t])), q.w - q.y - 1);
+                    for (int j = s_idx[t] - 1; j >= 0; --j) {
+                        const int4 r = s_box[j];
+                        if (in_rect(r, y, x)) apply_rect(r, s_bsz[j], y, x);
+                    }
+                    sp[u] = src + (size_t)y * a.pitch + x * 3;
+                }
+            }
+            uint32_t cv[G];
+#pragma unroll
+            for (int u = 0; u < G; ++u)
+                cv[u] = sp[u] ? (uint32_t)sp[u][0] | ((uint32_t)sp[u][1] << 8) | ((uint32_t)sp[u][2] << 16) : 0u;
+#pragma unroll
+            for (int u = 0; u < G; ++u)
+                if (sp[u]) s_lcell[i0 + 256 * u] = cv[u];
+        }
+    } else if (lcell_ok)
         for (int i = tid; i < s_ltot; i += 256) {
             int t = 0;
             while (t + 1 < nt && s_lb[t + 1] <= i) ++t;
@@ -810,6 +847,15 @@ __global__ __launch_bounds__(256) void mosaic_out_kernel(MosaicArgs a) {
 
 }  // namespace
 
+// Band height of the fused output pass (option mosaic_rows: 8 / 16 / 24 / 32; 0 = 16).
+// Measured (profiles/r06_mosaic_rows.txt): 24- and 32-row bands are slower at every
+// config (more row classes than the vector maps hold take the per-pixel scan, and the
+// prelude grows), so 16 stays the default.
+static int mosaic_rows_for(int n, int h, int opt) {
+    (void)n; (void)h;
+    return (opt == 8 || opt == 24 || opt == 32) ? opt : ROWS;
+}
+
 size_t vd_mosaic_table_bytes(int n, int tcap) {
     return (size_t)n * tcap * sizeof(MBox) + (size_t)n * (BOX_FAST + 1) * 4 + 16 +
            (size_t)n * CELL_CAP * 4;
@@ -831,6 +877,12 @@ hipError_t vd_launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w
     a.map_on = map_on;
     if (stages & 1) hipLaunchKernelGGL(mosaic_cell_kernel, dim3(cell_blocks, n), dim3(256), 0, s, a);
     if (stages & 2) hipLaunchKernelGGL(mosaic_out_kernel<false>, dim3((h + ROWS - 1) / ROWS, n), dim3(256), 0, s, a);
-    if (stages & 8) hipLaunchKernelGGL(mosaic_out_kernel<true>, dim3((h + ROWS - 1) / ROWS, n), dim3(256), 0, s, a);
+    if (stages & 8) {
+        const int r = mosaic_rows_for(n, h, map_on >> 8);
+        if (r == 8) hipLaunchKernelGGL((mosaic_out_kernel<true, 8>), dim3((h + 7) / 8, n), dim3(256), 0, s, a);
+        else if (r == 32) hipLaunchKernelGGL((mosaic_out_kernel<true, 32>), dim3((h + 31) / 32, n), dim3(256), 0, s, a);
+        else if (r == 24) hipLaunchKernelGGL((mosaic_out_kernel<true, 24>), dim3((h + 23) / 24, n), dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((mosaic_out_kernel<true, ROWS>), dim3((h + ROWS - 1) / ROWS, n), dim3(256), 0, s, a);
+    }
     return hipGetLastError();
 }

@@ -952,7 +952,7 @@ int Ctx::launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w, siz
     const int tcap = (cnt0 ? cap0 : 0) + (cnt1 ? cap1 : 0);
     int rc = ensure_staging(&mosaic_table, &mosaic_table_bytes, vd_mosaic_table_bytes(n, tcap) + 64);
     if (rc) return rc;
-    const int map_on = tune.mosaic_map | (tune.mosaic_nt << 1);
+    const int map_on = tune.mosaic_map | (tune.mosaic_nt << 1) | (tune.mosaic_gather ? 16 : 0) | ((tune.mosaic_rows & 63) << 8);
     auto launch = [&](int stages) {
         return vd_launch_mosaic(in, out, n, h, w, pitch, cnt0, xy0, cap0, cnt1, xy1, cap1, level, mosaic_table, stages,
                                 map_on, tune.mosaic_cells, stream);
@@ -1124,7 +1124,7 @@ int vd_set_option(vd_ctx* h, const char* name, int value) {
         {"conv_dual", &VdTune::conv_dual}, {"conv_taps", &VdTune::conv_taps}, {"conv_n192", &VdTune::conv_n192},
         {"conv_small", &VdTune::conv_small}, {"conv_big", &VdTune::conv_big},
         {"conv_big_kmin", &VdTune::conv_big_kmin}, {"stream_ntt", &VdTune::stream_ntt},
-        {"lb_pair", &VdTune::lb_pair}, {"mosaic_map", &VdTune::mosaic_map}, {"mosaic_nt", &VdTune::mosaic_nt}, {"mosaic_cells", &VdTune::mosaic_cells}, {"mosaic_fused", &VdTune::mosaic_fused}, {"block_fuse", &VdTune::block_fuse},
+        {"lb_pair", &VdTune::lb_pair}, {"mosaic_map", &VdTune::mosaic_map}, {"mosaic_nt", &VdTune::mosaic_nt}, {"mosaic_cells", &VdTune::mosaic_cells}, {"mosaic_fused", &VdTune::mosaic_fused}, {"mosaic_rows", &VdTune::mosaic_rows}, {"mosaic_gather", &VdTune::mosaic_gather}, {"block_fuse", &VdTune::block_fuse},
         {"chain", &VdTune::chain}, {"stem_pool", &VdTune::stem_pool}, {"ssh_fuse", &VdTune::ssh_fuse},
         {"plate_s2d", &VdTune::plate_s2d}, {"f32_split", &VdTune::f32_split},
         {"x6_small_k", &VdTune::x6_small_k}, {"x6_small_tiles", &VdTune::x6_small_tiles},
