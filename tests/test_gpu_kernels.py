@@ -569,12 +569,12 @@ def test_mosaic_output_forms_match_oracle(gpu, mapon):
         ctx.close()
 
 
-@pytest.mark.parametrize("fused,rows,gather", [(0, 0, 0), (1, 0, 0), (1, 8, 0), (1, 24, 0), (1, 32, 0), (1, 0, 1),
-                                               (1, 8, 1)])
+@pytest.mark.parametrize("fused,rows,gather", [(0, 0, 0), (1, 0, 0), (1, 4, 0), (1, 8, 0), (1, 16, 0), (1, 24, 0),
+                                               (1, 32, 0), (1, 0, 1), (1, 8, 1)])
 def test_mosaic_fused_and_two_launch_paths_match_oracle(gpu, fused, rows, gather):
     """Option mosaic_fused: 1 (default) = one launch, the output pass walks and gathers
     its bands' cells itself; 0 = cell-table kernel + output pass; the fused pass at
-    8 / 16 / 24 / 32 rows per band (option mosaic_rows; 0 = 16), with the band cells'
+    4 / 8 / 16 / 24 / 32 rows per band (option mosaic_rows), with the band cells'
     source loads batched (option mosaic_gather). All exact on random
     boxes (incl. degenerate / off-frame ones), nested chains, a level-2 band whose cells
     exceed the LDS slice, > MAPBOX boxes in a band and > BOX_FAST boxes in a frame."""

@@ -6,11 +6,12 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 OUT=gpurun_out/r06i
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu -p no:cacheprovider tests/test_gpu_kernels.py -k "mosaic" > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
+timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu -p no:cacheprovider tests/test_gpu_kernels.py -k "mosaic_fused" > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
 tail -1 $OUT/tests.log
 C2="--height 720 --width 1280 --batch 32 --precision bf16 --frames-src up2"
 C5="--height 2160 --width 3840 --batch 64 --precision fp16 --frames-src up2 --steps 10 --warmup 2"
-for r in ${ROWS_SET:-"16 8 16g 8g"}; do
+RS="${ROWS_SET:-16 8 16g 8g}"
+for r in $RS; do
   G=0; case $r in *g) G=1; r=${r%g};; esac
   for cfg in C2 C5 C3; do
     case $cfg in C2) A=$C2;; C5) A=$C5;; C3) A="";; esac

@@ -853,7 +853,7 @@ __global__ __launch_bounds__(256) void mosaic_out_kernel(MosaicArgs a) {
 // prelude grows), so 16 stays the default.
 static int mosaic_rows_for(int n, int h, int opt) {
     (void)n; (void)h;
-    return (opt == 8 || opt == 24 || opt == 32) ? opt : ROWS;
+    return (opt == 4 || opt == 8 || opt == 24 || opt == 32) ? opt : ROWS;
 }
 
 size_t vd_mosaic_table_bytes(int n, int tcap) {
@@ -880,6 +880,7 @@ hipError_t vd_launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w
     if (stages & 8) {
         const int r = mosaic_rows_for(n, h, map_on >> 8);
         if (r == 8) hipLaunchKernelGGL((mosaic_out_kernel<true, 8>), dim3((h + 7) / 8, n), dim3(256), 0, s, a);
+        else if (r == 4) hipLaunchKernelGGL((mosaic_out_kernel<true, 4>), dim3((h + 3) / 4, n), dim3(256), 0, s, a);
         else if (r == 32) hipLaunchKernelGGL((mosaic_out_kernel<true, 32>), dim3((h + 31) / 32, n), dim3(256), 0, s, a);
         else if (r == 24) hipLaunchKernelGGL((mosaic_out_kernel<true, 24>), dim3((h + 23) / 24, n), dim3(256), 0, s, a);
         else hipLaunchKernelGGL((mosaic_out_kernel<true, ROWS>), dim3((h + ROWS - 1) / ROWS, n), dim3(256), 0, s, a);
