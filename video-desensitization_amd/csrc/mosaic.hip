@@ -847,13 +847,14 @@ __global__ __launch_bounds__(256) void mosaic_out_kernel(MosaicArgs a) {
 
 }  // namespace
 
-// Band height of the fused output pass (option mosaic_rows: 8 / 16 / 24 / 32; 0 = 16).
-// Measured (profiles/r06_mosaic_rows.txt): 24- and 32-row bands are slower at every
-// config (more row classes than the vector maps hold take the per-pixel scan, and the
-// prelude grows), so 16 stays the default.
-static int mosaic_rows_for(int n, int h, int opt) {
-    (void)n; (void)h;
-    return (opt == 4 || opt == 8 || opt == 24 || opt == 32) ? opt : ROWS;
+// Band height of the fused output pass (option mosaic_rows: 4 / 8 / 16 / 24 / 32; 0 =
+// auto). Measured (profiles/r06_mosaic_rows.txt): bands of ~30-45 KB of pixels stream
+// best -- 8 rows at 720p / 1080p (1080p blur 0.52 -> 0.55 of the HBM peak), 4 rows at 4K
+// (0.50 -> 0.64); 24- / 32-row bands are slower everywhere (more row classes than the
+// vector maps hold take the per-pixel scan, and the prelude grows).
+static int mosaic_rows_for(int w, int opt) {
+    if (opt == 4 || opt == 8 || opt == ROWS || opt == 24 || opt == 32) return opt;
+    return w * 3 >= 8192 ? 4 : 8;
 }
 
 size_t vd_mosaic_table_bytes(int n, int tcap) {
@@ -878,7 +879,7 @@ hipError_t vd_launch_mosaic(const uint8_t* in, uint8_t* out, int n, int h, int w
     if (stages & 1) hipLaunchKernelGGL(mosaic_cell_kernel, dim3(cell_blocks, n), dim3(256), 0, s, a);
     if (stages & 2) hipLaunchKernelGGL(mosaic_out_kernel<false>, dim3((h + ROWS - 1) / ROWS, n), dim3(256), 0, s, a);
     if (stages & 8) {
-        const int r = mosaic_rows_for(n, h, map_on >> 8);
+        const int r = mosaic_rows_for(w, map_on >> 8);
         if (r == 8) hipLaunchKernelGGL((mosaic_out_kernel<true, 8>), dim3((h + 7) / 8, n), dim3(256), 0, s, a);
         else if (r == 4) hipLaunchKernelGGL((mosaic_out_kernel<true, 4>), dim3((h + 3) / 4, n), dim3(256), 0, s, a);
         else if (r == 32) hipLaunchKernelGGL((mosaic_out_kernel<true, 32>), dim3((h + 31) / 32, n), dim3(256), 0, s, a);

@@ -62,7 +62,8 @@ struct VdTune {
     int mosaic_nt = 0;        //   non-temporal output stores (1), and source loads (3)
     int mosaic_cells = 32;    //   cell-table kernel: workgroups per frame
     int mosaic_gather = 0;    //   fused output pass: a thread's band cells walked, then their loads issued together
-    int mosaic_rows = 0;      //   fused output pass: rows per band (8 / 16 / 24 / 32; 0 = 16)
+    int mosaic_rows = 0;      //   fused output pass: rows per band (4 / 8 / 16 / 24 / 32; 0 = auto: 4 for rows
+                              //   of >= 8 KB (4K), else 8)
     int mosaic_fused = 1;     //   one launch: the output pass computes its bands' cell colours itself (0: cell kernel + output pass)
     int block_fuse = 1;       // plan: fused layer1 bottlenecks (block.hip)
     int block32_xd = 2;       //   block32 stage-1 x loads in flight + 1 (register sets: 2, 3, 4)
