@@ -208,6 +208,40 @@ def test_process_plate_release_point(gpu, stage):
         np.testing.assert_array_equal(res[stage][2][b], res[3][2][b])
 
 
+@pytest.mark.parametrize("mosaic_plates", [False, True])
+def test_process_detect_early_and_mosaic_early_identical(gpu, mosaic_plates):
+    """Round 6 scheduling options: plate_detect_early (each YOLO Detect level right after
+    its P level; default 1) and mosaic_early (without MOSAIC_PLATES the face mosaic runs
+    before the plate branch joins; default 1). Order only: the plate raw heads, both box
+    lists and the mosaicked frames equal the all-at-the-end schedule's, in both plate modes
+    (combine_detect.py:239 discards plate boxes; the intended mode blurs them)."""
+    import vdmi
+    from vdmi import _lib, synth, weights
+    fr = synth.frames(3, 1080, 1920, seed=23)
+    flags = _lib.VD_PROC_FACES | _lib.VD_PROC_PLATES | _lib.VD_PROC_MOSAIC
+    if mosaic_plates:
+        flags |= _lib.VD_PROC_MOSAIC_PLATES
+    res = {}
+    for key, opts in (("new", {}), ("old", {"plate_detect_early": 0, "mosaic_early": 0})):
+        c = vdmi.Context(precision="fp32", max_batch=3, options=opts)
+        try:
+            c.load_weights(0, weights.retinaface_state_dict(0))
+            c.load_weights(1, weights.yolov8n_state_dict(0))
+            raw = c.plate_raw(fr)
+            for _ in range(2):
+                out, faces, plates = c.process(fr, flags=flags)
+            res[key] = (raw, out.copy(), [faces.frame(b)[0].copy() for b in range(3)],
+                        [plates.frame(b)[0].copy() for b in range(3)])
+        finally:
+            c.close()
+    np.testing.assert_array_equal(res["new"][0], res["old"][0])
+    np.testing.assert_array_equal(res["new"][1], res["old"][1])
+    assert sum(len(x) for x in res["old"][2]) > 0
+    for b in range(3):
+        np.testing.assert_array_equal(res["new"][2][b], res["old"][2][b])
+        np.testing.assert_array_equal(res["new"][3][b], res["old"][3][b])
+
+
 @pytest.mark.parametrize("prec,plates,groups", [("fp32", True, 2), ("fp32", False, 2), ("bf16", True, 2),
                                                ("fp32", True, 3), ("fp16", False, 4)])
 def test_process_face_groups_bit_identical(gpu, prec, plates, groups):

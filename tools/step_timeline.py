@@ -20,7 +20,7 @@ def load(d):
     rows = []
     for r in csv.DictReader(open(tr)):
         rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Stream_Id"],
-                     r["Kernel_Name"].replace("void (anonymous namespace)::", "").split("(")[0]))
+                     r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]))
     return sorted(rows)
 
 

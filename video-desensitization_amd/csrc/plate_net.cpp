@@ -245,14 +245,10 @@ int build_plan(Ctx& c, int ch, int cw, Net& net) {
     p.up(p.buf("cat20"), 128, p.buf("cat11"), 0, 256);                                   // 10,11
     p.c2f("model.12", 1, false, p.buf("cat11"), 0, "C12", "T12", p.buf("cat17"), 64);   // -> cat17[64:192)
     p.up(p.buf("cat17"), 64, p.buf("cat14"), 0, 128);                                    // 13,14
-    p.c2f("model.15", 1, false, p.buf("cat14"), 0, "C15", "T15", p.buf("P3"), 0);
-    p.conv("model.16", p.buf("P3"), 0, p.buf("cat17"), 0);                               // 16,17
-    p.c2f("model.18", 1, false, p.buf("cat17"), 0, "C18", "T18", p.buf("P4"), 0);
-    p.conv("model.19", p.buf("P4"), 0, p.buf("cat20"), 0);                               // 19,20
-    p.c2f("model.21", 1, false, p.buf("cat20"), 0, "C21", "T21", p.buf("P5"), 0);
-    // Detect
+    // Detect level i (model.22 cv2.i / cv3.i on P3 / P4 / P5, combine_detect.py:872 via
+    // ultralytics [ext]); each level reads only its P buffer and writes its own head slice
     const char* lv[3] = {"P3", "P4", "P5"};
-    for (int i = 0; i < 3; ++i) {
+    auto detect = [&](int i) {
         const std::string I = std::to_string(i);
         Act d0 = p.buf("D0_" + I), d1 = p.buf("D1_" + I);
         Act hd = P.head[i];
@@ -266,7 +262,19 @@ int build_plan(Ctx& c, int ch, int cw, Net& net) {
         }
         p.conv("box." + I, d1, 0, hd, 0);
         p.conv("cls." + I, d1, 64, hd, 64);
-    }
+    };
+    // option plate_detect_early (default 1): each Detect level right after its P level is
+    // produced, so the heavy level-0 head (P3, 80 x 48) overlaps the face net instead of
+    // ending the plate branch -- the branch's last launches are then the small 20 x 12 tail
+    const bool early = c.tune.plate_detect_early != 0;
+    p.c2f("model.15", 1, false, p.buf("cat14"), 0, "C15", "T15", p.buf("P3"), 0);
+    if (early) detect(0);
+    p.conv("model.16", p.buf("P3"), 0, p.buf("cat17"), 0);                               // 16,17
+    p.c2f("model.18", 1, false, p.buf("cat17"), 0, "C18", "T18", p.buf("P4"), 0);
+    if (early) detect(1);
+    p.conv("model.19", p.buf("P4"), 0, p.buf("cat20"), 0);                               // 19,20
+    p.c2f("model.21", 1, false, p.buf("cat20"), 0, "C21", "T21", p.buf("P5"), 0);
+    for (int i = early ? 2 : 0; i < 3; ++i) detect(i);
     return p.rc;
 }
 }  // namespace

@@ -1129,7 +1129,7 @@ int vd_set_option(vd_ctx* h, const char* name, int value) {
         {"plate_s2d", &VdTune::plate_s2d}, {"f32_split", &VdTune::f32_split},
         {"x6_small_k", &VdTune::x6_small_k}, {"x6_small_tiles", &VdTune::x6_small_tiles},
         {"x6_stream", &VdTune::x6_stream}, {"x6_small_k2", &VdTune::x6_small_k2}, {"x6_bn256", &VdTune::x6_bn256},
-        {"x6_exact", &VdTune::x6_exact}, {"x6_mid", &VdTune::x6_mid}, {"block_fuse32", &VdTune::block_fuse32}, {"x6_mf32", &VdTune::x6_mf32}, {"x6_tail", &VdTune::x6_tail}, {"x6_stream_silu", &VdTune::x6_stream_silu}, {"x6_slots", &VdTune::x6_slots}, {"x6_halo", &VdTune::x6_halo}, {"x6_halo_narrow", &VdTune::x6_halo_narrow}, {"x6_halo_s2", &VdTune::x6_halo_s2}, {"x6_adepth", &VdTune::x6_adepth}, {"x6_gemm1x1", &VdTune::x6_gemm1x1}, {"x6_taps", &VdTune::x6_taps}, {"x6_halo_tr", &VdTune::x6_halo_tr}, {"x6_halo_dma", &VdTune::x6_halo_dma}, {"x6_halo_pf", &VdTune::x6_halo_pf}, {"x6_gemm_pf", &VdTune::x6_gemm_pf}, {"x6_stream256", &VdTune::x6_stream256}, {"plate_stage", &VdTune::plate_stage}, {"ssh_side", &VdTune::ssh_side}, {"face_groups", &VdTune::face_groups}, {"plate_s2d32", &VdTune::plate_s2d32}, {"det_group", &VdTune::det_group}, {"chain_gpw", &VdTune::chain_gpw}, {"block32_xd", &VdTune::block32_xd}, {"block32_pipe", &VdTune::block32_pipe}, {"x6_one", &VdTune::x6_one},
+        {"x6_exact", &VdTune::x6_exact}, {"x6_mid", &VdTune::x6_mid}, {"block_fuse32", &VdTune::block_fuse32}, {"x6_mf32", &VdTune::x6_mf32}, {"x6_tail", &VdTune::x6_tail}, {"x6_stream_silu", &VdTune::x6_stream_silu}, {"x6_slots", &VdTune::x6_slots}, {"x6_halo", &VdTune::x6_halo}, {"x6_halo_narrow", &VdTune::x6_halo_narrow}, {"x6_halo_s2", &VdTune::x6_halo_s2}, {"x6_adepth", &VdTune::x6_adepth}, {"x6_gemm1x1", &VdTune::x6_gemm1x1}, {"x6_taps", &VdTune::x6_taps}, {"x6_halo_tr", &VdTune::x6_halo_tr}, {"x6_halo_dma", &VdTune::x6_halo_dma}, {"x6_halo_pf", &VdTune::x6_halo_pf}, {"x6_gemm_pf", &VdTune::x6_gemm_pf}, {"x6_stream256", &VdTune::x6_stream256}, {"plate_stage", &VdTune::plate_stage}, {"plate_detect_early", &VdTune::plate_detect_early}, {"mosaic_early", &VdTune::mosaic_early}, {"ssh_side", &VdTune::ssh_side}, {"face_groups", &VdTune::face_groups}, {"plate_s2d32", &VdTune::plate_s2d32}, {"det_group", &VdTune::det_group}, {"chain_gpw", &VdTune::chain_gpw}, {"block32_xd", &VdTune::block32_xd}, {"block32_pipe", &VdTune::block32_pipe}, {"x6_one", &VdTune::x6_one},
         {"jenc_gpu", &VdTune::jenc_gpu}, {"jdec_gpu", &VdTune::jdec_gpu}, {"jdec_chunk", &VdTune::jdec_chunk}, {"jdec_sync", &VdTune::jdec_sync}, {"jdec_group", &VdTune::jdec_group},
     };
     for (const Opt& o : opts)
@@ -1334,28 +1334,36 @@ int vd_process(vd_ctx* h, const uint8_t* in, uint8_t* out, int n, int fh, int fw
         ctx->stream = main;
         if (rc) return rc;
     }
-    if (fork) {
-        VD_CHECK_HIP(hipEventRecord(ctx->ev_join, plate_stream));
-        VD_CHECK_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
-    }
-    if (do_mosaic) {
+    // the mosaic reads plate boxes only with MOSAIC_PLATES (the reference discards them,
+    // combine_detect.py:239): otherwise it runs on the face stream before the plate branch
+    // joins, beside the branch's last launches (option mosaic_early)
+    const bool mosaic_first = do_mosaic && fork && !mosaic_plates && ctx->tune.mosaic_early;
+    auto mosaic = [&]() -> int {
         uint8_t* dout = out;
         size_t bytes = (size_t)n * fh * pitch;
         if (where == VD_HOST) {
-            if ((rc = ctx->ensure_staging(&ctx->stage_out, &ctx->stage_out_bytes, bytes))) return rc;
+            int r = ctx->ensure_staging(&ctx->stage_out, &ctx->stage_out_bytes, bytes);
+            if (r) return r;
             dout = (uint8_t*)ctx->stage_out;
         }
         // every kept box, from the library's complete keep lists (the caller's arrays
         // may hold fewer: cap), faces in NMS order then plates (combine_detect.py:241-249)
         const PostScratch& fp = ctx->face.post;
         const PostScratch& pp = ctx->plate.post;
-        if ((rc = ctx->launch_mosaic(d, dout, n, fh, fw, pitch, do_faces ? fp.kcount : nullptr,
-                                     do_faces ? fp.kxyxy : nullptr, do_faces ? fp.kcap : 0,
-                                     mosaic_plates ? pp.kcount : nullptr, mosaic_plates ? pp.kxyxy : nullptr,
-                                     mosaic_plates ? pp.kcap : 0, ctx->cfg.mosaic_level)))
-            return rc;
+        int r = ctx->launch_mosaic(d, dout, n, fh, fw, pitch, do_faces ? fp.kcount : nullptr,
+                                   do_faces ? fp.kxyxy : nullptr, do_faces ? fp.kcap : 0,
+                                   mosaic_plates ? pp.kcount : nullptr, mosaic_plates ? pp.kxyxy : nullptr,
+                                   mosaic_plates ? pp.kcap : 0, ctx->cfg.mosaic_level);
+        if (r) return r;
         if (where == VD_HOST) VD_CHECK_HIP(hipMemcpyAsync(out, dout, bytes, hipMemcpyDeviceToHost, ctx->stream));
+        return VD_OK;
+    };
+    if (mosaic_first && (rc = mosaic())) return rc;
+    if (fork) {
+        VD_CHECK_HIP(hipEventRecord(ctx->ev_join, plate_stream));
+        VD_CHECK_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
     }
+    if (do_mosaic && !mosaic_first && (rc = mosaic())) return rc;
     int rc2 = VD_OK;
     if (do_faces) rc2 = ctx->box_finish(faces, n, tf);
     if (do_plates) {

@@ -88,6 +88,8 @@ struct VdTune {
     int plate_s2d32 = 1;      // fp32 plan: the plate stem on the fp16 space-to-depth canvas (with plate_s2d)
     int face_groups = 2;      // face net as G frame groups on G streams (the tails of one group's launches
                               //   fill with the others'; bit-identical; 0 / 1: one launch over the batch)
+    int plate_detect_early = 1; // plan: each YOLO Detect level right after its P level (0: all three at the end)
+    int mosaic_early = 1;     // vd_process without MOSAIC_PLATES: the face mosaic runs before the plate branch joins
     int plate_stage = 3;      // plate branch starts after face stage N (0: with the stem; 1-4: after
                               //   layerN; 5: after the whole face net). After layer3 its HBM-bound
                               //   convs overlap the MFMA-bound late face layers: 30.8 -> 30.0 ms/step
