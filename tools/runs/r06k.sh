@@ -9,8 +9,9 @@ export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu -p no:cacheprovider tests/test_gpu_plates.py > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
 tail -1 $OUT/tests.log
 for r in 1 2; do
-  for cfg in old new; do
-    case $cfg in old) O="--option plate_detect_early=0 --option mosaic_early=0";; new) O="";; esac
+  for cfg in old new ps1 ps2; do
+    case $cfg in old) O="--option plate_detect_early=0 --option mosaic_early=0";; new) O="";;
+                 ps1) O="--option plate_stage=1";; ps2) O="--option plate_stage=2";; esac
     timeout -k 10 300 python bench.py --steps 20 --warmup 3 --compare "" --no-cpu-baseline --host-pipeline 0 $O > $OUT/${cfg}$r.json 2>> $OUT/err.log || { tail -20 $OUT/err.log; exit 1; }
     python -c "import json;d=json.load(open('$OUT/${cfg}$r.json'));print('$cfg$r',d['value'],d['ms_per_step'],d['roofline']['frac'])"
   done

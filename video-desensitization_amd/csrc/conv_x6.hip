@@ -1197,9 +1197,14 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
 // (off the frame -> zeros, conv padding) for every k-step. TERMS = 1: integer-valued
 // input (x_exact canvases) on one plane against both weight planes. NTT = 1: 16
 // output channels, a lane stores 4 consecutive ones.
-template <int KS, int NTT, int ACT, int RES, int TERMS, bool TAPS = false>
+// RL (round 6, option x6_stream_rl; plain 1x1 form only): the next group's input refills
+// each k-step's registers right after that k-step is split (one register set instead of
+// two), and the registers saved carry this group's residual, loaded at the top of the
+// group beside the MFMAs instead of in the epilogue where its latency stood exposed.
+template <int KS, int NTT, int ACT, int RES, int TERMS, bool TAPS = false, bool RL = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(TAPS ? 4 : 1)))   // TAPS: two workgroups per CU
 void conv1x1_x6_kernel(ConvArgs a, int nchunks, int groups) {
+    static_assert(!(RL && (TAPS || NTT == 1)), "RL: the plain 1x1 form with 8-channel lanes");
     constexpr int WT = TERMS == 1 ? 2 : TERMS;             // weight planes
     constexpr int NCH = 16 * NTT, PL = KS * NCH * 64;     // bytes per weight plane
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1277,6 +1282,123 @@ void conv1x1_x6_kernel(ConvArgs a, int nchunks, int groups) {
     u32x4 xf[KS][2];
     int g = mblk * 8 + wid;
     if (g < groups) load(g, xf);
+    if constexpr (RL) {
+        // pixel m's element offset of its input row (this lane's 8 channels)
+        auto xrow = [&](int gg) -> const float* {
+            const int mu = gg * 16 + p_lane;
+            const int m = mu < a.M ? mu : a.M - 1;
+            const int b = m / ohw, rem = m - b * ohw;
+            const int oy = rem / a.yw, ox = rem - oy * a.yw;
+            return (const float*)a.x + (((size_t)b * a.xh + oy * a.stride) * a.xw + ox * a.stride) * a.ldx + a.xcoff +
+                   q * 8;
+        };
+        // the frame range of the group being split, loaded one group ahead (its load would
+        // otherwise sit behind this group's residual loads in the in-order vmcnt)
+        auto frame_max = [&](int gg) -> float {
+            const int mu = gg * 16 + p_lane;
+            return a.xmax ? __uint_as_float(a.xmax[(mu < a.M ? mu : a.M - 1) / ohw]) : a.xbound;
+        };
+        float xm_cur = g < groups ? frame_max(g) : 0.f;
+        const __amdgpu_buffer_rsrc_t rsrc_r = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)a.res, 0, RES != VD_RES_NONE ? (int)std::min<long>((long)a.M * a.res_ld * 4, 0x7fffffffL) : 0,
+            0x00020000);
+        for (; g < groups; g += wstride) {
+            asm volatile("" ::: "memory");
+            const int gn = g + wstride;
+            const float* xpn = xrow(gn < groups ? gn : g);
+            const float xm_next = frame_max(gn < groups ? gn : g);   // unconditional: straight-line vmcnt
+            const int mu = g * 16 + p_lane;
+            const int mcl = mu < a.M ? mu : a.M - 1;
+            // this group's residual rows, in flight under the MFMAs
+            float4 rr[NTT / 2][2];
+            if constexpr (RES != VD_RES_NONE) {
+                size_t roff;
+                if (a.res_up) {
+                    const int b = mcl / ohw, rem = mcl - b * ohw;
+                    const int oy = rem / a.yw, ox = rem - oy * a.yw;
+                    roff = ((size_t)(b * a.rh + (oy >> 1)) * a.rw + (ox >> 1)) * a.res_ld;
+                } else {
+                    roff = (size_t)mcl * a.res_ld;
+                }
+                roff += a.res_coff + n0 + q * 8;
+                // buffer loads (rows past M read zeros): unconditional, issued here, not sunk
+                // into the epilogue where their latency would stand exposed again
+                const bool okr = mu < a.M;
+#pragma unroll
+                for (int i = 0; i < NTT / 2; ++i) {
+                    const unsigned o = okr ? (unsigned)((roff + 32 * i) * 4) : 0x80000000u;
+                    rr[i][0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc_r, (int)o, 0, 0));
+                    rr[i][1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rsrc_r, (int)o, 16, 0));
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            f32x4_t acc[NTT];
+#pragma unroll
+            for (int j = 0; j < NTT; ++j) acc[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+            const int fb = mcl / ohw;
+            const int kexp = TERMS == 2 ? act_scale_exp_of(xm_cur) : 0;
+            const float sa = __builtin_ldexpf(1.f, kexp), inv_sa = __builtin_ldexpf(1.f, -kexp);
+            xm_cur = xm_next;
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+                float e8[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) e8[e] = __uint_as_float(xf[ks][e >> 2][e & 3]);
+                u32x4 xb[3];
+                split_pack<TERMS>(e8, sa, xb);
+                // refill this k-step's registers with the next group's (the last group re-reads
+                // its own rows: no branch, so the compiler counts vmcnt exactly)
+                xf[ks][0] = *(const u32x4*)(xpn + ks * 32);
+                xf[ks][1] = *(const u32x4*)(xpn + ks * 32 + 4);
+#pragma unroll
+                for (int j = 0; j < NTT; ++j) {
+                    u32x4 wf[3];
+#pragma unroll
+                    for (int p = 0; p < WT; ++p)
+                        wf[p] = *(const u32x4*)(smem + p * PL + ks * NCH * 64 + swz(16 * j + p_lane, q));
+                    acc[j] = mfma_terms<TERMS>(wf, xb, acc[j]);
+                }
+            }
+            float vmax = 0.f;
+            if (mu < a.M) {
+                const size_t yo = (size_t)mu * a.ldy + a.ycoff + n0 + q * 8;
+#pragma unroll
+                for (int i = 0; i < NTT / 2; ++i) {
+                    const int c = 32 * i + q * 8;
+                    const float4 s0 = *(const float4*)(s_scale + c), s1 = *(const float4*)(s_scale + c + 4);
+                    const float4 h0 = *(const float4*)(s_shift + c), h1 = *(const float4*)(s_shift + c + 4);
+                    const f32x4_t& lo = acc[2 * i];
+                    const f32x4_t& hi = acc[2 * i + 1];
+                    float v[8] = {(lo[0] * inv_sa) * s0.x + h0.x, (lo[1] * inv_sa) * s0.y + h0.y,
+                                  (lo[2] * inv_sa) * s0.z + h0.z, (lo[3] * inv_sa) * s0.w + h0.w,
+                                  (hi[0] * inv_sa) * s1.x + h1.x, (hi[1] * inv_sa) * s1.y + h1.y,
+                                  (hi[2] * inv_sa) * s1.z + h1.z, (hi[3] * inv_sa) * s1.w + h1.w};
+                    float rv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+                    if constexpr (RES != VD_RES_NONE) {
+                        rv[0] = rr[i][0].x; rv[1] = rr[i][0].y; rv[2] = rr[i][0].z; rv[3] = rr[i][0].w;
+                        rv[4] = rr[i][1].x; rv[5] = rr[i][1].y; rv[6] = rr[i][1].z; rv[7] = rr[i][1].w;
+                    }
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        float t = v[e];
+                        if constexpr (RES == VD_RES_PRE_ACT) t += rv[e];
+                        t = act_apply(t, ACT, a.slope);
+                        if constexpr (RES == VD_RES_POST_ACT) t += rv[e];
+                        v[e] = t;
+                        vmax = fmaxf(vmax, fabsf(t));
+                    }
+                    *(float4*)((float*)a.y + yo + 32 * i) = make_float4(v[0], v[1], v[2], v[3]);
+                    *(float4*)((float*)a.y + yo + 32 * i + 4) = make_float4(v[4], v[5], v[6], v[7]);
+                }
+            }
+            if (a.ymax) amax_lds_add(s_amax, mu < a.M ? fb : -1, vmax);
+        }
+        if (a.ymax) {
+            __syncthreads();
+            amax_lds_flush(s_amax, a.ymax, a.B);
+        }
+        return;
+    }
     for (; g < groups; g += wstride) {
         asm volatile("" ::: "memory");
         u32x4 xn[KS][2];
@@ -1553,17 +1675,20 @@ hipError_t launch_dual_x6(const ConvArgs& a0, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <int KS, int NTT, int ACT, int RES, int TERMS, bool TAPS = false>
+template <int KS, int NTT, int ACT, int RES, int TERMS, bool TAPS = false, bool RL = false>
 hipError_t launch_stream_x6(const ConvArgs& a, hipStream_t s) {
+    if constexpr (!TAPS && !RL && NTT >= 2 && TERMS == 2) {   // option x6_stream_rl
+        if (a.tune && a.tune->x6_stream_rl) return launch_stream_x6<KS, NTT, ACT, RES, TERMS, false, true>(a, s);
+    }
     constexpr int NCH = 16 * NTT;
     constexpr int lds = (TERMS == 1 ? 2 : TERMS) * KS * NCH * 64 + 2 * NCH * 4;
     static const int resident = [] {
-        (void)hipFuncSetAttribute((const void*)conv1x1_x6_kernel<KS, NTT, ACT, RES, TERMS, TAPS>,
+        (void)hipFuncSetAttribute((const void*)conv1x1_x6_kernel<KS, NTT, ACT, RES, TERMS, TAPS, RL>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, lds + 4 * kAmaxFrames);
         int dev = 0, cus = 256, per_cu = 1;
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv1x1_x6_kernel<KS, NTT, ACT, RES, TERMS, TAPS>,
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, conv1x1_x6_kernel<KS, NTT, ACT, RES, TERMS, TAPS, RL>,
                                                            512, lds);
         return std::max(1, cus * std::max(1, per_cu));
     }();
@@ -1571,7 +1696,7 @@ hipError_t launch_stream_x6(const ConvArgs& a, hipStream_t s) {
     const int groups = (a.M + 15) / 16;
     int k = std::max(1, resident / (8 * nchunks));
     k = std::min(k, std::max(1, (groups + 63) / 64));
-    hipLaunchKernelGGL((conv1x1_x6_kernel<KS, NTT, ACT, RES, TERMS, TAPS>), dim3(8 * nchunks * k), dim3(512),
+    hipLaunchKernelGGL((conv1x1_x6_kernel<KS, NTT, ACT, RES, TERMS, TAPS, RL>), dim3(8 * nchunks * k), dim3(512),
                        lds + (a.ymax ? 4 * a.B : 0), s, a, nchunks, groups);
     return hipGetLastError();
 }

@@ -94,6 +94,8 @@ struct VdTune {
                               //   layerN; 5: after the whole face net). After layer3 its HBM-bound
                               //   convs overlap the MFMA-bound late face layers: 30.8 -> 30.0 ms/step
     int x6_stream = 1;        // fp32 split: streaming 1x1 kernel for K in {64, 128, 256}
+    int x6_stream_rl = 0;     //   streaming 1x1: one input register set refilled per k-step, the residual loaded
+                              //   at the top of each pixel group (beside the MFMAs) instead of in the epilogue
     int x6_stream_silu = 1;   //   fp16 pairs: also SiLU 1x1 convs (YOLO C2f / SPPF) with K in {32..256}
     int x6_stream256 = 2;     //   fp16 pairs, Cout % 256 == 0: 256-channel slices for K = 64 (2: and K = 128;
                               //   each pixel read by half as many workgroups: faces 27.31 -> 26.96 ms/step)
@@ -352,6 +354,15 @@ struct JpegArgs {
 // all of K, so the accumulator is scaled back per row in the epilogue (exact:
 // powers of two), and a frame's result does not depend on the rest of its batch.
 // Returns the exponent k (operand * 2^k) for frame b.
+// the exponent from a frame's max |x| already loaded (act_scale_exp split for prefetching)
+__device__ __forceinline__ int act_scale_exp_of(float m) {
+    if (!(m > 0.f) || !(m < 3.0e38f)) return 0;
+    int e;
+    (void)frexpf(m, &e);                              // m < 2^e
+    const int k = 15 - e;
+    return k < -100 ? -100 : (k > 100 ? 100 : k);
+}
+
 __device__ __forceinline__ int act_scale_exp(const ConvArgs& a, int b) {
     const float m = a.xmax ? __uint_as_float(a.xmax[b]) : a.xbound;
     if (!(m > 0.f) || !(m < 3.0e38f)) return 0;
