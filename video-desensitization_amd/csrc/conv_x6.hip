@@ -1677,7 +1677,10 @@ hipError_t launch_dual_x6(const ConvArgs& a0, hipStream_t s) {
 
 template <int KS, int NTT, int ACT, int RES, int TERMS, bool TAPS = false, bool RL = false>
 hipError_t launch_stream_x6(const ConvArgs& a, hipStream_t s) {
-    if constexpr (!TAPS && !RL && NTT >= 2 && TERMS == 2) {   // option x6_stream_rl
+    // option x6_stream_rl (default 1): the RL form for the layers with a residual (layer3
+    // conv3 330 -> 299 us, layer2 conv3 416 -> 404 in x6bench); without one it measured
+    // slower (layer2.0 conv1 577 -> 603), so those keep the two-set form
+    if constexpr (!TAPS && !RL && NTT >= 2 && TERMS == 2 && RES != VD_RES_NONE) {
         if (a.tune && a.tune->x6_stream_rl) return launch_stream_x6<KS, NTT, ACT, RES, TERMS, false, true>(a, s);
     }
     constexpr int NCH = 16 * NTT;
