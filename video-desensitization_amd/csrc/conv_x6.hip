@@ -383,6 +383,105 @@ __device__ __forceinline__ void x6_epilogue(const ConvArgs& a, AccT (&acc)[S::TM
 template <class S>
 __device__ __forceinline__ void x6_epilogue_tr(const ConvArgs& a, f32x4_t (&acc)[S::TM][S::TN], int m0, int n0,
                                                int wm, int wn, int lane, unsigned* s_amax) {
+    constexpr int TM = S::TM, TN = S::TN, NJ = TN / 2;
+    static_assert(TN % 2 == 0, "TR tiles pair the channel blocks");
+    const int ohw = a.yh * a.yw;
+    const int q = lane >> 4, pl = lane & 15;
+    const int cb = n0 + wn * S::WTN + 8 * q;
+    int fbs[TM];
+    unsigned yrow[TM], rrow[TM];                     // byte offsets of the lane's output / residual row (channel 0)
+    float inv[TM], vmax[TM];
+    const bool res = a.res_mode != VD_RES_NONE;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int m = m0 + wm * S::WTM + 16 * i + pl;
+        const bool ok = m < a.M;
+        fbs[i] = ok ? m / ohw : -1;
+        inv[i] = __builtin_ldexpf(1.f, -act_scale_exp(a, ok ? fbs[i] : 0));
+        vmax[i] = 0.f;
+        yrow[i] = ok ? (unsigned)(((size_t)m * a.ldy + a.ycoff) * 4) : 0x80000000u;
+        rrow[i] = 0x80000000u;
+        if (ok && res) {
+            size_t roff;
+            if (a.res_up) {
+                const int b = fbs[i], rem = m - b * ohw;
+                const int oy = rem / a.yw, ox = rem - oy * a.yw;
+                roff = ((size_t)(b * a.rh + (oy >> 1)) * a.rw + (ox >> 1)) * a.res_ld;
+            } else {
+                roff = (size_t)m * a.res_ld;
+            }
+            rrow[i] = (unsigned)((roff + a.res_coff) * 4);
+        }
+    }
+    // Buffer loads / stores (rows past M, channels past cout: out of range -> zeros /
+    // dropped) keep the epilogue straight-line, and column pair jp + 1's residual and
+    // BN rows are loaded before pair jp's stores: vmcnt retires loads and stores in issue
+    // order, so a residual load issued after a store waited for that store too (the
+    // round-5 epilogue waited on every (jp, i) row behind the stores before it).
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(a.y, 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc((void*)a.res, 0, res ? 0x7fffffff : 0,
+                                                                         0x00020000);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.scale, 0, a.cout * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc((void*)a.shift, 0, a.cout * 4, 0x00020000);
+    u32x4 rq[2][TM][2], sq[2][4];
+    auto fetch = [&](int jp, int slot) {
+        const unsigned cbytes = (unsigned)((cb + 32 * jp) * 4);
+        sq[slot][0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)cbytes, 0, 0));
+        sq[slot][1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)cbytes, 16, 0));
+        sq[slot][2] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rh, (int)cbytes, 0, 0));
+        sq[slot][3] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rh, (int)cbytes, 16, 0));
+        if (res) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const unsigned o = rrow[i] == 0x80000000u ? rrow[i] : rrow[i] + cbytes;
+                rq[slot][i][0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, (int)o, 0, 0));
+                rq[slot][i][1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, (int)o, 16, 0));
+            }
+        }
+    };
+    fetch(0, 0);
+#pragma unroll
+    for (int jp = 0; jp < NJ; ++jp) {
+        if (jp + 1 < NJ) fetch(jp + 1, (jp + 1) & 1);
+        const int sl = jp & 1;
+        const bool cok = cb + 32 * jp < a.cout;
+        const unsigned cbytes = (unsigned)((cb + 32 * jp) * 4);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float ev = e < 4 ? acc[i][2 * jp][e] : acc[i][2 * jp + 1][e - 4];
+                const float sc = __uint_as_float(sq[sl][e >> 2][e & 3]), sh = __uint_as_float(sq[sl][2 + (e >> 2)][e & 3]);
+                const float rv = res ? __uint_as_float(rq[sl][i][e >> 2][e & 3]) : 0.f;
+                float t = (ev * inv[i]) * sc + sh;
+                if (a.res_mode == VD_RES_PRE_ACT) t += rv;
+                t = act_apply(t, a.act, a.slope);
+                if (a.res_mode == VD_RES_POST_ACT) t += rv;
+                v[e] = t;
+                if (cok && fbs[i] >= 0) vmax[i] = fmaxf(vmax[i], fabsf(t));
+            }
+            const unsigned o = (yrow[i] == 0x80000000u || !cok) ? 0x80000000u : yrow[i] + cbytes;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned,
+                                                                      make_float4(v[0], v[1], v[2], v[3])),
+                                                   ry, (int)o, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned,
+                                                                      make_float4(v[4], v[5], v[6], v[7])),
+                                                   ry, (int)o, 16, 0);
+        }
+    }
+    if (a.ymax) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) amax_lds_add(s_amax, fbs[i], vmax[i]);
+        __syncthreads();
+        amax_lds_flush(s_amax, a.ymax, a.B);
+    }
+}
+
+// the round-5 form (option x6_tr_epi = 0): residual and BN rows loaded row by row behind the stores
+template <class S>
+__device__ __forceinline__ void x6_epilogue_tr_r5(const ConvArgs& a, f32x4_t (&acc)[S::TM][S::TN], int m0, int n0,
+                                               int wm, int wn, int lane, unsigned* s_amax) {
     constexpr int TM = S::TM, TN = S::TN;
     static_assert(TN % 2 == 0, "TR tiles pair the channel blocks");
     const int ohw = a.yh * a.yw;
@@ -453,6 +552,14 @@ __device__ __forceinline__ void x6_epilogue_tr(const ConvArgs& a, f32x4_t (&acc)
 // LDS row -> weight row of a TR tile: row 16 j + i of each 32-row group holds channel
 // 8 (i >> 2) + 4 (j & 1) + (i & 3) of the group, so blocks 2jp, 2jp+1 give a lane 8
 // consecutive channels (conv1x1_x6_kernel's permutation)
+// the register epilogue (x6_epilogue_tr) addresses y and the residual by 32-bit buffer offsets
+static bool tr_bytes_ok(const ConvArgs& a) {
+    const double lim = 2147483647.0;
+    if ((double)a.M * a.ldy * 4 >= lim) return false;
+    if (a.res_mode != VD_RES_NONE && (double)a.M * a.res_ld * 4 >= lim) return false;
+    return true;
+}
+
 __device__ __forceinline__ int x6_tr_row(int row) {
     const int j = (row >> 4) & 1, i = row & 15;
     return (row & ~31) + 8 * (i >> 2) + 4 * j + (i & 3);
@@ -804,7 +911,8 @@ __global__ __launch_bounds__(NT, NT == 256 && BM == 256 ? 1 : 2) void conv_x6_ke
             if (acc[0][0][0] == 1234.5f) ((float*)a.y)[tid] = 1.f;
             return;
         }
-        x6_epilogue_tr<S>(a, acc, m0, n0, wm, wn, lane, (unsigned*)(smem + S::LDS));
+        if (a.dbg & 512) x6_epilogue_tr_r5<S>(a, acc, m0, n0, wm, wn, lane, (unsigned*)(smem + S::LDS));
+        else x6_epilogue_tr<S>(a, acc, m0, n0, wm, wn, lane, (unsigned*)(smem + S::LDS));
     } else {
         __syncthreads();
         x6_epilogue<S, MF>(a, acc, m0, n0, wm, wn, tid, lane, smem, S::LDS);
@@ -1174,7 +1282,8 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
     }
     }
     if constexpr (TR) {
-        x6_epilogue_tr<S>(a, acc, m0, n0, wm, wn, lane, (unsigned*)(smem + amax_off));
+        if (a.dbg & 512) x6_epilogue_tr_r5<S>(a, acc, m0, n0, wm, wn, lane, (unsigned*)(smem + amax_off));
+        else x6_epilogue_tr<S>(a, acc, m0, n0, wm, wn, lane, (unsigned*)(smem + amax_off));
     } else {
         __syncthreads();
         x6_epilogue<S, 16>(a, acc, m0, n0, wm, wn, tid, lane, smem, amax_off);
@@ -1879,7 +1988,7 @@ static hipError_t launch_x6_halo_t(const ConvArgs& a, hipStream_t s) {
 // x6_halo_tr: 1 the 128 / 192 / 256-wide tiles, 2 the narrow ones too)
 template <int BN, int NSB>
 static hipError_t launch_x6_halo_n(const ConvArgs& a, hipStream_t s) {
-    const bool tr = a.tune && a.tune->x6_halo_tr >= (BN >= 128 ? 1 : 2) && !((a.ldy | a.ycoff) & 7) &&
+    const bool tr = a.tune && a.tune->x6_halo_tr >= (BN >= 128 ? 1 : 2) && !((a.ldy | a.ycoff) & 7) && tr_bytes_ok(a) &&
                     (a.res_mode == VD_RES_NONE || !((a.res_ld | a.res_coff) & 7));
     if constexpr (NSB == 3 && BN >= 64) {   // stride 2: the phase halos (x6_halo_ok)
         if (a.stride == 2) return tr ? launch_x6_halo_t<BN, 3, true, true>(a, s) : launch_x6_halo_t<BN, 3, false, true>(a, s);
@@ -1945,7 +2054,7 @@ static int stream_x6_nch(const ConvArgs& a, int terms) {
 // stages): its main loop ran 5-10 % slower than the LDS-staged one (layer3 conv1
 // 215 -> 235 us without epilogue). Needs 8-channel 16-B output / residual vectors.
 static bool x6_tr_ok(const ConvArgs& a) {
-    if (a.kh != 1 || a.kw != 1 || a.pad != 0 || a.cout % 128) return false;
+    if (a.kh != 1 || a.kw != 1 || a.pad != 0 || a.cout % 128 || !tr_bytes_ok(a)) return false;
     if ((a.ldy | a.ycoff) & 7) return false;
     return a.res_mode == VD_RES_NONE || !((a.res_ld | a.res_coff) & 7);
 }
@@ -2078,7 +2187,7 @@ bool vd_conv1x1_x6_dual_ok(const ConvArgs& a) {
 hipError_t vd_launch_conv_x6(const ConvArgs& a0, hipStream_t s) {
     ConvArgs a = a0;
     a.dbg = a.tune ? (a.tune->x6_dbg & 3) | (a.tune->x6_one ? 4 : 0) | ((a.tune->x6_halo_dma & 3) << 3) |
-                     (((a.tune->x6_dbg >> 2) & 15) << 5) : 0;
+                     (((a.tune->x6_dbg >> 2) & 15) << 5) | (a.tune->x6_tr_epi ? 0 : 512) : 0;
     if (a.grp_co) {   // grouped: the halo form only, one 64-wide N tile per group
         if (a.grp_co != 64 || a.f32_split != 2 || !a.wx3 || !a.tune || !x6_halo_ok(a) || (a.ymax && a.B > kAmaxFrames))
             return hipErrorInvalidValue;

@@ -121,6 +121,8 @@ struct VdTune {
     int x6_halo_pf = 1;       //   halo tiles (128-256 wide): B fragments of block j + 1 read before block j's MFMAs
     int x6_halo_dma = 2;      //   halo tiles: where a K step issues the B DMA two steps ahead (0 after the
                               //   barrier, 1 after the step's MFMAs, 2 one piece between MFMA groups)
+    int x6_tr_epi = 1;        // TR register epilogue: 1 = residual / BN rows of column pair jp + 1 loaded before pair
+                              //   jp's stores (buffer ops, straight-line), 0 = the round-5 row-by-row form
     int x6_halo_tr = 2;       // fp32 plan: halo 3x3 tiles with D^T accumulators and the register epilogue
                               //   (1: the 128-256-wide tiles, 2: all; bit-identical)
     int x6_one = 1;           // fp16 pairs, GEMM tiles: 1x1 convs load A at row offset + scalar K offset (no tap stepping)
