@@ -1,7 +1,7 @@
 """GpuJpegStages on the bench's 64 noise / structured 1080p frames: frames/s and host stage
 times for decode_overlap True / False / "auto" (noise JPEG regression study).
 
-    python tools/jpeg_exp.py [noise|structured] [steps]
+    python tools/jpeg_exp.py [noise|structured] [steps] [modes: comma list of true,false,auto] [codec opts k=v,...]
 """
 import os
 import sys
@@ -39,8 +39,10 @@ def main():
         ctx.process(d, o, flags=flags)
     ctx.sync()
     print(f"{kind}: process alone {(time.perf_counter() - t) / steps * 1e3:.1f} ms/batch", flush=True)
-    for mode in (True, False, "auto"):
-        st = GpuJpegStages(ctx, B, flags, quality=95, subsampling=2, decode_overlap=mode)
+    sel = (sys.argv[3] if len(sys.argv) > 3 else "true,false,auto").split(",")
+    for mode in [{"true": True, "false": False, "auto": "auto"}[m] for m in sel]:
+        copts = dict((k, int(v)) for k, v in (o.split("=") for o in sys.argv[4].split(","))) if len(sys.argv) > 4 else None
+        st = GpuJpegStages(ctx, B, flags, quality=95, subsampling=2, decode_overlap=mode, codec_options=copts)
         try:
             st.run(((s, lambda: jp, None) for s in range(3)), lambda *a: None)
             torch.cuda.synchronize()
