@@ -38,6 +38,8 @@ static const Layer kLayers[] = {
     {"l4.1.c3", 20, 20, 512, 2048, 1, 1, 0, 1},   {"fpn.o1", 80, 80, 512, 256, 1, 1, 0, 0},
     {"fpn.o2", 40, 40, 1024, 256, 1, 1, 0, 0},    {"fpn.o3", 20, 20, 2048, 256, 1, 1, 0, 0},
     {"fpn.m1", 80, 80, 256, 256, 3, 1, 1, 0},     {"ssh0.c51", 80, 80, 256, 192, 3, 1, 1, 0},
+    {"ssh0.c52", 80, 80, 64, 128, 3, 1, 1, 0},    {"ssh0.c73", 80, 80, 64, 64, 3, 1, 1, 0},
+    {"ssh1.c52", 40, 40, 64, 128, 3, 1, 1, 0},
 };
 
 struct TuneField { const char* name; int VdTune::*f; };
@@ -46,7 +48,7 @@ static const TuneField kTune[] = {
     {"x6_mid", &VdTune::x6_mid},         {"x6_mf32", &VdTune::x6_mf32},           {"x6_tail", &VdTune::x6_tail},
     {"x6_halo", &VdTune::x6_halo},       {"x6_halo_s2", &VdTune::x6_halo_s2}, {"x6_adepth", &VdTune::x6_adepth},       {"x6_small_k", &VdTune::x6_small_k},
     {"x6_small_tiles", &VdTune::x6_small_tiles}, {"x6_gemm1x1", &VdTune::x6_gemm1x1}, {"x6_dbg", &VdTune::x6_dbg},
-    {"x6_halo_tr", &VdTune::x6_halo_tr}, {"x6_halo_dma", &VdTune::x6_halo_dma}, {"x6_halo_pf", &VdTune::x6_halo_pf}, {"x6_gemm_pf", &VdTune::x6_gemm_pf}, {"x6_stream_rl", &VdTune::x6_stream_rl}, {"x6_tr_epi", &VdTune::x6_tr_epi}, {"x6_one", &VdTune::x6_one},
+    {"x6_halo_tr", &VdTune::x6_halo_tr}, {"x6_halo_dma", &VdTune::x6_halo_dma}, {"x6_halo_pf", &VdTune::x6_halo_pf}, {"x6_gemm_pf", &VdTune::x6_gemm_pf}, {"x6_stream_rl", &VdTune::x6_stream_rl}, {"x6_tr_epi", &VdTune::x6_tr_epi}, {"x6_halo_n64", &VdTune::x6_halo_n64}, {"x6_one", &VdTune::x6_one},
 };
 
 static float frand(uint32_t& st) {

@@ -2164,8 +2164,13 @@ static hipError_t launch_terms(const ConvArgs& a0, hipStream_t s) {
             if (x6_halo_ok(a)) return launch_x6_halo<192>(a, s);
             return launch_x6_big<192, TERMS>(a, s);
         }
-        // every eligible layer on the halo form whatever the batch (its K order differs)
-        if (x6_halo_ok(a)) return launch_x6_halo<128>(a, s);
+        // every eligible layer on the halo form whatever the batch (its K order differs);
+        // option x6_halo_n64: Cout-128 layers with K <= x6_halo_n64 as two 64-wide N tiles,
+        // two workgroups per CU (one's prologue / epilogue beside the other's main loop)
+        if (x6_halo_ok(a)) {
+            if (a.tune && a.cout == 128 && a.kpad <= a.tune->x6_halo_n64 && a.stride == 1) return launch_x6_halo<64>(a, s);
+            return launch_x6_halo<128>(a, s);
+        }
         if (a.tune && a.tune->x6_mf32) return launch_x6<256, 128, 512, 2, TERMS, 32>(a, s);
     }
     return launch_x6_big<128, TERMS>(a, s);

@@ -118,6 +118,7 @@ struct VdTune {
     int x6_adepth = 2;        // A register sets of the 256 x {128, 64, 32} fp16-pair tiles (2 or 4; 4 measured level)
     int x6_slots = 0;         //   workgroup slots of one round (0: the CU count; tests force small values)
     int x6_gemm_pf = 1;       // GEMM tiles with wide wave tiles (TN > TM): the same pipelined B-fragment reads
+    int x6_halo_n64 = 0;      //   halo tiles: Cout-128 3x3 layers with K <= this as two 64-wide N tiles (0: off)
     int x6_halo_pf = 1;       //   halo tiles (128-256 wide): B fragments of block j + 1 read before block j's MFMAs
     int x6_halo_dma = 2;      //   halo tiles: where a K step issues the B DMA two steps ahead (0 after the
                               //   barrier, 1 after the step's MFMAs, 2 one piece between MFMA groups)
