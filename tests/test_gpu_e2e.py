@@ -526,12 +526,14 @@ def test_heads_fp32_pipelined_b_reads_bit_identical(gpu):
     block j + 1 before block j's MFMAs (options x6_halo_pf / x6_gemm_pf, default 1) and
     issue the DMA two K steps ahead between MFMA groups (x6_halo_dma: 0 after the
     barrier, 1 after the MFMAs, 2 between groups, default); the streaming 1x1 layers
-    with a residual load it beside the MFMAs (x6_stream_rl, default 1). Schedule only:
+    with a residual load it beside the MFMAs (x6_stream_rl, default 1); the 1x1 GEMM
+    loop issues the same loads every K tile (x6_gemm_uni, default 1). Schedule only:
     the same products in the same order, heads bit-identical to the round-5 schedule."""
     import vdmi
     fr = _frames(2, 1080, 1920, seed=43)
     heads = {}
-    for key, opts in (("r5", {"x6_halo_pf": 0, "x6_gemm_pf": 0, "x6_halo_dma": 0, "x6_stream_rl": 0}), ("pf", {}),
+    for key, opts in (("r5", {"x6_halo_pf": 0, "x6_gemm_pf": 0, "x6_halo_dma": 0, "x6_stream_rl": 0,
+                              "x6_gemm_uni": 0}), ("pf", {}),
                       ("d1", {"x6_halo_dma": 1})):
         ctx = vdmi.Context(precision="fp32", max_batch=2, options=opts)
         try:

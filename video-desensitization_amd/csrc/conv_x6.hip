@@ -628,6 +628,11 @@ __global__ __launch_bounds__(NT, NT == 256 && BM == 256 ? 1 : 2) void conv_x6_ke
             pix0[i] = m0 + arow + AROWS * i < a.M ? pix0[i] * 4 + apair * 32 : (int)0x80000000;
     }
     int lk = 0;                                     // K tiles loaded so far (one: the scalar offset)
+    // The two-stage main loop on 1x1 convs (UNI) issues the same loads and DMAs every
+    // iteration (past nk: the last tile again, L2 hits), branch-free, so that the
+    // compiler's own waits on the A registers count every younger op -- with the refills
+    // under `if`s (and the runtime `one` branch) it assumed none and waited for the NEXT
+    // tile's loads (just issued) in the middle of the MFMAs
 
     // two register sets of A (8 f32 of each of 2 rows): tile t lives in set t & 1,
     // loaded two iterations before it is split into LDS
@@ -644,7 +649,7 @@ __global__ __launch_bounds__(NT, NT == 256 && BM == 256 ? 1 : 2) void conv_x6_ke
         tdy[h] = t / a.kw;
         tdx[h] = t - tdy[h] * a.kw;
     }
-    auto load_a = [&](u32x4 (&r)[AIT][2]) {
+    auto load_a_any = [&](u32x4 (&r)[AIT][2]) {
         if (one) {
             const int so = lk * (KT * 4);
 #pragma unroll
@@ -708,12 +713,13 @@ __global__ __launch_bounds__(NT, NT == 256 && BM == 256 ? 1 : 2) void conv_x6_ke
 #pragma unroll
         for (int q = 0; q < (NDMA + WAVES - 1) / WAVES; ++q) {
             const int j = wid + WAVES * q;
-            if (j < NDMA) {
+            if (NDMA % WAVES == 0 || j < NDMA) {
                 const int p = j / RB, r0 = (j % RB) * 16;
                 const int row = r0 + (lane >> 2), slot = lane & 3;
                 const int chunk = slot ^ (((row >> 3) & 1) * 3);
                 const int wrow = TR ? x6_tr_row(row) : row;
-                const unsigned off = (unsigned)((((long)(n0 + wrow) * nk + kt) * S::TB + p) * 64 + chunk * 16);
+                const int ktc = kt < nk ? kt : nk - 1;     // UNI tail: the last tile again (a scalar min)
+                const unsigned off = (unsigned)((((long)(n0 + wrow) * nk + ktc) * S::TB + p) * 64 + chunk * 16);
                 __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc_w, (lds_void_t*)(Bs + p * PL_B + r0 * 64), 16, off, 0,
                                                          0, 0);
             }
@@ -847,23 +853,41 @@ __global__ __launch_bounds__(NT, NT == 256 && BM == 256 ? 1 : 2) void conv_x6_ke
     // A(NA), B(1), i.e. the ends of iterations -2 and -1. At the top of iteration t the
     // ops younger than B(t) are those of iteration t-1's end, and A(t+1) is older than
     // B(t), so both retire at vmcnt(2 AIT + my_dma) (fewer when the tail issued less).
+    // UNI (default; option x6_gemm_uni 0 = the round-5 loop): every iteration issues its
+    // loads and DMA (past nk: out of range), the loop runs whole rounds of NA iterations
+    // and a tail after it, so the compiler's waits on the A registers see every younger op
+    auto main_loop = [&](auto uni_tag) {
+    constexpr bool UNI = decltype(uni_tag)::value;
+    auto load_a = [&](u32x4 (&r)[AIT][2]) {
+        if constexpr (UNI) {                                  // 1x1 (one): no tap stepping, no branch
+            const int so = (lk < nk ? lk : nk - 1) * (KT * 4);
+#pragma unroll
+            for (int i = 0; i < AIT; ++i) {
+                r[i][0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc_x, pix0[i], so, 0));
+                r[i][1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc_x, pix0[i] + 16, so, 0));
+            }
+            ++lk;
+        } else {
+            load_a_any(r);
+        }
+    };
     load_a(ra[0]);
 #pragma unroll
     for (int q = 0; q < AIT; ++q) store_item(0, ra[0], q);
 #pragma unroll
     for (int j = 1; j < NA; ++j)
-        if (j < nk) load_a(ra[j]);
+        if (UNI || j < nk) load_a(ra[j]);
     dma_b(0, 0);
-    if (NA < nk) load_a(ra[0]);
-    if (nk > 1) dma_b(1, 1);
+    if (UNI || NA < nk) load_a(ra[0]);
+    if (UNI || nk > 1) dma_b(1, 1);
     auto iter = [&](int kt, const u32x4 (&rnext)[AIT][2], u32x4 (&rfree)[AIT][2]) {
         if (S::NDMA % WAVES == 0 && !(a.dbg & 2)) {   // immediates: no runtime wait_vm branch tree
             constexpr int MYD = S::NDMA % WAVES == 0 ? S::NDMA / WAVES : 0;
-            if (kt + NA < nk) wait_vm_k<2 * AIT + MYD>();
+            if (UNI || kt + NA < nk) wait_vm_k<2 * AIT + MYD>();
             else if (kt + 1 < nk) wait_vm_k<MYD>();
             else wait_vm_k<0>();
         } else {
-            wait_vm((kt + NA < nk ? 2 * AIT : 0) + (kt + 1 < nk ? my_dma : 0));
+            wait_vm(UNI ? 2 * AIT + my_dma : (kt + NA < nk ? 2 * AIT : 0) + (kt + 1 < nk ? my_dma : 0));
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this thread's A(kt) ds_writes
         __builtin_amdgcn_s_barrier();
@@ -872,25 +896,40 @@ __global__ __launch_bounds__(NT, NT == 256 && BM == 256 ? 1 : 2) void conv_x6_ke
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();                        // everyone done reading stage kt & 1
         asm volatile("" ::: "memory");
-        if (kt + 1 + NA < nk) load_a(rfree);                  // A(kt+1+NA) into the set A(kt+1) just left
-        if (kt + 2 < nk) dma_b(kt + 2, kt & 1);
+        if (UNI || kt + 1 + NA < nk) load_a(rfree);           // A(kt+1+NA) into the set A(kt+1) just left
+        if (UNI || kt + 2 < nk) dma_b(kt + 2, kt & 1);
     };
     // Raw barriers with counted waits: __syncthreads() would add vmcnt(0) and drain
     // the prefetch. Unrolled by NA so the register sets are indexed statically.
-    for (int kt = 0; kt < nk; kt += NA) {
+    if constexpr (UNI) {
+        int kt = 0;
+        for (; kt + NA <= nk; kt += NA) {
 #pragma unroll
-        for (int u = 0; u < NA; ++u)
+            for (int u = 0; u < NA; ++u) iter(kt + u, ra[(u + 1) % NA], ra[(u + 1) % NA]);
+        }
+#pragma unroll
+        for (int u = 0; u < NA - 1; ++u)
             if (kt + u < nk) iter(kt + u, ra[(u + 1) % NA], ra[(u + 1) % NA]);
+        wait_vm_k<0>();                                       // the out-of-range tail ops
+    } else {
+        for (int kt = 0; kt < nk; kt += NA) {
+#pragma unroll
+            for (int u = 0; u < NA; ++u)
+                if (kt + u < nk) iter(kt + u, ra[(u + 1) % NA], ra[(u + 1) % NA]);
+        }
     }
+    };
+    if (one && !(a.dbg & 1024)) main_loop(std::true_type{});
+    else main_loop(std::false_type{});
     } else {
     // ---- one LDS stage: per tile, B(kt) DMA and the split A(kt) write, then
     // compute; A(kt+1)'s loads run under it (registers), B waits for the stage
-    load_a(ra[0]);
+    load_a_any(ra[0]);
     auto iter1 = [&](int kt, const u32x4 (&rcur)[AIT][2], u32x4 (&rnext)[AIT][2]) {
         dma_b(kt, 0);
 #pragma unroll
         for (int q = 0; q < AIT; ++q) store_item(0, rcur, q);   // compiler waits for A(kt)'s loads
-        if (kt + 1 < nk) load_a(rnext);
+        if (kt + 1 < nk) load_a_any(rnext);
         if (kt + 1 < nk) wait_vm_k<2 * AIT>();                // B(kt) landed (older than A(kt+1))
         else wait_vm_k<0>();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -2192,7 +2231,8 @@ bool vd_conv1x1_x6_dual_ok(const ConvArgs& a) {
 hipError_t vd_launch_conv_x6(const ConvArgs& a0, hipStream_t s) {
     ConvArgs a = a0;
     a.dbg = a.tune ? (a.tune->x6_dbg & 3) | (a.tune->x6_one ? 4 : 0) | ((a.tune->x6_halo_dma & 3) << 3) |
-                     (((a.tune->x6_dbg >> 2) & 15) << 5) | (a.tune->x6_tr_epi ? 0 : 512) : 0;
+                     (((a.tune->x6_dbg >> 2) & 15) << 5) | (a.tune->x6_tr_epi ? 0 : 512) |
+                     (a.tune->x6_gemm_uni ? 0 : 1024) : 0;
     if (a.grp_co) {   // grouped: the halo form only, one 64-wide N tile per group
         if (a.grp_co != 64 || a.f32_split != 2 || !a.wx3 || !a.tune || !x6_halo_ok(a) || (a.ymax && a.B > kAmaxFrames))
             return hipErrorInvalidValue;
