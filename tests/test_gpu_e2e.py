@@ -527,21 +527,22 @@ def test_heads_fp32_pipelined_b_reads_bit_identical(gpu):
     issue the DMA two K steps ahead between MFMA groups (x6_halo_dma: 0 after the
     barrier, 1 after the MFMAs, 2 between groups, default); the streaming 1x1 layers
     with a residual load it beside the MFMAs (x6_stream_rl, default 1); the 1x1 GEMM
-    loop issues the same loads every K tile (x6_gemm_uni, default 1). Schedule only:
+    loop issues the same loads every K tile with one barrier per tile (x6_gemm_uni 2,
+    default; 1 keeps two barriers). Schedule only:
     the same products in the same order, heads bit-identical to the round-5 schedule."""
     import vdmi
     fr = _frames(2, 1080, 1920, seed=43)
     heads = {}
     for key, opts in (("r5", {"x6_halo_pf": 0, "x6_gemm_pf": 0, "x6_halo_dma": 0, "x6_stream_rl": 0,
                               "x6_gemm_uni": 0}), ("pf", {}),
-                      ("d1", {"x6_halo_dma": 1})):
+                      ("d1", {"x6_halo_dma": 1}), ("u1", {"x6_gemm_uni": 1})):
         ctx = vdmi.Context(precision="fp32", max_batch=2, options=opts)
         try:
             ctx.load_weights(0, face_weights("default"))
             heads[key] = ctx.forward_heads(fr)
         finally:
             ctx.close()
-    for k in ("pf", "d1"):
+    for k in ("pf", "d1", "u1"):
         for a, b in zip(heads[k], heads["r5"]):
             np.testing.assert_array_equal(a, b)
 
@@ -552,7 +553,7 @@ def test_heads_fp32_halo_conv(gpu):
     32-channel chunk over the tile's halo; option x6_halo, 2 = three B stages). Same
     products, K summed chunk-major instead of tap-major: heads within f32 rounding of
     the tap-major kernel, identical boxes; the two- and three-stage forms bit-identical
-    (same K order); batch-invariant (a frame's heads do not depend on its batch mates,
+    (same K order; two stages with one or two barriers per step, option x6_halo_1b); batch-invariant (a frame's heads do not depend on its batch mates,
     so halos that straddle frames read only zero padding)."""
     import vdmi
     fr = _frames(3, 1080, 1920, seed=37)
@@ -570,8 +571,15 @@ def test_heads_fp32_halo_conv(gpu):
                     np.testing.assert_array_equal(a[0], b[1])
         finally:
             ctx.close()
-    for a, b in zip(heads[2], heads[1]):
+    ctx = vdmi.Context(precision="fp32", max_batch=3, options={"x6_halo": 1, "x6_halo_1b": 0})
+    try:   # two B stages with two barriers per step (the round-5 loop; default one)
+        ctx.load_weights(0, face_weights("default"))
+        heads["1b0"] = ctx.forward_heads(fr)
+    finally:
+        ctx.close()
+    for a, b, c in zip(heads[2], heads[1], heads["1b0"]):
         np.testing.assert_array_equal(a, b)
+        np.testing.assert_array_equal(c, b)
     for a, b in zip(heads[1], heads[0]):
         assert np.abs(a - b).max() <= 6e-6 * (np.abs(b).max() + 1e-6), np.abs(a - b).max() / np.abs(b).max()
     assert sum(len(x) for x in boxes[0]) > 0

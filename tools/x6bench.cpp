@@ -48,7 +48,7 @@ static const TuneField kTune[] = {
     {"x6_mid", &VdTune::x6_mid},         {"x6_mf32", &VdTune::x6_mf32},           {"x6_tail", &VdTune::x6_tail},
     {"x6_halo", &VdTune::x6_halo},       {"x6_halo_s2", &VdTune::x6_halo_s2}, {"x6_adepth", &VdTune::x6_adepth},       {"x6_small_k", &VdTune::x6_small_k},
     {"x6_small_tiles", &VdTune::x6_small_tiles}, {"x6_gemm1x1", &VdTune::x6_gemm1x1}, {"x6_dbg", &VdTune::x6_dbg},
-    {"x6_halo_tr", &VdTune::x6_halo_tr}, {"x6_halo_dma", &VdTune::x6_halo_dma}, {"x6_halo_pf", &VdTune::x6_halo_pf}, {"x6_gemm_pf", &VdTune::x6_gemm_pf}, {"x6_gemm_uni", &VdTune::x6_gemm_uni}, {"x6_stream_rl", &VdTune::x6_stream_rl}, {"x6_tr_epi", &VdTune::x6_tr_epi}, {"x6_halo_n64", &VdTune::x6_halo_n64}, {"x6_one", &VdTune::x6_one},
+    {"x6_halo_tr", &VdTune::x6_halo_tr}, {"x6_halo_dma", &VdTune::x6_halo_dma}, {"x6_halo_pf", &VdTune::x6_halo_pf}, {"x6_gemm_pf", &VdTune::x6_gemm_pf}, {"x6_gemm_uni", &VdTune::x6_gemm_uni}, {"x6_halo_1b", &VdTune::x6_halo_1b}, {"x6_stream_rl", &VdTune::x6_stream_rl}, {"x6_tr_epi", &VdTune::x6_tr_epi}, {"x6_halo_n64", &VdTune::x6_halo_n64}, {"x6_one", &VdTune::x6_one},
 };
 
 static float frand(uint32_t& st) {

@@ -856,8 +856,12 @@ __global__ __launch_bounds__(NT, NT == 256 && BM == 256 ? 1 : 2) void conv_x6_ke
     // UNI (default; option x6_gemm_uni 0 = the round-5 loop): every iteration issues its
     // loads and DMA (past nk: out of range), the loop runs whole rounds of NA iterations
     // and a tail after it, so the compiler's waits on the A registers see every younger op
-    auto main_loop = [&](auto uni_tag) {
-    constexpr bool UNI = decltype(uni_tag)::value;
+    // ONEB (option x6_gemm_uni 2): one barrier per K tile -- B(kt+1)'s DMA and A(kt+NA)'s
+    // loads issued right after tile kt's barrier (stage (kt+1) & 1 was last read by tile
+    // kt-1, which every wave has finished there), so the barrier after the MFMAs goes
+    auto main_loop = [&](auto mode_tag) {
+    constexpr int MODE = decltype(mode_tag)::value;
+    constexpr bool UNI = MODE >= 1;
     auto load_a = [&](u32x4 (&r)[AIT][2]) {
         if constexpr (UNI) {                                  // 1x1 (one): no tap stepping, no branch
             const int so = (lk < nk ? lk : nk - 1) * (KT * 4);
@@ -874,6 +878,39 @@ __global__ __launch_bounds__(NT, NT == 256 && BM == 256 ? 1 : 2) void conv_x6_ke
     load_a(ra[0]);
 #pragma unroll
     for (int q = 0; q < AIT; ++q) store_item(0, ra[0], q);
+    if constexpr (MODE == 2) {
+        // VMEM order: A(1..NA-2), B(0), A(NA-1) | per tile kt after its barrier: B(kt+1),
+        // A(kt+NA). Younger than B(kt) at the top of kt: A(kt-1+NA) only.
+#pragma unroll
+        for (int j = 1; j < NA - 1; ++j) load_a(ra[j]);
+        dma_b(0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("" ::: "memory");
+        load_a(ra[NA - 1]);
+        auto iterb = [&](int kt, const u32x4 (&rnext)[AIT][2], u32x4 (&rfree)[AIT][2]) {
+            wait_vm_k<2 * AIT>();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this thread's A(kt) ds_writes
+            __builtin_amdgcn_s_barrier();                        // B(kt), A(kt) visible; tile kt-1 done
+            asm volatile("" ::: "memory");
+            dma_b(kt + 1, (kt + 1) & 1);
+            // the wait above counts the A loads as the youngest ops: the scheduler may not
+            // interleave them with the DMA (it did, and a DMA left in flight raced the reads)
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("" ::: "memory");
+            load_a(rfree);                                       // A(kt+NA) into the set A(kt) left
+            compute(kt & 1, kt + 1 < nk, (kt + 1) & 1, rnext);
+        };
+        int kt = 0;
+        for (; kt + NA <= nk; kt += NA) {
+#pragma unroll
+            for (int u = 0; u < NA; ++u) iterb(kt + u, ra[(u + 1) % NA], ra[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < NA - 1; ++u)
+            if (kt + u < nk) iterb(kt + u, ra[(u + 1) % NA], ra[u]);
+        wait_vm_k<0>();                                          // the tail's DMA / loads (past nk)
+        return;
+    }
 #pragma unroll
     for (int j = 1; j < NA; ++j)
         if (UNI || j < nk) load_a(ra[j]);
@@ -919,8 +956,17 @@ __global__ __launch_bounds__(NT, NT == 256 && BM == 256 ? 1 : 2) void conv_x6_ke
         }
     }
     };
-    if (one && !(a.dbg & 1024)) main_loop(std::true_type{});
-    else main_loop(std::false_type{});
+    bool looped = false;
+    if constexpr (S::NDMA % WAVES == 0) {
+        if (one && (a.dbg & 2048)) {
+            main_loop(std::integral_constant<int, 2>{});
+            looped = true;
+        }
+    }
+    if (!looped) {
+        if (one && !(a.dbg & 1024)) main_loop(std::integral_constant<int, 1>{});
+        else main_loop(std::integral_constant<int, 0>{});
+    }
     } else {
     // ---- one LDS stage: per tile, B(kt) DMA and the split A(kt) write, then
     // compute; A(kt+1)'s loads run under it (registers), B waits for the stage
@@ -1189,7 +1235,7 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
                 }
                 __builtin_amdgcn_sched_group_barrier(0x0008, 3 * TM, 0);
                 if constexpr (MYD > 0 && TN % MYD == 0) {   // x6_halo_dma = 2: a DMA piece per group
-                    if (dstep >= 0 && j % (TN / MYD) == 0) dma_piece(dstep, dstep % 3, j / (TN / MYD));
+                    if (dstep >= 0 && j % (TN / MYD) == 0) dma_piece(dstep, dstep % NSB, j / (TN / MYD));
                 }
             }
         } else {
@@ -1212,7 +1258,7 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
                     else acc[i][j] = mfma_terms<2>(af[i], bf, acc[i][j]);
                 }
                 if constexpr (MYD > 0 && TN % MYD == 0) {   // x6_halo_dma = 2: a DMA piece per group
-                    if (dstep >= 0 && j % (TN / MYD) == 0) dma_piece(dstep, dstep % 3, j / (TN / MYD));
+                    if (dstep >= 0 && j % (TN / MYD) == 0) dma_piece(dstep, dstep % NSB, j / (TN / MYD));
                 }
             }
         }
@@ -1224,7 +1270,8 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
     store_halo();
     if (tid < 8) *(u32x4*)(Ah + (tid >> 2) * PL_H + swzh(HR, tid & 3)) = u32x4{0u, 0u, 0u, 0u};
     dma_b(0, 0);
-    if (nsteps > 1) dma_b(1, 1);
+    const bool one_bar = NSB == 2 && MYD > 0 && !(a.dbg & 4096);
+    if (nsteps > 1 && !one_bar) dma_b(1, 1);
     if (nhalo > 1) load_halo(1);
     // Per thread VMEM issue order: ... [halo loads of chunk c+2 at the end of step
     // 9c+8], B(s+2) at the end of step s. At the top of step s, younger than B(s):
@@ -1295,6 +1342,35 @@ __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(Con
                 store_halo();
                 if (c + 2 < CH) load_halo(c + 2);
                 if (s + 2 < nsteps) dma_b(s + 2, (s + 2) % 3);
+            }
+        }
+    } else if (MYD > 0 && !(a.dbg & 4096)) {
+        // two B stages, ONE barrier per step (option x6_halo_1b): B(s+1)'s DMA is issued
+        // after step s's barrier (its stage was last read by step s-1, which every wave has
+        // finished there); a halo refill (tap 8) takes a second barrier. Younger than B(s)
+        // at the top of s: the halo loads issued at the end of step s-1 (or in the prologue,
+        // s = 0), behind the refill barrier's memory clobbers.
+        int hcur = 0;
+        for (int s = 0; s < nsteps; ++s) {
+            const int tap = s % 9;
+            const bool halo_prev = s == 0 ? nhalo > 1 : (tap == 0 && hcur + 1 < nhalo);
+            if (halo_prev) wait_vm_k<2 * QI>();
+            else wait_vm_k<0>();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (!(hdbg & 8)) __builtin_amdgcn_s_barrier();   // B(s) visible; stage (s + 1) & 1 free
+            asm volatile("" ::: "memory");
+            // B(s+1) right after the barrier (one step of latency cover: measured 3-4 % faster
+            // on the 256-wide tiles than pieces between the MFMA groups, r06t)
+            if (s + 1 < nsteps && !(hdbg & 1)) dma_b(s + 1, (s + 1) & 1);
+            const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
+            compute(s & 1, dy, dx, -1);
+            if (tap == 8 && hcur + 1 < nhalo) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                if (!(hdbg & 8)) __builtin_amdgcn_s_barrier();   // every wave is done with halo hcur
+                asm volatile("" ::: "memory");
+                if (!(hdbg & 2)) store_halo();
+                ++hcur;
+                if (hcur + 1 < nhalo && !(hdbg & 2)) load_halo(hcur + 1);
             }
         }
     } else {
@@ -2232,7 +2308,8 @@ hipError_t vd_launch_conv_x6(const ConvArgs& a0, hipStream_t s) {
     ConvArgs a = a0;
     a.dbg = a.tune ? (a.tune->x6_dbg & 3) | (a.tune->x6_one ? 4 : 0) | ((a.tune->x6_halo_dma & 3) << 3) |
                      (((a.tune->x6_dbg >> 2) & 15) << 5) | (a.tune->x6_tr_epi ? 0 : 512) |
-                     (a.tune->x6_gemm_uni ? 0 : 1024) : 0;
+                     (a.tune->x6_gemm_uni ? 0 : 1024) | (a.tune->x6_gemm_uni == 2 ? 2048 : 0) |
+                     (a.tune->x6_halo_1b ? 0 : 4096) : 0;
     if (a.grp_co) {   // grouped: the halo form only, one 64-wide N tile per group
         if (a.grp_co != 64 || a.f32_split != 2 || !a.wx3 || !a.tune || !x6_halo_ok(a) || (a.ymax && a.B > kAmaxFrames))
             return hipErrorInvalidValue;

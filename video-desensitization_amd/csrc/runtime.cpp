@@ -1129,7 +1129,7 @@ int vd_set_option(vd_ctx* h, const char* name, int value) {
         {"plate_s2d", &VdTune::plate_s2d}, {"f32_split", &VdTune::f32_split},
         {"x6_small_k", &VdTune::x6_small_k}, {"x6_small_tiles", &VdTune::x6_small_tiles},
         {"x6_stream", &VdTune::x6_stream}, {"x6_small_k2", &VdTune::x6_small_k2}, {"x6_bn256", &VdTune::x6_bn256},
-        {"x6_exact", &VdTune::x6_exact}, {"x6_mid", &VdTune::x6_mid}, {"block_fuse32", &VdTune::block_fuse32}, {"x6_mf32", &VdTune::x6_mf32}, {"x6_tail", &VdTune::x6_tail}, {"x6_stream_silu", &VdTune::x6_stream_silu}, {"x6_stream_rl", &VdTune::x6_stream_rl}, {"x6_gemm_uni", &VdTune::x6_gemm_uni}, {"x6_slots", &VdTune::x6_slots}, {"x6_halo", &VdTune::x6_halo}, {"x6_halo_narrow", &VdTune::x6_halo_narrow}, {"x6_halo_s2", &VdTune::x6_halo_s2}, {"x6_adepth", &VdTune::x6_adepth}, {"x6_gemm1x1", &VdTune::x6_gemm1x1}, {"x6_taps", &VdTune::x6_taps}, {"x6_halo_tr", &VdTune::x6_halo_tr}, {"x6_tr_epi", &VdTune::x6_tr_epi}, {"x6_halo_dma", &VdTune::x6_halo_dma}, {"x6_halo_pf", &VdTune::x6_halo_pf}, {"x6_halo_n64", &VdTune::x6_halo_n64}, {"x6_gemm_pf", &VdTune::x6_gemm_pf}, {"x6_stream256", &VdTune::x6_stream256}, {"plate_stage", &VdTune::plate_stage}, {"plate_detect_early", &VdTune::plate_detect_early}, {"mosaic_early", &VdTune::mosaic_early}, {"ssh_side", &VdTune::ssh_side}, {"face_groups", &VdTune::face_groups}, {"plate_s2d32", &VdTune::plate_s2d32}, {"det_group", &VdTune::det_group}, {"chain_gpw", &VdTune::chain_gpw}, {"block32_xd", &VdTune::block32_xd}, {"block32_pipe", &VdTune::block32_pipe}, {"x6_one", &VdTune::x6_one},
+        {"x6_exact", &VdTune::x6_exact}, {"x6_mid", &VdTune::x6_mid}, {"block_fuse32", &VdTune::block_fuse32}, {"x6_mf32", &VdTune::x6_mf32}, {"x6_tail", &VdTune::x6_tail}, {"x6_stream_silu", &VdTune::x6_stream_silu}, {"x6_stream_rl", &VdTune::x6_stream_rl}, {"x6_gemm_uni", &VdTune::x6_gemm_uni}, {"x6_halo_1b", &VdTune::x6_halo_1b}, {"x6_slots", &VdTune::x6_slots}, {"x6_halo", &VdTune::x6_halo}, {"x6_halo_narrow", &VdTune::x6_halo_narrow}, {"x6_halo_s2", &VdTune::x6_halo_s2}, {"x6_adepth", &VdTune::x6_adepth}, {"x6_gemm1x1", &VdTune::x6_gemm1x1}, {"x6_taps", &VdTune::x6_taps}, {"x6_halo_tr", &VdTune::x6_halo_tr}, {"x6_tr_epi", &VdTune::x6_tr_epi}, {"x6_halo_dma", &VdTune::x6_halo_dma}, {"x6_halo_pf", &VdTune::x6_halo_pf}, {"x6_halo_n64", &VdTune::x6_halo_n64}, {"x6_gemm_pf", &VdTune::x6_gemm_pf}, {"x6_stream256", &VdTune::x6_stream256}, {"plate_stage", &VdTune::plate_stage}, {"plate_detect_early", &VdTune::plate_detect_early}, {"mosaic_early", &VdTune::mosaic_early}, {"ssh_side", &VdTune::ssh_side}, {"face_groups", &VdTune::face_groups}, {"plate_s2d32", &VdTune::plate_s2d32}, {"det_group", &VdTune::det_group}, {"chain_gpw", &VdTune::chain_gpw}, {"block32_xd", &VdTune::block32_xd}, {"block32_pipe", &VdTune::block32_pipe}, {"x6_one", &VdTune::x6_one},
         {"jenc_gpu", &VdTune::jenc_gpu}, {"jdec_gpu", &VdTune::jdec_gpu}, {"jdec_chunk", &VdTune::jdec_chunk}, {"jdec_sync", &VdTune::jdec_sync}, {"jdec_group", &VdTune::jdec_group},
     };
     for (const Opt& o : opts)

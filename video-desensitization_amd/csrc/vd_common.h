@@ -117,8 +117,10 @@ struct VdTune {
     int x6_halo_s2 = 1;       // ... also 3x3 stride-2 convs (phase halos; Cout > 32)
     int x6_adepth = 2;        // A register sets of the 256 x {128, 64, 32} fp16-pair tiles (2 or 4; 4 measured level)
     int x6_slots = 0;         //   workgroup slots of one round (0: the CU count; tests force small values)
-    int x6_gemm_uni = 1;      // GEMM two-stage loop: the same loads / DMAs every K tile (past the end: out of
-                              //   range), so the compiler's register waits stay off the next tile (0: round-5 loop)
+    int x6_halo_1b = 1;       // halo tiles with two B stages (wide frames): one barrier per step (0: two)
+    int x6_gemm_uni = 2;      // 1x1 GEMM two-stage loop: the same loads / DMAs every K tile (past the end: the
+                              //   last tile again), so the compiler's register waits stay off the next tile
+                              //   (0: round-5 loop; 2: also one barrier per K tile)
     int x6_gemm_pf = 1;       // GEMM tiles with wide wave tiles (TN > TM): the same pipelined B-fragment reads
     int x6_halo_n64 = 0;      //   halo tiles: Cout-128 3x3 layers with K <= this as two 64-wide N tiles (0: off)
     int x6_halo_pf = 1;       //   halo tiles (128-256 wide): B fragments of block j + 1 read before block j's MFMAs
