@@ -2176,6 +2176,8 @@ static bool x6_tr_ok(const ConvArgs& a) {
 
 static hipError_t launch_tr(const ConvArgs& a, hipStream_t s) {
     const long t256 = (long)((a.M + 255) / 256) * (a.cout / 256);
+    // (Measured and not kept, round 6: Cout >= 512 1x1 layers with K <= 512-2048 on the
+    // 128 x 128 tile at two workgroups per CU -- level to 8 % slower, tools/runs/r06y.sh)
     if (a.cout % 256 == 0 && t256 >= 192) return launch_x6<256, 256, 512, 2, 2, 16, 2, true>(a, s);
     if (a.cout == 128 && a.tune->x6_mid && a.kpad <= a.tune->x6_mid) return launch_x6<128, 128, 256, 2, 2, 16, 2, true>(a, s);
     return launch_x6<256, 128, 512, 2, 2, 16, 2, true>(a, s);
