@@ -40,7 +40,7 @@ static const Layer kLayers[] = {
     {"fpn.m1", 80, 80, 256, 256, 3, 1, 1, 0},     {"ssh0.c51", 80, 80, 256, 192, 3, 1, 1, 0},
     {"ssh0.c52", 80, 80, 64, 128, 3, 1, 1, 0},    {"ssh0.c73", 80, 80, 64, 64, 3, 1, 1, 0},
     {"ssh1.c52", 40, 40, 64, 128, 3, 1, 1, 0},   {"l4.0.c3", 20, 20, 512, 2048, 1, 1, 0, 1},
-    {"l3.0.c3", 40, 40, 256, 1024, 1, 1, 0, 1},
+    {"l3.0.c3", 40, 40, 256, 1024, 1, 1, 0, 1},   {"l4.0.c2", 40, 40, 512, 512, 3, 2, 1, 0},
 };
 
 struct TuneField { const char* name; int VdTune::*f; };

@@ -1045,10 +1045,10 @@ __device__ __forceinline__ int swzh(int row, int chunk) { return row * 64 + ((ch
 // it); here ~1.3 (the phase halos' overlap). K runs chunk-major in phase order: a
 // fixed order for every output (batch invariance), another f32 summation order than
 // the tap-major GEMM.
-__host__ __device__ constexpr int s2_tap(int j) {   // step j of a chunk -> weight tap (dy + 1) * 3 + dx + 1
+__host__ __device__ __forceinline__ constexpr int s2_tap(int j) {   // step j of a chunk -> weight tap (dy + 1) * 3 + dx + 1
     return j == 0 ? 8 : j == 1 ? 6 : j == 2 ? 2 : j == 3 ? 0 : j == 4 ? 7 : j == 5 ? 1 : j == 6 ? 5 : j == 7 ? 3 : 4;
 }
-__host__ __device__ constexpr bool s2_last(int j) { return j == 3 || j == 5 || j == 7 || j == 8; }   // a phase ends
+__host__ __device__ __forceinline__ constexpr bool s2_last(int j) { return j == 3 || j == 5 || j == 7 || j == 8; }   // a phase ends
 
 template <int BN, int NSB, bool TR = false, bool S2 = false, bool PF = false>
 __global__ __launch_bounds__(512, BN <= 64 ? 4 : 2) void conv_x6_halo_kernel(ConvArgs a) {
