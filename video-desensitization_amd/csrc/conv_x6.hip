@@ -1518,9 +1518,15 @@ void conv1x1_x6_kernel(ConvArgs a, int nchunks, int groups) {
         };
         // the frame range of the group being split, loaded one group ahead (its load would
         // otherwise sit behind this group's residual loads in the in-order vmcnt)
+        // (a buffer load, issued whether or not the range slots exist -- num_records 0 then
+        // -- so the compiler's count of younger ops stays exact)
+        const __amdgpu_buffer_rsrc_t rsrc_m =
+            __builtin_amdgcn_make_buffer_rsrc((void*)a.xmax, 0, a.xmax ? a.B * 4 : 0, 0x00020000);
         auto frame_max = [&](int gg) -> float {
             const int mu = gg * 16 + p_lane;
-            return a.xmax ? __uint_as_float(a.xmax[(mu < a.M ? mu : a.M - 1) / ohw]) : a.xbound;
+            const int f = (mu < a.M ? mu : a.M - 1) / ohw;
+            const float v = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rsrc_m, f * 4, 0, 0));
+            return a.xmax ? v : a.xbound;
         };
         float xm_cur = g < groups ? frame_max(g) : 0.f;
         const __amdgpu_buffer_rsrc_t rsrc_r = __builtin_amdgcn_make_buffer_rsrc(
@@ -1904,8 +1910,10 @@ hipError_t launch_stream_x6(const ConvArgs& a, hipStream_t s) {
     // option x6_stream_rl (default 1): the RL form for the layers with a residual (layer3
     // conv3 330 -> 299 us, layer2 conv3 416 -> 404 in x6bench); without one it measured
     // slower (layer2.0 conv1 577 -> 603), so those keep the two-set form
-    if constexpr (!TAPS && !RL && NTT >= 2 && TERMS == 2 && RES != VD_RES_NONE) {
-        if (a.tune && a.tune->x6_stream_rl) return launch_stream_x6<KS, NTT, ACT, RES, TERMS, false, true>(a, s);
+    if constexpr (!TAPS && !RL && NTT >= 2 && TERMS == 2) {
+        // x6_stream_rl 2: also the layers without a residual
+        if (a.tune && (RES != VD_RES_NONE ? a.tune->x6_stream_rl : a.tune->x6_stream_rl >= 2))
+            return launch_stream_x6<KS, NTT, ACT, RES, TERMS, false, true>(a, s);
     }
     constexpr int NCH = 16 * NTT;
     constexpr int lds = (TERMS == 1 ? 2 : TERMS) * KS * NCH * 64 + 2 * NCH * 4;

@@ -96,6 +96,7 @@ struct VdTune {
     int x6_stream = 1;        // fp32 split: streaming 1x1 kernel for K in {64, 128, 256}
     int x6_stream_rl = 1;     //   streaming 1x1 with a residual: one input register set refilled per k-step, the
                               //   residual loaded at the top of each pixel group (beside the MFMAs), not in the epilogue
+                              //   (2: also the layers without a residual -- measured level, r06ag)
     int x6_stream_silu = 1;   //   fp16 pairs: also SiLU 1x1 convs (YOLO C2f / SPPF) with K in {32..256}
     int x6_stream256 = 2;     //   fp16 pairs, Cout % 256 == 0: 256-channel slices for K = 64 (2: and K = 128;
                               //   each pixel read by half as many workgroups: faces 27.31 -> 26.96 ms/step)
